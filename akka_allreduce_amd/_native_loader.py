@@ -1,0 +1,30 @@
+"""Loads the in-tree native extension, building it on first use if needed.
+
+The extension is the only implementation of the engine/kernels: there is no
+Python fallback, so a missing or broken build fails loudly here.
+"""
+from __future__ import annotations
+
+import importlib
+import os
+import threading
+
+_lock = threading.Lock()
+_mod = None
+
+
+def load():
+    global _mod
+    if _mod is not None:
+        return _mod
+    with _lock:
+        if _mod is not None:
+            return _mod
+        import torch  # noqa: F401  (loads torch's HIP runtime + RCCL first: one copy per process)
+
+        from . import _build
+
+        if not os.path.exists(_build.ext_path()) or os.environ.get("AKKA_REBUILD") == "1":
+            _build.build()
+        _mod = importlib.import_module("akka_allreduce_amd._native")
+        return _mod

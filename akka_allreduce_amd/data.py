@@ -1,0 +1,122 @@
+"""User I/O contract (reference: ``DataWrapper.scala:3-7``).
+
+``AllReduceInputRequest(iteration)`` -> ``AllReduceInput(data)`` is the data
+source; ``AllReduceOutput(data, count, iteration)`` goes to the data sink.
+
+``count`` is the per-element contributor count of the reference
+(ReducedDataBuffer.getWithCounts, RB:26-53).  It is carried compactly as one
+count per (block, chunk) and expanded to one int32 per element only when the
+``count`` attribute is first read (a gfx950 kernel on GPU), so a sink that
+never looks at counts does not pay an extra S-element int32 write per round.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Any, Optional
+
+import torch
+
+
+@dataclass(frozen=True)
+class Geometry:
+    """Block/chunk layout (W:240-250 with exact integer arithmetic)."""
+
+    dataSize: int
+    workerNum: int
+    maxChunkSize: int
+
+    @property
+    def step(self) -> int:
+        return (self.dataSize + self.workerNum - 1) // self.workerNum
+
+    def block_range(self, j: int) -> tuple[int, int]:
+        s = min(j * self.step, self.dataSize)
+        e = self.dataSize if j >= self.workerNum - 1 else min((j + 1) * self.step, self.dataSize)
+        return s, e
+
+    def block_len(self, j: int) -> int:
+        s, e = self.block_range(j)
+        return e - s
+
+    def num_chunks(self, j: int) -> int:
+        return -(-self.block_len(j) // self.maxChunkSize)
+
+    @property
+    def kmax(self) -> int:
+        return max(1, max(self.num_chunks(j) for j in range(self.workerNum)))
+
+    @property
+    def total_chunks(self) -> int:
+        return sum(self.num_chunks(j) for j in range(self.workerNum))
+
+    def chunk_range(self, j: int, k: int) -> tuple[int, int]:
+        s, e = self.block_range(j)
+        cs = s + k * self.maxChunkSize
+        return cs, min(cs + self.maxChunkSize, e)
+
+    def expand_counts(self, per_chunk: torch.Tensor) -> torch.Tensor:
+        """[N, kmax] counts -> [S] per-element counts (torch reference path)."""
+        per_chunk = per_chunk.reshape(self.workerNum, self.kmax)
+        idx = torch.arange(self.dataSize, device=per_chunk.device, dtype=torch.int64)
+        step = max(self.step, 1)
+        blk = torch.clamp(idx // step, max=self.workerNum - 1)
+        k = (idx - blk * step) // self.maxChunkSize
+        return per_chunk.reshape(-1)[blk * self.kmax + k].to(torch.int32)
+
+
+@dataclass
+class AllReduceInputRequest:
+    iteration: int
+
+
+@dataclass
+class AllReduceInput:
+    data: Any
+
+
+class AllReduceOutput:
+    """Reduced vector of one round + contributor counts.
+
+    ``data``: 1-D tensor of ``dataSize`` elements (sum over contributors;
+    chunks that did not reach the completion threshold are 0).
+    ``count``: int32 tensor, per-element contributor count (0 where missing).
+    ``iteration``: the round.
+    """
+
+    __slots__ = ("data", "iteration", "counts_per_chunk", "geometry", "_count", "_expander")
+
+    def __init__(
+        self,
+        data: torch.Tensor,
+        count: Optional[torch.Tensor] = None,
+        iteration: int = 0,
+        *,
+        counts_per_chunk: Optional[torch.Tensor] = None,
+        geometry: Optional[Geometry] = None,
+        expander: Any = None,
+    ):
+        self.data = data
+        self.iteration = iteration
+        self.counts_per_chunk = counts_per_chunk
+        self.geometry = geometry
+        self._count = count
+        self._expander = expander
+
+    @property
+    def count(self) -> torch.Tensor:
+        if self._count is None:
+            if self.counts_per_chunk is None or self.geometry is None:
+                raise ValueError("AllReduceOutput has no count information")
+            if self._expander is not None:
+                self._count = self._expander(self.counts_per_chunk)
+            else:
+                self._count = self.geometry.expand_counts(self.counts_per_chunk)
+        return self._count
+
+    def mean(self) -> torch.Tensor:
+        """Element-wise average over the contributors that made it (0 where none)."""
+        c = self.count.to(self.data.dtype if self.data.is_floating_point() else torch.float32)
+        return torch.where(c > 0, self.data / c.clamp(min=1), torch.zeros_like(self.data))
+
+    def __repr__(self) -> str:  # pragma: no cover - debugging aid
+        return f"AllReduceOutput(iteration={self.iteration}, n={self.data.numel()}, dtype={self.data.dtype})"

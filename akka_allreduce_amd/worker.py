@@ -1,0 +1,331 @@
+"""AllreduceWorker: one per rank (reference ``AllreduceWorker.scala:7-363``).
+
+The worker is an actor-style object: ``tell(msg)`` / ``receive(msg)`` accept
+the reference's messages (``InitWorkers``, ``StartAllreduce``, ``ScatterBlock``,
+``ReduceBlock``) plus ``WorkerTerminated``.  All round/threshold logic runs in
+the native engine (``csrc/engine/engine.cpp``); this class owns the round
+memory (torch tensors), calls the user's data source/sink, and routes outgoing
+messages to peer references.
+
+Transports
+----------
+``outbox``  every outgoing ScatterBlock/ReduceBlock is materialised as a message
+            and handed to the destination reference's ``tell`` (the TestKit
+            probe in the spec tests, a TCP proxy in a CPU cluster, an in-process
+            mailbox in the local actor system).
+``stream``  production: sends/receives are RCCL p2p groups over xGMI scheduled
+            by the native StreamLink; no per-chunk Python work at all.  Also
+            runs on the CPU p2p simulator (``transport_spec=("sim", hub, rank)``).
+
+Every handler is wrapped like the reference's ``tryCatch`` (W:287-299): errors
+are logged and recorded in ``errors`` and the worker keeps going, unless
+``strict=True``.
+"""
+from __future__ import annotations
+
+import logging
+from typing import Any, Callable, Dict, List, Optional, Tuple
+
+import torch
+
+from .data import AllReduceInput, AllReduceInputRequest, AllReduceOutput, Geometry
+from .messages import (
+    CompleteAllreduce,
+    InitWorkers,
+    ReduceBlock,
+    ScatterBlock,
+    StartAllreduce,
+    WorkerTerminated,
+)
+
+log = logging.getLogger("akka_allreduce_amd.worker")
+
+DataSource = Callable[[AllReduceInputRequest], AllReduceInput]
+DataSink = Callable[[AllReduceOutput], None]
+
+_DTYPES = {torch.float32: "float32", torch.bfloat16: "bfloat16"}
+
+
+def _native():
+    from . import _native_loader
+
+    return _native_loader.load()
+
+
+def _resolve_device(device: Any) -> torch.device:
+    if device is None or device == "cpu":
+        return torch.device("cpu")
+    if device == "auto":
+        return torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
+    d = torch.device(device)
+    if d.type == "cuda" and d.index is None:
+        d = torch.device("cuda", torch.cuda.current_device())
+    return d
+
+
+class AllreduceWorker:
+    """Threshold-allreduce worker (one per GPU rank, or per CPU process)."""
+
+    def __init__(
+        self,
+        dataSource: Optional[DataSource] = None,
+        dataSink: Optional[DataSink] = None,
+        *,
+        device: Any = None,
+        dtype: torch.dtype = torch.float32,
+        transport: str = "outbox",
+        transport_spec: Optional[Tuple[Any, ...]] = None,
+        broadcast_lag: int = 2,
+        strict: bool = False,
+        name: str = "worker",
+    ):
+        if dtype not in _DTYPES:
+            raise ValueError(f"unsupported dtype {dtype}; use float32 or bfloat16")
+        self.dataSource = dataSource if dataSource is not None else self._feed_source
+        self.dataSink = dataSink
+        self.device = _resolve_device(device)
+        self.dtype = dtype
+        self.transport = transport
+        self.transport_spec = transport_spec
+        self.strict = strict
+        self.name = name
+        n = _native()
+        deferred = bool(transport_spec and transport_spec[0] == "sim")
+        dev_index = self.device.index if self.device.type == "cuda" else -1
+        self._core = n.WorkerCore(self, transport, dev_index, _DTYPES[dtype], deferred, broadcast_lag)
+        self.id: int = -1
+        self.peers: Dict[int, Any] = {}
+        self.master: Any = None
+        self.geometry: Optional[Geometry] = None
+        self.errors: List[BaseException] = []
+        self._rounds: Dict[int, Dict[str, torch.Tensor]] = {}
+        self._pre_init: List[Any] = []
+        self._to_release: List[int] = []
+        self._feed: Dict[int, torch.Tensor] = {}
+        self._outputs: Dict[int, AllReduceOutput] = {}
+        self._next_round = 0
+        self._in_call = 0
+
+    # ------------------------------------------------------------------ actor API
+    def tell(self, msg: Any, sender: Any = None) -> None:
+        self.receive(msg)
+
+    def receive(self, msg: Any) -> None:
+        self._in_call += 1
+        try:
+            self._dispatch(msg)
+        except Exception as e:  # tryCatch: log and keep the worker alive (W:287-299)
+            self.errors.append(e)
+            log.error("%s: error handling %s: %s", self.name, type(msg).__name__, e)
+            if self.strict:
+                raise
+        finally:
+            self._in_call -= 1
+            if self._in_call == 0:
+                self._flush_outbox()
+                self._release_pending()
+
+    def _dispatch(self, msg: Any) -> None:
+        if isinstance(msg, InitWorkers):
+            self._on_init(msg)
+        elif isinstance(msg, StartAllreduce):
+            if not self.initialized:
+                self._pre_init.append(msg)
+            else:
+                self._core.start(int(msg.round))
+        elif isinstance(msg, ScatterBlock):
+            if not self.initialized:
+                self._pre_init.append(msg)
+                return
+            t = self._payload(msg.value)
+            self._core.scatter_in(int(msg.srcId), int(msg.destId), int(msg.chunkId), int(msg.round),
+                                  t.data_ptr(), t.numel(), t.device.type == "cpu")
+            self._sync_if_device_payload(t)
+        elif isinstance(msg, ReduceBlock):
+            if not self.initialized:
+                self._pre_init.append(msg)
+                return
+            t = self._payload(msg.value)
+            self._core.reduce_in(int(msg.srcId), int(msg.destId), int(msg.chunkId), int(msg.round), int(msg.count),
+                                 t.data_ptr(), t.numel(), t.device.type == "cpu")
+            self._sync_if_device_payload(t)
+        elif isinstance(msg, WorkerTerminated):
+            self.peers.pop(int(msg.workerId), None)
+            if self.initialized:
+                self._core.peer_terminated(int(msg.workerId))
+        else:
+            raise TypeError(f"unhandled message {msg!r}")
+
+    def _on_init(self, m: InitWorkers) -> None:
+        peers = [(int(i), ref is self) for i, ref in m.workers.items()]
+        first = self._core.init(int(m.destId), int(m.workerNum), float(m.thReduce), float(m.thComplete),
+                                int(m.maxLag), int(m.dataSize), int(m.maxChunkSize), peers)
+        self.peers = dict(m.workers)
+        if not first:
+            return  # re-init only replaces the peer map (W:87-89)
+        self.id = int(m.destId)
+        self.master = m.master
+        self.geometry = Geometry(int(m.dataSize), int(m.workerNum), int(m.maxChunkSize))
+        self._connect_transport()
+        self._core.attach()
+        st = self._core.state()
+        log.info("%s: id=%d peers %d/%d thReduce=%s thComplete=%s maxLag=%d scatter threshold=%d reduce threshold=%d",
+                 self.name, self.id, len(self.peers), m.workerNum, m.thReduce, m.thComplete, m.maxLag,
+                 st["min_scatter_required"], st["min_reduced_required"])
+        pending, self._pre_init = self._pre_init, []
+        for p in pending:
+            self._dispatch(p)
+
+    def _connect_transport(self) -> None:
+        if self.transport != "stream":
+            return
+        spec = self.transport_spec or (("local",) if self.geometry.workerNum == 1 else None)
+        if spec is None:
+            raise RuntimeError("stream transport needs transport_spec=('rccl', uid, rank, nranks) or ('sim', hub, rank)")
+        kind = spec[0]
+        if kind == "rccl":
+            _, uid, rank, nranks = spec
+            self._core.connect_rccl(uid, int(rank), int(nranks))
+        elif kind == "sim":
+            _, hub, rank = spec
+            self._core.connect_sim(hub, int(rank))
+        elif kind == "local":
+            self._core.connect_local()
+        else:
+            raise ValueError(f"unknown transport spec {spec!r}")
+
+    # ------------------------------------------------------------------ properties
+    @property
+    def initialized(self) -> bool:
+        return self.id >= 0
+
+    def state(self) -> Dict[str, Any]:
+        return self._core.state()
+
+    @property
+    def round(self) -> int:
+        return self._core.state()["round"]
+
+    @property
+    def maxRound(self) -> int:
+        return self._core.state()["max_round"]
+
+    @property
+    def completed(self) -> List[int]:
+        return self._core.state()["completed"]
+
+    # ------------------------------------------------------------------ collective convenience API
+    def allreduce(self, tensor: torch.Tensor) -> Optional[AllReduceOutput]:
+        """Start the next round with ``tensor`` as this worker's contribution.
+
+        For the scheduled (RCCL) transport the round's whole schedule is
+        enqueued on the GPU before this returns, and the returned output is
+        valid in the caller's current stream order.  Returns ``None`` if the
+        round has not completed yet (threshold transports driven by messages).
+        """
+        r = self._next_round
+        self._next_round += 1
+        self._feed[r] = tensor
+        self.receive(StartAllreduce(r))
+        return self._outputs.pop(r, None)
+
+    def _feed_source(self, req: AllReduceInputRequest) -> AllReduceInput:
+        t = self._feed.pop(req.iteration, None)
+        if t is None:
+            raise KeyError(f"no input fed for round {req.iteration}")
+        return AllReduceInput(t)
+
+    # ------------------------------------------------------------------ engine callbacks
+    def _stream_ptr(self) -> int:
+        if self.device.type != "cuda":
+            return 0
+        return torch.cuda.current_stream(self.device).cuda_stream
+
+    def _fetch(self, round_: int) -> None:
+        inp = self.dataSource(AllReduceInputRequest(round_))
+        data = inp.data if isinstance(inp, AllReduceInput) else inp
+        t = torch.as_tensor(data)
+        if t.numel() != self.geometry.dataSize:  # W:200-202
+            raise ValueError(f"Input data size {t.numel()} is different from initialization time "
+                             f"{self.geometry.dataSize}!")
+        t = t.reshape(-1).to(device=self.device, dtype=self.dtype).contiguous()
+        rec = self._rounds.setdefault(round_, {})
+        rec["input"] = t
+        self._core.bind_input(round_, t.data_ptr(), self._stream_ptr())
+
+    def _alloc_output(self, round_: int) -> None:
+        g = self.geometry
+        out = torch.empty(g.dataSize, dtype=self.dtype, device=self.device)
+        counts = torch.zeros(g.workerNum * g.kmax, dtype=torch.int32, device=self.device)
+        rec = self._rounds.setdefault(round_, {})
+        rec["output"], rec["counts"] = out, counts
+        self._core.bind_output(round_, out.data_ptr(), counts.data_ptr())
+
+    def _deliver(self, round_: int) -> None:
+        rec = self._rounds[round_]
+        if self.device.type == "cuda":
+            self._core.stream_wait_done(round_, self._stream_ptr())
+        g = self.geometry
+        out = AllReduceOutput(rec["output"], iteration=round_,
+                              counts_per_chunk=rec["counts"].view(g.workerNum, g.kmax), geometry=g,
+                              expander=self._expand_counts if self.device.type == "cuda" else None)
+        self._to_release.append(round_)
+        if self.dataSink is not None:
+            self.dataSink(out)
+        else:
+            self._outputs[round_] = out
+
+    def _notify_complete(self, round_: int) -> None:
+        self._flush_outbox()  # keep message order: peer traffic emitted before completion goes first
+        if self.master is not None:  # reference NPEs on a None master (W:276)
+            self.master.tell(CompleteAllreduce(self.id, round_))
+
+    def _release(self, round_: int) -> None:
+        self._to_release.append(round_)
+
+    def _expand_counts(self, per_chunk: torch.Tensor) -> torch.Tensor:
+        out = torch.empty(self.geometry.dataSize, dtype=torch.int32, device=per_chunk.device)
+        self._core.expand_counts(out.data_ptr(), per_chunk.contiguous().data_ptr(), self._stream_ptr())
+        return out
+
+    # ------------------------------------------------------------------ helpers
+    def _payload(self, value: Any) -> torch.Tensor:
+        t = value if isinstance(value, torch.Tensor) else torch.as_tensor(value)
+        if t.dtype != self.dtype:
+            t = t.to(self.dtype)
+        t = t.reshape(-1)
+        if t.device.type == "cuda" and self.device.type == "cpu":
+            t = t.cpu()
+        return t.contiguous()
+
+    def _sync_if_device_payload(self, t: torch.Tensor) -> None:
+        if t.device.type == "cuda":
+            self._core.sync_all()  # the async D2D copy must finish before `t` can be freed
+
+    def _flush_outbox(self) -> None:
+        for m in self._core.drain():
+            value = torch.frombuffer(bytearray(m.data), dtype=self.dtype) if len(m.data) else torch.empty(0, dtype=self.dtype)
+            if m.kind == 1:
+                msg: Any = ScatterBlock(value, m.src, m.dest, m.chunk, m.round)
+            else:
+                msg = ReduceBlock(value, m.src, m.dest, m.chunk, m.round, m.count)
+            ref = self.peers.get(m.dest)
+            if ref is None:
+                continue  # peer left the cluster
+            ref.tell(msg, self)
+
+    def _release_pending(self) -> None:
+        if not self._to_release:
+            return
+        todo, self._to_release = self._to_release, []
+        for r in todo:
+            if r in self._rounds:
+                self._core.unbind(r)
+                del self._rounds[r]
+
+    def synchronize(self) -> None:
+        """Block until all of this worker's queued device work is done."""
+        self._core.sync_all()
+
+    def __repr__(self) -> str:
+        return f"AllreduceWorker(name={self.name!r}, id={self.id}, device={self.device}, transport={self.transport})"

@@ -1,0 +1,334 @@
+// pybind11 module `akka_allreduce_amd._native`.
+//
+// Exposes one worker core (engine + data plane + link) per rank, the kernels
+// (for tests/bench), RCCL bootstrap helpers and the CPU p2p simulator.
+// Python owns all round memory (torch tensors) and passes raw pointers +
+// stream handles; nothing here depends on libtorch, so the module builds with
+// plain hipcc in seconds and loads on CPU-only machines.
+#include <hip/hip_runtime.h>
+#include <pybind11/functional.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "../engine/engine.h"
+#include "../kernels/kernels.h"
+#include "../transport/p2p.h"
+#include "../transport/stream_link.h"
+
+namespace py = pybind11;
+using namespace akka;
+
+namespace {
+
+struct PySimHub {
+  std::shared_ptr<SimHub> hub;
+};
+
+struct OutMsg {
+  int32_t kind;  // 1 scatter, 2 reduce
+  int32_t src, dest, chunk, round, count;
+  py::bytes data;
+};
+
+class OutboxLink final : public Link {
+ public:
+  explicit OutboxLink(int32_t me) : me_(me) {}
+  void bind(DataPlane* dp) { dp_ = dp; }
+  void send_scatter(int32_t dest, int32_t chunk, int32_t round, const Payload& p) override {
+    box_.push_back(make(1, dest, chunk, round, 0, p));
+  }
+  void send_reduce(int32_t dest, int32_t chunk, int32_t round, int32_t count, const Payload& p) override {
+    box_.push_back(make(2, dest, chunk, round, count, p));
+  }
+  std::vector<OutMsg> drain() {
+    std::vector<OutMsg> out;
+    out.swap(box_);
+    return out;
+  }
+  size_t size() const { return box_.size(); }
+
+ private:
+  OutMsg make(int32_t kind, int32_t dest, int32_t chunk, int32_t round, int32_t count, const Payload& p) {
+    std::string buf(size_t(p.len) * dp_->esize(), '\0');
+    dp_->read_payload(p, buf.data());
+    return OutMsg{kind, me_, dest, chunk, round, count, py::bytes(buf)};
+  }
+  int32_t me_;
+  DataPlane* dp_ = nullptr;
+  std::vector<OutMsg> box_;
+};
+
+class WorkerCore final : public EngineHost {
+ public:
+  WorkerCore(py::object host, std::string link, int32_t device, std::string dtype, bool deferred, int32_t lag)
+      : host_(std::move(host)), link_kind_(std::move(link)), device_idx_(device), deferred_(deferred), lag_(lag) {
+    if (dtype == "float32" || dtype == "f32" || dtype == "fp32") dt_ = DType::F32;
+    else if (dtype == "bfloat16" || dtype == "bf16") dt_ = DType::BF16;
+    else throw AkkaError("akka: unsupported dtype " + dtype);
+    AKKA_CHECK(link_kind_ == "outbox" || link_kind_ == "stream", "link must be 'outbox' or 'stream'");
+    engine_ = std::make_unique<Engine>(this, nullptr);
+  }
+  ~WorkerCore() override {
+    // Order: link and data plane reference the device and the engine.
+    stream_link_.reset();
+    dp_.reset();
+    p2p_.reset();
+    dev_.reset();
+  }
+
+  // ---- control -------------------------------------------------------------
+  bool init(int32_t id, int32_t n, float th_reduce, float th_complete, int32_t max_lag, int64_t data_size,
+            int64_t max_chunk, std::vector<std::pair<int32_t, bool>> peers) {
+    InitParams p;
+    p.id = id;
+    p.worker_num = n;
+    p.th_reduce = th_reduce;
+    p.th_complete = th_complete;
+    p.max_lag = max_lag;
+    p.data_size = data_size;
+    p.max_chunk_size = max_chunk;
+    std::vector<PeerEntry> pe;
+    for (auto& kv : peers) pe.push_back({kv.first, kv.second});
+    bool first = engine_->init(p, pe);
+    if (!first) return false;
+    if (device_idx_ < 0) dev_ = make_host_device(deferred_);
+    else dev_ = make_hip_device(device_idx_, true);
+    dp_ = std::make_unique<DataPlane>(dev_.get(), engine_->geometry(), id, max_lag + 1, dt_);
+    if (link_kind_ == "outbox") {
+      outbox_ = std::make_unique<OutboxLink>(id);
+      outbox_->bind(dp_.get());
+      engine_->set_link(outbox_.get());
+    }
+    return true;
+  }
+  // Must be called after init for link == "stream", before attach.
+  void connect_rccl(py::bytes uid, int32_t rank, int32_t nranks) {
+    std::string s = uid;
+    std::vector<uint8_t> v(s.begin(), s.end());
+    AKKA_CHECK(dev_ && !dev_->is_host(), "RCCL transport needs a HIP device");
+    p2p_ = make_rccl_p2p(v, rank, nranks, device_idx_);
+    make_stream_link();
+  }
+  void connect_sim(const PySimHub& hub, int32_t rank) {
+    AKKA_CHECK(dev_ && dev_->is_host() && deferred_, "sim transport needs a deferred host device");
+    p2p_ = make_sim_p2p(hub.hub, rank, dev_.get());
+    make_stream_link();
+  }
+  void connect_local() {  // N == 1: stream link without peers
+    AKKA_CHECK(engine_->geometry().N == 1, "connect_local is for single-worker jobs");
+    make_stream_link();
+  }
+  void attach() {
+    AKKA_CHECK(dp_, "attach before init");
+    if (link_kind_ == "stream") AKKA_CHECK(stream_link_, "stream link not connected");
+    engine_->attach(dp_.get());
+  }
+
+  void start(int32_t r) { engine_->start(r); }
+  void scatter_in(int32_t src, int32_t dest, int32_t chunk, int32_t round, uintptr_t ptr, int64_t len, bool on_host) {
+    Payload p{reinterpret_cast<const void*>(ptr), len, PayloadKind::External, on_host};
+    engine_->on_scatter(src, dest, chunk, round, p);
+  }
+  void reduce_in(int32_t src, int32_t dest, int32_t chunk, int32_t round, int32_t count, uintptr_t ptr, int64_t len,
+                 bool on_host) {
+    Payload p{reinterpret_cast<const void*>(ptr), len, PayloadKind::External, on_host};
+    engine_->on_reduce(src, dest, chunk, round, count, p);
+  }
+  void peer_terminated(int32_t id) { engine_->on_peer_terminated(id); }
+
+  // ---- memory bindings -----------------------------------------------------
+  void bind_input(int32_t round, uintptr_t ptr, uintptr_t stream) {
+    dp_->bind_input(round, reinterpret_cast<const void*>(ptr), reinterpret_cast<StreamH>(stream));
+  }
+  void bind_output(int32_t round, uintptr_t out, uintptr_t counts) {
+    dp_->bind_output(round, reinterpret_cast<void*>(out), reinterpret_cast<int32_t*>(counts));
+  }
+  void unbind(int32_t round) { dp_->unbind(round); }
+  void stream_wait_done(int32_t round, uintptr_t stream) {
+    dp_->stream_wait_done(round, reinterpret_cast<StreamH>(stream));
+  }
+  void sync_done(int32_t round) { dp_->sync_done(round); }
+  void sync_all() {
+    if (!dev_) return;
+    dev_->sync_stream(dev_->compute_stream());
+    dev_->sync_stream(dev_->comm_stream());
+  }
+  void expand_counts(uintptr_t out, uintptr_t counts, uintptr_t stream) {
+    const Geometry& g = engine_->geometry();
+    AKKA_CHECK(dev_ && !dev_->is_host(), "expand_counts: device path only");
+    launch_count_expand(reinterpret_cast<hipStream_t>(stream), reinterpret_cast<int32_t*>(out),
+                        reinterpret_cast<const int32_t*>(counts), g.S, g.step, g.N, g.C, dp_->kmax());
+  }
+
+  std::vector<OutMsg> drain() { return outbox_ ? outbox_->drain() : std::vector<OutMsg>{}; }
+  Device* device() const { return dev_.get(); }
+
+  // ---- introspection -------------------------------------------------------
+  py::dict state() const {
+    py::dict d;
+    d["id"] = engine_->id();
+    d["round"] = engine_->round();
+    d["max_round"] = engine_->max_round();
+    d["max_scattered"] = engine_->max_scattered();
+    d["completed"] = engine_->completed();
+    d["initialized"] = engine_->initialized();
+    std::vector<int32_t> ids;
+    for (auto& p : engine_->peers()) ids.push_back(p.id);
+    d["peers"] = ids;
+    if (engine_->id() >= 0) {
+      const Geometry& g = engine_->geometry();
+      d["step"] = g.step;
+      d["kmax"] = std::max(1, g.max_block_len_chunks());
+      d["min_scatter_required"] = engine_->min_scatter_required();
+      d["min_reduced_required"] = engine_->min_reduced_required();
+      d["ring_rows"] = engine_->params().max_lag + 1;
+    }
+    const EngineStats& s = engine_->stats();
+    py::dict st;
+    st["scatters_in"] = s.scatters_in;
+    st["reduces_in"] = s.reduces_in;
+    st["outdated_dropped"] = s.outdated_dropped;
+    st["future_started"] = s.future_started;
+    st["chunks_reduced"] = s.chunks_reduced;
+    st["forced_reduces"] = s.forced_reduces;
+    st["rounds_completed"] = s.rounds_completed;
+    st["rounds_forced"] = s.rounds_forced;
+    d["stats"] = st;
+    if (stream_link_) {
+      py::dict ls;
+      ls["groups"] = stream_link_->stats().groups;
+      ls["ops"] = stream_link_->stats().ops;
+      ls["bytes_sent"] = stream_link_->stats().bytes_sent;
+      ls["rounds"] = stream_link_->stats().rounds;
+      ls["lag"] = stream_link_->lag();
+      d["link"] = ls;
+    }
+    return d;
+  }
+  int32_t scatter_count(int32_t round, int32_t chunk) const { return engine_->scatter_count(round, chunk); }
+  int32_t reduced_arrivals(int32_t round) const { return engine_->reduced_arrivals(round); }
+
+  // ---- EngineHost -------------------------------------------------------------
+  void fetch(int32_t round) override { host_.attr("_fetch")(round); }
+  void alloc_output(int32_t round) override { host_.attr("_alloc_output")(round); }
+  void deliver(int32_t round) override { host_.attr("_deliver")(round); }
+  void notify_complete(int32_t round) override { host_.attr("_notify_complete")(round); }
+  void release(int32_t round) override { host_.attr("_release")(round); }
+
+ private:
+  void make_stream_link() {
+    AKKA_CHECK(link_kind_ == "stream", "worker was not created with link='stream'");
+    stream_link_ = std::make_unique<StreamLink>(engine_.get(), p2p_.get(), lag_);
+    stream_link_->bind(dp_.get());
+    engine_->set_link(stream_link_.get());
+  }
+
+  py::object host_;
+  std::string link_kind_;
+  int32_t device_idx_;
+  bool deferred_;
+  int32_t lag_;
+  DType dt_ = DType::F32;
+  std::unique_ptr<Device> dev_;
+  std::unique_ptr<DataPlane> dp_;
+  std::unique_ptr<P2P> p2p_;
+  std::unique_ptr<StreamLink> stream_link_;
+  std::unique_ptr<OutboxLink> outbox_;
+  std::unique_ptr<Engine> engine_;
+};
+
+hipStream_t as_stream(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
+
+}  // namespace
+
+PYBIND11_MODULE(_native, m) {
+  m.doc() = "MI355X-native threshold allreduce core (engine, gfx950 kernels, RCCL/xGMI transport)";
+  py::register_exception<AkkaError>(m, "AkkaError", PyExc_RuntimeError);
+
+  py::class_<OutMsg>(m, "OutMsg")
+      .def_readonly("kind", &OutMsg::kind)
+      .def_readonly("src", &OutMsg::src)
+      .def_readonly("dest", &OutMsg::dest)
+      .def_readonly("chunk", &OutMsg::chunk)
+      .def_readonly("round", &OutMsg::round)
+      .def_readonly("count", &OutMsg::count)
+      .def_readonly("data", &OutMsg::data);
+
+  py::class_<PySimHub>(m, "SimHub")
+      .def(py::init([](int32_t n) { return PySimHub{make_sim_hub(n)}; }))
+      .def("bytes_moved", [](const PySimHub& h) { return sim_bytes_moved(h.hub); });
+
+  py::class_<WorkerCore>(m, "WorkerCore")
+      .def(py::init<py::object, std::string, int32_t, std::string, bool, int32_t>(), py::arg("host"),
+           py::arg("link") = "outbox", py::arg("device") = -1, py::arg("dtype") = "float32",
+           py::arg("deferred") = false, py::arg("lag") = 2)
+      .def("init", &WorkerCore::init)
+      .def("connect_rccl", &WorkerCore::connect_rccl)
+      .def("connect_sim", &WorkerCore::connect_sim)
+      .def("connect_local", &WorkerCore::connect_local)
+      .def("attach", &WorkerCore::attach)
+      .def("start", &WorkerCore::start)
+      .def("scatter_in", &WorkerCore::scatter_in)
+      .def("reduce_in", &WorkerCore::reduce_in)
+      .def("peer_terminated", &WorkerCore::peer_terminated)
+      .def("bind_input", &WorkerCore::bind_input)
+      .def("bind_output", &WorkerCore::bind_output)
+      .def("unbind", &WorkerCore::unbind)
+      .def("stream_wait_done", &WorkerCore::stream_wait_done)
+      .def("sync_done", &WorkerCore::sync_done)
+      .def("sync_all", &WorkerCore::sync_all)
+      .def("expand_counts", &WorkerCore::expand_counts)
+      .def("drain", &WorkerCore::drain)
+      .def("state", &WorkerCore::state)
+      .def("scatter_count", &WorkerCore::scatter_count)
+      .def("reduced_arrivals", &WorkerCore::reduced_arrivals);
+
+  m.def("sim_run", [](const PySimHub& hub, std::vector<WorkerCore*> cores, int64_t max_iters) {
+    std::vector<Device*> devs;
+    for (auto* c : cores) devs.push_back(c->device());
+    sim_run(hub.hub, devs, max_iters);
+  }, py::arg("hub"), py::arg("cores"), py::arg("max_iters") = 100000000);
+
+  m.def("rccl_unique_id", []() {
+    auto v = rccl_unique_id();
+    return py::bytes(reinterpret_cast<const char*>(v.data()), v.size());
+  });
+  m.def("rccl_version", []() { return std::string(rccl_version_string()); });
+
+  // ---- kernels (tests / microbench) ----------------------------------------------
+  m.def("reduce", [](uintptr_t dst, std::vector<uintptr_t> srcs, int64_t n, std::string dtype, uintptr_t stream,
+                     std::string impl) {
+    DType dt = (dtype == "bfloat16" || dtype == "bf16") ? DType::BF16 : DType::F32;
+    ReduceImpl im = ReduceImpl::Auto;
+    if (impl == "vec") im = ReduceImpl::Vec;
+    else if (impl == "lds") im = ReduceImpl::Lds;
+    else if (impl == "scalar") im = ReduceImpl::Scalar;
+    std::vector<const void*> ptrs;
+    for (auto p : srcs) ptrs.push_back(reinterpret_cast<const void*>(p));
+    AKKA_CHECK(!ptrs.empty(), "reduce: no sources");
+    for (const auto& spec : split_reduce(reinterpret_cast<void*>(dst), ptrs, n)) launch_reduce(as_stream(stream), spec, dt, im);
+  }, py::arg("dst"), py::arg("srcs"), py::arg("n"), py::arg("dtype") = "float32", py::arg("stream") = 0,
+        py::arg("impl") = "auto");
+  m.def("count_expand", [](uintptr_t out, uintptr_t counts, int64_t S, int64_t step, int32_t N, int64_t C,
+                           int32_t kmax, uintptr_t stream) {
+    launch_count_expand(as_stream(stream), reinterpret_cast<int32_t*>(out), reinterpret_cast<const int32_t*>(counts),
+                        S, step, N, C, kmax);
+  });
+  m.def("geometry", [](int64_t S, int32_t N, int64_t C) {
+    Geometry g(S, N, C);
+    py::dict d;
+    std::vector<std::pair<int64_t, int64_t>> blocks;
+    std::vector<int32_t> nch;
+    for (int32_t j = 0; j < N; ++j) {
+      blocks.push_back({g.block_start(j), g.block_end(j)});
+      nch.push_back(g.num_chunks(j));
+    }
+    d["step"] = g.step;
+    d["blocks"] = blocks;
+    d["num_chunks"] = nch;
+    d["total_chunks"] = g.total_chunks();
+    return d;
+  });
+  m.def("float_threshold", &float_threshold);
+  m.attr("build_arch") = "gfx950";
+}

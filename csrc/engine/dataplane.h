@@ -1,0 +1,131 @@
+// Data plane: where chunks live and the two compute ops on them.
+//
+// Replaces the reference's buffer layer (buffer/AllReduceBuffer.scala,
+// ScatteredDataBuffer.scala, ReducedDataBuffer.scala) with a layout built for
+// zero-copy device transport:
+//
+//  * scatter ring  [L][N][myBlockLen]   -- peers' contributions to MY block
+//    (ScatteredDataBuffer's temporalBuffer, AllReduceBuffer.scala:11-21).
+//    My own contribution is never copied: its slot aliases the round's input
+//    tensor (the reference short-circuits self messages, W:228-232).
+//  * output row    [S] per round         -- the reduced vector at its final
+//    offsets, bound per round by the embedding layer (a fresh torch tensor),
+//    so ReducedDataBuffer.getWithCounts' concatenation (RB:26-53) is free:
+//    peers' reduced chunks are received straight into place.
+//  * counts        [N][Kmax] int32       -- contributor count per (block, chunk);
+//    the per-element expansion of RB:41-47 is a lazy kernel (count_expand).
+//
+// All bookkeeping (arrival masks, thresholds, landed flags) lives in the Engine;
+// the data plane only owns memory, streams and kernels.
+#pragma once
+
+#include <map>
+#include <memory>
+#include <vector>
+
+#include "device.h"
+#include "geometry.h"
+
+namespace akka {
+
+class DataPlane {
+ public:
+  DataPlane(Device* dev, const Geometry& g, int32_t me, int32_t ring_rows, DType dt);
+  ~DataPlane();
+  DataPlane(const DataPlane&) = delete;
+  DataPlane& operator=(const DataPlane&) = delete;
+
+  Device* device() const { return dev_; }
+  const Geometry& geometry() const { return g_; }
+  int32_t me() const { return me_; }
+  DType dtype() const { return dt_; }
+  size_t esize() const { return dtype_size(dt_); }
+  int32_t ring_rows() const { return L_; }
+  int32_t kmax() const { return kmax_; }
+
+  // --- per-round bindings (memory owned by the embedding layer) ------------
+  // `ready_stream` is the stream that produced `input` (nullptr: already ready).
+  void bind_input(int32_t round, const void* input, StreamH ready_stream);
+  void bind_output(int32_t round, void* output, int32_t* counts);
+  bool has_input(int32_t round) const;
+  bool has_output(int32_t round) const;
+  void unbind(int32_t round);
+
+  // --- views ---------------------------------------------------------------
+  Payload input_chunk(int32_t round, int32_t block, int32_t k) const;
+  Payload output_chunk(int32_t round, int32_t block, int32_t k) const;
+  void* scatter_slot(int32_t round, int32_t src, int32_t k) const;
+  void* output_at(int32_t round, int32_t block, int32_t k) const;
+  int32_t* counts_row(int32_t round, int32_t block) const;
+
+  // --- phase 1 receive side + the chunk N-way sum ----------------------------
+  void store_scatter(int32_t round, int32_t src, int32_t k, const Payload& p);
+  // Sum the listed sources' copies of my chunk k into the output row; returns a
+  // ReducedView payload of the result (what gets broadcast).
+  Payload reduce(int32_t round, int32_t k, const std::vector<int32_t>& srcs);
+
+  // --- phase 2 receive side --------------------------------------------------
+  void store_reduced(int32_t round, int32_t src, int32_t k, const Payload& p);
+  void set_count(int32_t round, int32_t block, int32_t k, int32_t count);
+  // Copy host-known counts of the given blocks into the round's counts tensor.
+  void upload_counts(int32_t round, const std::vector<int32_t>& blocks, StreamH s);
+
+  // Zero data+count of chunks that never landed (landed: [N][kmax] flags), join
+  // the comm and compute streams and record the round's done event.
+  void finalize(int32_t round, const std::vector<uint8_t>& landed);
+  // Make `stream` wait for the round's done event (stream-ordered hand-off).
+  void stream_wait_done(int32_t round, StreamH stream);
+  // Host-blocking wait for the round (used by the host/outbox paths).
+  void sync_done(int32_t round);
+
+  // Copy a payload to host bytes (probe/TCP transports). Synchronous.
+  void read_payload(const Payload& p, void* host_dst) const;
+
+  // Stream hooks for the scheduled link.
+  EventH record_compute();
+  EventH record_comm();
+  void compute_wait(EventH e) { dev_->wait(dev_->compute_stream(), e); }
+  void comm_wait(EventH e) { dev_->wait(dev_->comm_stream(), e); }
+  // Event after the last compute op that reads ring row of `round`.
+  EventH row_release_event(int32_t round) const;
+
+ private:
+  struct Binding {
+    const void* input = nullptr;
+    void* output = nullptr;
+    int32_t* counts = nullptr;
+    EventH input_ready = nullptr;  // recorded on the producer stream
+    bool input_waited = false;
+    EventH done = nullptr;
+    bool finalized = false;
+  };
+  struct Row {
+    int32_t round = -1;
+    std::vector<uint8_t> self_alias;  // [K_me]: slot[me] of chunk k aliases the input
+    EventH released = nullptr;        // compute-stream event after last reader
+    EventH staging_done = nullptr;    // comm-stream event after last counts upload
+  };
+
+  Row& row_for(int32_t round);
+  const Binding& binding(int32_t round) const;
+  Binding& binding_mut(int32_t round);
+  void ensure_input_waited(Binding& b);
+  EventH pooled_event();
+
+  Device* dev_;
+  Geometry g_;
+  int32_t me_;
+  int32_t L_;
+  DType dt_;
+  int32_t kme_;
+  int32_t kmax_;
+  int64_t my_len_;
+  void* scatter_ring_ = nullptr;   // [L][N][my_len]
+  int32_t* staging_ = nullptr;     // pinned [L][N][kmax]
+  std::vector<Row> rows_;
+  std::map<int32_t, Binding> bind_;
+  std::vector<EventH> events_;     // all events created (destroyed at teardown)
+  std::vector<EventH> free_events_;
+};
+
+}  // namespace akka

@@ -1,0 +1,78 @@
+// Device abstraction: the data plane and the stream-scheduled link are written
+// once against this interface and run either on a HIP device (production,
+// gfx950 kernels + HIP streams/events) or on the host (CPU dev boxes, the
+// spec-test probe, and the multi-rank p2p simulator that checks the RCCL
+// schedule without a GPU).
+//
+// The reference has no device boundary at all: every buffer is a JVM array and
+// every copy is System.arraycopy (AllReduceBuffer.scala:25-32,
+// ReducedDataBuffer.scala:38); the N-way chunk sum is a scalar JVM loop
+// (ScatteredDataBuffer.scala:20-32).
+#pragma once
+
+#include <functional>
+#include <memory>
+#include <vector>
+
+#include "common.h"
+
+namespace akka {
+
+using StreamH = void*;
+using EventH = void*;
+
+// Sources per reduce launch; more sources are folded in extra passes.
+constexpr int kMaxReduceSrc = 16;
+
+// dst[0:n) = sum_i srcs[i][0:n)   (fp32 accumulate; dst may alias srcs[0])
+struct ReduceSpec {
+  void* dst = nullptr;
+  const void* srcs[kMaxReduceSrc] = {};
+  int32_t nsrc = 0;
+  int64_t n = 0;
+};
+
+enum class CopyKind : int32_t { Default = 0, HostToDevice = 1, DeviceToHost = 2, DeviceToDevice = 3, HostToHost = 4 };
+
+class Device {
+ public:
+  virtual ~Device() = default;
+  virtual bool is_host() const = 0;
+  virtual int32_t device_index() const { return -1; }
+
+  virtual void* alloc(size_t bytes) = 0;
+  virtual void release(void* p) = 0;
+  // Page-locked host staging memory (plain host memory on the host device).
+  virtual void* alloc_pinned(size_t bytes) = 0;
+  virtual void release_pinned(void* p) = 0;
+
+  virtual StreamH comm_stream() = 0;
+  virtual StreamH compute_stream() = 0;
+
+  virtual EventH create_event() = 0;
+  virtual void destroy_event(EventH e) = 0;
+  virtual void record(EventH e, StreamH s) = 0;
+  virtual void wait(StreamH s, EventH e) = 0;
+  virtual bool query(EventH e) = 0;
+  virtual void sync_event(EventH e) = 0;
+  virtual void sync_stream(StreamH s) = 0;
+
+  virtual void reduce(StreamH s, const ReduceSpec* specs, int32_t nspecs, DType dt) = 0;
+  virtual void copy(StreamH s, void* dst, const void* src, size_t bytes, CopyKind kind) = 0;
+  virtual void zero(StreamH s, void* dst, size_t bytes) = 0;
+
+  // Host-device only: deferred execution queue used by the p2p simulator.
+  virtual void enqueue_host_op(StreamH, std::function<bool()>) {
+    throw AkkaError("enqueue_host_op: not a host device");
+  }
+};
+
+// Reduce specs with more than kMaxReduceSrc sources: fold into passes where
+// pass p>0 accumulates into dst (dst is its own first source).
+std::vector<ReduceSpec> split_reduce(void* dst, const std::vector<const void*>& srcs, int64_t n);
+
+std::unique_ptr<Device> make_host_device(bool deferred);
+// Defined in hip_device.cpp (HIP build only).
+std::unique_ptr<Device> make_hip_device(int32_t device_index, bool high_priority_comm);
+
+}  // namespace akka

@@ -1,0 +1,175 @@
+// Host implementation of the Device interface.
+//
+// Immediate mode executes every op at the call (the spec-test probe path and
+// CPU-only clusters).  Deferred mode appends ops to one in-order queue per
+// device; the p2p simulator (sim_p2p.cpp) drains the queues of N simulated
+// ranks together, so grouped send/recv rendezvous, matching order and deadlock
+// freedom of the RCCL schedule are exercised on a CPU box.
+#include <cmath>
+#include <cstdlib>
+#include <deque>
+
+#include "device.h"
+
+namespace akka {
+
+static inline float bf16_to_f32(uint16_t v) {
+  uint32_t u = uint32_t(v) << 16;
+  float f;
+  std::memcpy(&f, &u, 4);
+  return f;
+}
+static inline uint16_t f32_to_bf16(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x007fffffu)) return uint16_t((u >> 16) | 0x40);  // keep NaN
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return uint16_t(u >> 16);
+}
+
+static void host_reduce(const ReduceSpec& s, DType dt) {
+  if (dt == DType::F32) {
+    float* d = static_cast<float*>(s.dst);
+    std::vector<float> acc(static_cast<size_t>(s.n), 0.0f);
+    for (int32_t i = 0; i < s.nsrc; ++i) {
+      const float* p = static_cast<const float*>(s.srcs[i]);
+      for (int64_t j = 0; j < s.n; ++j) acc[j] += p[j];
+    }
+    std::memcpy(d, acc.data(), size_t(s.n) * 4);
+  } else {
+    uint16_t* d = static_cast<uint16_t*>(s.dst);
+    std::vector<float> acc(static_cast<size_t>(s.n), 0.0f);
+    for (int32_t i = 0; i < s.nsrc; ++i) {
+      const uint16_t* p = static_cast<const uint16_t*>(s.srcs[i]);
+      for (int64_t j = 0; j < s.n; ++j) acc[j] += bf16_to_f32(p[j]);
+    }
+    for (int64_t j = 0; j < s.n; ++j) d[j] = f32_to_bf16(acc[j]);
+  }
+}
+
+std::vector<ReduceSpec> split_reduce(void* dst, const std::vector<const void*>& srcs, int64_t n) {
+  std::vector<ReduceSpec> out;
+  size_t i = 0;
+  bool first = true;
+  do {
+    ReduceSpec s;
+    s.dst = dst;
+    s.n = n;
+    if (!first) s.srcs[s.nsrc++] = dst;
+    while (i < srcs.size() && s.nsrc < kMaxReduceSrc) s.srcs[s.nsrc++] = srcs[i++];
+    out.push_back(s);
+    first = false;
+  } while (i < srcs.size());
+  return out;
+}
+
+namespace {
+
+class HostDevice final : public Device {
+ public:
+  explicit HostDevice(bool deferred) : deferred_(deferred) {}
+  ~HostDevice() override = default;
+
+  bool is_host() const override { return true; }
+  void* alloc(size_t bytes) override {
+    void* p = std::calloc(bytes ? bytes : 1, 1);
+    AKKA_CHECK(p, "host alloc failed");
+    return p;
+  }
+  void release(void* p) override { std::free(p); }
+  void* alloc_pinned(size_t bytes) override { return alloc(bytes); }
+  void release_pinned(void* p) override { std::free(p); }
+
+  StreamH comm_stream() override { return reinterpret_cast<StreamH>(1); }
+  StreamH compute_stream() override { return reinterpret_cast<StreamH>(2); }
+
+  // One in-order queue: events carry no information beyond program order.
+  EventH create_event() override { return reinterpret_cast<EventH>(new int(0)); }
+  void destroy_event(EventH e) override { delete reinterpret_cast<int*>(e); }
+  void record(EventH, StreamH) override {}
+  void wait(StreamH, EventH) override {}
+  bool query(EventH) override { return !deferred_ || queue_.empty(); }
+  void sync_event(EventH) override {
+    if (!deferred_) return;
+    step();  // best effort: a simulated rank cannot block on its peers
+  }
+  void sync_stream(StreamH) override { drain_or_throw(); }
+
+  void reduce(StreamH, const ReduceSpec* specs, int32_t n, DType dt) override {
+    std::vector<ReduceSpec> v(specs, specs + n);
+    run([v, dt]() {
+      for (const auto& s : v) host_reduce(s, dt);
+      return true;
+    });
+  }
+  void copy(StreamH, void* dst, const void* src, size_t bytes, CopyKind kind) override {
+    if (dst == src || bytes == 0) return;
+    if (deferred_ && kind == CopyKind::HostToDevice) {
+      // Host->device copies read their (pinned / message-owned) source when
+      // issued; snapshot it so the deferred queue models that contract.
+      auto snap = std::make_shared<std::vector<char>>(static_cast<const char*>(src),
+                                                      static_cast<const char*>(src) + bytes);
+      run([=]() {
+        std::memcpy(dst, snap->data(), bytes);
+        return true;
+      });
+      return;
+    }
+    run([=]() {
+      std::memmove(dst, src, bytes);
+      return true;
+    });
+  }
+  void zero(StreamH, void* dst, size_t bytes) override {
+    run([=]() {
+      std::memset(dst, 0, bytes);
+      return true;
+    });
+  }
+  void enqueue_host_op(StreamH, std::function<bool()> op) override {
+    AKKA_CHECK(deferred_, "enqueue_host_op requires a deferred host device");
+    queue_.push_back(std::move(op));
+  }
+
+  // Simulator hooks.
+  bool deferred() const { return deferred_; }
+  // Run queue head ops until one blocks; returns true if any progress was made.
+  bool step() {
+    bool progress = false;
+    while (!queue_.empty()) {
+      if (!queue_.front()()) break;
+      queue_.pop_front();
+      progress = true;
+    }
+    return progress;
+  }
+  bool idle() const { return queue_.empty(); }
+
+ private:
+  void run(std::function<bool()> f) {
+    if (deferred_) {
+      queue_.push_back(std::move(f));
+    } else {
+      f();
+    }
+  }
+  void drain_or_throw() {
+    if (!deferred_) return;
+    step();
+    AKKA_CHECK(queue_.empty(),
+               "host device sync would block: the simulated stream waits on a peer (drive the simulator instead)");
+  }
+
+  bool deferred_;
+  std::deque<std::function<bool()>> queue_;
+};
+
+}  // namespace
+
+std::unique_ptr<Device> make_host_device(bool deferred) { return std::make_unique<HostDevice>(deferred); }
+
+// Exposed to sim_p2p.cpp.
+bool host_device_step(Device* d) { return static_cast<HostDevice*>(d)->step(); }
+bool host_device_idle(Device* d) { return static_cast<HostDevice*>(d)->idle(); }
+
+}  // namespace akka

@@ -1,0 +1,176 @@
+// HIP implementation of the Device interface (MI355X, gfx950).
+//
+// Two streams per worker: `comm` carries the RCCL groups (and the counts
+// upload), `compute` the chunk reduces and copies; they synchronise through
+// events only, so a reduce of chunk k overlaps the xGMI transfer of step k+1.
+// Pinned staging memory is hipHostMalloc'd.  Reduce launches of consecutive
+// chunks with identical source layouts are merged before launch (a worker
+// whose whole round is self-contained, e.g. N=1, issues ONE kernel per round).
+#include <hip/hip_runtime.h>
+
+#include <mutex>
+
+#include "../engine/device.h"
+#include "kernels.h"
+
+namespace akka {
+
+#define AKKA_HIP(call)                                                                        \
+  do {                                                                                        \
+    hipError_t e_ = (call);                                                                   \
+    if (e_ != hipSuccess)                                                                     \
+      throw AkkaError(std::string("akka: ") + #call + " failed: " + hipGetErrorString(e_));   \
+  } while (0)
+
+namespace {
+
+class HipDevice final : public Device {
+ public:
+  HipDevice(int32_t dev, bool high_priority_comm) : dev_(dev) {
+    AKKA_HIP(hipSetDevice(dev));
+    int lo = 0, hi = 0;
+    AKKA_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    AKKA_HIP(hipStreamCreateWithPriority(&comm_, hipStreamNonBlocking, high_priority_comm ? hi : lo));
+    AKKA_HIP(hipStreamCreateWithPriority(&compute_, hipStreamNonBlocking, lo));
+    impl_ = reduce_impl_from_env();
+  }
+  ~HipDevice() override {
+    hipSetDevice(dev_);
+    hipStreamSynchronize(comm_);
+    hipStreamSynchronize(compute_);
+    hipStreamDestroy(comm_);
+    hipStreamDestroy(compute_);
+  }
+
+  bool is_host() const override { return false; }
+  int32_t device_index() const override { return dev_; }
+
+  void* alloc(size_t bytes) override {
+    void* p = nullptr;
+    AKKA_HIP(hipSetDevice(dev_));
+    AKKA_HIP(hipMalloc(&p, bytes ? bytes : 16));
+    return p;
+  }
+  void release(void* p) override {
+    if (p) hipFree(p);
+  }
+  void* alloc_pinned(size_t bytes) override {
+    void* p = nullptr;
+    AKKA_HIP(hipHostMalloc(&p, bytes ? bytes : 16, hipHostMallocDefault));
+    return p;
+  }
+  void release_pinned(void* p) override {
+    if (p) hipHostFree(p);
+  }
+
+  StreamH comm_stream() override { return comm_; }
+  StreamH compute_stream() override { return compute_; }
+
+  EventH create_event() override {
+    hipEvent_t e;
+    AKKA_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    return e;
+  }
+  void destroy_event(EventH e) override { hipEventDestroy(static_cast<hipEvent_t>(e)); }
+  void record(EventH e, StreamH s) override {
+    flush_if(s);
+    AKKA_HIP(hipEventRecord(static_cast<hipEvent_t>(e), static_cast<hipStream_t>(s)));
+  }
+  void wait(StreamH s, EventH e) override {
+    flush_if(s);
+    AKKA_HIP(hipStreamWaitEvent(static_cast<hipStream_t>(s), static_cast<hipEvent_t>(e), 0));
+  }
+  bool query(EventH e) override {
+    flush_all();
+    hipError_t r = hipEventQuery(static_cast<hipEvent_t>(e));
+    if (r == hipSuccess) return true;
+    if (r == hipErrorNotReady) return false;
+    AKKA_HIP(r);
+    return false;
+  }
+  void sync_event(EventH e) override {
+    flush_all();
+    AKKA_HIP(hipEventSynchronize(static_cast<hipEvent_t>(e)));
+  }
+  void sync_stream(StreamH s) override {
+    flush_if(s);
+    AKKA_HIP(hipStreamSynchronize(static_cast<hipStream_t>(s)));
+  }
+
+  void reduce(StreamH s, const ReduceSpec* specs, int32_t n, DType dt) override {
+    for (int32_t i = 0; i < n; ++i) {
+      const ReduceSpec& sp = specs[i];
+      if (pending_.size() && pending_stream_ == s && pending_dt_ == dt && mergeable(pending_.back(), sp)) {
+        pending_.back().n += sp.n;
+        continue;
+      }
+      flush_if(s);
+      flush_all();
+      pending_.push_back(sp);
+      pending_stream_ = s;
+      pending_dt_ = dt;
+    }
+  }
+  void copy(StreamH s, void* dst, const void* src, size_t bytes, CopyKind kind) override {
+    if (bytes == 0 || dst == src) return;
+    flush_if(s);
+    hipMemcpyKind k = hipMemcpyDefault;
+    switch (kind) {
+      case CopyKind::HostToDevice:
+        k = hipMemcpyHostToDevice;
+        break;
+      case CopyKind::DeviceToHost:
+        k = hipMemcpyDeviceToHost;
+        break;
+      case CopyKind::DeviceToDevice:
+        k = hipMemcpyDeviceToDevice;
+        break;
+      default:
+        k = hipMemcpyDefault;
+    }
+    AKKA_HIP(hipMemcpyAsync(dst, src, bytes, k, static_cast<hipStream_t>(s)));
+  }
+  void zero(StreamH s, void* dst, size_t bytes) override {
+    if (!bytes) return;
+    flush_if(s);
+    AKKA_HIP(hipMemsetAsync(dst, 0, bytes, static_cast<hipStream_t>(s)));
+  }
+
+ private:
+  bool mergeable(const ReduceSpec& a, const ReduceSpec& b) const {
+    if (a.nsrc != b.nsrc) return false;
+    const size_t es = dtype_size(pending_dt_);
+    const size_t off = size_t(a.n) * es;
+    if (static_cast<char*>(a.dst) + off != b.dst) return false;
+    for (int i = 0; i < a.nsrc; ++i) {
+      // dst-as-accumulator passes (split_reduce) never merge
+      if (a.srcs[i] == a.dst) return false;
+      if (static_cast<const char*>(a.srcs[i]) + off != b.srcs[i]) return false;
+    }
+    return true;
+  }
+  void flush_if(StreamH s) {
+    if (!pending_.empty() && pending_stream_ == s) flush_all();
+  }
+  void flush_all() {
+    if (pending_.empty()) return;
+    for (const auto& sp : pending_) launch_reduce(static_cast<hipStream_t>(pending_stream_), sp, pending_dt_, impl_);
+    pending_.clear();
+  }
+
+  int32_t dev_;
+  hipStream_t comm_ = nullptr;
+  hipStream_t compute_ = nullptr;
+  ReduceImpl impl_;
+  std::vector<ReduceSpec> pending_;
+  StreamH pending_stream_ = nullptr;
+  DType pending_dt_ = DType::F32;
+};
+
+}  // namespace
+
+std::unique_ptr<Device> make_hip_device(int32_t device_index, bool high_priority_comm) {
+  return std::make_unique<HipDevice>(device_index, high_priority_comm);
+}
+
+}  // namespace akka

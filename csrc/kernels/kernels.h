@@ -1,0 +1,26 @@
+// Launchers for the gfx950 kernels (kernels.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "../engine/device.h"
+
+namespace akka {
+
+enum class ReduceImpl : int32_t {
+  Auto = 0,    // pick per call (currently: Vec)
+  Vec = 1,     // 16-B global loads straight to VGPRs, all sources in flight per thread
+  Lds = 2,     // global_load_lds (LDS-DMA) double-buffered staging, then ds_read + sum
+  Scalar = 3,  // unaligned fallback
+};
+
+// dst = sum(srcs) over n elements (fp32 accumulate).
+void launch_reduce(hipStream_t s, const ReduceSpec& spec, DType dt, ReduceImpl impl);
+// counts[N][kmax] (per block, per chunk) -> out[S] (per element), RB:41-47.
+void launch_count_expand(hipStream_t s, int32_t* out, const int32_t* counts, int64_t S, int64_t step, int32_t N,
+                         int64_t C, int32_t kmax);
+// Standalone kernels for tests/bench: out = a (+ b ...) via a pointer table on device.
+ReduceImpl reduce_impl_from_env();
+const char* reduce_impl_name(ReduceImpl i);
+
+}  // namespace akka

@@ -1,0 +1,348 @@
+// gfx950 (MI355X / CDNA4) kernels for the threshold allreduce.
+//
+// Hot spot K1 of SURVEY §2.3: the chunk N-way sum (reference: the scalar JVM
+// loop of ScatteredDataBuffer.reduce, SB:20-32), plus the count expansion of
+// ReducedDataBuffer.getWithCounts (RB:41-47).
+//
+// The sum is pure HBM streaming (nsrc reads + 1 write per element, no reuse),
+// so the design goal is bytes-in-flight, not arithmetic:
+//   * Vec: every lane issues 16-B loads for ALL sources of UNROLL vectors before
+//     the first add (NSRC*UNROLL independent loads per lane), grid-stride over
+//     the chunk with a grid capped at 8 blocks/CU x 256 CUs.  fp32 accumulate.
+//   * Lds: each wave streams its own 1-KiB-per-source tiles through LDS with
+//     global_load_lds_dwordx4 (LDS-DMA, no VGPR destination), double-buffered
+//     with a counted vmcnt so tile t+1 is in flight while tile t is summed.
+// Both are templated on the source count so the loads unroll completely.
+// 64-lane waves throughout; blocks of 256 threads = 4 waves.
+#include <hip/hip_runtime.h>
+
+#include <cstdlib>
+#include <cstring>
+
+#include "kernels.h"
+
+namespace akka {
+
+namespace {
+
+using v4u = unsigned int __attribute__((ext_vector_type(4)));
+constexpr int kBlock = 256;
+constexpr int kMaxGrid = 256 * 8;  // 256 CUs x 8 blocks
+
+struct SrcTable {
+  const void* p[kMaxReduceSrc];
+};
+
+__device__ __forceinline__ void add_vec(float (&acc)[4], const v4u& v, float) {
+  acc[0] += __uint_as_float(v.x);
+  acc[1] += __uint_as_float(v.y);
+  acc[2] += __uint_as_float(v.z);
+  acc[3] += __uint_as_float(v.w);
+}
+
+__device__ __forceinline__ void add_vec(float (&acc)[8], const v4u& v, unsigned short) {
+  acc[0] += __uint_as_float(v.x << 16);
+  acc[1] += __uint_as_float(v.x & 0xffff0000u);
+  acc[2] += __uint_as_float(v.y << 16);
+  acc[3] += __uint_as_float(v.y & 0xffff0000u);
+  acc[4] += __uint_as_float(v.z << 16);
+  acc[5] += __uint_as_float(v.z & 0xffff0000u);
+  acc[6] += __uint_as_float(v.w << 16);
+  acc[7] += __uint_as_float(v.w & 0xffff0000u);
+}
+
+__device__ __forceinline__ uint32_t pack_bf16x2(float lo, float hi) {
+  // Plain casts lower to v_cvt_pk_bf16_f32 on gfx950 (RNE, NaN-preserving).
+  __bf16 a = static_cast<__bf16>(lo);
+  __bf16 b = static_cast<__bf16>(hi);
+  return uint32_t(__builtin_bit_cast(unsigned short, a)) | (uint32_t(__builtin_bit_cast(unsigned short, b)) << 16);
+}
+
+__device__ __forceinline__ v4u pack_vec(const float (&acc)[4]) {
+  return v4u{__float_as_uint(acc[0]), __float_as_uint(acc[1]), __float_as_uint(acc[2]), __float_as_uint(acc[3])};
+}
+__device__ __forceinline__ v4u pack_vec(const float (&acc)[8]) {
+  return v4u{pack_bf16x2(acc[0], acc[1]), pack_bf16x2(acc[2], acc[3]), pack_bf16x2(acc[4], acc[5]),
+             pack_bf16x2(acc[6], acc[7])};
+}
+
+template <typename T>
+struct VecTraits;
+template <>
+struct VecTraits<float> {
+  static constexpr int kElems = 4;
+};
+template <>
+struct VecTraits<unsigned short> {
+  static constexpr int kElems = 8;
+};
+
+// ---- Vec: loads straight to VGPRs ----------------------------------------------
+template <typename T, int NSRC, int UNROLL>
+__global__ __launch_bounds__(kBlock) void reduce_vec_kernel(SrcTable srcs, v4u* __restrict__ dst, int64_t nvec) {
+  constexpr int E = VecTraits<T>::kElems;
+  const int64_t stride = int64_t(gridDim.x) * kBlock;
+  for (int64_t base = int64_t(blockIdx.x) * kBlock + threadIdx.x; base < nvec; base += stride * UNROLL) {
+    v4u v[UNROLL][NSRC];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const int64_t i = base + u * stride;
+      if (i < nvec) {
+#pragma unroll
+        for (int s = 0; s < NSRC; ++s) v[u][s] = __builtin_nontemporal_load(static_cast<const v4u*>(srcs.p[s]) + i);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const int64_t i = base + u * stride;
+      if (i < nvec) {
+        float acc[E];
+#pragma unroll
+        for (int e = 0; e < E; ++e) acc[e] = 0.f;
+#pragma unroll
+        for (int s = 0; s < NSRC; ++s) add_vec(acc, v[u][s], T{});
+        dst[i] = pack_vec(acc);
+      }
+    }
+  }
+}
+
+// ---- Lds: LDS-DMA staging, per-wave double buffer ----------------------------------
+// Wave w of the block owns LDS [buf][src][w][64 lanes] x 16 B.  A tile is 64
+// vectors (1 KiB) per source.  global_load_lds writes lane l's 16 B at
+// wave_base + 16*l, i.e. exactly where lane l reads it back.
+template <typename T, int NSRC>
+__global__ __launch_bounds__(kBlock) void reduce_lds_kernel(SrcTable srcs, v4u* __restrict__ dst, int64_t nvec) {
+  constexpr int E = VecTraits<T>::kElems;
+  constexpr int kWaves = kBlock / 64;
+  __shared__ v4u lds[2][NSRC][kWaves][64];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int64_t ntiles = nvec / 64;  // full wave tiles; the tail goes through VGPRs
+  const int64_t wave_id = int64_t(blockIdx.x) * kWaves + wave;
+  const int64_t wave_stride = int64_t(gridDim.x) * kWaves;
+
+  auto issue = [&](int64_t tile, int buf) {
+#pragma unroll
+    for (int s = 0; s < NSRC; ++s) {
+      const v4u* g = static_cast<const v4u*>(srcs.p[s]) + tile * 64 + lane;
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)g,
+                                       (__attribute__((address_space(3))) void*)&lds[buf][s][wave][0], 16, 0, 0);
+    }
+  };
+
+  int64_t t = wave_id;
+  int buf = 0;
+  if (t < ntiles) issue(t, 0);
+  for (; t < ntiles; t += wave_stride) {
+    const int64_t nt = t + wave_stride;
+    if (nt < ntiles) {
+      issue(nt, buf ^ 1);
+      // NSRC loads of the next tile may stay in flight; the current tile's are retired
+      // (loads retire in order; an interleaved store only makes the wait stricter).
+      if constexpr (NSRC == 1) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+      else if constexpr (NSRC == 2) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      else if constexpr (NSRC == 3) asm volatile("s_waitcnt vmcnt(3)" ::: "memory");
+      else if constexpr (NSRC == 4) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else if constexpr (NSRC == 5) asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+      else if constexpr (NSRC == 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else if constexpr (NSRC == 7) asm volatile("s_waitcnt vmcnt(7)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    float acc[E];
+#pragma unroll
+    for (int e = 0; e < E; ++e) acc[e] = 0.f;
+#pragma unroll
+    for (int s = 0; s < NSRC; ++s) add_vec(acc, lds[buf][s][wave][lane], T{});
+    dst[t * 64 + lane] = pack_vec(acc);
+    // The reads of `buf` must land before tile t+2 re-targets it.
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    buf ^= 1;
+  }
+  // Tail (< 64 vectors): first wave of the grid, through VGPRs.
+  if (wave_id == 0) {
+    const int64_t i = ntiles * 64 + lane;
+    if (i < nvec) {
+      float acc[E];
+#pragma unroll
+      for (int e = 0; e < E; ++e) acc[e] = 0.f;
+#pragma unroll
+      for (int s = 0; s < NSRC; ++s) add_vec(acc, static_cast<const v4u*>(srcs.p[s])[i], T{});
+      dst[i] = pack_vec(acc);
+    }
+  }
+}
+
+// ---- Scalar: unaligned pointers / sub-vector tails --------------------------------
+template <typename T>
+__device__ __forceinline__ float to_f(T v);
+template <>
+__device__ __forceinline__ float to_f<float>(float v) {
+  return v;
+}
+template <>
+__device__ __forceinline__ float to_f<unsigned short>(unsigned short v) {
+  return __uint_as_float(uint32_t(v) << 16);
+}
+template <typename T>
+__device__ __forceinline__ T from_f(float v);
+template <>
+__device__ __forceinline__ float from_f<float>(float v) {
+  return v;
+}
+template <>
+__device__ __forceinline__ unsigned short from_f<unsigned short>(float v) {
+  return __builtin_bit_cast(unsigned short, static_cast<__bf16>(v));
+}
+
+template <typename T>
+__global__ __launch_bounds__(kBlock) void reduce_scalar_kernel(SrcTable srcs, int nsrc, T* __restrict__ dst,
+                                                               int64_t n) {
+  const int64_t stride = int64_t(gridDim.x) * kBlock;
+  for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride) {
+    float acc = 0.f;
+    for (int s = 0; s < nsrc; ++s) acc += to_f(static_cast<const T*>(srcs.p[s])[i]);
+    dst[i] = from_f<T>(acc);
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void count_expand_kernel(int32_t* __restrict__ out,
+                                                              const int32_t* __restrict__ counts, int64_t S,
+                                                              int64_t step, int32_t N, int64_t C, int32_t kmax) {
+  const int64_t stride = int64_t(gridDim.x) * kBlock;
+  for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < S; i += stride) {
+    int64_t j = step > 0 ? i / step : 0;
+    if (j > N - 1) j = N - 1;
+    const int64_t k = (i - j * step) / C;
+    out[i] = counts[j * kmax + k];
+  }
+}
+
+template <typename T, int NSRC>
+void launch_vec_n(hipStream_t s, const SrcTable& t, v4u* dst, int64_t nvec) {
+  constexpr int UNROLL = NSRC <= 4 ? 4 : (NSRC <= 8 ? 2 : 1);
+  int64_t want = (nvec + int64_t(kBlock) * UNROLL - 1) / (int64_t(kBlock) * UNROLL);
+  int grid = int(want < kMaxGrid ? (want < 1 ? 1 : want) : kMaxGrid);
+  hipLaunchKernelGGL((reduce_vec_kernel<T, NSRC, UNROLL>), dim3(grid), dim3(kBlock), 0, s, t, dst, nvec);
+}
+
+template <typename T, int NSRC>
+void launch_lds_n(hipStream_t s, const SrcTable& t, v4u* dst, int64_t nvec) {
+  constexpr int kWaves = kBlock / 64;
+  int64_t tiles = nvec / 64;
+  int64_t want = (tiles + kWaves * 2 - 1) / (kWaves * 2);  // >= 2 tiles per wave to pipeline
+  int grid = int(want < kMaxGrid ? (want < 1 ? 1 : want) : kMaxGrid);
+  hipLaunchKernelGGL((reduce_lds_kernel<T, NSRC>), dim3(grid), dim3(kBlock), 0, s, t, dst, nvec);
+}
+
+template <typename T>
+void launch_vec(hipStream_t s, const SrcTable& t, int nsrc, v4u* dst, int64_t nvec, bool lds) {
+#define AKKA_CASE(K)                                        \
+  case K:                                                   \
+    if (lds && K <= 8) launch_lds_n<T, (K <= 8 ? K : 8)>(s, t, dst, nvec); \
+    else launch_vec_n<T, K>(s, t, dst, nvec);               \
+    break;
+  switch (nsrc) {
+    AKKA_CASE(1)
+    AKKA_CASE(2)
+    AKKA_CASE(3)
+    AKKA_CASE(4)
+    AKKA_CASE(5)
+    AKKA_CASE(6)
+    AKKA_CASE(7)
+    AKKA_CASE(8)
+    AKKA_CASE(9)
+    AKKA_CASE(10)
+    AKKA_CASE(11)
+    AKKA_CASE(12)
+    AKKA_CASE(13)
+    AKKA_CASE(14)
+    AKKA_CASE(15)
+    AKKA_CASE(16)
+    default:
+      throw AkkaError("reduce: unsupported source count");
+  }
+#undef AKKA_CASE
+}
+
+inline void check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw AkkaError(std::string("akka: ") + what + ": " + hipGetErrorString(e));
+}
+
+}  // namespace
+
+ReduceImpl reduce_impl_from_env() {
+  const char* v = std::getenv("AKKA_REDUCE_IMPL");
+  if (!v) return ReduceImpl::Auto;
+  if (!std::strcmp(v, "vec")) return ReduceImpl::Vec;
+  if (!std::strcmp(v, "lds")) return ReduceImpl::Lds;
+  if (!std::strcmp(v, "scalar")) return ReduceImpl::Scalar;
+  return ReduceImpl::Auto;
+}
+
+const char* reduce_impl_name(ReduceImpl i) {
+  switch (i) {
+    case ReduceImpl::Vec:
+      return "vec";
+    case ReduceImpl::Lds:
+      return "lds";
+    case ReduceImpl::Scalar:
+      return "scalar";
+    default:
+      return "auto";
+  }
+}
+
+void launch_reduce(hipStream_t s, const ReduceSpec& spec, DType dt, ReduceImpl impl) {
+  if (spec.n <= 0) return;
+  AKKA_CHECK(spec.nsrc >= 1 && spec.nsrc <= kMaxReduceSrc, "reduce: bad source count");
+  SrcTable t{};
+  bool aligned = (reinterpret_cast<uintptr_t>(spec.dst) & 15) == 0;
+  for (int i = 0; i < spec.nsrc; ++i) {
+    t.p[i] = spec.srcs[i];
+    aligned &= (reinterpret_cast<uintptr_t>(spec.srcs[i]) & 15) == 0;
+  }
+  const int64_t per_vec = dt == DType::F32 ? 4 : 8;
+  const int64_t nvec = aligned ? spec.n / per_vec : 0;
+  if (impl == ReduceImpl::Scalar) {
+    // forced scalar path over everything
+  } else if (nvec > 0) {
+    const bool lds = impl == ReduceImpl::Lds;
+    if (dt == DType::F32) launch_vec<float>(s, t, spec.nsrc, static_cast<v4u*>(spec.dst), nvec, lds);
+    else launch_vec<unsigned short>(s, t, spec.nsrc, static_cast<v4u*>(spec.dst), nvec, lds);
+    check_launch("reduce_vec");
+  }
+  const int64_t done = impl == ReduceImpl::Scalar ? 0 : nvec * per_vec;
+  const int64_t rest = spec.n - done;
+  if (rest > 0) {
+    const size_t es = dt == DType::F32 ? 4 : 2;
+    SrcTable tt{};
+    for (int i = 0; i < spec.nsrc; ++i) tt.p[i] = static_cast<const char*>(spec.srcs[i]) + done * es;
+    int64_t want = (rest + kBlock - 1) / kBlock;
+    int grid = int(want < kMaxGrid ? want : kMaxGrid);
+    if (dt == DType::F32) {
+      hipLaunchKernelGGL(reduce_scalar_kernel<float>, dim3(grid), dim3(kBlock), 0, s, tt, spec.nsrc,
+                         reinterpret_cast<float*>(static_cast<char*>(spec.dst) + done * es), rest);
+    } else {
+      hipLaunchKernelGGL(reduce_scalar_kernel<unsigned short>, dim3(grid), dim3(kBlock), 0, s, tt, spec.nsrc,
+                         reinterpret_cast<unsigned short*>(static_cast<char*>(spec.dst) + done * es), rest);
+    }
+    check_launch("reduce_scalar");
+  }
+}
+
+void launch_count_expand(hipStream_t s, int32_t* out, const int32_t* counts, int64_t S, int64_t step, int32_t N,
+                         int64_t C, int32_t kmax) {
+  if (S <= 0) return;
+  int64_t want = (S + kBlock - 1) / kBlock;
+  int grid = int(want < kMaxGrid ? want : kMaxGrid);
+  hipLaunchKernelGGL(count_expand_kernel, dim3(grid), dim3(kBlock), 0, s, out, counts, S, step, N, C, kmax);
+  check_launch("count_expand");
+}
+
+}  // namespace akka

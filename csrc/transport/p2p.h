@@ -1,0 +1,52 @@
+// Grouped point-to-point transport.
+//
+// The reference's data plane is Akka remoting: every ScatterBlock/ReduceBlock
+// is an independent TCP message into an unbounded mailbox.  On
+// MI355X the data plane is RCCL send/recv over xGMI: a group of sends/recvs to
+// all peers runs concurrently, one peer per xGMI link.  RCCL p2p is a
+// rendezvous (a send completes only against the matching recv, matched in
+// issue order per peer pair), so the schedule that issues the groups
+// (stream_link.h) must be symmetric across ranks; SimP2P checks exactly that
+// on the CPU.
+#pragma once
+
+#include <memory>
+#include <vector>
+
+#include "../engine/device.h"
+
+namespace akka {
+
+struct P2POp {
+  bool send = false;
+  int32_t peer = -1;
+  void* buf = nullptr;
+  size_t bytes = 0;
+};
+
+class P2P {
+ public:
+  virtual ~P2P() = default;
+  virtual int32_t rank() const = 0;
+  virtual int32_t nranks() const = 0;
+  // Enqueue one group of ops on `stream` (RCCL: ncclGroupStart .. ncclGroupEnd).
+  virtual void group(StreamH stream, const std::vector<P2POp>& ops) = 0;
+  virtual const char* name() const = 0;
+};
+
+// ---- CPU simulator ------------------------------------------------------------
+class SimHub;
+std::shared_ptr<SimHub> make_sim_hub(int32_t nranks);
+// Endpoint for `rank`; ops are queued on the rank's deferred host device.
+std::unique_ptr<P2P> make_sim_p2p(std::shared_ptr<SimHub> hub, int32_t rank, Device* dev);
+// Drive all ranks' deferred devices until every queue is empty.  Throws with a
+// diagnostic if no rank can make progress (a schedule deadlock).
+void sim_run(const std::shared_ptr<SimHub>& hub, const std::vector<Device*>& devices, int64_t max_iters);
+int64_t sim_bytes_moved(const std::shared_ptr<SimHub>& hub);
+
+// ---- RCCL ---------------------------------------------------------------------
+std::vector<uint8_t> rccl_unique_id();
+std::unique_ptr<P2P> make_rccl_p2p(const std::vector<uint8_t>& uid, int32_t rank, int32_t nranks, int32_t device);
+const char* rccl_version_string();
+
+}  // namespace akka

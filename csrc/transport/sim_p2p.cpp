@@ -1,0 +1,137 @@
+// CPU simulator of RCCL grouped p2p semantics (rendezvous, per-pair in-order
+// matching, whole-group completion) over deferred host devices.
+#include <deque>
+#include <map>
+#include <sstream>
+
+#include "p2p.h"
+
+namespace akka {
+
+bool host_device_step(Device* d);
+bool host_device_idle(Device* d);
+
+struct SimSend {
+  const void* buf;
+  size_t bytes;
+  bool consumed = false;
+};
+
+class SimHub {
+ public:
+  explicit SimHub(int32_t n) : n_(n) {}
+  int32_t n_;
+  // fifo[src][dst]: sends posted by src to dst not yet consumed, in order.
+  std::map<std::pair<int32_t, int32_t>, std::deque<std::shared_ptr<SimSend>>> fifo;
+  int64_t bytes = 0;
+  int64_t groups = 0;
+};
+
+std::shared_ptr<SimHub> make_sim_hub(int32_t nranks) { return std::make_shared<SimHub>(nranks); }
+int64_t sim_bytes_moved(const std::shared_ptr<SimHub>& hub) { return hub->bytes; }
+
+namespace {
+
+class SimP2P final : public P2P {
+ public:
+  SimP2P(std::shared_ptr<SimHub> hub, int32_t rank, Device* dev) : hub_(std::move(hub)), rank_(rank), dev_(dev) {}
+  int32_t rank() const override { return rank_; }
+  int32_t nranks() const override { return hub_->n_; }
+  const char* name() const override { return "sim"; }
+
+  void group(StreamH s, const std::vector<P2POp>& ops) override {
+    for (const auto& op : ops) {
+      AKKA_CHECK(op.peer >= 0 && op.peer < hub_->n_ && op.peer != rank_, "sim p2p: bad peer");
+    }
+    struct State {
+      bool posted = false;
+      std::vector<std::shared_ptr<SimSend>> sends;
+      std::vector<bool> recv_done;
+    };
+    auto st = std::make_shared<State>();
+    auto hub = hub_;
+    const int32_t me = rank_;
+    dev_->enqueue_host_op(s, [st, hub, me, ops]() {
+      if (!st->posted) {
+        for (const auto& op : ops) {
+          if (!op.send) continue;
+          auto snd = std::make_shared<SimSend>(SimSend{op.buf, op.bytes});
+          hub->fifo[{me, op.peer}].push_back(snd);
+          st->sends.push_back(snd);
+        }
+        st->recv_done.assign(ops.size(), false);
+        st->posted = true;
+        hub->groups++;
+      }
+      // Receives match the oldest unconsumed send of their pair, in op order.
+      bool all = true;
+      for (size_t i = 0; i < ops.size(); ++i) {
+        const auto& op = ops[i];
+        if (op.send || st->recv_done[i]) continue;
+        // Earlier recvs from the same peer in this group must match first.
+        bool blocked = false;
+        for (size_t j = 0; j < i; ++j)
+          if (!ops[j].send && ops[j].peer == op.peer && !st->recv_done[j]) blocked = true;
+        if (blocked) {
+          all = false;
+          continue;
+        }
+        auto& q = hub->fifo[{op.peer, me}];
+        if (q.empty()) {
+          all = false;
+          continue;
+        }
+        auto snd = q.front();
+        if (snd->bytes != op.bytes) {
+          std::ostringstream os;
+          os << "sim p2p: size mismatch " << op.peer << "->" << me << " send " << snd->bytes << " B vs recv "
+             << op.bytes << " B";
+          throw AkkaError(os.str());
+        }
+        if (op.bytes) std::memcpy(op.buf, snd->buf, op.bytes);
+        hub->bytes += int64_t(op.bytes);
+        snd->consumed = true;
+        q.pop_front();
+        st->recv_done[i] = true;
+      }
+      for (const auto& snd : st->sends)
+        if (!snd->consumed) all = false;
+      return all;
+    });
+  }
+
+ private:
+  std::shared_ptr<SimHub> hub_;
+  int32_t rank_;
+  Device* dev_;
+};
+
+}  // namespace
+
+std::unique_ptr<P2P> make_sim_p2p(std::shared_ptr<SimHub> hub, int32_t rank, Device* dev) {
+  AKKA_CHECK(dev->is_host(), "sim p2p needs a deferred host device");
+  return std::make_unique<SimP2P>(std::move(hub), rank, dev);
+}
+
+void sim_run(const std::shared_ptr<SimHub>& hub, const std::vector<Device*>& devices, int64_t max_iters) {
+  for (int64_t it = 0; it < max_iters; ++it) {
+    bool progress = false, idle = true;
+    for (Device* d : devices) {
+      progress |= host_device_step(d);
+      idle &= host_device_idle(d);
+    }
+    if (idle) return;
+    if (!progress) {
+      std::ostringstream os;
+      os << "sim p2p: deadlock - no rank can progress; pending sends per pair:";
+      for (auto& kv : hub->fifo)
+        if (!kv.second.empty()) os << " " << kv.first.first << "->" << kv.first.second << ":" << kv.second.size();
+      for (size_t i = 0; i < devices.size(); ++i)
+        if (!host_device_idle(devices[i])) os << " [rank " << i << " blocked]";
+      throw AkkaError(os.str());
+    }
+  }
+  throw AkkaError("sim p2p: iteration limit reached");
+}
+
+}  // namespace akka
