@@ -1,0 +1,51 @@
+"""2-layer MLP trained with data-parallel SGD through the threshold allreduce
+(BASELINE config 5: "gradient allreduce inside a 2-layer MLP SGD loop on
+synthetic data").
+
+The reference ships no model (the library is the primitive a DP
+trainer calls); this is the minimal consumer that exercises the data-source /
+data-sink contract end to end with real gradients.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..parallel.dp import AllreduceFn, GradientBucket, sgd_step
+
+
+class MLP(nn.Module):
+    def __init__(self, d_in: int, d_hidden: int, d_out: int):
+        super().__init__()
+        self.fc1 = nn.Linear(d_in, d_hidden)
+        self.fc2 = nn.Linear(d_hidden, d_out)
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        return self.fc2(F.relu(self.fc1(x)))
+
+
+def dp_sgd_step(model: nn.Module, x: torch.Tensor, y: torch.Tensor, lr: float,
+                allreduce: Optional[AllreduceFn], bucket: Optional[GradientBucket] = None) -> float:
+    """forward + backward + gradient allreduce (mean over contributors) + SGD update."""
+    if bucket is None:
+        bucket = getattr(model, "_akka_bucket", None)
+        if bucket is None:
+            bucket = GradientBucket(list(model.parameters()))
+            model._akka_bucket = bucket  # type: ignore[attr-defined]
+    bucket.zero_()
+    loss = F.cross_entropy(model(x), y)
+    loss.backward()
+    bucket.average(allreduce)
+    sgd_step(bucket.params, lr)
+    return float(loss.detach())
+
+
+def synthetic_batch(batch: int, d_in: int, n_classes: int, *, device, generator: Optional[torch.Generator] = None):
+    """Linearly separable synthetic classification data (no dataset download)."""
+    x = torch.randn(batch, d_in, device=device, generator=generator)
+    w = torch.arange(d_in * n_classes, device=device, dtype=torch.float32).reshape(d_in, n_classes).sin()
+    y = (x @ w).argmax(dim=1)
+    return x, y

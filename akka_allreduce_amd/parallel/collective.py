@@ -1,0 +1,112 @@
+"""SPMD front end: one process per GPU (torchrun), RCCL p2p over xGMI.
+
+``ThresholdAllreduce`` wraps one ``AllreduceWorker`` per rank on the scheduled
+(``stream``) transport.  Every rank starts round r when it calls the object
+(each rank is its own master for pacing; with ``thAllreduce = 1`` and
+lock-step callers this is exactly the reference's master behaviour, M:54-63,
+without a control-plane round trip per round).  The RCCL unique id is shared
+through ``torch.distributed`` (any backend; gloo is enough) or a TCPStore.
+
+Usage::
+
+    ar = ThresholdAllreduce(data_size=x.numel(), max_chunk_size=1 << 20)
+    out = ar(x)          # AllReduceOutput; out.data is valid in stream order
+"""
+from __future__ import annotations
+
+import os
+from typing import Any, Optional
+
+import torch
+
+from .._native_loader import load as _load
+from ..data import AllReduceOutput
+from ..messages import InitWorkers
+from ..worker import AllreduceWorker
+
+
+class _RemoteRank:
+    """Placeholder reference for a peer rank: the scheduled transport never tells it anything."""
+
+    def __init__(self, rank: int):
+        self.rank = rank
+
+    def tell(self, msg: Any, sender: Any = None) -> None:  # pragma: no cover - never called
+        raise RuntimeError(f"message {type(msg).__name__} routed to remote rank {self.rank} outside RCCL")
+
+
+def env_rank_world() -> tuple[int, int, int]:
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", str(rank)))
+    return rank, world, local
+
+
+def share_unique_id(rank: int, world: int, store: Any = None) -> bytes:
+    """RCCL unique id from rank 0 to everyone (torch.distributed or a TCPStore)."""
+    n = _load()
+    if world == 1:
+        return b""
+    if store is not None:
+        if rank == 0:
+            store.set("akka/rccl_uid", n.rccl_unique_id())
+        return bytes(store.get("akka/rccl_uid"))
+    import torch.distributed as dist
+
+    if not dist.is_initialized():
+        raise RuntimeError("initialise torch.distributed (gloo is enough) or pass a TCPStore to share the RCCL id")
+    obj = [n.rccl_unique_id() if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0)
+    return obj[0]
+
+
+class ThresholdAllreduce:
+    def __init__(
+        self,
+        data_size: int,
+        *,
+        max_chunk_size: int = 1 << 20,
+        dtype: torch.dtype = torch.float32,
+        th_reduce: float = 1.0,
+        th_complete: float = 1.0,
+        max_lag: int = 2,
+        broadcast_lag: int = 2,
+        rank: Optional[int] = None,
+        world_size: Optional[int] = None,
+        device: Optional[torch.device] = None,
+        store: Any = None,
+        data_sink: Any = None,
+    ):
+        r, w, local = env_rank_world()
+        self.rank = r if rank is None else int(rank)
+        self.world_size = w if world_size is None else int(world_size)
+        if device is None:
+            device = torch.device("cuda", local % max(1, torch.cuda.device_count())) if torch.cuda.is_available() \
+                else torch.device("cpu")
+        self.device = torch.device(device)
+        if self.device.type != "cuda":
+            raise RuntimeError("ThresholdAllreduce runs on MI355X ranks; use the cluster/outbox worker on CPU")
+        torch.cuda.set_device(self.device)
+        uid = share_unique_id(self.rank, self.world_size, store)
+        spec = ("rccl", uid, self.rank, self.world_size) if self.world_size > 1 else ("local",)
+        self.worker = AllreduceWorker(None, data_sink, device=self.device, dtype=dtype, transport="stream",
+                                      transport_spec=spec, broadcast_lag=broadcast_lag, strict=True,
+                                      name=f"rank{self.rank}")
+        peers = {i: (self.worker if i == self.rank else _RemoteRank(i)) for i in range(self.world_size)}
+        self.worker.tell(InitWorkers(peers, self.world_size, None, self.rank, th_reduce, th_complete, max_lag,
+                                     int(data_size), int(max_chunk_size)))
+        self.data_size = int(data_size)
+
+    def __call__(self, x: torch.Tensor) -> AllReduceOutput:
+        if x.numel() != self.data_size:
+            raise ValueError(f"expected {self.data_size} elements, got {x.numel()}")
+        out = self.worker.allreduce(x)
+        if out is None:
+            raise RuntimeError("round did not complete (thresholds need every rank in the scheduled transport)")
+        return out
+
+    def state(self) -> dict:
+        return self.worker.state()
+
+    def synchronize(self) -> None:
+        self.worker.synchronize()

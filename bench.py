@@ -1,0 +1,172 @@
+#!/usr/bin/env python3
+"""Headline benchmark: allreduce algbw (GB/s) on a 256 MB fp32 buffer, 1/2/4/8 MI355X.
+
+Metric and config come from BASELINE.json.  One rank per GPU; for N>1 the
+driver launches this file under ``torch.distributed.run`` (RANK/LOCAL_RANK/
+WORLD_SIZE/MASTER_* in the env).  Each timed step is one full threshold-
+allreduce round through the native engine: scatter of every chunk to its
+owner over RCCL/xGMI, the gfx950 chunk-reduce kernel, broadcast of the reduced
+chunks, counts exchange, and hand-off of a fresh output tensor.  Data is
+synthetic random fp32 (no dataset involved).  Exact thresholds (1.0/1.0/1.0)
+as in BASELINE config 2.
+
+algbw = buffer bytes / seconds per round; busbw = algbw * 2(N-1)/N.
+Rank 0 prints ONE JSON line.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+BASELINE_METRIC = "allreduce algbw (GB/s) on 256 MB fp32 buffer at 1/2/4/8 MI355X"
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--size-mb", type=float, default=256.0, help="buffer size in MiB (256 MB headline)")
+    p.add_argument("--dtype", default="float32", choices=["float32", "bfloat16"])
+    p.add_argument("--chunk-mb", type=float, default=4.0, help="maxChunkSize in MiB (BASELINE config 2: 4 MB)")
+    p.add_argument("--max-lag", type=int, default=2)
+    p.add_argument("--bcast-lag", type=int, default=2)
+    p.add_argument("--th-reduce", type=float, default=1.0)
+    p.add_argument("--th-complete", type=float, default=1.0)
+    p.add_argument("--compare-rccl", action="store_true", help="also time torch.distributed all_reduce (RCCL)")
+    p.add_argument("--no-check", action="store_true")
+    return p.parse_args()
+
+
+def main() -> int:
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            print(f"bench.py: --gpus {args.gpus} needs torch.distributed.run (WORLD_SIZE unset)", file=sys.stderr)
+            return 2
+    if not torch.cuda.is_available():
+        print("bench.py: no GPU visible", file=sys.stderr)
+        return 2
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    from akka_allreduce_amd.parallel import ThresholdAllreduce
+
+    dtype = torch.float32 if args.dtype == "float32" else torch.bfloat16
+    esize = 4 if dtype == torch.float32 else 2
+    nbytes = int(args.size_mb * (1 << 20))
+    S = nbytes // esize
+    C = max(1, int(args.chunk_mb * (1 << 20)) // esize)
+    ar = ThresholdAllreduce(S, max_chunk_size=C, dtype=dtype, th_reduce=args.th_reduce, th_complete=args.th_complete,
+                            max_lag=args.max_lag, broadcast_lag=args.bcast_lag, device=dev)
+
+    g = torch.Generator(device=dev)
+    g.manual_seed(1234 + rank)
+    x = torch.randn(S, device=dev, dtype=torch.float32, generator=g).to(dtype)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        out = ar(x)
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = ar(x)
+    torch.cuda.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    del out
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    ms = dt / args.steps * 1e3
+    algbw = nbytes / (dt / args.steps) / 1e9
+    busbw = algbw * (2 * (world - 1) / world) if world > 1 else 0.0
+
+    # Exactness check (untimed): every rank contributes rank+1 -> sum = N(N+1)/2 exactly.
+    ok = None
+    if not args.no_check:
+        y = torch.full((S,), float(rank + 1), device=dev, dtype=dtype)
+        o = ar(y)
+        want = float(world * (world + 1) // 2)
+        ok = bool(torch.all(o.data == want).item()) and bool(torch.all(o.count == world).item())
+        if world > 1:
+            f = torch.tensor([1 if ok else 0])
+            dist.all_reduce(f, op=dist.ReduceOp.MIN)
+            ok = bool(f.item())
+
+    rccl = None
+    if args.compare_rccl and world > 1:
+        dist.destroy_process_group()
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+        z = x.clone()
+        for _ in range(args.warmup):
+            dist.all_reduce(z)
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            dist.all_reduce(z)
+        torch.cuda.synchronize()
+        dist.barrier()
+        t1 = time.perf_counter() - t0
+        rccl = nbytes / (t1 / args.steps) / 1e9
+
+    st = ar.state()
+    if rank == 0:
+        line = {
+            "metric": BASELINE_METRIC,
+            "value": round(algbw, 3),
+            "unit": "GB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "bf16" if dtype == torch.bfloat16 else "fp32",
+            "data": "synthetic random tensors (torch.randn), exact thresholds",
+            "config": {
+                "model": f"threshold-allreduce {args.size_mb:g}MiB {args.dtype}",
+                "global_batch": world,
+                "seq_len": S,
+                "parallelism": f"dp{world}",
+                "buffer_bytes": nbytes,
+                "chunk_bytes": C * esize,
+                "max_lag": args.max_lag,
+                "broadcast_lag": args.bcast_lag,
+                "thresholds": [1.0, args.th_reduce, args.th_complete],
+                "transport": "rccl-p2p-xgmi" if world > 1 else "local",
+            },
+            "busbw_GBps": round(busbw, 3),
+            "exact": ok,
+            "groups_per_round": (st.get("link", {}).get("groups", 0) / max(1, st.get("link", {}).get("rounds", 1))),
+            "rccl_allreduce_algbw_GBps": round(rccl, 3) if rccl else None,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1 and dist.is_initialized():
+        dist.barrier()
+        dist.destroy_process_group()
+    return 0 if ok in (None, True) else 1
+
+
+if __name__ == "__main__":
+    sys.exit(main())
