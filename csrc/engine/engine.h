@@ -111,6 +111,8 @@ class Engine {
   void on_peer_terminated(int32_t id);
   void flush_deferred(int32_t round);
   void set_link(Link* link) { link_ = link; }
+  // Bind the round's output buffers now (a scheduled link receives into them).
+  void ensure_output(int32_t round);
 
   // --- introspection ------------------------------------------------------
   bool initialized() const { return id_ >= 0 && dp_ != nullptr; }
@@ -159,7 +161,6 @@ class Engine {
   void reduce_and_broadcast(int32_t r, int32_t chunk, bool forced);
   void complete(int32_t r);
   void finalize_round(int32_t r);
-  void ensure_output(int32_t r);
   void leave_scope();
 
   EngineHost* host_;

@@ -1,5 +1,7 @@
 // CPU simulator of RCCL grouped p2p semantics (rendezvous, per-pair in-order
 // matching, whole-group completion) over deferred host devices.
+#include <cstdio>
+#include <cstdlib>
 #include <deque>
 #include <map>
 #include <sstream>
@@ -25,6 +27,7 @@ class SimHub {
   std::map<std::pair<int32_t, int32_t>, std::deque<std::shared_ptr<SimSend>>> fifo;
   int64_t bytes = 0;
   int64_t groups = 0;
+  int64_t events = 0;  // posts + matches: progress that completes no queue op yet
 };
 
 std::shared_ptr<SimHub> make_sim_hub(int32_t nranks) { return std::make_shared<SimHub>(nranks); }
@@ -61,7 +64,13 @@ class SimP2P final : public P2P {
         }
         st->recv_done.assign(ops.size(), false);
         st->posted = true;
+        if (std::getenv("AKKA_SIM_TRACE")) {
+          std::fprintf(stderr, "[sim] rank %d posts group %lld:", me, (long long)hub->groups);
+          for (const auto& op : ops) std::fprintf(stderr, " %s%d:%zu", op.send ? "S" : "R", op.peer, op.bytes);
+          std::fprintf(stderr, "\n");
+        }
         hub->groups++;
+        hub->events++;
       }
       // Receives match the oldest unconsumed send of their pair, in op order.
       bool all = true;
@@ -93,6 +102,7 @@ class SimP2P final : public P2P {
         snd->consumed = true;
         q.pop_front();
         st->recv_done[i] = true;
+        hub->events++;
       }
       for (const auto& snd : st->sends)
         if (!snd->consumed) all = false;
@@ -116,11 +126,13 @@ std::unique_ptr<P2P> make_sim_p2p(std::shared_ptr<SimHub> hub, int32_t rank, Dev
 void sim_run(const std::shared_ptr<SimHub>& hub, const std::vector<Device*>& devices, int64_t max_iters) {
   for (int64_t it = 0; it < max_iters; ++it) {
     bool progress = false, idle = true;
+    const int64_t ev0 = hub->events;
     for (Device* d : devices) {
       progress |= host_device_step(d);
       idle &= host_device_idle(d);
     }
     if (idle) return;
+    progress |= hub->events != ev0;
     if (!progress) {
       std::ostringstream os;
       os << "sim p2p: deadlock - no rank can progress; pending sends per pair:";

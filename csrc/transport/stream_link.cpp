@@ -51,6 +51,8 @@ void StreamLink::schedule(int32_t r) {
   const int32_t me = dp_->me();
   const int32_t N = g.N;
   if (N == 1) {  // nothing to move: the round was reduced in place during scatter()
+    engine_->ensure_output(r);
+    dp_->upload_counts(r, {me}, dp_->device()->comm_stream());
     mark_scheduled(r);
     return;
   }
@@ -63,6 +65,7 @@ void StreamLink::schedule(int32_t r) {
   const int32_t steps = g.max_block_len_chunks() + lag_;
 
   in_flight_.insert(r);
+  engine_->ensure_output(r);
   RoundQ& rq = q_[r];
   StreamH comm = dp_->device()->comm_stream();
   // The ring row for r was last read by round r-L's reduces (compute stream).
