@@ -251,7 +251,7 @@ class AllreduceWorker:
         t = t.reshape(-1).to(device=self.device, dtype=self.dtype).contiguous()
         rec = self._rounds.setdefault(round_, {})
         rec["input"] = t
-        self._core.bind_input(round_, t.data_ptr(), self._stream_ptr())
+        self._core.bind_input(round_, t.data_ptr(), self._stream_ptr(), self.device.type == "cuda")
 
     def _alloc_output(self, round_: int) -> None:
         g = self.geometry

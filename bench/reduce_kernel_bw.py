@@ -9,8 +9,12 @@ from __future__ import annotations
 
 import argparse
 import json
+import os
+import sys
 
-import torch
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
 
 from akka_allreduce_amd.ops import chunk_reduce
 

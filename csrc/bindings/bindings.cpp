@@ -137,8 +137,8 @@ class WorkerCore final : public EngineHost {
   void peer_terminated(int32_t id) { engine_->on_peer_terminated(id); }
 
   // ---- memory bindings -----------------------------------------------------
-  void bind_input(int32_t round, uintptr_t ptr, uintptr_t stream) {
-    dp_->bind_input(round, reinterpret_cast<const void*>(ptr), reinterpret_cast<StreamH>(stream));
+  void bind_input(int32_t round, uintptr_t ptr, uintptr_t stream, bool has_stream) {
+    dp_->bind_input(round, reinterpret_cast<const void*>(ptr), reinterpret_cast<StreamH>(stream), has_stream);
   }
   void bind_output(int32_t round, uintptr_t out, uintptr_t counts) {
     dp_->bind_output(round, reinterpret_cast<void*>(out), reinterpret_cast<int32_t*>(counts));

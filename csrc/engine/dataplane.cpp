@@ -95,11 +95,11 @@ DataPlane::Binding& DataPlane::binding_mut(int32_t round) {
   return const_cast<Binding&>(static_cast<const DataPlane*>(this)->binding(round));
 }
 
-void DataPlane::bind_input(int32_t round, const void* input, StreamH ready_stream) {
+void DataPlane::bind_input(int32_t round, const void* input, StreamH ready_stream, bool has_stream) {
   Binding& b = bind_[round];
   b.input = input;
   b.input_waited = false;
-  if (ready_stream) {
+  if (has_stream && !dev_->is_host()) {
     if (!b.input_ready) b.input_ready = dev_->create_event();
     dev_->record(b.input_ready, ready_stream);
   }

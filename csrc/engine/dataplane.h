@@ -44,8 +44,9 @@ class DataPlane {
   int32_t kmax() const { return kmax_; }
 
   // --- per-round bindings (memory owned by the embedding layer) ------------
-  // `ready_stream` is the stream that produced `input` (nullptr: already ready).
-  void bind_input(int32_t round, const void* input, StreamH ready_stream);
+  // `ready_stream` is the stream that produced `input`; it may be the null
+  // stream (handle 0), so `has_stream` says whether there is one at all.
+  void bind_input(int32_t round, const void* input, StreamH ready_stream, bool has_stream);
   void bind_output(int32_t round, void* output, int32_t* counts);
   bool has_input(int32_t round) const;
   bool has_output(int32_t round) const;
