@@ -11,6 +11,7 @@ never looks at counts does not pay an extra S-element int32 write per round.
 """
 from __future__ import annotations
 
+import functools
 from dataclasses import dataclass
 from typing import Any, Optional
 
@@ -41,11 +42,11 @@ class Geometry:
     def num_chunks(self, j: int) -> int:
         return -(-self.block_len(j) // self.maxChunkSize)
 
-    @property
+    @functools.cached_property
     def kmax(self) -> int:
         return max(1, max(self.num_chunks(j) for j in range(self.workerNum)))
 
-    @property
+    @functools.cached_property
     def total_chunks(self) -> int:
         return sum(self.num_chunks(j) for j in range(self.workerNum))
 

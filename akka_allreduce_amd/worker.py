@@ -105,6 +105,7 @@ class AllreduceWorker:
         self._outputs: Dict[int, AllReduceOutput] = {}
         self._next_round = 0
         self._in_call = 0
+        self._stream_cache: Optional[int] = None
 
     # ------------------------------------------------------------------ actor API
     def tell(self, msg: Any, sender: Any = None) -> None:
@@ -226,7 +227,12 @@ class AllreduceWorker:
         r = self._next_round
         self._next_round += 1
         self._feed[r] = tensor
-        self.receive(StartAllreduce(r))
+        # one stream lookup per call instead of one per callback
+        self._stream_cache = torch.cuda.current_stream(self.device).cuda_stream if self.device.type == "cuda" else 0
+        try:
+            self.receive(StartAllreduce(r))
+        finally:
+            self._stream_cache = None
         return self._outputs.pop(r, None)
 
     def _feed_source(self, req: AllReduceInputRequest) -> AllReduceInput:
@@ -239,6 +245,8 @@ class AllreduceWorker:
     def _stream_ptr(self) -> int:
         if self.device.type != "cuda":
             return 0
+        if self._stream_cache is not None:
+            return self._stream_cache
         return torch.cuda.current_stream(self.device).cuda_stream
 
     def _fetch(self, round_: int) -> None:
@@ -256,7 +264,8 @@ class AllreduceWorker:
     def _alloc_output(self, round_: int) -> None:
         g = self.geometry
         out = torch.empty(g.dataSize, dtype=self.dtype, device=self.device)
-        counts = torch.zeros(g.workerNum * g.kmax, dtype=torch.int32, device=self.device)
+        # every entry the count expansion reads is written (uploaded or received)
+        counts = torch.empty(g.workerNum * g.kmax, dtype=torch.int32, device=self.device)
         rec = self._rounds.setdefault(round_, {})
         rec["output"], rec["counts"] = out, counts
         self._core.bind_output(round_, out.data_ptr(), counts.data_ptr())

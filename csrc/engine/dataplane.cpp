@@ -35,11 +35,7 @@ DataPlane::~DataPlane() {
     dev_->sync_stream(dev_->comm_stream());
   } catch (...) {
   }
-  for (auto& kv : bind_) {
-    if (kv.second.input_ready) dev_->destroy_event(kv.second.input_ready);
-    if (kv.second.done) dev_->destroy_event(kv.second.done);
-  }
-  for (EventH e : events_) dev_->destroy_event(e);
+  for (EventH e : events_) dev_->destroy_event(e);  // includes every binding/spare event
   dev_->release(scatter_ring_);
   dev_->release_pinned(staging_);
 }
@@ -84,7 +80,14 @@ DataPlane::Row& DataPlane::row_for(int32_t round) {
   return r;
 }
 
-EventH DataPlane::row_release_event(int32_t round) const { return rows_[size_t(round % L_)].released; }
+EventH DataPlane::row_release_event(int32_t round) {
+  // Recorded on demand (not after every reduce, which would split the merged
+  // reduce launches): everything issued on the compute stream so far, which
+  // includes every reduce that read this ring row for an older round.
+  Row& r = rows_[size_t(round % L_)];
+  dev_->record(r.released, dev_->compute_stream());
+  return r.released;
+}
 
 const DataPlane::Binding& DataPlane::binding(int32_t round) const {
   auto it = bind_.find(round);
@@ -100,17 +103,29 @@ void DataPlane::bind_input(int32_t round, const void* input, StreamH ready_strea
   b.input = input;
   b.input_waited = false;
   if (has_stream && !dev_->is_host()) {
-    if (!b.input_ready) b.input_ready = dev_->create_event();
+    if (!b.input_ready) b.input_ready = binding_event();
     dev_->record(b.input_ready, ready_stream);
   }
-  row_for(round);
+}
+
+EventH DataPlane::binding_event() {
+  // Per-round events are recycled: once a round is unbound nobody waits on
+  // its input/done events again, so re-recording them later is safe.
+  if (!spare_events_.empty()) {
+    EventH e = spare_events_.back();
+    spare_events_.pop_back();
+    return e;
+  }
+  EventH e = dev_->create_event();
+  events_.push_back(e);
+  return e;
 }
 
 void DataPlane::bind_output(int32_t round, void* output, int32_t* counts) {
   Binding& b = bind_[round];
   b.output = output;
   b.counts = counts;
-  if (!b.done) b.done = dev_->create_event();
+  if (!b.done) b.done = binding_event();
   b.finalized = false;
 }
 
@@ -126,8 +141,8 @@ bool DataPlane::has_output(int32_t round) const {
 void DataPlane::unbind(int32_t round) {
   auto it = bind_.find(round);
   if (it == bind_.end()) return;
-  if (it->second.input_ready) dev_->destroy_event(it->second.input_ready);
-  if (it->second.done) dev_->destroy_event(it->second.done);
+  if (it->second.input_ready) spare_events_.push_back(it->second.input_ready);
+  if (it->second.done) spare_events_.push_back(it->second.done);
   bind_.erase(it);
 }
 
@@ -219,7 +234,6 @@ Payload DataPlane::reduce(int32_t round, int32_t k, const std::vector<int32_t>& 
     auto specs = split_reduce(dst, ptrs, n);
     dev_->reduce(dev_->compute_stream(), specs.data(), int32_t(specs.size()), dt_);
   }
-  dev_->record(r.released, dev_->compute_stream());
   return output_chunk(round, me_, k);
 }
 

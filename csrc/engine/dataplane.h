@@ -88,7 +88,7 @@ class DataPlane {
   void compute_wait(EventH e) { dev_->wait(dev_->compute_stream(), e); }
   void comm_wait(EventH e) { dev_->wait(dev_->comm_stream(), e); }
   // Event after the last compute op that reads ring row of `round`.
-  EventH row_release_event(int32_t round) const;
+  EventH row_release_event(int32_t round);
 
  private:
   struct Binding {
@@ -112,6 +112,7 @@ class DataPlane {
   Binding& binding_mut(int32_t round);
   void ensure_input_waited(Binding& b);
   EventH pooled_event();
+  EventH binding_event();
 
   Device* dev_;
   Geometry g_;
@@ -127,6 +128,7 @@ class DataPlane {
   std::map<int32_t, Binding> bind_;
   std::vector<EventH> events_;     // all events created (destroyed at teardown)
   std::vector<EventH> free_events_;
+  std::vector<EventH> spare_events_;  // recycled per-round (input_ready / done) events
 };
 
 }  // namespace akka
