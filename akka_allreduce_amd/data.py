@@ -84,7 +84,7 @@ class AllReduceOutput:
     ``iteration``: the round.
     """
 
-    __slots__ = ("data", "iteration", "counts_per_chunk", "geometry", "_count", "_expander")
+    __slots__ = ("data", "iteration", "counts_per_chunk", "geometry", "_count", "_expander", "_event")
 
     def __init__(
         self,
@@ -95,6 +95,7 @@ class AllReduceOutput:
         counts_per_chunk: Optional[torch.Tensor] = None,
         geometry: Optional[Geometry] = None,
         expander: Any = None,
+        event: Any = None,
     ):
         self.data = data
         self.iteration = iteration
@@ -102,9 +103,17 @@ class AllReduceOutput:
         self.geometry = geometry
         self._count = count
         self._expander = expander
+        self._event = event
+
+    def wait(self) -> "AllReduceOutput":
+        """Async rounds: make the current stream wait for the result (no-op otherwise)."""
+        if self._event is not None:
+            torch.cuda.current_stream(self.data.device).wait_event(self._event)
+        return self
 
     @property
     def count(self) -> torch.Tensor:
+        self.wait()
         if self._count is None:
             if self.counts_per_chunk is None or self.geometry is None:
                 raise ValueError("AllReduceOutput has no count information")

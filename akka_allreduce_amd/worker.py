@@ -106,6 +106,8 @@ class AllreduceWorker:
         self._next_round = 0
         self._in_call = 0
         self._stream_cache: Optional[int] = None
+        self._async = False
+        self._ext_streams = None
 
     # ------------------------------------------------------------------ actor API
     def tell(self, msg: Any, sender: Any = None) -> None:
@@ -216,24 +218,44 @@ class AllreduceWorker:
         return self._core.state()["completed"]
 
     # ------------------------------------------------------------------ collective convenience API
-    def allreduce(self, tensor: torch.Tensor) -> Optional[AllReduceOutput]:
+    def allreduce(self, tensor: torch.Tensor, async_op: bool = False) -> Optional[AllReduceOutput]:
         """Start the next round with ``tensor`` as this worker's contribution.
 
         For the scheduled (RCCL) transport the round's whole schedule is
-        enqueued on the GPU before this returns, and the returned output is
-        valid in the caller's current stream order.  Returns ``None`` if the
-        round has not completed yet (threshold transports driven by messages).
+        enqueued on the GPU before this returns.  By default the returned
+        output is valid in the caller's current stream order.  With
+        ``async_op=True`` (torch.distributed's convention) the caller's stream
+        is NOT made to wait: call ``out.wait()`` before using ``out.data``.
+        Back-to-back async rounds then pipeline without a cross-stream hop per
+        round; all tensors involved are ``record_stream``-ed on the internal
+        streams so the caching allocator cannot recycle them early.
+        Returns ``None`` if the round has not completed yet (threshold
+        transports driven by messages).
         """
         r = self._next_round
         self._next_round += 1
         self._feed[r] = tensor
         # one stream lookup per call instead of one per callback
         self._stream_cache = torch.cuda.current_stream(self.device).cuda_stream if self.device.type == "cuda" else 0
+        self._async = bool(async_op) and self.device.type == "cuda"
         try:
             self.receive(StartAllreduce(r))
         finally:
             self._stream_cache = None
+            self._async = False
         return self._outputs.pop(r, None)
+
+    def _internal_streams(self):
+        if self._ext_streams is None:
+            comm, compute = self._core.streams()
+            self._ext_streams = (torch.cuda.ExternalStream(comm, device=self.device),
+                                 torch.cuda.ExternalStream(compute, device=self.device))
+        return self._ext_streams
+
+    def _keep_alive_on_internal_streams(self, *tensors: torch.Tensor) -> None:
+        for s in self._internal_streams():
+            for t in tensors:
+                t.record_stream(s)
 
     def _feed_source(self, req: AllReduceInputRequest) -> AllReduceInput:
         t = self._feed.pop(req.iteration, None)
@@ -259,6 +281,8 @@ class AllreduceWorker:
         t = t.reshape(-1).to(device=self.device, dtype=self.dtype).contiguous()
         rec = self._rounds.setdefault(round_, {})
         rec["input"] = t
+        if self._async:
+            self._keep_alive_on_internal_streams(t)
         self._core.bind_input(round_, t.data_ptr(), self._stream_ptr(), self.device.type == "cuda")
 
     def _alloc_output(self, round_: int) -> None:
@@ -268,16 +292,25 @@ class AllreduceWorker:
         counts = torch.empty(g.workerNum * g.kmax, dtype=torch.int32, device=self.device)
         rec = self._rounds.setdefault(round_, {})
         rec["output"], rec["counts"] = out, counts
+        if self._async:
+            self._keep_alive_on_internal_streams(out, counts)
         self._core.bind_output(round_, out.data_ptr(), counts.data_ptr())
 
     def _deliver(self, round_: int) -> None:
         rec = self._rounds[round_]
+        event = None
         if self.device.type == "cuda":
-            self._core.stream_wait_done(round_, self._stream_ptr())
+            if self._async:
+                # finalize() already queued the round's done point on the compute stream
+                event = torch.cuda.Event()
+                event.record(self._internal_streams()[1])
+            else:
+                self._core.stream_wait_done(round_, self._stream_ptr())
         g = self.geometry
         out = AllReduceOutput(rec["output"], iteration=round_,
                               counts_per_chunk=rec["counts"].view(g.workerNum, g.kmax), geometry=g,
-                              expander=self._expand_counts if self.device.type == "cuda" else None)
+                              expander=self._expand_counts if self.device.type == "cuda" else None,
+                              event=event)
         self._to_release.append(round_)
         if self.dataSink is not None:
             self.dataSink(out)

@@ -38,6 +38,8 @@ def parse():
     p.add_argument("--th-complete", type=float, default=1.0)
     p.add_argument("--compare-rccl", action="store_true", help="also time torch.distributed all_reduce (RCCL)")
     p.add_argument("--no-check", action="store_true")
+    p.add_argument("--sync-op", dest="async_op", action="store_false",
+                   help="make the caller's stream wait after every round (default: async rounds)")
     return p.parse_args()
 
 
@@ -79,19 +81,28 @@ def main() -> int:
         if world > 1:
             dist.barrier()
 
+    # Rounds are issued back to back (async_op, like nccl-tests / torch's
+    # async_op=True): every round's output is waited for on the current stream
+    # before the closing synchronize, so all K rounds complete inside the timing.
     for _ in range(args.warmup):
-        out = ar(x)
+        out = ar(x, async_op=args.async_op)
+    out.wait()
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    outs = []
     for _ in range(args.steps):
-        out = ar(x)
+        outs.append(ar(x, async_op=args.async_op))
+        if len(outs) > 4:
+            outs.pop(0).wait()
+    for o in outs:
+        o.wait()
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    del out
+    del out, outs
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

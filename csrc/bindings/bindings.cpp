@@ -160,6 +160,10 @@ class WorkerCore final : public EngineHost {
                         reinterpret_cast<const int32_t*>(counts), g.S, g.step, g.N, g.C, dp_->kmax());
   }
 
+  std::pair<uintptr_t, uintptr_t> streams() const {
+    AKKA_CHECK(dev_, "streams() before init");
+    return {reinterpret_cast<uintptr_t>(dev_->comm_stream()), reinterpret_cast<uintptr_t>(dev_->compute_stream())};
+  }
   std::vector<OutMsg> drain() { return outbox_ ? outbox_->drain() : std::vector<OutMsg>{}; }
   Device* device() const { return dev_.get(); }
 
@@ -279,6 +283,7 @@ PYBIND11_MODULE(_native, m) {
       .def("sync_all", &WorkerCore::sync_all)
       .def("expand_counts", &WorkerCore::expand_counts)
       .def("drain", &WorkerCore::drain)
+      .def("streams", &WorkerCore::streams)
       .def("state", &WorkerCore::state)
       .def("scatter_count", &WorkerCore::scatter_count)
       .def("reduced_arrivals", &WorkerCore::reduced_arrivals);

@@ -210,15 +210,33 @@ __global__ __launch_bounds__(kBlock) void reduce_scalar_kernel(SrcTable srcs, in
   }
 }
 
+// One workgroup per (block, chunk) region at a time: the count is a
+// wave-uniform scalar and the region is filled with 16-B stores (scalar head /
+// tail where the region is not 16-B aligned); no per-element division.
 __global__ __launch_bounds__(kBlock) void count_expand_kernel(int32_t* __restrict__ out,
                                                               const int32_t* __restrict__ counts, int64_t S,
                                                               int64_t step, int32_t N, int64_t C, int32_t kmax) {
-  const int64_t stride = int64_t(gridDim.x) * kBlock;
-  for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < S; i += stride) {
-    int64_t j = step > 0 ? i / step : 0;
-    if (j > N - 1) j = N - 1;
-    const int64_t k = (i - j * step) / C;
-    out[i] = counts[j * kmax + k];
+  const int64_t nregions = int64_t(N) * kmax;
+  for (int64_t reg = blockIdx.x; reg < nregions; reg += gridDim.x) {
+    const int32_t j = int32_t(reg / kmax);
+    const int64_t k = reg - int64_t(j) * kmax;
+    const int64_t bs = j * step < S ? j * step : S;
+    const int64_t be = j >= N - 1 ? S : ((j + 1) * step < S ? (j + 1) * step : S);
+    const int64_t s = bs + k * C;
+    if (s >= be) continue;
+    const int64_t e = s + C < be ? s + C : be;
+    const int32_t v = counts[reg];
+    int64_t a = (s + 3) & ~int64_t(3);  // first 16-B aligned element
+    if (a > e) a = e;
+    const int64_t nv = (e - a) >> 2;
+    if (blockIdx.y == 0) {
+      for (int64_t i = s + threadIdx.x; i < a; i += kBlock) out[i] = v;
+      for (int64_t i = a + nv * 4 + threadIdx.x; i < e; i += kBlock) out[i] = v;
+    }
+    int4* o4 = reinterpret_cast<int4*>(out + a);
+    const int4 vv = make_int4(v, v, v, v);
+    // gridDim.y workgroups share one region when there are few regions
+    for (int64_t i = int64_t(blockIdx.y) * kBlock + threadIdx.x; i < nv; i += int64_t(kBlock) * gridDim.y) o4[i] = vv;
   }
 }
 
@@ -339,9 +357,16 @@ void launch_reduce(hipStream_t s, const ReduceSpec& spec, DType dt, ReduceImpl i
 void launch_count_expand(hipStream_t s, int32_t* out, const int32_t* counts, int64_t S, int64_t step, int32_t N,
                          int64_t C, int32_t kmax) {
   if (S <= 0) return;
-  int64_t want = (S + kBlock - 1) / kBlock;
-  int grid = int(want < kMaxGrid ? want : kMaxGrid);
-  hipLaunchKernelGGL(count_expand_kernel, dim3(grid), dim3(kBlock), 0, s, out, counts, S, step, N, C, kmax);
+  // out must be 16-B aligned for the vector stores (torch allocations are)
+  AKKA_CHECK((reinterpret_cast<uintptr_t>(out) & 15) == 0, "count_expand: output not 16-B aligned");
+  const int64_t regions = int64_t(N) * kmax;
+  int grid = int(regions < kMaxGrid ? regions : kMaxGrid);
+  int split = int(kMaxGrid / grid);
+  const int64_t per_region_vecs = (S / regions) / 4 + 1;
+  const int64_t useful = (per_region_vecs + kBlock - 1) / kBlock;
+  if (split > useful) split = int(useful);
+  if (split < 1) split = 1;
+  hipLaunchKernelGGL(count_expand_kernel, dim3(grid, split), dim3(kBlock), 0, s, out, counts, S, step, N, C, kmax);
   check_launch("count_expand");
 }
 

@@ -38,6 +38,19 @@ def test_output_stream_ordering_under_reuse():
         assert bool((o.data == float(r)).all()), r
 
 
+def test_async_rounds_pipeline():
+    """async_op rounds: no per-round stream hop; results valid after wait()."""
+    dev = torch.device("cuda", 0)
+    S = (1 << 22) + 3
+    ar = ThresholdAllreduce(S, max_chunk_size=1 << 20, device=dev, rank=0, world_size=1, max_lag=2)
+    xs = [torch.full((S,), float(r), device=dev) for r in range(8)]
+    outs = [ar(x, async_op=True) for x in xs]
+    for r, o in enumerate(outs):
+        o.wait()
+        assert bool((o.data == float(r)).all()), r
+        assert bool((o.count == 1).all())
+
+
 def test_mlp_dp_sgd_through_allreduce():
     from akka_allreduce_amd.models.mlp import MLP, dp_sgd_step, synthetic_batch
     from akka_allreduce_amd.parallel.dp import GradientBucket
