@@ -49,6 +49,7 @@ class OutboxLink final : public Link {
 
  private:
   OutMsg make(int32_t kind, int32_t dest, int32_t chunk, int32_t round, int32_t count, const Payload& p) {
+    if (p.kind == PayloadKind::InputView) dp_->wait_input(round, dp_->device()->compute_stream());
     std::string buf(size_t(p.len) * dp_->esize(), '\0');
     dp_->read_payload(p, buf.data());
     return OutMsg{kind, me_, dest, chunk, round, count, py::bytes(buf)};

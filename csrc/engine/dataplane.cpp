@@ -101,7 +101,7 @@ DataPlane::Binding& DataPlane::binding_mut(int32_t round) {
 void DataPlane::bind_input(int32_t round, const void* input, StreamH ready_stream, bool has_stream) {
   Binding& b = bind_[round];
   b.input = input;
-  b.input_waited = false;
+  b.input_waited_compute = b.input_waited_comm = false;
   if (has_stream && !dev_->is_host()) {
     if (!b.input_ready) b.input_ready = binding_event();
     dev_->record(b.input_ready, ready_stream);
@@ -146,13 +146,18 @@ void DataPlane::unbind(int32_t round) {
   bind_.erase(it);
 }
 
-void DataPlane::ensure_input_waited(Binding& b) {
-  if (b.input_ready && !b.input_waited) {
-    dev_->wait(dev_->compute_stream(), b.input_ready);
-    dev_->wait(dev_->comm_stream(), b.input_ready);
-    b.input_waited = true;
-  }
+void DataPlane::wait_input(int32_t round, StreamH s) {
+  // Each consumer stream waits for the input's producer once per round, and
+  // only if it actually reads the input (N=1 never touches the comm stream).
+  Binding& b = binding_mut(round);
+  if (!b.input_ready) return;
+  bool& done = (s == dev_->comm_stream()) ? b.input_waited_comm : b.input_waited_compute;
+  if (done) return;
+  dev_->wait(s, b.input_ready);
+  done = true;
 }
+
+void DataPlane::mark_comm_used(int32_t round) { binding_mut(round).comm_used = true; }
 
 Payload DataPlane::input_chunk(int32_t round, int32_t block, int32_t k) const {
   const Binding& b = binding(round);
@@ -162,7 +167,6 @@ Payload DataPlane::input_chunk(int32_t round, int32_t block, int32_t k) const {
   p.len = g_.chunk_len(block, k);
   p.kind = PayloadKind::InputView;
   p.on_host = dev_->is_host();
-  const_cast<DataPlane*>(this)->ensure_input_waited(const_cast<Binding&>(b));
   return p;
 }
 
@@ -222,7 +226,7 @@ Payload DataPlane::reduce(int32_t round, int32_t k, const std::vector<int32_t>& 
   ptrs.reserve(srcs.size());
   for (int32_t s : srcs) {
     if (s == me_ && r.self_alias[size_t(k)]) {
-      ensure_input_waited(b);
+      wait_input(round, dev_->compute_stream());
       ptrs.push_back(static_cast<const char*>(b.input) + size_t(g_.chunk_offset(me_, k)) * esize());
     } else {
       ptrs.push_back(scatter_slot(round, s, k));
@@ -258,11 +262,23 @@ void DataPlane::upload_counts(int32_t round, const std::vector<int32_t>& blocks,
   Row& r = row_for(round);
   const Binding& b = binding(round);
   if (!b.counts) return;
+  bool copied = false;
   for (int32_t blk : blocks) {
     const int32_t* src = staging_ + (size_t(round % L_) * g_.N + size_t(blk)) * kmax_;
-    dev_->copy(s, b.counts + size_t(blk) * kmax_, src, size_t(kmax_) * sizeof(int32_t), CopyKind::HostToDevice);
+    const int32_t kb = std::max(1, g_.num_chunks(blk));
+    bool uniform = true;
+    for (int32_t k = 1; k < kb && uniform; ++k) uniform = src[k] == src[0];
+    if (uniform) {
+      // exact thresholds: every chunk has the same count -> a 32-bit fill,
+      // no host staging read on the stream
+      dev_->fill_i32(s, b.counts + size_t(blk) * kmax_, src[0], size_t(kb));
+    } else {
+      dev_->copy(s, b.counts + size_t(blk) * kmax_, src, size_t(kmax_) * sizeof(int32_t), CopyKind::HostToDevice);
+      copied = true;
+    }
   }
-  dev_->record(r.staging_done, s);
+  if (s == dev_->comm_stream()) binding_mut(round).comm_used = true;
+  if (copied) dev_->record(r.staging_done, s);
 }
 
 void DataPlane::finalize(int32_t round, const std::vector<uint8_t>& landed) {
@@ -270,8 +286,10 @@ void DataPlane::finalize(int32_t round, const std::vector<uint8_t>& landed) {
   AKKA_CHECK(landed.size() == size_t(g_.N) * kmax_, "landed mask has wrong shape");
   StreamH cs = dev_->compute_stream();
   // Join: everything the comm stream wrote into this round's output.
-  EventH ce = record_comm();
-  dev_->wait(cs, ce);
+  if (b.comm_used) {
+    EventH ce = record_comm();
+    dev_->wait(cs, ce);
+  }
   for (int32_t j = 0; j < g_.N; ++j) {
     int32_t kj = g_.num_chunks(j);
     int32_t k = 0;

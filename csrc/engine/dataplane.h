@@ -87,6 +87,10 @@ class DataPlane {
   EventH record_comm();
   void compute_wait(EventH e) { dev_->wait(dev_->compute_stream(), e); }
   void comm_wait(EventH e) { dev_->wait(dev_->comm_stream(), e); }
+  // Make `s` wait (once per round) for the stream that produced the input.
+  void wait_input(int32_t round, StreamH s);
+  // The comm stream wrote into this round's output (finalize must join it).
+  void mark_comm_used(int32_t round);
   // Event after the last compute op that reads ring row of `round`.
   EventH row_release_event(int32_t round);
 
@@ -96,7 +100,9 @@ class DataPlane {
     void* output = nullptr;
     int32_t* counts = nullptr;
     EventH input_ready = nullptr;  // recorded on the producer stream
-    bool input_waited = false;
+    bool input_waited_compute = false;
+    bool input_waited_comm = false;
+    bool comm_used = false;  // the comm stream wrote into this round (join at finalize)
     EventH done = nullptr;
     bool finalized = false;
   };
@@ -110,7 +116,7 @@ class DataPlane {
   Row& row_for(int32_t round);
   const Binding& binding(int32_t round) const;
   Binding& binding_mut(int32_t round);
-  void ensure_input_waited(Binding& b);
+
   EventH pooled_event();
   EventH binding_event();
 

@@ -60,6 +60,7 @@ class Device {
   virtual void reduce(StreamH s, const ReduceSpec* specs, int32_t nspecs, DType dt) = 0;
   virtual void copy(StreamH s, void* dst, const void* src, size_t bytes, CopyKind kind) = 0;
   virtual void zero(StreamH s, void* dst, size_t bytes) = 0;
+  virtual void fill_i32(StreamH s, int32_t* dst, int32_t value, size_t n) = 0;
 
   // Host-device only: deferred execution queue used by the p2p simulator.
   virtual void enqueue_host_op(StreamH, std::function<bool()>) {

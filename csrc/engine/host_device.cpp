@@ -126,6 +126,12 @@ class HostDevice final : public Device {
       return true;
     });
   }
+  void fill_i32(StreamH, int32_t* dst, int32_t value, size_t n) override {
+    run([=]() {
+      for (size_t i = 0; i < n; ++i) dst[i] = value;
+      return true;
+    });
+  }
   void enqueue_host_op(StreamH, std::function<bool()> op) override {
     AKKA_CHECK(deferred_, "enqueue_host_op requires a deferred host device");
     queue_.push_back(std::move(op));

@@ -136,6 +136,12 @@ class HipDevice final : public Device {
     AKKA_HIP(hipMemsetAsync(dst, 0, bytes, static_cast<hipStream_t>(s)));
   }
 
+  void fill_i32(StreamH s, int32_t* dst, int32_t value, size_t n) override {
+    if (!n) return;
+    flush_if(s);
+    AKKA_HIP(hipMemsetD32Async(dst, value, n, static_cast<hipStream_t>(s)));
+  }
+
  private:
   bool mergeable(const ReduceSpec& a, const ReduceSpec& b) const {
     if (a.nsrc != b.nsrc) return false;

@@ -52,7 +52,7 @@ void StreamLink::schedule(int32_t r) {
   const int32_t N = g.N;
   if (N == 1) {  // nothing to move: the round was reduced in place during scatter()
     engine_->ensure_output(r);
-    dp_->upload_counts(r, {me}, dp_->device()->comm_stream());
+    dp_->upload_counts(r, {me}, dp_->device()->compute_stream());
     mark_scheduled(r);
     return;
   }
@@ -70,6 +70,8 @@ void StreamLink::schedule(int32_t r) {
   StreamH comm = dp_->device()->comm_stream();
   // The ring row for r was last read by round r-L's reduces (compute stream).
   dp_->comm_wait(dp_->row_release_event(r));
+  dp_->wait_input(r, comm);  // scatter sends read the input
+  dp_->mark_comm_used(r);
 
   std::vector<P2POp> ops;
   for (int32_t s = 0; s < steps; ++s) {
