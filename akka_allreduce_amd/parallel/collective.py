@@ -84,11 +84,15 @@ class ThresholdAllreduce:
             device = torch.device("cuda", local % max(1, torch.cuda.device_count())) if torch.cuda.is_available() \
                 else torch.device("cpu")
         self.device = torch.device(device)
-        if self.device.type != "cuda":
-            raise RuntimeError("ThresholdAllreduce runs on MI355X ranks; use the cluster/outbox worker on CPU")
-        torch.cuda.set_device(self.device)
-        uid = share_unique_id(self.rank, self.world_size, store)
-        spec = ("rccl", uid, self.rank, self.world_size) if self.world_size > 1 else ("local",)
+        if self.device.type == "cuda":
+            torch.cuda.set_device(self.device)
+            uid = share_unique_id(self.rank, self.world_size, store)
+            spec = ("rccl", uid, self.rank, self.world_size) if self.world_size > 1 else ("local",)
+        else:
+            # CPU processes: the same schedule over torch.distributed (gloo) p2p
+            from .gloo import make_group_fn
+
+            spec = ("callback", make_group_fn(), self.rank, self.world_size) if self.world_size > 1 else ("local",)
         self.worker = AllreduceWorker(None, data_sink, device=self.device, dtype=dtype, transport="stream",
                                       transport_spec=spec, broadcast_lag=broadcast_lag, strict=True,
                                       name=f"rank{self.rank}")

@@ -1,0 +1,37 @@
+"""Grouped p2p over ``torch.distributed`` (gloo) for CPU processes.
+
+The native StreamLink issues the same step groups it issues to RCCL on
+MI355X; here each group becomes a set of ``isend``/``irecv`` on raw views of
+the worker's host buffers, waited together (group semantics).  gloo matches
+point-to-point messages per (peer, tag) in issue order -- the same
+per-pair FIFO contract as RCCL -- so the production schedule runs unchanged
+across real processes on a CPU-only machine (multi-process tests, dev boxes).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Callable, List, Tuple
+
+import torch
+import torch.distributed as dist
+
+Op = Tuple[bool, int, int, int]
+
+
+def _view(ptr: int, nbytes: int) -> torch.Tensor:
+    buf = (ctypes.c_uint8 * nbytes).from_address(ptr)
+    return torch.frombuffer(buf, dtype=torch.uint8)
+
+
+def make_group_fn(group=None) -> Callable[[List[Op]], None]:
+    def run(ops: List[Op]) -> None:
+        reqs = []
+        for send, peer, ptr, nbytes in ops:
+            if nbytes == 0:
+                continue
+            t = _view(ptr, nbytes)
+            reqs.append(dist.isend(t, peer, group=group) if send else dist.irecv(t, peer, group=group))
+        for r in reqs:
+            r.wait()
+
+    return run

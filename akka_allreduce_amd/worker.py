@@ -160,7 +160,11 @@ class AllreduceWorker:
             raise TypeError(f"unhandled message {msg!r}")
 
     def _on_init(self, m: InitWorkers) -> None:
-        peers = [(int(i), ref is self) for i, ref in m.workers.items()]
+        # a reference to this worker itself (or a local wrapper of it) short-circuits (W:228)
+        peers = [(int(i), ref is self or getattr(ref, "actor", None) is self) for i, ref in m.workers.items()]
+        tinfo = getattr(m, "transport", None)
+        if tinfo and tinfo.get("kind") == "rccl" and self.transport == "stream" and self.transport_spec is None:
+            self.transport_spec = ("rccl", tinfo["uid"], int(m.destId), int(m.workerNum))
         first = self._core.init(int(m.destId), int(m.workerNum), float(m.thReduce), float(m.thComplete),
                                 int(m.maxLag), int(m.dataSize), int(m.maxChunkSize), peers)
         self.peers = dict(m.workers)
@@ -194,6 +198,9 @@ class AllreduceWorker:
             self._core.connect_sim(hub, int(rank))
         elif kind == "local":
             self._core.connect_local()
+        elif kind == "callback":
+            _, fn, rank, nranks = spec
+            self._core.connect_callback(fn, int(rank), int(nranks))
         else:
             raise ValueError(f"unknown transport spec {spec!r}")
 

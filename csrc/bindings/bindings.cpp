@@ -59,6 +59,27 @@ class OutboxLink final : public Link {
   std::vector<OutMsg> box_;
 };
 
+// Grouped p2p delegated to a Python callable: ops = [(send, peer, ptr, bytes)].
+// Used with torch.distributed (gloo) to run the production schedule across
+// real processes on CPU-only machines.
+class PyCallbackP2P final : public P2P {
+ public:
+  PyCallbackP2P(py::function fn, int32_t rank, int32_t n) : fn_(std::move(fn)), rank_(rank), n_(n) {}
+  int32_t rank() const override { return rank_; }
+  int32_t nranks() const override { return n_; }
+  const char* name() const override { return "callback"; }
+  void group(StreamH, const std::vector<P2POp>& ops) override {
+    py::list l;
+    for (const auto& op : ops)
+      l.append(py::make_tuple(op.send, op.peer, reinterpret_cast<uintptr_t>(op.buf), op.bytes));
+    fn_(l);
+  }
+
+ private:
+  py::function fn_;
+  int32_t rank_, n_;
+};
+
 class WorkerCore final : public EngineHost {
  public:
   WorkerCore(py::object host, std::string link, int32_t device, std::string dtype, bool deferred, int32_t lag)
@@ -113,6 +134,11 @@ class WorkerCore final : public EngineHost {
   void connect_sim(const PySimHub& hub, int32_t rank) {
     AKKA_CHECK(dev_ && dev_->is_host() && deferred_, "sim transport needs a deferred host device");
     p2p_ = make_sim_p2p(hub.hub, rank, dev_.get());
+    make_stream_link();
+  }
+  void connect_callback(py::function fn, int32_t rank, int32_t nranks) {
+    AKKA_CHECK(dev_ && dev_->is_host() && !deferred_, "callback p2p runs on an immediate host device");
+    p2p_ = std::make_unique<PyCallbackP2P>(std::move(fn), rank, nranks);
     make_stream_link();
   }
   void connect_local() {  // N == 1: stream link without peers
@@ -271,6 +297,7 @@ PYBIND11_MODULE(_native, m) {
       .def("connect_rccl", &WorkerCore::connect_rccl)
       .def("connect_sim", &WorkerCore::connect_sim)
       .def("connect_local", &WorkerCore::connect_local)
+      .def("connect_callback", &WorkerCore::connect_callback)
       .def("attach", &WorkerCore::attach)
       .def("start", &WorkerCore::start)
       .def("scatter_in", &WorkerCore::scatter_in)

@@ -78,6 +78,9 @@ class HipDevice final : public Device {
   }
   void wait(StreamH s, EventH e) override {
     flush_if(s);
+    // An event that already completed needs no barrier packet on the stream
+    // (each cross-stream wait costs the command processor several us).
+    if (hipEventQuery(static_cast<hipEvent_t>(e)) == hipSuccess) return;
     AKKA_HIP(hipStreamWaitEvent(static_cast<hipStream_t>(s), static_cast<hipEvent_t>(e), 0));
   }
   bool query(EventH e) override {

@@ -1,0 +1,85 @@
+"""Master/worker cluster runtime (TCP control + data plane on CPU).
+
+* README demo (BASELINE config 1): master + 2 workers, dataSize 10, chunk 2.
+* scripts config: 4 workers, dataSize 778, chunk 3, maxLag 3, exact (x4).
+* failure detection: a worker dies mid-run; with thresholds < 1 the survivors
+  keep completing rounds and the master (live-count pacing) reaches maxRound.
+* separate OS processes via the CLI (`python -m akka_allreduce_amd demo`).
+"""
+import os
+import subprocess
+import sys
+import time
+
+import pytest
+
+from akka_allreduce_amd.config import DataConfig, ThresholdConfig, WorkerConfig
+from akka_allreduce_amd.parallel.cluster import start_master, start_worker
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _run_cluster(n, size, chunk, rounds, max_lag=1, th=(1.0, 1.0, 1.0), assert_multiple=None, checkpoint=5):
+    m = start_master(ThresholdConfig(*th), DataConfig(size, chunk, rounds), WorkerConfig(n, max_lag), port=0,
+                     transport="tcp", unreachable_after_s=30.0)
+    am = n if assert_multiple is None else assert_multiple
+    ws = [start_worker(m.address, size, checkpoint=checkpoint, assert_multiple=am, printer=lambda *_: None)
+          for _ in range(n)]
+    try:
+        assert m.wait(60), f"master stuck at round {m.master.round}"
+        for w in ws:
+            assert w.wait(10)
+        return m, ws
+    finally:
+        m.stop()
+        for w in ws:
+            w.stop()
+
+
+def test_readme_demo_two_workers():
+    m, ws = _run_cluster(2, 10, 2, 40)
+    assert m.master.round == 40
+    for w in ws:
+        assert w.worker.dataSink.failures == 0
+        assert w.worker.dataSink.rounds >= 41
+
+
+def test_scripts_config_four_workers_exact():
+    # scripts/testAllreduceMaster.sc: 4 workers, 778 floats, chunk 3, maxLag 3, thresholds 1 (maxRound cut to 30)
+    m, ws = _run_cluster(4, 778, 3, 30, max_lag=3, checkpoint=10)
+    for w in ws:
+        assert w.worker.dataSink.failures == 0
+    assert sorted(w.worker.id for w in ws) == [0, 1, 2, 3]
+
+
+def test_worker_death_with_thresholds():
+    n, size, chunk, rounds = 3, 300, 10, 400
+    # thReduce .66 -> 1 of 3 copies, thComplete .3 of 30 chunks, thAllreduce .6 of live workers
+    m = start_master(ThresholdConfig(0.6, 0.66, 0.3), DataConfig(size, chunk, rounds), WorkerConfig(n, 2), port=0,
+                     transport="tcp", unreachable_after_s=1.0, heartbeat_interval_s=0.2)
+    ws = [start_worker(m.address, size, checkpoint=1000, printer=lambda *_: None, heartbeat_interval_s=0.2)
+          for _ in range(n)]
+    try:
+        t0 = time.time()
+        while m.master.round < 5 and time.time() - t0 < 20:
+            time.sleep(0.05)
+        assert m.master.round >= 5
+        victim = ws[2]
+        victim.stop()  # dies: stops heartbeating and serving
+        assert m.wait(60), f"stalled at round {m.master.round} with {len(m.master.workers)} workers"
+        assert len(m.master.workers) == n - 1
+    finally:
+        m.stop()
+        for w in ws:
+            w.stop()
+
+
+def test_cli_demo_processes():
+    env = dict(os.environ, PYTHONUNBUFFERED="1")
+    port = 26000 + (os.getpid() % 3000)
+    r = subprocess.run([sys.executable, "-m", "akka_allreduce_amd", "--log-level", "WARNING", "demo", "--port",
+                        str(port), "--workers", "2", "--data-size", "10", "--max-chunk-size", "2", "--max-round", "25",
+                        "--checkpoint", "5", "--assert-multiple", "2", "--timeout", "120"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+    assert "failures=0" in r.stdout
