@@ -328,6 +328,22 @@ PYBIND11_MODULE(_native, m) {
   });
   m.def("rccl_version", []() { return std::string(rccl_version_string()); });
 
+  // Raw grouped-p2p endpoint (tests / microbenchmarks of the RCCL data plane).
+  py::class_<P2P>(m, "P2PEndpoint")
+      .def("rank", &P2P::rank)
+      .def("nranks", &P2P::nranks)
+      .def("group", [](P2P& p, uintptr_t stream, const std::vector<std::tuple<bool, int32_t, uintptr_t, size_t>>& ops) {
+        std::vector<P2POp> v;
+        v.reserve(ops.size());
+        for (const auto& o : ops)
+          v.push_back({std::get<0>(o), std::get<1>(o), reinterpret_cast<void*>(std::get<2>(o)), std::get<3>(o)});
+        p.group(reinterpret_cast<StreamH>(stream), v);
+      });
+  m.def("rccl_endpoint", [](py::bytes uid, int32_t rank, int32_t nranks, int32_t device) {
+    std::string s = uid;
+    return make_rccl_p2p(std::vector<uint8_t>(s.begin(), s.end()), rank, nranks, device);
+  });
+
   // ---- kernels (tests / microbench) ----------------------------------------------
   m.def("reduce", [](uintptr_t dst, std::vector<uintptr_t> srcs, int64_t n, std::string dtype, uintptr_t stream,
                      std::string impl) {

@@ -327,6 +327,13 @@ void launch_reduce(hipStream_t s, const ReduceSpec& spec, DType dt, ReduceImpl i
   }
   const int64_t per_vec = dt == DType::F32 ? 4 : 8;
   const int64_t nvec = aligned ? spec.n / per_vec : 0;
+  if (impl == ReduceImpl::Auto) {
+    // Measured (profiles/README.md): LDS-DMA staging wins while the working set
+    // sits in the 256 MiB Infinity Cache (chunk-sized reduces inside a round,
+    // data just landed from xGMI); direct 16-B loads win for HBM-resident streams.
+    const int64_t bytes = int64_t(spec.nsrc + 1) * spec.n * (dt == DType::F32 ? 4 : 2);
+    impl = (bytes <= (int64_t(96) << 20) && spec.nsrc <= 8) ? ReduceImpl::Lds : ReduceImpl::Vec;
+  }
   if (impl == ReduceImpl::Scalar) {
     // forced scalar path over everything
   } else if (nvec > 0) {

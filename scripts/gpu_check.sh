@@ -9,7 +9,7 @@ R=$(pwd)
 O=$R/gpurun_out
 mkdir -p $O
 export HSA_ENABLE_IPC_MODE_LEGACY=0
-STEPS="${STEPS:-env pytest smoke bench micro hostovh bf16 mlp prof}"
+STEPS="${STEPS:-env pytest smoke bench micro hostovh bf16 mlp rcclp2p prof}"
 
 step() {  # step <name> <timeout-s> <cmd...>
   local name=$1 t=$2; shift 2
@@ -30,5 +30,6 @@ step micro 400 bash -c "python bench/reduce_kernel_bw.py --torch-ref > $O/reduce
 step hostovh 200 bash -c "python bench.py --steps 200 --warmup 20 --size-mb 0.0625 --chunk-mb 0.015625 --no-check > $O/bench_small.json 2>&1; cat $O/bench_small.json"
 step bf16 300 bash -c "python bench.py --dtype bfloat16 --size-mb 1024 --chunk-mb 8 --steps 10 --warmup 3 > $O/bench_bf16_1g.json 2>&1; tail -1 $O/bench_bf16_1g.json"
 step mlp 300 bash -c "python examples/mlp_sgd.py > $O/mlp.json 2>&1; tail -1 $O/mlp.json"
+step rcclp2p 200 bash -c "python bench/rccl_p2p_overhead.py > $O/rccl_p2p.jsonl 2>&1; tail -4 $O/rccl_p2p.jsonl"
 step prof 400 bash -c "cd /tmp && export TMPDIR=/tmp && rocprofv3 --kernel-trace --stats -d $O/prof -o bench -- python $R/bench.py --steps 10 --warmup 3 > $O/prof.log 2>&1; tail -3 $O/prof.log; python $R/scripts/prof_summary.py $O/prof/bench_results.db 40 > $O/prof_summary.txt 2>&1; head -12 $O/prof_summary.txt"
 exit 0
