@@ -29,6 +29,7 @@ from typing import Any, Callable, Dict, List, Optional, Tuple
 import torch
 
 from .data import AllReduceInput, AllReduceInputRequest, AllReduceOutput, Geometry
+from .utils import tracing as _tracing
 from .messages import (
     CompleteAllreduce,
     InitWorkers,
@@ -246,7 +247,8 @@ class AllreduceWorker:
         self._stream_cache = torch.cuda.current_stream(self.device).cuda_stream if self.device.type == "cuda" else 0
         self._async = bool(async_op) and self.device.type == "cuda"
         try:
-            self.receive(StartAllreduce(r))
+            with _tracing.range_(f"akka.round {r}"):
+                self.receive(StartAllreduce(r))
         finally:
             self._stream_cache = None
             self._async = False
