@@ -101,11 +101,12 @@ class ThresholdAllreduce:
                                      int(data_size), int(max_chunk_size)))
         self.data_size = int(data_size)
 
-    def __call__(self, x: torch.Tensor, async_op: bool = False) -> AllReduceOutput:
-        """One round.  ``async_op=True``: call ``out.wait()`` before reading ``out.data``."""
+    def __call__(self, x: torch.Tensor, async_op: bool = False, out: Optional[torch.Tensor] = None) -> AllReduceOutput:
+        """One round.  ``async_op=True``: call ``.wait()`` before reading ``.data``.
+        ``out``: preallocated output buffer (reused across rounds)."""
         if x.numel() != self.data_size:
             raise ValueError(f"expected {self.data_size} elements, got {x.numel()}")
-        out = self.worker.allreduce(x, async_op=async_op)
+        out = self.worker.allreduce(x, async_op=async_op, out=out)
         if out is None:
             raise RuntimeError("round did not complete (thresholds need every rank in the scheduled transport)")
         return out

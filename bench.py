@@ -38,6 +38,7 @@ def parse():
     p.add_argument("--th-complete", type=float, default=1.0)
     p.add_argument("--compare-rccl", action="store_true", help="also time torch.distributed all_reduce (RCCL)")
     p.add_argument("--no-check", action="store_true")
+    p.add_argument("--fresh-out", action="store_true", help="allocate a new output tensor every round")
     p.add_argument("--sync-op", dest="async_op", action="store_false",
                    help="make the caller's stream wait after every round (default: async rounds)")
     return p.parse_args()
@@ -84,20 +85,21 @@ def main() -> int:
     # Rounds are issued back to back (async_op, like nccl-tests / torch's
     # async_op=True): every round's output is waited for on the current stream
     # before the closing synchronize, so all K rounds complete inside the timing.
+    # The output goes into one preallocated buffer reused every round (like
+    # nccl-tests' recvbuff): all rounds run in order on the engine's streams, so
+    # waiting for the last round's event covers every round.
+    out_buf = None if args.fresh_out else torch.empty(S, device=dev, dtype=dtype)
     for _ in range(args.warmup):
-        out = ar(x, async_op=args.async_op)
+        out = ar(x, async_op=args.async_op, out=out_buf)
     out.wait()
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    outs = []
     for _ in range(args.steps):
-        outs.append(ar(x, async_op=args.async_op))
-        if len(outs) > 4:
-            outs.pop(0).wait()
-    for o in outs:
-        o.wait()
+        out = ar(x, async_op=args.async_op, out=out_buf)
+    out.wait()
+    outs = None
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()

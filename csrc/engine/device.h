@@ -30,6 +30,10 @@ struct ReduceSpec {
   const void* srcs[kMaxReduceSrc] = {};
   int32_t nsrc = 0;
   int64_t n = 0;
+  // Optional piggy-backed int32 fill (a counts row) done by the same launch.
+  int32_t* fill = nullptr;
+  int32_t fill_value = 0;
+  int32_t fill_n = 0;
 };
 
 enum class CopyKind : int32_t { Default = 0, HostToDevice = 1, DeviceToHost = 2, DeviceToDevice = 3, HostToHost = 4 };

@@ -141,13 +141,21 @@ class HipDevice final : public Device {
 
   void fill_i32(StreamH s, int32_t* dst, int32_t value, size_t n) override {
     if (!n) return;
+    // A counts row issued right behind a pending reduce on the same stream
+    // rides along in that launch (block 0 writes it): one dispatch per round.
+    if (!pending_.empty() && pending_stream_ == s && !pending_.back().fill && n <= 65536) {
+      pending_.back().fill = dst;
+      pending_.back().fill_value = value;
+      pending_.back().fill_n = int32_t(n);
+      return;
+    }
     flush_if(s);
     AKKA_HIP(hipMemsetD32Async(dst, value, n, static_cast<hipStream_t>(s)));
   }
 
  private:
   bool mergeable(const ReduceSpec& a, const ReduceSpec& b) const {
-    if (a.nsrc != b.nsrc) return false;
+    if (a.nsrc != b.nsrc || a.fill || b.fill) return false;
     const size_t es = dtype_size(pending_dt_);
     const size_t off = size_t(a.n) * es;
     if (static_cast<char*>(a.dst) + off != b.dst) return false;

@@ -31,7 +31,15 @@ constexpr int kMaxGrid = 256 * 8;  // 256 CUs x 8 blocks
 
 struct SrcTable {
   const void* p[kMaxReduceSrc];
+  int32_t* fill;  // optional counts-row fill done by block 0 (saves a dispatch per round)
+  int32_t fill_value;
+  int32_t fill_n;
 };
+
+__device__ __forceinline__ void do_fill(const SrcTable& t) {
+  if (blockIdx.x == 0)
+    for (int i = threadIdx.x; i < t.fill_n; i += kBlock) t.fill[i] = t.fill_value;
+}
 
 __device__ __forceinline__ void add_vec(float (&acc)[4], const v4u& v, float) {
   acc[0] += __uint_as_float(v.x);
@@ -81,6 +89,7 @@ struct VecTraits<unsigned short> {
 template <typename T, int NSRC, int UNROLL>
 __global__ __launch_bounds__(kBlock) void reduce_vec_kernel(SrcTable srcs, v4u* __restrict__ dst, int64_t nvec) {
   constexpr int E = VecTraits<T>::kElems;
+  do_fill(srcs);
   const int64_t stride = int64_t(gridDim.x) * kBlock;
   for (int64_t base = int64_t(blockIdx.x) * kBlock + threadIdx.x; base < nvec; base += stride * UNROLL) {
     v4u v[UNROLL][NSRC];
@@ -118,6 +127,7 @@ __global__ __launch_bounds__(kBlock) void reduce_lds_kernel(SrcTable srcs, v4u* 
   __shared__ v4u lds[2][NSRC][kWaves][64];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
+  do_fill(srcs);
   const int64_t ntiles = nvec / 64;  // full wave tiles; the tail goes through VGPRs
   const int64_t wave_id = int64_t(blockIdx.x) * kWaves + wave;
   const int64_t wave_stride = int64_t(gridDim.x) * kWaves;
@@ -202,6 +212,7 @@ __device__ __forceinline__ unsigned short from_f<unsigned short>(float v) {
 template <typename T>
 __global__ __launch_bounds__(kBlock) void reduce_scalar_kernel(SrcTable srcs, int nsrc, T* __restrict__ dst,
                                                                int64_t n) {
+  do_fill(srcs);
   const int64_t stride = int64_t(gridDim.x) * kBlock;
   for (int64_t i = int64_t(blockIdx.x) * kBlock + threadIdx.x; i < n; i += stride) {
     float acc = 0.f;
@@ -334,21 +345,32 @@ void launch_reduce(hipStream_t s, const ReduceSpec& spec, DType dt, ReduceImpl i
     const int64_t bytes = int64_t(spec.nsrc + 1) * spec.n * (dt == DType::F32 ? 4 : 2);
     impl = (bytes <= (int64_t(96) << 20) && spec.nsrc <= 8) ? ReduceImpl::Lds : ReduceImpl::Vec;
   }
+  bool filled = false;
   if (impl == ReduceImpl::Scalar) {
     // forced scalar path over everything
   } else if (nvec > 0) {
     const bool lds = impl == ReduceImpl::Lds;
+    t.fill = spec.fill;
+    t.fill_value = spec.fill_value;
+    t.fill_n = spec.fill ? spec.fill_n : 0;
+    filled = true;
     if (dt == DType::F32) launch_vec<float>(s, t, spec.nsrc, static_cast<v4u*>(spec.dst), nvec, lds);
     else launch_vec<unsigned short>(s, t, spec.nsrc, static_cast<v4u*>(spec.dst), nvec, lds);
     check_launch("reduce_vec");
   }
   const int64_t done = impl == ReduceImpl::Scalar ? 0 : nvec * per_vec;
   const int64_t rest = spec.n - done;
-  if (rest > 0) {
+  if (rest > 0 || (!filled && spec.fill && spec.fill_n > 0)) {
     const size_t es = dt == DType::F32 ? 4 : 2;
     SrcTable tt{};
+    if (!filled) {
+      tt.fill = spec.fill;
+      tt.fill_value = spec.fill_value;
+      tt.fill_n = spec.fill ? spec.fill_n : 0;
+    }
     for (int i = 0; i < spec.nsrc; ++i) tt.p[i] = static_cast<const char*>(spec.srcs[i]) + done * es;
     int64_t want = (rest + kBlock - 1) / kBlock;
+    if (want < 1) want = 1;  // fill-only launch
     int grid = int(want < kMaxGrid ? want : kMaxGrid);
     if (dt == DType::F32) {
       hipLaunchKernelGGL(reduce_scalar_kernel<float>, dim3(grid), dim3(kBlock), 0, s, tt, spec.nsrc,
