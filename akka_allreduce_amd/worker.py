@@ -326,9 +326,14 @@ class AllreduceWorker:
         event = None
         if self.device.type == "cuda":
             if self._async:
-                # finalize() already queued the round's done point on the compute stream
+                # finalize() already queued the round's done point on the stream
+                # that ran it: the compute stream, or the caller's own stream for
+                # a purely local (N=1) round
                 event = torch.cuda.Event()
-                event.record(self._internal_streams()[1])
+                if self._core.exec_on_producer(round_):
+                    event.record(torch.cuda.current_stream(self.device))
+                else:
+                    event.record(self._internal_streams()[1])
             else:
                 self._core.stream_wait_done(round_, self._stream_ptr())
         g = self.geometry

@@ -175,6 +175,7 @@ class WorkerCore final : public EngineHost {
     dp_->stream_wait_done(round, reinterpret_cast<StreamH>(stream));
   }
   void sync_done(int32_t round) { dp_->sync_done(round); }
+  bool exec_on_producer(int32_t round) const { return dp_->exec_on_producer(round); }
   void sync_all() {
     if (!dev_) return;
     dev_->sync_stream(dev_->compute_stream());
@@ -308,6 +309,7 @@ PYBIND11_MODULE(_native, m) {
       .def("unbind", &WorkerCore::unbind)
       .def("stream_wait_done", &WorkerCore::stream_wait_done)
       .def("sync_done", &WorkerCore::sync_done)
+      .def("exec_on_producer", &WorkerCore::exec_on_producer)
       .def("sync_all", &WorkerCore::sync_all)
       .def("expand_counts", &WorkerCore::expand_counts)
       .def("drain", &WorkerCore::drain)

@@ -103,9 +103,27 @@ void DataPlane::bind_input(int32_t round, const void* input, StreamH ready_strea
   b.input = input;
   b.input_waited_compute = b.input_waited_comm = false;
   if (has_stream && !dev_->is_host()) {
+    if (g_.N == 1) {
+      // A purely local round (no peers, no comm stream) runs its reduce on the
+      // producer's own stream: no cross-stream event hop per round.
+      b.exec = ready_stream;
+      b.exec_on_producer = true;
+      return;
+    }
     if (!b.input_ready) b.input_ready = binding_event();
     dev_->record(b.input_ready, ready_stream);
   }
+}
+
+StreamH DataPlane::exec_stream(int32_t round) const {
+  auto it = bind_.find(round);
+  if (it != bind_.end() && it->second.exec_on_producer) return it->second.exec;
+  return dev_->compute_stream();
+}
+
+bool DataPlane::exec_on_producer(int32_t round) const {
+  auto it = bind_.find(round);
+  return it != bind_.end() && it->second.exec_on_producer;
 }
 
 EventH DataPlane::binding_event() {
@@ -213,7 +231,7 @@ void DataPlane::store_scatter(int32_t round, int32_t src, int32_t k, const Paylo
   if (p.kind == PayloadKind::Landed) return;
   void* dst = scatter_slot(round, src, k);
   CopyKind ck = p.on_host ? CopyKind::HostToDevice : CopyKind::DeviceToDevice;
-  dev_->copy(dev_->compute_stream(), dst, p.ptr, size_t(p.len) * esize(), ck);
+  dev_->copy(exec_stream(round), dst, p.ptr, size_t(p.len) * esize(), ck);
 }
 
 Payload DataPlane::reduce(int32_t round, int32_t k, const std::vector<int32_t>& srcs) {
@@ -224,19 +242,20 @@ Payload DataPlane::reduce(int32_t round, int32_t k, const std::vector<int32_t>& 
   void* dst = output_at(round, me_, k);
   std::vector<const void*> ptrs;
   ptrs.reserve(srcs.size());
+  const StreamH cs = exec_stream(round);
   for (int32_t s : srcs) {
     if (s == me_ && r.self_alias[size_t(k)]) {
-      wait_input(round, dev_->compute_stream());
+      wait_input(round, cs);
       ptrs.push_back(static_cast<const char*>(b.input) + size_t(g_.chunk_offset(me_, k)) * esize());
     } else {
       ptrs.push_back(scatter_slot(round, s, k));
     }
   }
   if (ptrs.empty()) {
-    dev_->zero(dev_->compute_stream(), dst, size_t(n) * esize());
+    dev_->zero(cs, dst, size_t(n) * esize());
   } else {
     auto specs = split_reduce(dst, ptrs, n);
-    dev_->reduce(dev_->compute_stream(), specs.data(), int32_t(specs.size()), dt_);
+    dev_->reduce(cs, specs.data(), int32_t(specs.size()), dt_);
   }
   return output_chunk(round, me_, k);
 }
@@ -250,7 +269,7 @@ void DataPlane::store_reduced(int32_t round, int32_t src, int32_t k, const Paylo
   void* dst = output_at(round, src, k);
   if (p.ptr == dst) return;
   CopyKind ck = p.on_host ? CopyKind::HostToDevice : CopyKind::DeviceToDevice;
-  dev_->copy(dev_->compute_stream(), dst, p.ptr, size_t(p.len) * esize(), ck);
+  dev_->copy(exec_stream(round), dst, p.ptr, size_t(p.len) * esize(), ck);
 }
 
 void DataPlane::set_count(int32_t round, int32_t block, int32_t k, int32_t count) {
@@ -284,7 +303,7 @@ void DataPlane::upload_counts(int32_t round, const std::vector<int32_t>& blocks,
 void DataPlane::finalize(int32_t round, const std::vector<uint8_t>& landed) {
   Binding& b = binding_mut(round);
   AKKA_CHECK(landed.size() == size_t(g_.N) * kmax_, "landed mask has wrong shape");
-  StreamH cs = dev_->compute_stream();
+  const StreamH cs = exec_stream(round);
   // Join: everything the comm stream wrote into this round's output.
   if (b.comm_used) {
     EventH ce = record_comm();
@@ -314,6 +333,7 @@ void DataPlane::finalize(int32_t round, const std::vector<uint8_t>& landed) {
 void DataPlane::stream_wait_done(int32_t round, StreamH stream) {
   const Binding& b = binding(round);
   AKKA_CHECK(b.finalized, "round not finalized");
+  if (b.exec_on_producer && stream == b.exec) return;  // already in that stream's order
   dev_->wait(stream, b.done);
 }
 

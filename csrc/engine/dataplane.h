@@ -87,6 +87,10 @@ class DataPlane {
   EventH record_comm();
   void compute_wait(EventH e) { dev_->wait(dev_->compute_stream(), e); }
   void comm_wait(EventH e) { dev_->wait(dev_->comm_stream(), e); }
+  // Stream that runs the round's reduces/copies/finalize: the compute stream,
+  // or -- for a purely local round (N == 1) -- the input producer's stream.
+  StreamH exec_stream(int32_t round) const;
+  bool exec_on_producer(int32_t round) const;
   // Make `s` wait (once per round) for the stream that produced the input.
   void wait_input(int32_t round, StreamH s);
   // The comm stream wrote into this round's output (finalize must join it).
@@ -103,6 +107,8 @@ class DataPlane {
     bool input_waited_compute = false;
     bool input_waited_comm = false;
     bool comm_used = false;  // the comm stream wrote into this round (join at finalize)
+    StreamH exec = nullptr;  // stream running this round's compute when exec_on_producer
+    bool exec_on_producer = false;
     EventH done = nullptr;
     bool finalized = false;
   };

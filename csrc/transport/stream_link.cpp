@@ -52,7 +52,7 @@ void StreamLink::schedule(int32_t r) {
   const int32_t N = g.N;
   if (N == 1) {  // nothing to move: the round was reduced in place during scatter()
     engine_->ensure_output(r);
-    dp_->upload_counts(r, {me}, dp_->device()->compute_stream());
+    dp_->upload_counts(r, {me}, dp_->exec_stream(r));
     mark_scheduled(r);
     return;
   }
