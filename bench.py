@@ -39,8 +39,9 @@ def parse():
     p.add_argument("--compare-rccl", action="store_true", help="also time torch.distributed all_reduce (RCCL)")
     p.add_argument("--no-check", action="store_true")
     p.add_argument("--fresh-out", action="store_true", help="allocate a new output tensor every round")
-    p.add_argument("--sync-op", dest="async_op", action="store_false",
-                   help="make the caller's stream wait after every round (default: async rounds)")
+    p.add_argument("--async-op", choices=["auto", "on", "off"], default="auto",
+                   help="async rounds (event hand-off) -- auto: on for N>1 (saves a stream hop per round), off for "
+                        "N=1 (local rounds run on the caller's stream, nothing to hop)")
     return p.parse_args()
 
 
@@ -89,6 +90,7 @@ def main() -> int:
     # nccl-tests' recvbuff): all rounds run in order on the engine's streams, so
     # waiting for the last round's event covers every round.
     out_buf = None if args.fresh_out else torch.empty(S, device=dev, dtype=dtype)
+    args.async_op = (world > 1) if args.async_op == "auto" else (args.async_op == "on")
     for _ in range(args.warmup):
         out = ar(x, async_op=args.async_op, out=out_buf)
     out.wait()
@@ -168,6 +170,8 @@ def main() -> int:
                 "broadcast_lag": args.bcast_lag,
                 "thresholds": [1.0, args.th_reduce, args.th_complete],
                 "transport": "rccl-p2p-xgmi" if world > 1 else "local",
+                "async_op": args.async_op,
+                "output": "fresh tensor per round" if args.fresh_out else "preallocated, reused",
             },
             "busbw_GBps": round(busbw, 3),
             "exact": ok,
