@@ -68,32 +68,39 @@ def _run(cmd: list[str], verbose: bool) -> None:
         raise RuntimeError(f"build step failed ({r.returncode}):\n{' '.join(cmd)}\n{r.stdout}")
 
 
-def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -> str:
+def build(force: bool = False, jobs: int | None = None, verbose: bool = False, sanitize: str | None = None) -> str:
+    """Compile and link.  ``sanitize`` (e.g. ``"address,undefined"``) builds an
+    instrumented HOST-code variant into ``build/native-<san>/`` (never the
+    in-tree module); device code is not instrumented (no GPU sanitizers on
+    this pool).  Load it with ``AKKA_NATIVE_PATH=<path>``."""
     import pybind11
 
-    os.makedirs(BUILD, exist_ok=True)
+    tag = sanitize.replace(",", "-") if sanitize else None
+    bdir = os.path.join(ROOT, "build", f"native-{tag}") if tag else BUILD
+    os.makedirs(bdir, exist_ok=True)
     py_inc = sysconfig.get_paths()["include"]
-    common = ["-O3", "-fPIC", "-std=c++17", "-Wall", "-Wno-unused-function", "-I" + CSRC]
-    host_flags = common + [
+    opt = ["-O1", "-g", "-fno-omit-frame-pointer", f"-fsanitize={sanitize}"] if sanitize else ["-O3"]
+    common = ["-fPIC", "-std=c++17", "-Wall", "-Wno-unused-function", "-I" + CSRC]
+    host_flags = opt + common + [
         "-D__HIP_PLATFORM_AMD__",
         "-I" + os.path.join(ROCM, "include"),
         "-I" + pybind11.get_include(),
         "-I" + py_inc,
         "-fvisibility=hidden",
     ]
-    hip_flags = common + [f"--offload-arch={ARCH}", "-I" + os.path.join(ROCM, "include")]
+    hip_flags = ["-O3"] + common + [f"--offload-arch={ARCH}", "-I" + os.path.join(ROCM, "include")]
     headers = _headers()
     steps = []
     objs = []
     for rel in HOST_SOURCES:
         src = os.path.join(CSRC, rel)
-        obj = os.path.join(BUILD, rel.replace("/", "_") + ".o")
+        obj = os.path.join(bdir, rel.replace("/", "_") + ".o")
         objs.append(obj)
         if force or _stale(obj, src, headers):
             steps.append(["g++", *host_flags, "-c", src, "-o", obj])
     for rel in HIP_SOURCES:
         src = os.path.join(CSRC, rel)
-        obj = os.path.join(BUILD, rel.replace("/", "_") + ".o")
+        obj = os.path.join(bdir, rel.replace("/", "_") + ".o")
         objs.append(obj)
         if force or _stale(obj, src, headers):
             steps.append([os.path.join(ROCM, "bin", "hipcc"), *hip_flags, "-c", src, "-o", obj])
@@ -101,11 +108,12 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         for f in [ex.submit(_run, s, verbose) for s in steps]:
             f.result()
-    out = ext_path()
+    out = os.path.join(bdir, "_native" + sysconfig.get_config_var("EXT_SUFFIX")) if tag else ext_path()
     if force or steps or not os.path.exists(out):
         tlib = _torch_lib()
+        linker = ["g++", f"-fsanitize={sanitize}"] if sanitize else [os.path.join(ROCM, "bin", "hipcc")]
         link = [
-            os.path.join(ROCM, "bin", "hipcc"),
+            *linker,
             "-shared",
             "-fPIC",
             *objs,
@@ -122,5 +130,6 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False) -
 
 
 if __name__ == "__main__":
-    path = build(force="--force" in sys.argv, verbose="-v" in sys.argv)
+    san = next((a.split("=", 1)[1] for a in sys.argv if a.startswith("--sanitize=")), None)
+    path = build(force="--force" in sys.argv, verbose="-v" in sys.argv, sanitize=san)
     print(path)

@@ -2,11 +2,15 @@
 
 The extension is the only implementation of the engine/kernels: there is no
 Python fallback, so a missing or broken build fails loudly here.
+``AKKA_NATIVE_PATH`` loads an alternative build of the same module (e.g. the
+AddressSanitizer variant from ``_build.build(sanitize=...)``).
 """
 from __future__ import annotations
 
 import importlib
+import importlib.util
 import os
+import sys
 import threading
 
 _lock = threading.Lock()
@@ -21,6 +25,15 @@ def load():
         if _mod is not None:
             return _mod
         import torch  # noqa: F401  (loads torch's HIP runtime + RCCL first: one copy per process)
+
+        alt = os.environ.get("AKKA_NATIVE_PATH")
+        if alt:
+            spec = importlib.util.spec_from_file_location("akka_allreduce_amd._native", alt)
+            mod = importlib.util.module_from_spec(spec)
+            sys.modules["akka_allreduce_amd._native"] = mod
+            spec.loader.exec_module(mod)
+            _mod = mod
+            return _mod
 
         from . import _build
 
