@@ -200,6 +200,9 @@ class AllreduceWorker:
             self._core.connect_sim(hub, int(rank))
         elif kind == "local":
             self._core.connect_local()
+        elif kind == "loopback":
+            _, hub, rank = spec
+            self._core.connect_loopback(hub, int(rank))
         elif kind == "callback":
             _, fn, rank, nranks = spec
             self._core.connect_callback(fn, int(rank), int(nranks))

@@ -10,6 +10,10 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <chrono>
+#include <condition_variable>
+#include <mutex>
+
 #include "../engine/engine.h"
 #include "../kernels/kernels.h"
 #include "../transport/p2p.h"
@@ -80,6 +84,115 @@ class PyCallbackP2P final : public P2P {
   int32_t rank_, n_;
 };
 
+// ---------------------------------------------------------------------------
+// GPU loopback p2p: N ranks of ONE process on ONE GPU, each with its own HIP
+// streams.  A group is a host rendezvous of all ranks (the GIL is released
+// while waiting); receives are device copies on the receiver's stream after
+// the sender's "posted" event, and a sender's stream continues only after its
+// receivers' "copied" events.  Every event is recorded before anyone waits on
+// it, so this exercises the real stream/event ordering of the GPU data plane
+// and StreamLink at N > 1 without RCCL (which needs one GPU per rank).
+struct LoopbackHub {
+  explicit LoopbackHub(int32_t n) : n(n), ops(n), streams(n, nullptr), posted(n, nullptr), copied(n, nullptr) {
+    for (int32_t i = 0; i < n; ++i) {
+      hipEventCreateWithFlags(reinterpret_cast<hipEvent_t*>(&posted[i]), hipEventDisableTiming);
+      hipEventCreateWithFlags(reinterpret_cast<hipEvent_t*>(&copied[i]), hipEventDisableTiming);
+    }
+  }
+  ~LoopbackHub() {
+    for (int32_t i = 0; i < n; ++i) {
+      hipEventDestroy(static_cast<hipEvent_t>(posted[i]));
+      hipEventDestroy(static_cast<hipEvent_t>(copied[i]));
+    }
+  }
+  void barrier() {
+    std::unique_lock<std::mutex> lk(mu);
+    const int64_t gen = generation;
+    if (++arrived == n) {
+      arrived = 0;
+      ++generation;
+      cv.notify_all();
+      return;
+    }
+    if (!cv.wait_for(lk, std::chrono::seconds(120), [&] { return generation != gen; }))
+      throw AkkaError("akka: loopback p2p rendezvous timed out (ranks issued different schedules)");
+  }
+  int32_t n;
+  std::mutex mu;
+  std::condition_variable cv;
+  int32_t arrived = 0;
+  int64_t generation = 0;
+  std::vector<std::vector<P2POp>> ops;
+  std::vector<StreamH> streams;
+  std::vector<EventH> posted, copied;
+  int64_t bytes = 0;
+};
+
+struct PyLoopbackHub {
+  std::shared_ptr<LoopbackHub> hub;
+};
+
+class LoopbackP2P final : public P2P {
+ public:
+  LoopbackP2P(std::shared_ptr<LoopbackHub> hub, int32_t rank) : hub_(std::move(hub)), rank_(rank) {}
+  int32_t rank() const override { return rank_; }
+  int32_t nranks() const override { return hub_->n; }
+  const char* name() const override { return "loopback"; }
+  void group(StreamH stream, const std::vector<P2POp>& ops) override {
+    py::gil_scoped_release nogil;
+    LoopbackHub& h = *hub_;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    check(hipEventRecord(static_cast<hipEvent_t>(h.posted[rank_]), s));
+    {
+      std::lock_guard<std::mutex> lk(h.mu);
+      h.ops[rank_] = ops;
+      h.streams[rank_] = stream;
+    }
+    h.barrier();  // every rank posted this group
+    // my receives: j-th recv from p <-> j-th send from p to me, in this group
+    std::vector<int32_t> taken(h.n, 0);
+    int64_t moved = 0;
+    for (const auto& op : ops) {
+      if (op.send) continue;
+      const auto& pops = h.ops[op.peer];
+      int32_t seen = 0;
+      const P2POp* match = nullptr;
+      for (const auto& q : pops) {
+        if (q.send && q.peer == rank_ && seen++ == taken[op.peer]) {
+          match = &q;
+          break;
+        }
+      }
+      AKKA_CHECK(match, "loopback p2p: recv from " + std::to_string(op.peer) + " has no matching send");
+      AKKA_CHECK(match->bytes == op.bytes, "loopback p2p: size mismatch");
+      ++taken[op.peer];
+      check(hipStreamWaitEvent(s, static_cast<hipEvent_t>(h.posted[op.peer]), 0));
+      if (op.bytes) check(hipMemcpyAsync(op.buf, match->buf, op.bytes, hipMemcpyDeviceToDevice, s));
+      moved += int64_t(op.bytes);
+    }
+    check(hipEventRecord(static_cast<hipEvent_t>(h.copied[rank_]), s));
+    {
+      std::lock_guard<std::mutex> lk(h.mu);
+      h.bytes += moved;
+    }
+    h.barrier();  // every receiver enqueued its copies + recorded `copied`
+    std::vector<bool> seen_peer(h.n, false);
+    for (const auto& op : ops)
+      if (op.send && !seen_peer[op.peer]) {
+        seen_peer[op.peer] = true;
+        check(hipStreamWaitEvent(s, static_cast<hipEvent_t>(h.copied[op.peer]), 0));
+      }
+    h.barrier();  // nobody re-records posted/copied before all waits are enqueued
+  }
+
+ private:
+  static void check(hipError_t e) {
+    if (e != hipSuccess) throw AkkaError(std::string("akka: loopback p2p: ") + hipGetErrorString(e));
+  }
+  std::shared_ptr<LoopbackHub> hub_;
+  int32_t rank_;
+};
+
 class WorkerCore final : public EngineHost {
  public:
   WorkerCore(py::object host, std::string link, int32_t device, std::string dtype, bool deferred, int32_t lag)
@@ -139,6 +252,11 @@ class WorkerCore final : public EngineHost {
   void connect_callback(py::function fn, int32_t rank, int32_t nranks) {
     AKKA_CHECK(dev_ && dev_->is_host() && !deferred_, "callback p2p runs on an immediate host device");
     p2p_ = std::make_unique<PyCallbackP2P>(std::move(fn), rank, nranks);
+    make_stream_link();
+  }
+  void connect_loopback(const PyLoopbackHub& hub, int32_t rank) {
+    AKKA_CHECK(dev_ && !dev_->is_host(), "loopback p2p needs a HIP device");
+    p2p_ = std::make_unique<LoopbackP2P>(hub.hub, rank);
     make_stream_link();
   }
   void connect_local() {  // N == 1: stream link without peers
@@ -286,6 +404,10 @@ PYBIND11_MODULE(_native, m) {
       .def_readonly("count", &OutMsg::count)
       .def_readonly("data", &OutMsg::data);
 
+  py::class_<PyLoopbackHub>(m, "LoopbackHub")
+      .def(py::init([](int32_t n) { return PyLoopbackHub{std::make_shared<LoopbackHub>(n)}; }))
+      .def("bytes_moved", [](const PyLoopbackHub& h) { return h.hub->bytes; });
+
   py::class_<PySimHub>(m, "SimHub")
       .def(py::init([](int32_t n) { return PySimHub{make_sim_hub(n)}; }))
       .def("bytes_moved", [](const PySimHub& h) { return sim_bytes_moved(h.hub); });
@@ -299,6 +421,7 @@ PYBIND11_MODULE(_native, m) {
       .def("connect_sim", &WorkerCore::connect_sim)
       .def("connect_local", &WorkerCore::connect_local)
       .def("connect_callback", &WorkerCore::connect_callback)
+      .def("connect_loopback", &WorkerCore::connect_loopback)
       .def("attach", &WorkerCore::attach)
       .def("start", &WorkerCore::start)
       .def("scatter_in", &WorkerCore::scatter_in)
