@@ -52,6 +52,9 @@ class Device {
 
   virtual StreamH comm_stream() = 0;
   virtual StreamH compute_stream() = 0;
+  // Extra streams (per-peer streams of the reactive transport).
+  virtual StreamH create_stream() = 0;
+  virtual void destroy_stream(StreamH s) = 0;
 
   virtual EventH create_event() = 0;
   virtual void destroy_event(EventH e) = 0;

@@ -8,6 +8,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <deque>
+#include <map>
 
 #include "device.h"
 
@@ -65,9 +66,20 @@ std::vector<ReduceSpec> split_reduce(void* dst, const std::vector<const void*>& 
 
 namespace {
 
+// Host event: record() bumps `recorded` at enqueue time and the stream op sets
+// `completed` when it runs; wait() captures the target generation at enqueue
+// time (CUDA/HIP semantics: a wait refers to the most recent record).
+struct HostEvent {
+  int64_t recorded = 0;
+  int64_t completed = 0;
+};
+
 class HostDevice final : public Device {
  public:
-  explicit HostDevice(bool deferred) : deferred_(deferred) {}
+  explicit HostDevice(bool deferred) : deferred_(deferred) {
+    queues_[reinterpret_cast<StreamH>(1)];
+    queues_[reinterpret_cast<StreamH>(2)];
+  }
   ~HostDevice() override = default;
 
   bool is_host() const override { return true; }
@@ -82,92 +94,130 @@ class HostDevice final : public Device {
 
   StreamH comm_stream() override { return reinterpret_cast<StreamH>(1); }
   StreamH compute_stream() override { return reinterpret_cast<StreamH>(2); }
-
-  // One in-order queue: events carry no information beyond program order.
-  EventH create_event() override { return reinterpret_cast<EventH>(new int(0)); }
-  void destroy_event(EventH e) override { delete reinterpret_cast<int*>(e); }
-  void record(EventH, StreamH) override {}
-  void wait(StreamH, EventH) override {}
-  bool query(EventH) override { return !deferred_ || queue_.empty(); }
-  void sync_event(EventH) override {
-    if (!deferred_) return;
-    step();  // best effort: a simulated rank cannot block on its peers
+  StreamH create_stream() override {
+    StreamH s = reinterpret_cast<StreamH>(next_stream_++);
+    queues_[s];
+    return s;
   }
-  void sync_stream(StreamH) override { drain_or_throw(); }
+  void destroy_stream(StreamH s) override { queues_.erase(s); }
 
-  void reduce(StreamH, const ReduceSpec* specs, int32_t n, DType dt) override {
-    std::vector<ReduceSpec> v(specs, specs + n);
-    run([v, dt]() {
-      for (const auto& s : v) host_reduce(s, dt);
+  EventH create_event() override { return new HostEvent(); }
+  void destroy_event(EventH e) override { delete static_cast<HostEvent*>(e); }
+  void record(EventH e, StreamH s) override {
+    auto* ev = static_cast<HostEvent*>(e);
+    const int64_t gen = ++ev->recorded;
+    run(s, [ev, gen]() {
+      if (ev->completed < gen) ev->completed = gen;
       return true;
     });
   }
-  void copy(StreamH, void* dst, const void* src, size_t bytes, CopyKind kind) override {
+  void wait(StreamH s, EventH e) override {
+    auto* ev = static_cast<HostEvent*>(e);
+    const int64_t target = ev->recorded;
+    if (ev->completed >= target) return;
+    run(s, [ev, target]() { return ev->completed >= target; });
+  }
+  bool query(EventH e) override {
+    auto* ev = static_cast<HostEvent*>(e);
+    return ev->completed >= ev->recorded;
+  }
+  void sync_event(EventH e) override {
+    if (!deferred_) return;
+    auto* ev = static_cast<HostEvent*>(e);
+    while (ev->completed < ev->recorded && step()) {
+    }  // best effort: a simulated rank cannot block on its peers
+  }
+  void sync_stream(StreamH s) override {
+    if (!deferred_) return;
+    while (!queue_of(s).empty() && step()) {
+    }
+    AKKA_CHECK(queue_of(s).empty(),
+               "host device sync would block: the simulated stream waits on a peer (drive the simulator instead)");
+  }
+
+  void reduce(StreamH s, const ReduceSpec* specs, int32_t n, DType dt) override {
+    std::vector<ReduceSpec> v(specs, specs + n);
+    run(s, [v, dt]() {
+      for (const auto& sp : v) {
+        host_reduce(sp, dt);
+        if (sp.fill)
+          for (int32_t i = 0; i < sp.fill_n; ++i) sp.fill[i] = sp.fill_value;
+      }
+      return true;
+    });
+  }
+  void copy(StreamH s, void* dst, const void* src, size_t bytes, CopyKind kind) override {
     if (dst == src || bytes == 0) return;
     if (deferred_ && kind == CopyKind::HostToDevice) {
       // Host->device copies read their (pinned / message-owned) source when
       // issued; snapshot it so the deferred queue models that contract.
       auto snap = std::make_shared<std::vector<char>>(static_cast<const char*>(src),
                                                       static_cast<const char*>(src) + bytes);
-      run([=]() {
+      run(s, [=]() {
         std::memcpy(dst, snap->data(), bytes);
         return true;
       });
       return;
     }
-    run([=]() {
+    run(s, [=]() {
       std::memmove(dst, src, bytes);
       return true;
     });
   }
-  void zero(StreamH, void* dst, size_t bytes) override {
-    run([=]() {
+  void zero(StreamH s, void* dst, size_t bytes) override {
+    run(s, [=]() {
       std::memset(dst, 0, bytes);
       return true;
     });
   }
-  void fill_i32(StreamH, int32_t* dst, int32_t value, size_t n) override {
-    run([=]() {
+  void fill_i32(StreamH s, int32_t* dst, int32_t value, size_t n) override {
+    run(s, [=]() {
       for (size_t i = 0; i < n; ++i) dst[i] = value;
       return true;
     });
   }
-  void enqueue_host_op(StreamH, std::function<bool()> op) override {
+  void enqueue_host_op(StreamH s, std::function<bool()> op) override {
     AKKA_CHECK(deferred_, "enqueue_host_op requires a deferred host device");
-    queue_.push_back(std::move(op));
+    queue_of(s).push_back(std::move(op));
   }
 
-  // Simulator hooks.
-  bool deferred() const { return deferred_; }
-  // Run queue head ops until one blocks; returns true if any progress was made.
-  bool step() {
+  // Simulator hooks.  step(): run every stream's head ops until each blocks;
+  // `rotate` changes which stream goes first (schedule fuzzing).
+  bool step(uint32_t rotate = 0) {
     bool progress = false;
-    while (!queue_.empty()) {
-      if (!queue_.front()()) break;
-      queue_.pop_front();
-      progress = true;
+    const size_t n = queues_.size();
+    std::vector<std::deque<std::function<bool()>>*> qs;
+    qs.reserve(n);
+    for (auto& kv : queues_) qs.push_back(&kv.second);
+    for (size_t i = 0; i < n; ++i) {
+      auto& q = *qs[(i + rotate) % n];
+      while (!q.empty()) {
+        if (!q.front()()) break;
+        q.pop_front();
+        progress = true;
+      }
     }
     return progress;
   }
-  bool idle() const { return queue_.empty(); }
+  bool idle() const {
+    for (const auto& kv : queues_)
+      if (!kv.second.empty()) return false;
+    return true;
+  }
 
  private:
-  void run(std::function<bool()> f) {
+  std::deque<std::function<bool()>>& queue_of(StreamH s) { return queues_[s]; }
+  void run(StreamH s, std::function<bool()> f) {
     if (deferred_) {
-      queue_.push_back(std::move(f));
+      queue_of(s).push_back(std::move(f));
     } else {
       f();
     }
   }
-  void drain_or_throw() {
-    if (!deferred_) return;
-    step();
-    AKKA_CHECK(queue_.empty(),
-               "host device sync would block: the simulated stream waits on a peer (drive the simulator instead)");
-  }
 
   bool deferred_;
-  std::deque<std::function<bool()>> queue_;
+  std::map<StreamH, std::deque<std::function<bool()>>> queues_;
+  uintptr_t next_stream_ = 16;
 };
 
 }  // namespace
@@ -175,7 +225,7 @@ class HostDevice final : public Device {
 std::unique_ptr<Device> make_host_device(bool deferred) { return std::make_unique<HostDevice>(deferred); }
 
 // Exposed to sim_p2p.cpp.
-bool host_device_step(Device* d) { return static_cast<HostDevice*>(d)->step(); }
+bool host_device_step(Device* d, uint32_t rotate) { return static_cast<HostDevice*>(d)->step(rotate); }
 bool host_device_idle(Device* d) { return static_cast<HostDevice*>(d)->idle(); }
 
 }  // namespace akka

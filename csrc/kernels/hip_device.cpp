@@ -65,6 +65,19 @@ class HipDevice final : public Device {
 
   StreamH comm_stream() override { return comm_; }
   StreamH compute_stream() override { return compute_; }
+  StreamH create_stream() override {
+    int lo = 0, hi = 0;
+    AKKA_HIP(hipSetDevice(dev_));
+    AKKA_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    hipStream_t s;
+    AKKA_HIP(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, hi));
+    return s;
+  }
+  void destroy_stream(StreamH s) override {
+    flush_if(s);
+    hipStreamSynchronize(static_cast<hipStream_t>(s));
+    hipStreamDestroy(static_cast<hipStream_t>(s));
+  }
 
   EventH create_event() override {
     hipEvent_t e;

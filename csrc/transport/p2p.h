@@ -43,6 +43,9 @@ std::unique_ptr<P2P> make_sim_p2p(std::shared_ptr<SimHub> hub, int32_t rank, Dev
 // diagnostic if no rank can make progress (a schedule deadlock).
 void sim_run(const std::shared_ptr<SimHub>& hub, const std::vector<Device*>& devices, int64_t max_iters);
 int64_t sim_bytes_moved(const std::shared_ptr<SimHub>& hub);
+int64_t sim_events(const std::shared_ptr<SimHub>& hub);
+// Step every stream of the given (deferred host) devices once; returns progress.
+bool sim_step(const std::shared_ptr<SimHub>& hub, const std::vector<Device*>& devices, uint32_t rotate);
 
 // ---- RCCL ---------------------------------------------------------------------
 std::vector<uint8_t> rccl_unique_id();

@@ -10,7 +10,7 @@
 
 namespace akka {
 
-bool host_device_step(Device* d);
+bool host_device_step(Device* d, uint32_t rotate);
 bool host_device_idle(Device* d);
 
 struct SimSend {
@@ -32,6 +32,7 @@ class SimHub {
 
 std::shared_ptr<SimHub> make_sim_hub(int32_t nranks) { return std::make_shared<SimHub>(nranks); }
 int64_t sim_bytes_moved(const std::shared_ptr<SimHub>& hub) { return hub->bytes; }
+int64_t sim_events(const std::shared_ptr<SimHub>& hub) { return hub->events; }
 
 namespace {
 
@@ -123,12 +124,19 @@ std::unique_ptr<P2P> make_sim_p2p(std::shared_ptr<SimHub> hub, int32_t rank, Dev
   return std::make_unique<SimP2P>(std::move(hub), rank, dev);
 }
 
+bool sim_step(const std::shared_ptr<SimHub>& hub, const std::vector<Device*>& devices, uint32_t rotate) {
+  const int64_t ev0 = hub->events;
+  bool progress = false;
+  for (Device* d : devices) progress |= host_device_step(d, rotate);
+  return progress || hub->events != ev0;
+}
+
 void sim_run(const std::shared_ptr<SimHub>& hub, const std::vector<Device*>& devices, int64_t max_iters) {
   for (int64_t it = 0; it < max_iters; ++it) {
     bool progress = false, idle = true;
     const int64_t ev0 = hub->events;
     for (Device* d : devices) {
-      progress |= host_device_step(d);
+      progress |= host_device_step(d, uint32_t(it));
       idle &= host_device_idle(d);
     }
     if (idle) return;
