@@ -29,6 +29,7 @@ HOST_SOURCES = [
     "engine/engine.cpp",
     "transport/sim_p2p.cpp",
     "transport/stream_link.cpp",
+    "transport/reactive_link.cpp",
     "transport/rccl_p2p.cpp",
     "kernels/hip_device.cpp",
     "bindings/bindings.cpp",

@@ -49,3 +49,86 @@ class SimCluster:
 
     def bytes_moved(self) -> int:
         return self.hub.bytes_moved()
+
+
+class ReactiveSimCluster:
+    """N ranks on the reactive (straggler-tolerant) transport, on the CPU.
+
+    Same production code as on MI355X -- ReactiveLink with one stream per peer,
+    per-pair grouped p2p, event-polled arrivals, staged data plane -- over the
+    p2p simulator.  The driver decides which ranks' streams advance and when
+    each rank's host polls, so stragglers, frozen ranks and arbitrary stream
+    interleavings are reproducible.
+    """
+
+    def __init__(self, n: int, data_size: int, max_chunk_size: int, *, dtype: torch.dtype = torch.float32,
+                 th_reduce: float = 1.0, th_complete: float = 1.0, max_lag: int = 1, seed: int = 0):
+        import random
+
+        nat = _load()
+        self._nat = nat
+        self.n = n
+        self.hub = nat.SimHub(n)
+        self.rng = random.Random(seed)
+        self.workers: List[AllreduceWorker] = [
+            AllreduceWorker(None, None, device="cpu", dtype=dtype, transport="reactive",
+                            transport_spec=("sim", self.hub, r), strict=True, name=f"rsim{r}")
+            for r in range(n)
+        ]
+        for r, w in enumerate(self.workers):
+            peers = {i: (w if i == r else _RemoteRank(i)) for i in range(n)}
+            w.tell(InitWorkers(peers, n, None, r, th_reduce, th_complete, max_lag, data_size, max_chunk_size))
+        self.outputs: List[dict] = [dict() for _ in range(n)]
+
+    def start(self, rank: int, x: torch.Tensor) -> None:
+        """Rank ``rank`` starts its next round with contribution ``x``."""
+        self.workers[rank].allreduce(x)
+        self._collect(rank)
+
+    def _collect(self, rank: int) -> None:
+        w = self.workers[rank]
+        for r in list(w._outputs):
+            self.outputs[rank][r] = w._outputs.pop(r)
+
+    def step(self, active: Sequence[int] = None, shuffle: bool = False) -> bool:
+        """Advance the streams of the ``active`` ranks once, then let them poll."""
+        active = list(range(self.n)) if active is None else list(active)
+        if shuffle:
+            self.rng.shuffle(active)
+        rot = self.rng.randrange(1 << 16) if shuffle else 0
+        moved = bool(self._nat.sim_step(self.hub, [self.workers[r]._core for r in active], rot))
+        for r in active:
+            moved |= self.workers[r].poll()
+            self._collect(r)
+        return moved
+
+    def run(self, until, active: Sequence[int] = None, shuffle: bool = False, max_idle: int = 50,
+            max_steps: int = 1_000_000) -> None:
+        """Step until ``until()`` holds; raise if nothing moves for ``max_idle`` steps."""
+        idle = 0
+        for _ in range(max_steps):
+            if until():
+                return
+            if self.step(active, shuffle):
+                idle = 0
+            else:
+                idle += 1
+                if idle > max_idle:
+                    raise RuntimeError("reactive sim: no progress (deadlock) -- "
+                                       + "; ".join(f"rank {r}: in_flight={w._core.in_flight()} round={w.round}"
+                                                   for r, w in enumerate(self.workers)))
+        raise RuntimeError("reactive sim: step budget exhausted")
+
+    def done(self, rank: int, round_: int) -> bool:
+        return round_ in self.outputs[rank]
+
+    def drain(self, active: Sequence[int] = None) -> None:
+        """Run until every in-flight transfer of the active ranks finished."""
+        ranks = list(range(self.n)) if active is None else list(active)
+        self.run(lambda: all(self.workers[r]._core.in_flight() == 0 for r in ranks), active)
+
+    def settle(self, active: Sequence[int] = None) -> None:
+        """Run the active ranks' streams until nothing moves (outputs are then readable)."""
+        quiet = 0
+        while quiet < 3:
+            quiet = 0 if self.step(active) else quiet + 1

@@ -110,6 +110,8 @@ class AllreduceWorker:
         self._async = False
         self._ext_streams = None
         self._out_override: Dict[int, torch.Tensor] = {}
+        self._delivered: set = set()
+        self._core_reactive = transport == "reactive"
 
     # ------------------------------------------------------------------ actor API
     def tell(self, msg: Any, sender: Any = None) -> None:
@@ -165,7 +167,8 @@ class AllreduceWorker:
         # a reference to this worker itself (or a local wrapper of it) short-circuits (W:228)
         peers = [(int(i), ref is self or getattr(ref, "actor", None) is self) for i, ref in m.workers.items()]
         tinfo = getattr(m, "transport", None)
-        if tinfo and tinfo.get("kind") == "rccl" and self.transport == "stream" and self.transport_spec is None:
+        if tinfo and tinfo.get("kind") == "rccl" and self.transport in ("stream", "reactive") \
+                and self.transport_spec is None:
             self.transport_spec = ("rccl", tinfo["uid"], int(m.destId), int(m.workerNum))
         first = self._core.init(int(m.destId), int(m.workerNum), float(m.thReduce), float(m.thComplete),
                                 int(m.maxLag), int(m.dataSize), int(m.maxChunkSize), peers)
@@ -186,7 +189,7 @@ class AllreduceWorker:
             self._dispatch(p)
 
     def _connect_transport(self) -> None:
-        if self.transport != "stream":
+        if self.transport not in ("stream", "reactive"):
             return
         spec = self.transport_spec or (("local",) if self.geometry.workerNum == 1 else None)
         if spec is None:
@@ -269,7 +272,47 @@ class AllreduceWorker:
         finally:
             self._stream_cache = None
             self._async = False
+        if self._core.reactive() and r not in self._outputs and not self._core_is_sim():
+            self.progress_until(r)
         return self._outputs.pop(r, None)
+
+    # ------------------------------------------------------------------ reactive transport progress
+    def _core_is_sim(self) -> bool:
+        return bool(self.transport_spec and self.transport_spec[0] == "sim")
+
+    def poll(self) -> bool:
+        """Reactive transport: hand completed transfers to the engine (which may
+        reduce, complete and deliver rounds).  Returns True on progress."""
+        self._in_call += 1
+        try:
+            return bool(self._core.poll())
+        except Exception as e:
+            self.errors.append(e)
+            if self.strict:
+                raise
+            log.error("%s: error in poll: %s", self.name, e)
+            return False
+        finally:
+            self._in_call -= 1
+            if self._in_call == 0:
+                self._flush_outbox()
+                self._release_pending()
+
+    def progress_until(self, round_: int, timeout: Optional[float] = None) -> None:
+        """Poll until ``round_`` completed locally (threshold reached) or timeout."""
+        import time as _time
+        deadline = None if timeout is None else _time.monotonic() + timeout
+        spins = 0
+        while round_ not in self._delivered:
+            if not self.poll():
+                spins += 1
+                if spins > 64:
+                    _time.sleep(0)  # yield the GIL to other ranks' threads
+                if deadline is not None and _time.monotonic() > deadline:
+                    raise TimeoutError(f"{self.name}: round {round_} did not complete within {timeout}s")
+            else:
+                spins = 0
+        self._delivered.discard(round_)
 
     def _internal_streams(self):
         if self._ext_streams is None:
@@ -307,7 +350,9 @@ class AllreduceWorker:
         t = t.reshape(-1).to(device=self.device, dtype=self.dtype).contiguous()
         rec = self._rounds.setdefault(round_, {})
         rec["input"] = t
-        if self._async:
+        if self._async or (self.transport == "reactive" and self.device.type == "cuda"):
+            # async hand-off, or the reactive transport's staging copy (compute
+            # stream) may still read the tensor after this call returns
             self._keep_alive_on_internal_streams(t)
         self._core.bind_input(round_, t.data_ptr(), self._stream_ptr(), self.device.type == "cuda")
 
@@ -345,6 +390,10 @@ class AllreduceWorker:
                               expander=self._expand_counts if self.device.type == "cuda" else None,
                               event=event)
         self._to_release.append(round_)
+        if self._core_reactive:
+            self._delivered.add(round_)
+            if len(self._delivered) > 4096:  # rounds nobody waited for
+                self._delivered.discard(min(self._delivered))
         if self.dataSink is not None:
             self.dataSink(out)
         else:

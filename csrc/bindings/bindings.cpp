@@ -17,6 +17,7 @@
 #include "../engine/engine.h"
 #include "../kernels/kernels.h"
 #include "../transport/p2p.h"
+#include "../transport/reactive_link.h"
 #include "../transport/stream_link.h"
 
 namespace py = pybind11;
@@ -200,12 +201,14 @@ class WorkerCore final : public EngineHost {
     if (dtype == "float32" || dtype == "f32" || dtype == "fp32") dt_ = DType::F32;
     else if (dtype == "bfloat16" || dtype == "bf16") dt_ = DType::BF16;
     else throw AkkaError("akka: unsupported dtype " + dtype);
-    AKKA_CHECK(link_kind_ == "outbox" || link_kind_ == "stream", "link must be 'outbox' or 'stream'");
+    AKKA_CHECK(link_kind_ == "outbox" || link_kind_ == "stream" || link_kind_ == "reactive",
+               "link must be 'outbox', 'stream' or 'reactive'");
     engine_ = std::make_unique<Engine>(this, nullptr);
   }
   ~WorkerCore() override {
     // Order: link and data plane reference the device and the engine.
     stream_link_.reset();
+    reactive_link_.reset();
     dp_.reset();
     p2p_.reset();
     dev_.reset();
@@ -241,13 +244,19 @@ class WorkerCore final : public EngineHost {
     std::string s = uid;
     std::vector<uint8_t> v(s.begin(), s.end());
     AKKA_CHECK(dev_ && !dev_->is_host(), "RCCL transport needs a HIP device");
+    if (link_kind_ == "reactive") {
+      p2p_ = make_rccl_pair_p2p(v, rank, nranks, device_idx_);
+      make_reactive_link();
+      return;
+    }
     p2p_ = make_rccl_p2p(v, rank, nranks, device_idx_);
     make_stream_link();
   }
   void connect_sim(const PySimHub& hub, int32_t rank) {
     AKKA_CHECK(dev_ && dev_->is_host() && deferred_, "sim transport needs a deferred host device");
     p2p_ = make_sim_p2p(hub.hub, rank, dev_.get());
-    make_stream_link();
+    if (link_kind_ == "reactive") make_reactive_link();
+    else make_stream_link();
   }
   void connect_callback(py::function fn, int32_t rank, int32_t nranks) {
     AKKA_CHECK(dev_ && dev_->is_host() && !deferred_, "callback p2p runs on an immediate host device");
@@ -261,15 +270,20 @@ class WorkerCore final : public EngineHost {
   }
   void connect_local() {  // N == 1: stream link without peers
     AKKA_CHECK(engine_->geometry().N == 1, "connect_local is for single-worker jobs");
-    make_stream_link();
+    make_stream_link(/*any_kind=*/true);
   }
   void attach() {
     AKKA_CHECK(dp_, "attach before init");
     if (link_kind_ == "stream") AKKA_CHECK(stream_link_, "stream link not connected");
+    if (link_kind_ == "reactive") AKKA_CHECK(stream_link_ || reactive_link_, "reactive link not connected");
     engine_->attach(dp_.get());
   }
 
   void start(int32_t r) { engine_->start(r); }
+  // Reactive transport: deliver completed transfers to the engine.
+  bool poll() { return reactive_link_ ? reactive_link_->poll() : false; }
+  int32_t in_flight() const { return reactive_link_ ? reactive_link_->in_flight() : 0; }
+  bool reactive() const { return reactive_link_ != nullptr; }
   void scatter_in(int32_t src, int32_t dest, int32_t chunk, int32_t round, uintptr_t ptr, int64_t len, bool on_host) {
     Payload p{reinterpret_cast<const void*>(ptr), len, PayloadKind::External, on_host};
     engine_->on_scatter(src, dest, chunk, round, p);
@@ -353,6 +367,21 @@ class WorkerCore final : public EngineHost {
       ls["lag"] = stream_link_->lag();
       d["link"] = ls;
     }
+    if (reactive_link_) {
+      const auto& rs = reactive_link_->stats();
+      py::dict ls;
+      ls["groups"] = rs.groups;
+      ls["bytes_sent"] = rs.bytes_sent;
+      ls["p1_arrivals"] = rs.p1_arrivals;
+      ls["p2_arrivals"] = rs.p2_arrivals;
+      ls["unreduced_chunks"] = rs.unreduced_chunks;
+      ls["polls"] = rs.polls;
+      ls["reclaim_waits"] = rs.reclaim_waits;
+      ls["slots"] = dp_->slots_allocated();
+      ls["slots_busy"] = dp_->slots_busy();
+      ls["in_flight"] = reactive_link_->in_flight();
+      d["link"] = ls;
+    }
     return d;
   }
   int32_t scatter_count(int32_t round, int32_t chunk) const { return engine_->scatter_count(round, chunk); }
@@ -366,8 +395,14 @@ class WorkerCore final : public EngineHost {
   void release(int32_t round) override { host_.attr("_release")(round); }
 
  private:
-  void make_stream_link() {
-    AKKA_CHECK(link_kind_ == "stream", "worker was not created with link='stream'");
+  void make_reactive_link() {
+    AKKA_CHECK(engine_->geometry().N >= 2, "reactive link needs N >= 2");
+    reactive_link_ = std::make_unique<ReactiveLink>(engine_.get(), p2p_.get());
+    reactive_link_->bind(dp_.get());
+    engine_->set_link(reactive_link_.get());
+  }
+  void make_stream_link(bool any_kind = false) {
+    AKKA_CHECK(any_kind || link_kind_ == "stream", "worker was not created with link='stream'");
     stream_link_ = std::make_unique<StreamLink>(engine_.get(), p2p_.get(), lag_);
     stream_link_->bind(dp_.get());
     engine_->set_link(stream_link_.get());
@@ -383,6 +418,7 @@ class WorkerCore final : public EngineHost {
   std::unique_ptr<DataPlane> dp_;
   std::unique_ptr<P2P> p2p_;
   std::unique_ptr<StreamLink> stream_link_;
+  std::unique_ptr<ReactiveLink> reactive_link_;
   std::unique_ptr<OutboxLink> outbox_;
   std::unique_ptr<Engine> engine_;
 };
@@ -424,6 +460,9 @@ PYBIND11_MODULE(_native, m) {
       .def("connect_loopback", &WorkerCore::connect_loopback)
       .def("attach", &WorkerCore::attach)
       .def("start", &WorkerCore::start)
+      .def("poll", &WorkerCore::poll)
+      .def("in_flight", &WorkerCore::in_flight)
+      .def("reactive", &WorkerCore::reactive)
       .def("scatter_in", &WorkerCore::scatter_in)
       .def("reduce_in", &WorkerCore::reduce_in)
       .def("peer_terminated", &WorkerCore::peer_terminated)
@@ -441,6 +480,11 @@ PYBIND11_MODULE(_native, m) {
       .def("scatter_count", &WorkerCore::scatter_count)
       .def("reduced_arrivals", &WorkerCore::reduced_arrivals);
 
+  m.def("sim_step", [](const PySimHub& hub, std::vector<WorkerCore*> cores, uint32_t rotate) {
+    std::vector<Device*> devs;
+    for (auto* c : cores) devs.push_back(c->device());
+    return sim_step(hub.hub, devs, rotate);
+  }, py::arg("hub"), py::arg("cores"), py::arg("rotate") = 0);
   m.def("sim_run", [](const PySimHub& hub, std::vector<WorkerCore*> cores, int64_t max_iters) {
     std::vector<Device*> devs;
     for (auto* c : cores) devs.push_back(c->device());

@@ -38,6 +38,94 @@ DataPlane::~DataPlane() {
   for (EventH e : events_) dev_->destroy_event(e);  // includes every binding/spare event
   dev_->release(scatter_ring_);
   dev_->release_pinned(staging_);
+  for (auto& sl : slots_) {
+    dev_->release(sl.input);
+    dev_->release(sl.mine);
+    dev_->release(sl.wire);
+    dev_->release_pinned(sl.wire_h);
+  }
+  for (int32_t* p : retired_pinned_) dev_->release_pinned(p);
+  if (land_ring_) dev_->release(land_ring_);
+}
+
+void DataPlane::enable_staging(int32_t max_slots, std::function<bool(int32_t)> reclaim) {
+  AKKA_CHECK(!staging_on_, "staging already enabled");
+  AKKA_CHECK(max_slots >= L_ + 1, "send slot pool must exceed the ring depth");
+  land_ring_ = dev_->alloc(size_t(L_) * size_t(std::max<int64_t>(g_.S, 1)) * esize());
+  max_slots_ = max_slots;
+  reclaim_ = std::move(reclaim);
+  staging_on_ = true;
+}
+
+int32_t DataPlane::slots_busy() const { return int32_t(slot_of_.size()); }
+
+DataPlane::SendSlot& DataPlane::slot(int32_t round) {
+  AKKA_CHECK(staging_on_, "send slots need staged mode");
+  auto it = slot_of_.find(round);
+  if (it != slot_of_.end()) return slots_[it->second];
+  size_t idx = slots_.size();
+  for (size_t i = 0; i < slots_.size(); ++i)
+    if (slots_[i].round < 0) {
+      idx = i;
+      break;
+    }
+  if (idx == slots_.size()) {
+    if (int32_t(slots_.size()) < max_slots_) {
+      SendSlot s;
+      s.input = dev_->alloc(size_t(std::max<int64_t>(g_.S, 1)) * esize());
+      s.mine = dev_->alloc(size_t(std::max<int64_t>(my_len_, 1)) * esize());
+      s.wire = static_cast<int32_t*>(dev_->alloc(size_t(kmax_) * sizeof(int32_t)));
+      s.wire_h = static_cast<int32_t*>(dev_->alloc_pinned(size_t(kmax_) * sizeof(int32_t)));
+      slots_.push_back(s);
+    } else {
+      // Pool exhausted (a peer is far behind): reclaim the oldest slot whose
+      // round is over by making the compute stream wait for its transfers.
+      int32_t victim = -1;
+      for (auto& kv : slot_of_) {
+        const Binding* b = nullptr;
+        auto bi = bind_.find(kv.first);
+        if (bi != bind_.end()) b = &bi->second;
+        if (kv.first < round && (!b || b->finalized) && reclaim_(kv.first)) {
+          victim = kv.first;
+          break;
+        }
+      }
+      AKKA_CHECK(victim >= 0, "send slot pool exhausted with no finished round to reclaim");
+      idx = slot_of_[victim];
+      slot_of_.erase(victim);
+      // Its wire upload may not have executed yet: never rewrite that pinned row.
+      retired_pinned_.push_back(slots_[idx].wire_h);
+      slots_[idx].wire_h = static_cast<int32_t*>(dev_->alloc_pinned(size_t(kmax_) * sizeof(int32_t)));
+    }
+  }
+  SendSlot& s = slots_[idx];
+  s.round = round;
+  slot_of_[round] = idx;
+  return s;
+}
+
+void DataPlane::release_slot(int32_t round) {
+  auto it = slot_of_.find(round);
+  if (it == slot_of_.end()) return;
+  slots_[it->second].round = -1;
+  slot_of_.erase(it);
+}
+
+const void* DataPlane::staged_input(int32_t round, int32_t block) {
+  return static_cast<const char*>(slot(round).input) + size_t(g_.block_start(block)) * esize();
+}
+
+void* DataPlane::mine_at(int32_t round, int32_t k) {
+  return static_cast<char*>(slot(round).mine) + size_t(k) * size_t(g_.C) * esize();
+}
+
+int32_t* DataPlane::wire_dev(int32_t round) { return slot(round).wire; }
+int32_t* DataPlane::wire_host(int32_t round) { return slot(round).wire_h; }
+
+void* DataPlane::landing_at(int32_t round, int32_t block, int32_t k) const {
+  AKKA_CHECK(staging_on_, "landing_at: staging is off");
+  size_t off = size_t(round % L_) * size_t(std::max<int64_t>(g_.S, 1)) + size_t(g_.chunk_offset(block, k));
+  return static_cast<char*>(land_ring_) + off * esize();
 }
 
 EventH DataPlane::pooled_event() {
@@ -102,6 +190,24 @@ void DataPlane::bind_input(int32_t round, const void* input, StreamH ready_strea
   Binding& b = bind_[round];
   b.input = input;
   b.input_waited_compute = b.input_waited_comm = false;
+  if (staging_on_) {
+    // Stage the input on the compute stream; afterwards nothing reads the
+    // caller's tensor, so every consumer is ordered by the compute stream.
+    const StreamH cs = dev_->compute_stream();
+    if (has_stream && !dev_->is_host()) {
+      if (!b.input_ready) b.input_ready = binding_event();
+      dev_->record(b.input_ready, ready_stream);
+      dev_->wait(cs, b.input_ready);
+    }
+    void* dst = const_cast<void*>(staged_input(round, 0));
+    // HostToDevice on the host device: the simulator snapshots the source at
+    // issue, like a stream-ordered copy whose source the caller may then free.
+    dev_->copy(cs, dst, input, size_t(g_.S) * esize(),
+               dev_->is_host() ? CopyKind::HostToDevice : CopyKind::DeviceToDevice);
+    b.input = dst;
+    b.input_waited_compute = b.input_waited_comm = true;
+    return;
+  }
   if (has_stream && !dev_->is_host()) {
     if (g_.N == 1) {
       // A purely local round (no peers, no comm stream) runs its reduce on the
@@ -190,7 +296,8 @@ Payload DataPlane::input_chunk(int32_t round, int32_t block, int32_t k) const {
 
 Payload DataPlane::output_chunk(int32_t round, int32_t block, int32_t k) const {
   Payload p;
-  p.ptr = output_at(round, block, k);
+  p.ptr = !staging_on_ ? output_at(round, block, k)
+          : block == me_ ? const_cast<DataPlane*>(this)->mine_at(round, k) : landing_at(round, block, k);
   p.len = g_.chunk_len(block, k);
   p.kind = PayloadKind::ReducedView;
   p.on_host = dev_->is_host();
@@ -239,7 +346,7 @@ Payload DataPlane::reduce(int32_t round, int32_t k, const std::vector<int32_t>& 
   Row& r = row_for(round);
   Binding& b = binding_mut(round);
   int64_t n = g_.chunk_len(me_, k);
-  void* dst = output_at(round, me_, k);
+  void* dst = staging_on_ ? mine_at(round, k) : output_at(round, me_, k);
   std::vector<const void*> ptrs;
   ptrs.reserve(srcs.size());
   const StreamH cs = exec_stream(round);
@@ -266,7 +373,7 @@ void DataPlane::store_reduced(int32_t round, int32_t src, int32_t k, const Paylo
   int64_t want = g_.chunk_len(src, k);
   AKKA_CHECK(p.len <= want, "reduced payload overruns chunk");
   if (p.kind == PayloadKind::Landed) return;
-  void* dst = output_at(round, src, k);
+  void* dst = !staging_on_ ? output_at(round, src, k) : src == me_ ? mine_at(round, k) : landing_at(round, src, k);
   if (p.ptr == dst) return;
   CopyKind ck = p.on_host ? CopyKind::HostToDevice : CopyKind::DeviceToDevice;
   dev_->copy(exec_stream(round), dst, p.ptr, size_t(p.len) * esize(), ck);
@@ -308,6 +415,34 @@ void DataPlane::finalize(int32_t round, const std::vector<uint8_t>& landed) {
   if (b.comm_used) {
     EventH ce = record_comm();
     dev_->wait(cs, ce);
+  }
+  if (staging_on_) {
+    // Copy landed chunks (landing row / my send slot) -> output, coalescing
+    // runs of consecutive landed chunks within a block.
+    int64_t run0 = -1, run1 = -1;
+    const char* base = nullptr;  // source address of element run0
+    auto flush = [&]() {
+      if (run0 < 0) return;
+      dev_->copy(cs, static_cast<char*>(b.output) + size_t(run0) * esize(), base, size_t(run1 - run0) * esize(),
+                 dev_->is_host() ? CopyKind::HostToHost : CopyKind::DeviceToDevice);
+      run0 = run1 = -1;
+    };
+    for (int32_t j = 0; j < g_.N; ++j, flush())
+      for (int32_t k = 0; k < g_.num_chunks(j); ++k) {
+        if (!landed[size_t(j) * kmax_ + k]) {
+          flush();
+          continue;
+        }
+        int64_t o = g_.chunk_offset(j, k), e = o + g_.chunk_len(j, k);
+        if (run0 >= 0 && run1 == o) run1 = e;
+        else {
+          flush();
+          run0 = o;
+          run1 = e;
+          base = static_cast<const char*>(j == me_ ? mine_at(round, k) : landing_at(round, j, k));
+        }
+      }
+    flush();
   }
   for (int32_t j = 0; j < g_.N; ++j) {
     int32_t kj = g_.num_chunks(j);

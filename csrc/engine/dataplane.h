@@ -19,6 +19,7 @@
 // the data plane only owns memory, streams and kernels.
 #pragma once
 
+#include <functional>
 #include <map>
 #include <memory>
 #include <vector>
@@ -98,6 +99,33 @@ class DataPlane {
   // Event after the last compute op that reads ring row of `round`.
   EventH row_release_event(int32_t round);
 
+  // --- staged mode (reactive transport) ------------------------------------
+  // With per-peer streams a round can complete while some of its sends and
+  // receives are still in flight (the threshold semantics: a straggler's
+  // transfers finish later).  So nothing in flight may touch memory the
+  // caller owns:
+  //  * send side -- a per-round *send slot* from a pool: the staged input
+  //    (copied at bind time), my reduced block, my wire counts.  A slot stays
+  //    busy until its round completed and all its transfers finished; while a
+  //    peer is frozen the pool grows (up to `max_slots`), so fast ranks keep
+  //    going for that many rounds before the oldest slot must be reclaimed by
+  //    waiting (`reclaim(round)`: the link makes the compute stream wait for
+  //    that round's outstanding transfers).
+  //  * receive side -- peers' reduced blocks land in a ring row (receives on a
+  //    pair stream are ordered, so ring reuse is safe); finalize() copies the
+  //    landed chunks into the user's output.
+  void enable_staging(int32_t max_slots, std::function<bool(int32_t)> reclaim);
+  bool staging() const { return staging_on_; }
+  const void* staged_input(int32_t round, int32_t block);
+  void* mine_at(int32_t round, int32_t k);
+  int32_t* wire_dev(int32_t round);
+  int32_t* wire_host(int32_t round);
+  void* landing_at(int32_t round, int32_t block, int32_t k) const;
+  // The link is done with the round's send slot (completed + transfers done).
+  void release_slot(int32_t round);
+  int32_t slots_allocated() const { return int32_t(slots_.size()); }
+  int32_t slots_busy() const;
+
  private:
   struct Binding {
     const void* input = nullptr;
@@ -141,6 +169,22 @@ class DataPlane {
   std::vector<EventH> events_;     // all events created (destroyed at teardown)
   std::vector<EventH> free_events_;
   std::vector<EventH> spare_events_;  // recycled per-round (input_ready / done) events
+  // staged mode
+  struct SendSlot {
+    int32_t round = -1;
+    void* input = nullptr;      // [S]
+    void* mine = nullptr;       // [my block]
+    int32_t* wire = nullptr;    // device [kmax]
+    int32_t* wire_h = nullptr;  // pinned [kmax]
+  };
+  SendSlot& slot(int32_t round);
+  bool staging_on_ = false;
+  int32_t max_slots_ = 0;
+  std::vector<SendSlot> slots_;
+  std::map<int32_t, size_t> slot_of_;
+  std::vector<int32_t*> retired_pinned_;
+  void* land_ring_ = nullptr;  // [L][S]
+  std::function<bool(int32_t)> reclaim_;
 };
 
 }  // namespace akka

@@ -50,6 +50,9 @@ bool sim_step(const std::shared_ptr<SimHub>& hub, const std::vector<Device*>& de
 // ---- RCCL ---------------------------------------------------------------------
 std::vector<uint8_t> rccl_unique_id();
 std::unique_ptr<P2P> make_rccl_p2p(const std::vector<uint8_t>& uid, int32_t rank, int32_t nranks, int32_t device);
+// Per-pair communicators (reactive transport): a group holds ops to one peer.
+std::unique_ptr<P2P> make_rccl_pair_p2p(const std::vector<uint8_t>& uid, int32_t rank, int32_t nranks,
+                                        int32_t device);
 const char* rccl_version_string();
 
 }  // namespace akka

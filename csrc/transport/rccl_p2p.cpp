@@ -8,6 +8,8 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <algorithm>
+#include <cstring>
 #include <sstream>
 
 #include "p2p.h"
@@ -76,7 +78,72 @@ class RcclP2P final : public P2P {
   ncclComm_t comm_ = nullptr;
 };
 
+// One two-rank communicator per peer pair, split off the global one.  A group
+// may only hold ops to a single peer; it runs on that pair's communicator, so
+// transfers to different peers (issued on different streams) are independent
+// -- a slow peer stalls only its own pair (reactive_link.h).
+class RcclPairP2P final : public P2P {
+ public:
+  RcclPairP2P(const std::vector<uint8_t>& uid, int32_t rank, int32_t nranks, int32_t device)
+      : rank_(rank), n_(nranks), pair_(size_t(nranks), nullptr) {
+    AKKA_CHECK(uid.size() == sizeof(ncclUniqueId), "bad RCCL unique id size");
+    ncclUniqueId id;
+    std::memcpy(&id, uid.data(), sizeof(id));
+    if (hipSetDevice(device) != hipSuccess) throw AkkaError("akka: hipSetDevice failed");
+    AKKA_NCCL(ncclCommInitRank(&global_, nranks, id, rank));
+    // Round-robin tournament (circle method): P-1 rounds of disjoint pairs,
+    // one ncclCommSplit each; with odd N a dummy player sits one rank out.
+    const int32_t P = (nranks % 2) ? nranks + 1 : nranks;
+    for (int32_t t = 0; t + 1 < P; ++t) {
+      int32_t partner;
+      if (rank == P - 1) partner = t;
+      else if (rank == t) partner = P - 1;
+      else partner = ((2 * t - rank) % (P - 1) + (P - 1)) % (P - 1);
+      const bool real = partner < nranks && partner != rank;
+      ncclComm_t c = nullptr;
+      AKKA_NCCL(ncclCommSplit(global_, real ? std::min(rank, partner) : NCCL_SPLIT_NOCOLOR, rank, &c, nullptr));
+      if (real) pair_[size_t(partner)] = c;
+    }
+    for (int32_t p = 0; p < nranks; ++p)
+      AKKA_CHECK(p == rank || pair_[size_t(p)], "pair communicator missing for peer " + std::to_string(p));
+  }
+  ~RcclPairP2P() override {
+    for (ncclComm_t c : pair_)
+      if (c) ncclCommDestroy(c);
+    if (global_) ncclCommDestroy(global_);
+  }
+  int32_t rank() const override { return rank_; }
+  int32_t nranks() const override { return n_; }
+  const char* name() const override { return "rccl-pair"; }
+
+  void group(StreamH stream, const std::vector<P2POp>& ops) override {
+    if (ops.empty()) return;
+    const int32_t peer = ops.front().peer;
+    AKKA_CHECK(peer >= 0 && peer < n_ && peer != rank_, "pair group: bad peer");
+    ncclComm_t c = pair_[size_t(peer)];
+    const int32_t prank = peer < rank_ ? 0 : 1;  // split key = global rank
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    AKKA_NCCL(ncclGroupStart());
+    for (const auto& op : ops) {
+      AKKA_CHECK(op.peer == peer, "pair group holds ops to more than one peer");
+      if (op.send) AKKA_NCCL(ncclSend(op.buf, op.bytes, ncclUint8, prank, c, s));
+      else AKKA_NCCL(ncclRecv(op.buf, op.bytes, ncclUint8, prank, c, s));
+    }
+    AKKA_NCCL(ncclGroupEnd());
+  }
+
+ private:
+  int32_t rank_, n_;
+  ncclComm_t global_ = nullptr;
+  std::vector<ncclComm_t> pair_;
+};
+
 }  // namespace
+
+std::unique_ptr<P2P> make_rccl_pair_p2p(const std::vector<uint8_t>& uid, int32_t rank, int32_t nranks,
+                                        int32_t device) {
+  return std::make_unique<RcclPairP2P>(uid, rank, nranks, device);
+}
 
 std::unique_ptr<P2P> make_rccl_p2p(const std::vector<uint8_t>& uid, int32_t rank, int32_t nranks, int32_t device) {
   return std::make_unique<RcclP2P>(uid, rank, nranks, device);

@@ -1,0 +1,231 @@
+"""The reactive (straggler-tolerant) transport on the CPU p2p simulator.
+
+Same native code as on MI355X (ReactiveLink: one stream per peer, per-pair
+grouped p2p, event-polled arrivals, staged data plane); the simulator decides
+which ranks' streams advance, so frozen ranks, stragglers and arbitrary
+stream interleavings are reproducible.
+
+Inputs are x_i = 2^i * w (w = 1..3 per element), so every output element
+reveals exactly which ranks contributed to it: the contributor mask must have
+popcount == the delivered count (the reference's count semantics, RB:41-47).
+"""
+import random
+
+import pytest
+import torch
+
+from akka_allreduce_amd.data import Geometry
+from akka_allreduce_amd.messages import StartAllreduce
+from akka_allreduce_amd.parallel.sim import ReactiveSimCluster
+
+
+def _w(S):
+    return (torch.arange(S) % 3 + 1).float()
+
+
+def _x(i, S):
+    return _w(S) * float(1 << i)
+
+
+def _check_masks(o, S, n, allowed=None):
+    w = _w(S)
+    mask = (o.data / w).round().long()
+    assert torch.equal(mask.float() * w, o.data), "not a subset sum"
+    pc = torch.zeros_like(mask)
+    for b in range(n):
+        bit = (mask >> b) & 1
+        pc += bit
+        if allowed is not None and b not in allowed:
+            assert int(bit.sum()) == 0, f"rank {b} contributed but should not have"
+    assert torch.equal(pc.int(), o.count), "popcount(contributors) != count"
+    return mask
+
+
+@pytest.mark.parametrize("n", [2, 3, 4, 8])
+@pytest.mark.parametrize("S,C", [(64, 8), (1000, 7), (778, 3), (5, 1), (333, 1000)])
+def test_reactive_exact(n, S, C):
+    cl = ReactiveSimCluster(n, S, C, max_lag=1)
+    for r in range(3):
+        g = torch.Generator().manual_seed(r)
+        xs = [torch.randint(-8, 9, (S,), generator=g).float() for _ in range(n)]
+        for i in range(n):
+            cl.start(i, xs[i])
+        cl.run(lambda: all(cl.done(i, r) for i in range(n)))
+        cl.settle()
+        want = torch.stack(xs).sum(0)
+        for i in range(n):
+            o = cl.outputs[i][r]
+            assert torch.equal(o.data, want), (i, r)
+            assert bool((o.count == n).all())
+    cl.drain()
+    for w in cl.workers:
+        st = w.state()
+        assert st["round"] == 3 and st["link"]["in_flight"] == 0 and st["link"]["slots_busy"] == 0
+
+
+def test_reactive_bf16():
+    n, S, C = 4, 999, 50
+    cl = ReactiveSimCluster(n, S, C, dtype=torch.bfloat16)
+    xs = [torch.randint(-8, 9, (S,)).bfloat16() for _ in range(n)]
+    for i in range(n):
+        cl.start(i, xs[i])
+    cl.run(lambda: all(cl.done(i, 0) for i in range(n)))
+    cl.settle()
+    want = torch.stack([x.float() for x in xs]).sum(0).bfloat16()
+    assert all(torch.equal(cl.outputs[i][0].data, want) for i in range(n))
+
+
+def test_frozen_rank_does_not_stall_the_others():
+    """thReduce = thComplete = 0.75, rank 3 frozen: ranks 0-2 complete every
+    round from their own three contributions (the reference's core promise)."""
+    n, S, C, R = 4, 64, 4, 6
+    cl = ReactiveSimCluster(n, S, C, th_reduce=0.75, th_complete=0.75, max_lag=2)
+    fast = [0, 1, 2]
+    for r in range(R):
+        for i in fast:
+            cl.start(i, _x(i, S))
+        cl.run(lambda: all(cl.done(i, r) for i in fast), active=fast)
+    cl.settle(fast)
+    g = Geometry(S, n, C)
+    s3, e3 = g.block_range(3)
+    for i in fast:
+        for r in range(R):
+            o = cl.outputs[i][r]
+            mask = _check_masks(o, S, n, allowed={0, 1, 2})
+            assert bool((mask[:s3] == 0b111).all())
+            assert bool((o.count[s3:e3] == 0).all())  # rank 3's block never reduced
+    st = cl.workers[0].state()["link"]
+    assert st["slots_busy"] == R  # one pinned send slot per round the frozen peer owes
+    # the straggler wakes up and runs the same rounds: everything drains
+    for r in range(R):
+        cl.start(3, _x(3, S))
+    cl.run(lambda: all(cl.done(3, r) for r in range(R)))
+    cl.settle()
+    for r in range(R):
+        _check_masks(cl.outputs[3][r], S, n)
+    cl.drain()
+    assert all(w.state()["link"]["slots_busy"] == 0 for w in cl.workers)
+    assert all(w.round == R for w in cl.workers)
+
+
+def test_slow_rank_interleaved():
+    """A rank whose streams advance only every 5th step: exact thresholds still
+    give exact results; partial thresholds let the others run ahead."""
+    n, S, C = 4, 200, 16
+    for th in (1.0, 0.75):
+        cl = ReactiveSimCluster(n, S, C, th_reduce=th, th_complete=th, max_lag=3, seed=7)
+        started = [0] * n
+        R = 6
+        tick = 0
+        while not all(cl.done(i, R - 1) for i in range(n)):
+            tick += 1
+            active = [0, 1, 2] + ([3] if tick % 5 == 0 else [])
+            for i in active:
+                # a rank starts its next round once its previous one completed
+                if started[i] < R and (started[i] == 0 or cl.done(i, started[i] - 1)):
+                    cl.start(i, _x(i, S))
+                    started[i] += 1
+            cl.step(active, shuffle=True)
+            assert tick < 20000
+        cl.settle()
+        for i in range(n):
+            for r in range(R):
+                mask = _check_masks(cl.outputs[i][r], S, n)
+                if th == 1.0:
+                    assert bool((mask == 0b1111).all())
+        cl.drain()
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_random_interleavings(seed):
+    """Random stream interleavings and random per-step rank freezes."""
+    rng = random.Random(seed)
+    n = rng.choice([2, 3, 4, 5])
+    S = rng.choice([17, 100, 257])
+    C = rng.choice([1, 4, 9, 64])
+    th = rng.choice([1.0, 0.75, 0.6])
+    cl = ReactiveSimCluster(n, S, C, th_reduce=th, th_complete=th, max_lag=rng.choice([1, 2, 3]), seed=seed)
+    R = 5
+    started = [0] * n
+    steps = 0
+    while not all(cl.done(i, R - 1) for i in range(n)):
+        steps += 1
+        assert steps < 50000, "no progress"
+        active = [i for i in range(n) if rng.random() < 0.7] or [rng.randrange(n)]
+        for i in active:
+            if started[i] < R and (started[i] == 0 or cl.done(i, started[i] - 1)):
+                cl.start(i, _x(i, S))
+                started[i] += 1
+        cl.step(active, shuffle=True)
+    cl.settle()
+    for i in range(n):
+        for r in range(R):
+            mask = _check_masks(cl.outputs[i][r], S, n)
+            if th == 1.0:
+                assert bool((mask == (1 << n) - 1).all())
+    cl.drain()
+
+
+def test_cold_catch_up():
+    """A rank that was frozen receives StartAllreduce far ahead (master
+    pacing): it force-completes the rounds it missed (W:100-106), re-scatters
+    them for slower peers, and the pair streams stay aligned."""
+    n, S, C, lag = 4, 48, 4, 1
+    cl = ReactiveSimCluster(n, S, C, th_reduce=0.75, th_complete=0.75, max_lag=lag)
+    fast = [0, 1, 2]
+    R = 4
+    for r in range(R):
+        for i in fast:
+            cl.start(i, _x(i, S))
+        cl.run(lambda: all(cl.done(i, r) for i in fast), active=fast)
+    w3 = cl.workers[3]
+    for r in range(R):  # inputs for every round it will fetch
+        w3._feed[r] = _x(3, S)
+    w3._next_round = R
+    w3.receive(StartAllreduce(R - 1))
+    cl._collect(3)
+    st = w3.state()["stats"]
+    assert st["rounds_forced"] >= R - 1 - lag
+    cl.run(lambda: all(cl.done(3, r) for r in range(R)))
+    cl.settle()
+    for r in range(R):
+        _check_masks(cl.outputs[3][r], S, n)
+    # afterwards everyone runs full rounds together again
+    for r in range(R, R + 2):
+        for i in range(n):
+            cl.start(i, _x(i, S))
+        cl.run(lambda: all(cl.done(i, r) for i in range(n)))
+    cl.settle()
+    for i in range(n):
+        for r in range(R, R + 2):
+            _check_masks(cl.outputs[i][r], S, n)
+    cl.drain()
+    assert all(w.state()["link"]["slots_busy"] == 0 for w in cl.workers)
+
+
+def test_slot_pool_exhaustion_is_bounded_wait_not_error():
+    """More rounds than send slots while a peer is frozen: the oldest finished
+    round's slot is reclaimed by a stream wait, so the fast ranks stall
+    (bounded staleness) until the frozen rank wakes -- then everything drains."""
+    n, S, C = 3, 30, 5
+    cl = ReactiveSimCluster(n, S, C, th_reduce=0.6, th_complete=0.6, max_lag=1)
+    fast = [0, 1]
+    done_rounds = 0
+    for r in range(40):
+        for i in fast:
+            cl.start(i, _x(i, S))
+        try:
+            cl.run(lambda: all(cl.done(i, r) for i in fast), active=fast, max_idle=20)
+        except RuntimeError:
+            break
+        done_rounds = r + 1
+    slots = cl.workers[0].state()["link"]["slots"]
+    assert done_rounds >= slots - 2, (done_rounds, slots)
+    assert done_rounds < 40
+    # wake rank 2: it catches up, all pending transfers complete
+    for r in range(done_rounds + 1):
+        cl.start(2, _x(2, S))
+    cl.run(lambda: all(cl.done(2, r) for r in range(done_rounds + 1)))
+    cl.run(lambda: all(cl.done(i, done_rounds) for i in fast))
+    cl.settle()
+    cl.drain()
