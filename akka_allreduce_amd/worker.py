@@ -112,6 +112,7 @@ class AllreduceWorker:
         self._out_override: Dict[int, torch.Tensor] = {}
         self._delivered: set = set()
         self._core_reactive = transport == "reactive"
+        self.reactive_timeout: Optional[float] = None  # reactive allreduce(): max seconds to wait
 
     # ------------------------------------------------------------------ actor API
     def tell(self, msg: Any, sender: Any = None) -> None:
@@ -206,6 +207,9 @@ class AllreduceWorker:
         elif kind == "loopback":
             _, hub, rank = spec
             self._core.connect_loopback(hub, int(rank))
+        elif kind == "loopback_pair":
+            _, hub, rank = spec
+            self._core.connect_loopback_pair(hub, int(rank))
         elif kind == "callback":
             _, fn, rank, nranks = spec
             self._core.connect_callback(fn, int(rank), int(nranks))
@@ -273,7 +277,7 @@ class AllreduceWorker:
             self._stream_cache = None
             self._async = False
         if self._core.reactive() and r not in self._outputs and not self._core_is_sim():
-            self.progress_until(r)
+            self.progress_until(r, self.reactive_timeout)
         return self._outputs.pop(r, None)
 
     # ------------------------------------------------------------------ reactive transport progress
@@ -309,7 +313,9 @@ class AllreduceWorker:
                 if spins > 64:
                     _time.sleep(0)  # yield the GIL to other ranks' threads
                 if deadline is not None and _time.monotonic() > deadline:
-                    raise TimeoutError(f"{self.name}: round {round_} did not complete within {timeout}s")
+                    st = self._core.state()
+                    raise TimeoutError(f"{self.name}: round {round_} did not complete within {timeout}s "
+                                       f"(engine round {st['round']}, stats {st['stats']}, link {st.get('link')})")
             else:
                 spins = 0
         self._delivered.discard(round_)
@@ -350,10 +356,12 @@ class AllreduceWorker:
         t = t.reshape(-1).to(device=self.device, dtype=self.dtype).contiguous()
         rec = self._rounds.setdefault(round_, {})
         rec["input"] = t
-        if self._async or (self.transport == "reactive" and self.device.type == "cuda"):
-            # async hand-off, or the reactive transport's staging copy (compute
-            # stream) may still read the tensor after this call returns
+        if self._async:
             self._keep_alive_on_internal_streams(t)
+        # (Synchronous rounds need no record_stream: the caller's stream waits
+        # for the round's done event, which follows every read of the input --
+        # including the reactive transport's staging copy -- and the caching
+        # allocator only reuses the block in that stream's order.)
         self._core.bind_input(round_, t.data_ptr(), self._stream_ptr(), self.device.type == "cuda")
 
     def _alloc_output(self, round_: int) -> None:
@@ -446,6 +454,15 @@ class AllreduceWorker:
             if r in self._rounds:
                 self._core.unbind(r)
                 del self._rounds[r]
+
+    def close(self) -> None:
+        """Release the native core (streams, buffers) now.  Freeing device
+        memory synchronizes the whole GPU, so do it while no stream of this
+        process is parked on a peer (e.g. after the reactive link drained)."""
+        core, self._core = self._core, None
+        self._rounds.clear()
+        self._outputs.clear()
+        del core
 
     def synchronize(self) -> None:
         """Block until all of this worker's queued device work is done."""

@@ -10,8 +10,11 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <algorithm>
 #include <chrono>
 #include <condition_variable>
+#include <cstring>
+#include <deque>
 #include <mutex>
 
 #include "../engine/engine.h"
@@ -194,6 +197,119 @@ class LoopbackP2P final : public P2P {
   int32_t rank_;
 };
 
+// ---------------------------------------------------------------------------
+// Asynchronous per-pair loopback p2p (reactive transport harness): a group
+// holds ops to one peer and never blocks the host.  The first side of a pair
+// to post records a "posted" event and parks its stream on a signal word
+// (hipStreamWaitValue32); the second side, on its own stream, waits for the
+// first side's event, performs both directions' copies and releases the first
+// side with hipStreamWriteValue32.  Groups of a pair match in posting order,
+// like RCCL p2p on a pair communicator -- so a peer that never posts stalls
+// only its own pair's streams, which is exactly what the reactive link has to
+// tolerate.
+struct PairHub {
+  explicit PairHub(int32_t n) : n(n), posts(size_t(n) * n), flags(size_t(n) * n, nullptr), seq(size_t(n) * n, 0) {
+    // One coherent pinned block, one 64-byte line per signal word: the CP's
+    // wait-value packets poll it, the peer stream's write-value packet sets it.
+    if (hipHostMalloc(&block, size_t(n) * n * 64, hipHostMallocCoherent) != hipSuccess)
+      throw AkkaError("akka: pair loopback: cannot allocate signal memory");
+    std::memset(block, 0, size_t(n) * n * 64);
+    for (size_t i = 0; i < flags.size(); ++i) flags[i] = reinterpret_cast<uint32_t*>(static_cast<char*>(block) + i * 64);
+  }
+  ~PairHub() {
+    for (auto* e : events) hipEventDestroy(e);
+    if (block) hipHostFree(block);
+  }
+  struct Post {
+    int32_t rank;
+    StreamH stream;
+    std::vector<P2POp> ops;
+    hipEvent_t posted;
+    uint32_t seq;
+  };
+  hipEvent_t event() {
+    if (!free_events.empty()) {
+      hipEvent_t e = free_events.back();
+      free_events.pop_back();
+      return e;
+    }
+    hipEvent_t e;
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) throw AkkaError("akka: hipEventCreate");
+    events.push_back(e);
+    return e;
+  }
+  int32_t n;
+  std::mutex mu;
+  std::vector<std::deque<Post>> posts;  // [lo*n+hi] unmatched posts of that pair (one side at a time)
+  std::vector<uint32_t*> flags;         // [a*n+b]: a's stream waits here for its groups with b
+  std::vector<uint32_t> seq;            // [a*n+b]: groups a posted towards b
+  void* block = nullptr;
+  std::vector<hipEvent_t> events, free_events;
+  int64_t bytes = 0;
+};
+
+struct PyPairHub {
+  std::shared_ptr<PairHub> hub;
+};
+
+class LoopbackPairP2P final : public P2P {
+ public:
+  LoopbackPairP2P(std::shared_ptr<PairHub> hub, int32_t rank) : hub_(std::move(hub)), rank_(rank) {}
+  int32_t rank() const override { return rank_; }
+  int32_t nranks() const override { return hub_->n; }
+  const char* name() const override { return "loopback-pair"; }
+  void group(StreamH stream, const std::vector<P2POp>& ops) override {
+    if (ops.empty()) return;
+    PairHub& h = *hub_;
+    const int32_t peer = ops.front().peer;
+    for (const auto& op : ops) AKKA_CHECK(op.peer == peer, "pair group holds ops to more than one peer");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    std::lock_guard<std::mutex> lk(h.mu);
+    const size_t key = size_t(std::min(rank_, peer)) * h.n + size_t(std::max(rank_, peer));
+    auto& q = h.posts[key];
+    if (q.empty() || q.front().rank == rank_) {
+      PairHub::Post p{rank_, stream, ops, h.event(), ++h.seq[size_t(rank_) * h.n + peer]};
+      check(hipEventRecord(p.posted, s));
+      check(hipStreamWaitValue32(s, h.flags[size_t(rank_) * h.n + peer], p.seq, hipStreamWaitValueGte, 0xFFFFFFFFu));
+      q.push_back(std::move(p));
+      return;
+    }
+    PairHub::Post other = std::move(q.front());
+    q.pop_front();
+    check(hipStreamWaitEvent(s, other.posted, 0));
+    h.free_events.push_back(other.posted);  // the wait captured its record
+    int64_t moved = 0;
+    moved += copy_dir(other.ops, ops, s);  // other's sends -> my recvs
+    moved += copy_dir(ops, other.ops, s);  // my sends -> other's recvs
+    check(hipStreamWriteValue32(s, h.flags[size_t(other.rank) * h.n + rank_], other.seq, 0));
+    h.bytes += moved;
+  }
+
+ private:
+  // j-th send in `from` (to the other side) matches the j-th recv in `to`.
+  static int64_t copy_dir(const std::vector<P2POp>& from, const std::vector<P2POp>& to, hipStream_t s) {
+    std::vector<const P2POp*> sends, recvs;
+    for (const auto& op : from)
+      if (op.send) sends.push_back(&op);
+    for (const auto& op : to)
+      if (!op.send) recvs.push_back(&op);
+    AKKA_CHECK(sends.size() == recvs.size(), "pair loopback: send/recv count mismatch");
+    int64_t moved = 0;
+    for (size_t j = 0; j < sends.size(); ++j) {
+      AKKA_CHECK(sends[j]->bytes == recvs[j]->bytes, "pair loopback: size mismatch");
+      if (sends[j]->bytes)
+        check(hipMemcpyAsync(recvs[j]->buf, sends[j]->buf, sends[j]->bytes, hipMemcpyDeviceToDevice, s));
+      moved += int64_t(sends[j]->bytes);
+    }
+    return moved;
+  }
+  static void check(hipError_t e) {
+    if (e != hipSuccess) throw AkkaError(std::string("akka: pair loopback p2p: ") + hipGetErrorString(e));
+  }
+  std::shared_ptr<PairHub> hub_;
+  int32_t rank_;
+};
+
 class WorkerCore final : public EngineHost {
  public:
   WorkerCore(py::object host, std::string link, int32_t device, std::string dtype, bool deferred, int32_t lag)
@@ -268,6 +384,12 @@ class WorkerCore final : public EngineHost {
     p2p_ = std::make_unique<LoopbackP2P>(hub.hub, rank);
     make_stream_link();
   }
+  void connect_loopback_pair(const PyPairHub& hub, int32_t rank) {
+    AKKA_CHECK(dev_ && !dev_->is_host(), "pair loopback p2p needs a HIP device");
+    AKKA_CHECK(link_kind_ == "reactive", "pair loopback serves the reactive link");
+    p2p_ = std::make_unique<LoopbackPairP2P>(hub.hub, rank);
+    make_reactive_link();
+  }
   void connect_local() {  // N == 1: stream link without peers
     AKKA_CHECK(engine_->geometry().N == 1, "connect_local is for single-worker jobs");
     make_stream_link(/*any_kind=*/true);
@@ -322,6 +444,7 @@ class WorkerCore final : public EngineHost {
 
   std::pair<uintptr_t, uintptr_t> streams() const {
     AKKA_CHECK(dev_, "streams() before init");
+    dev_->mark_streams_exported();
     return {reinterpret_cast<uintptr_t>(dev_->comm_stream()), reinterpret_cast<uintptr_t>(dev_->compute_stream())};
   }
   std::vector<OutMsg> drain() { return outbox_ ? outbox_->drain() : std::vector<OutMsg>{}; }
@@ -444,6 +567,19 @@ PYBIND11_MODULE(_native, m) {
       .def(py::init([](int32_t n) { return PyLoopbackHub{std::make_shared<LoopbackHub>(n)}; }))
       .def("bytes_moved", [](const PyLoopbackHub& h) { return h.hub->bytes; });
 
+  py::class_<PyPairHub>(m, "PairLoopbackHub")
+      .def(py::init([](int32_t n) { return PyPairHub{std::make_shared<PairHub>(n)}; }))
+      .def("bytes_moved", [](const PyPairHub& h) {
+        std::lock_guard<std::mutex> lk(h.hub->mu);
+        return h.hub->bytes;
+      })
+      .def("release_all", [](const PyPairHub& h) {
+        // Un-park every stream waiting for a peer that will never post (test
+        // teardown after a failure): no hang at stream destruction.
+        std::lock_guard<std::mutex> lk(h.hub->mu);
+        for (auto* f : h.hub->flags) __atomic_store_n(f, 0x7fffffffu, __ATOMIC_SEQ_CST);
+      });
+
   py::class_<PySimHub>(m, "SimHub")
       .def(py::init([](int32_t n) { return PySimHub{make_sim_hub(n)}; }))
       .def("bytes_moved", [](const PySimHub& h) { return sim_bytes_moved(h.hub); });
@@ -458,6 +594,7 @@ PYBIND11_MODULE(_native, m) {
       .def("connect_local", &WorkerCore::connect_local)
       .def("connect_callback", &WorkerCore::connect_callback)
       .def("connect_loopback", &WorkerCore::connect_loopback)
+      .def("connect_loopback_pair", &WorkerCore::connect_loopback_pair)
       .def("attach", &WorkerCore::attach)
       .def("start", &WorkerCore::start)
       .def("poll", &WorkerCore::poll)

@@ -52,6 +52,11 @@ class Device {
 
   virtual StreamH comm_stream() = 0;
   virtual StreamH compute_stream() = 0;
+  // comm/compute were handed to a framework that may still reference them
+  // after this device is gone (torch ExternalStream + record_stream: the
+  // caching allocator records events on them when blocks are freed): never
+  // destroy them.
+  virtual void mark_streams_exported() {}
   // Extra streams (per-peer streams of the reactive transport).
   virtual StreamH create_stream() = 0;
   virtual void destroy_stream(StreamH s) = 0;

@@ -38,9 +38,11 @@ class HipDevice final : public Device {
     hipSetDevice(dev_);
     hipStreamSynchronize(comm_);
     hipStreamSynchronize(compute_);
+    if (exported_) return;  // see Device::mark_streams_exported
     hipStreamDestroy(comm_);
     hipStreamDestroy(compute_);
   }
+  void mark_streams_exported() override { exported_ = true; }
 
   bool is_host() const override { return false; }
   int32_t device_index() const override { return dev_; }
@@ -66,11 +68,12 @@ class HipDevice final : public Device {
   StreamH comm_stream() override { return comm_; }
   StreamH compute_stream() override { return compute_; }
   StreamH create_stream() override {
-    int lo = 0, hi = 0;
+    // Normal priority on purpose: HIP serves high-priority streams from a
+    // small pool of hardware queues, and a per-peer stream parked on a peer
+    // (p2p waiting for a straggler) must not share a queue with other streams.
     AKKA_HIP(hipSetDevice(dev_));
-    AKKA_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
     hipStream_t s;
-    AKKA_HIP(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, hi));
+    AKKA_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     return s;
   }
   void destroy_stream(StreamH s) override {
@@ -191,6 +194,7 @@ class HipDevice final : public Device {
   int32_t dev_;
   hipStream_t comm_ = nullptr;
   hipStream_t compute_ = nullptr;
+  bool exported_ = false;
   ReduceImpl impl_;
   std::vector<ReduceSpec> pending_;
   StreamH pending_stream_ = nullptr;

@@ -23,7 +23,8 @@ step() {  # step <name> <timeout-s> <cmd...>
 }
 
 step env 120 bash -c "python -c 'import torch;print(torch.__version__, torch.cuda.get_device_name(0))' > $O/env.txt 2>&1"
-step pytest 900 bash -c "python -m pytest tests -m gpu -q --maxfail=20 > $O/pytest_gpu.log 2>&1; tail -4 $O/pytest_gpu.log"
+step reactive 400 bash -c "python -m pytest tests/test_reactive_gpu.py -q -x > $O/pytest_reactive.log 2>&1; rc=\$?; tail -15 $O/pytest_reactive.log; exit \$rc"
+step pytest 900 bash -c "python -m pytest tests -m gpu -q --maxfail=20 > $O/pytest_gpu.log 2>&1; rc=\$?; tail -4 $O/pytest_gpu.log; exit \$rc"
 step smoke 300 bash -c "python __graft_entry__.py smoke > $O/smoke.log 2>&1; tail -2 $O/smoke.log"
 step bench 300 bash -c "python bench.py --steps 20 --warmup 5 > $O/bench1.json 2> $O/bench1.err; cat $O/bench1.json; tail -3 $O/bench1.err"
 step micro 400 bash -c "python bench/reduce_kernel_bw.py --torch-ref > $O/reduce_bw.jsonl 2>&1; cat $O/reduce_bw.jsonl"

@@ -3,6 +3,12 @@ import sys
 
 import pytest
 
+# The reactive transport runs one HIP stream per peer; with several ranks in
+# one process (GPU loopback tests) the streams must not share hardware queues
+# (a stream parked on a wait would block unrelated streams).  HIP reads this at
+# its first call, so set it before anything touches the GPU.  (<= 32 allowed.)
+os.environ["GPU_MAX_HW_QUEUES"] = "32"  # the box exports 4
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)

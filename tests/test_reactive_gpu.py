@@ -1,0 +1,103 @@
+"""Reactive transport on one MI355X: N ranks in one process, each with its
+own HIP streams (one per peer), staged data plane and ReactiveLink, over the
+asynchronous per-pair loopback (device copies released by stream
+write-value).  Checks exact sums at thresholds 1, the contributor-mask/count
+invariant at partial thresholds, and that a sleeping rank does not stall the
+others (then catches up)."""
+import pytest
+import torch
+
+from akka_allreduce_amd.data import Geometry
+from akka_allreduce_amd.parallel.loopback import ReactiveLoopbackCluster
+
+pytestmark = pytest.mark.gpu
+
+
+def _w(S):
+    return (torch.arange(S, device="cuda") % 3 + 1).float()
+
+
+def _check_masks(o, S, n, allowed=None):
+    w = _w(S)
+    mask = (o.data.float() / w).round().long()
+    assert torch.equal(mask.float() * w, o.data.float())
+    pc = torch.zeros_like(mask)
+    for b in range(n):
+        bit = (mask >> b) & 1
+        pc += bit
+        if allowed is not None and b not in allowed:
+            assert int(bit.sum()) == 0
+    assert torch.equal(pc.int(), o.count)
+    return mask
+
+
+@pytest.mark.parametrize("n", [2, 3, 4])
+@pytest.mark.parametrize("S,C", [(1 << 16, 1 << 12), (100_003, 777), (5, 1)])
+def test_reactive_loopback_exact(n, S, C):
+    with ReactiveLoopbackCluster(n, S, C, max_lag=1) as cl:
+        _exact(cl, n, S)
+
+
+def _exact(cl, n, S):
+    rounds = []
+    for k in range(4):
+        g = torch.Generator().manual_seed(k)
+        rounds.append([torch.randint(-8, 9, (S,), generator=g).float().cuda() for _ in range(n)])
+    outs = cl.run_rounds(rounds)
+    torch.cuda.synchronize()
+    for k, xs in enumerate(rounds):
+        want = torch.stack(xs).sum(0)
+        for r in range(n):
+            assert torch.equal(outs[r][k].data, want), (n, S, k, r)
+            assert bool((outs[r][k].count == n).all())
+
+
+def test_reactive_loopback_bf16():
+    n, S, C = 3, 300_001, 4096
+    with ReactiveLoopbackCluster(n, S, C, dtype=torch.bfloat16) as cl:
+        xs = [torch.randint(-8, 9, (S,)).bfloat16().cuda() for _ in range(n)]
+        outs = cl.run_rounds([xs])
+        want = torch.stack([x.float() for x in xs]).sum(0).bfloat16()
+        torch.cuda.synchronize()
+        assert all(torch.equal(outs[r][0].data, want) for r in range(n))
+
+
+def test_reactive_loopback_sleeping_rank():
+    """Rank 3 sleeps 3 s; at thresholds 0.75 ranks 0-2 finish all rounds long
+    before it wakes, summing only each other's data; then rank 3 catches up."""
+    n, S, C, R = 4, 1 << 14, 1 << 10, 4
+    cl = ReactiveLoopbackCluster(n, S, C, th_reduce=0.75, th_complete=0.75, max_lag=2)
+    try:
+        _sleeping(cl, n, S, C, R)
+    finally:
+        cl.close()
+
+
+def _sleeping(cl, n, S, C, R):
+    import time
+
+    rounds = [[_w(S) * float(1 << i) for i in range(n)] for _ in range(R)]
+    done_at = {}
+    orig = cl.workers[0].allreduce
+
+    t0 = time.monotonic()
+
+    def timed(x, **kw):
+        o = orig(x, **kw)
+        done_at[o.iteration] = time.monotonic() - t0
+        return o
+
+    cl.workers[0].allreduce = timed
+    outs = cl.run_rounds(rounds, delays=[0, 0, 0, 3.0])
+    torch.cuda.synchronize()
+    assert max(done_at.values()) < 2.5, done_at  # never waited for the sleeper
+    g = Geometry(S, n, C)
+    s3, _ = g.block_range(3)
+    for r in range(3):
+        for k in range(R):
+            mask = _check_masks(outs[r][k], S, n, allowed={0, 1, 2})
+            assert bool((mask[:s3] == 0b111).all())
+    for k in range(R):
+        _check_masks(outs[3][k], S, n)
+    cl.drain()
+    assert all(w.state()["link"]["slots_busy"] == 0 for w in cl.workers)
