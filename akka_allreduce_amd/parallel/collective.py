@@ -11,6 +11,13 @@ Usage::
 
     ar = ThresholdAllreduce(data_size=x.numel(), max_chunk_size=1 << 20)
     out = ar(x)          # AllReduceOutput; out.data is valid in stream order
+
+``transport="reactive"`` selects the straggler-tolerant data path
+(csrc/transport/reactive_link.h): one stream + one RCCL pair communicator per
+peer, arrivals polled from events, so with thresholds < 1 a rank completes
+rounds without waiting for slow peers (the reference's semantics).  It runs
+N+2 streams per process: set ``GPU_MAX_HW_QUEUES`` (<= 32) to at least N+4
+before the first HIP call, or parked streams share hardware queues.
 """
 from __future__ import annotations
 
@@ -76,7 +83,10 @@ class ThresholdAllreduce:
         device: Optional[torch.device] = None,
         store: Any = None,
         data_sink: Any = None,
+        transport: str = "stream",
     ):
+        if transport not in ("stream", "reactive"):
+            raise ValueError("transport must be 'stream' or 'reactive'")
         r, w, local = env_rank_world()
         self.rank = r if rank is None else int(rank)
         self.world_size = w if world_size is None else int(world_size)
@@ -84,6 +94,14 @@ class ThresholdAllreduce:
             device = torch.device("cuda", local % max(1, torch.cuda.device_count())) if torch.cuda.is_available() \
                 else torch.device("cpu")
         self.device = torch.device(device)
+        if transport == "reactive" and self.world_size > 1:
+            if self.device.type != "cuda":
+                raise ValueError("the reactive transport runs on GPUs (RCCL pair communicators)")
+            need = self.world_size + 4
+            have = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
+            if have < need:
+                raise RuntimeError(f"reactive transport at N={self.world_size} needs GPU_MAX_HW_QUEUES >= {need} "
+                                   f"(have {have}); export it (<= 32) before the first HIP call")
         if self.device.type == "cuda":
             torch.cuda.set_device(self.device)
             uid = share_unique_id(self.rank, self.world_size, store)
@@ -93,7 +111,8 @@ class ThresholdAllreduce:
             from .gloo import make_group_fn
 
             spec = ("callback", make_group_fn(), self.rank, self.world_size) if self.world_size > 1 else ("local",)
-        self.worker = AllreduceWorker(None, data_sink, device=self.device, dtype=dtype, transport="stream",
+        self.transport = transport if self.world_size > 1 else "stream"
+        self.worker = AllreduceWorker(None, data_sink, device=self.device, dtype=dtype, transport=self.transport,
                                       transport_spec=spec, broadcast_lag=broadcast_lag, strict=True,
                                       name=f"rank{self.rank}")
         peers = {i: (self.worker if i == self.rank else _RemoteRank(i)) for i in range(self.world_size)}

@@ -39,6 +39,9 @@ def parse():
     p.add_argument("--compare-rccl", action="store_true", help="also time torch.distributed all_reduce (RCCL)")
     p.add_argument("--no-check", action="store_true")
     p.add_argument("--fresh-out", action="store_true", help="allocate a new output tensor every round")
+    p.add_argument("--transport", choices=["stream", "reactive"], default="stream",
+                   help="stream: symmetric step schedule on one comm stream (default); reactive: per-peer streams + "
+                        "pair communicators, event-polled arrivals (straggler-tolerant)")
     p.add_argument("--async-op", choices=["auto", "on", "off"], default="auto",
                    help="async rounds (event hand-off) -- auto: on for N>1 (saves a stream hop per round), off for "
                         "N=1 (local rounds run on the caller's stream, nothing to hop)")
@@ -47,6 +50,9 @@ def parse():
 
 def main() -> int:
     args = parse()
+    if args.transport == "reactive":
+        # one stream per peer: must not share hardware queues (read at HIP init)
+        os.environ["GPU_MAX_HW_QUEUES"] = "32"
     import torch
     import torch.distributed as dist
 
@@ -73,7 +79,7 @@ def main() -> int:
     S = nbytes // esize
     C = max(1, int(args.chunk_mb * (1 << 20)) // esize)
     ar = ThresholdAllreduce(S, max_chunk_size=C, dtype=dtype, th_reduce=args.th_reduce, th_complete=args.th_complete,
-                            max_lag=args.max_lag, broadcast_lag=args.bcast_lag, device=dev)
+                            max_lag=args.max_lag, broadcast_lag=args.bcast_lag, device=dev, transport=args.transport)
 
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)
@@ -91,6 +97,8 @@ def main() -> int:
     # waiting for the last round's event covers every round.
     out_buf = None if args.fresh_out else torch.empty(S, device=dev, dtype=dtype)
     args.async_op = (world > 1) if args.async_op == "auto" else (args.async_op == "on")
+    if ar.transport == "reactive":
+        args.async_op = False  # reactive rounds return once complete (progress is host-polled)
     for _ in range(args.warmup):
         out = ar(x, async_op=args.async_op, out=out_buf)
     out.wait()
@@ -169,13 +177,15 @@ def main() -> int:
                 "max_lag": args.max_lag,
                 "broadcast_lag": args.bcast_lag,
                 "thresholds": [1.0, args.th_reduce, args.th_complete],
-                "transport": "rccl-p2p-xgmi" if world > 1 else "local",
+                "transport": ("rccl-pair-reactive" if ar.transport == "reactive" else "rccl-p2p-xgmi")
+                if world > 1 else "local",
                 "async_op": args.async_op,
                 "output": "fresh tensor per round" if args.fresh_out else "preallocated, reused",
             },
             "busbw_GBps": round(busbw, 3),
             "exact": ok,
-            "groups_per_round": (st.get("link", {}).get("groups", 0) / max(1, st.get("link", {}).get("rounds", 1))),
+            "groups_per_round": (st.get("link", {}).get("groups", 0)
+                                 / max(1, st.get("link", {}).get("rounds", st["stats"]["rounds_completed"]) or 1)),
             "rccl_allreduce_algbw_GBps": round(rccl, 3) if rccl else None,
         }
         print(json.dumps(line), flush=True)

@@ -633,6 +633,66 @@ PYBIND11_MODULE(_native, m) {
     return py::bytes(reinterpret_cast<const char*>(v.data()), v.size());
   });
   m.def("rccl_version", []() { return std::string(rccl_version_string()); });
+  m.def("hw_queue_probe", [](int32_t kmax, int32_t wait_ms) {
+    // How many streams can be parked on a wait-value before a fresh stream
+    // stops making progress (= the HW queues streams really get).  Returns the
+    // first k at which a memset on a fresh stream did not finish in wait_ms,
+    // or kmax+1.  Every parked stream is released before returning.
+    py::gil_scoped_release nogil;
+    uint32_t* flag = nullptr;
+    if (hipHostMalloc(reinterpret_cast<void**>(&flag), 64, hipHostMallocCoherent) != hipSuccess)
+      throw AkkaError("probe: hipHostMalloc failed");
+    *flag = 0;
+    void* buf = nullptr;
+    if (hipMalloc(&buf, 1 << 20) != hipSuccess) throw AkkaError("probe: hipMalloc failed");
+    std::vector<hipStream_t> parked;
+    int32_t result = kmax + 1;
+    for (int32_t k = 1; k <= kmax; ++k) {
+      hipStream_t s;
+      hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+      hipStreamWaitValue32(s, flag, 1, hipStreamWaitValueGte, 0xFFFFFFFFu);
+      parked.push_back(s);
+      hipStream_t f;
+      hipStreamCreateWithFlags(&f, hipStreamNonBlocking);
+      hipEvent_t e;
+      hipEventCreateWithFlags(&e, hipEventDisableTiming);
+      hipMemsetAsync(buf, k & 0xff, 1 << 20, f);
+      hipEventRecord(e, f);
+      auto t0 = std::chrono::steady_clock::now();
+      bool done = false;
+      while (std::chrono::steady_clock::now() - t0 < std::chrono::milliseconds(wait_ms)) {
+        if (hipEventQuery(e) == hipSuccess) {
+          done = true;
+          break;
+        }
+      }
+      if (!done) {
+        result = k;
+        __atomic_store_n(flag, 1u, __ATOMIC_SEQ_CST);
+        hipEventSynchronize(e);
+      }
+      hipEventDestroy(e);
+      parked.push_back(f);
+      if (!done) break;
+    }
+    __atomic_store_n(flag, 1u, __ATOMIC_SEQ_CST);
+    for (auto s : parked) {
+      hipStreamSynchronize(s);
+      hipStreamDestroy(s);
+    }
+    hipFree(buf);
+    hipHostFree(flag);
+    return result;
+  }, py::arg("kmax") = 40, py::arg("wait_ms") = 200);
+  m.def("tournament", [](int32_t n) {
+    std::vector<std::vector<int32_t>> rounds;
+    for (int32_t t = 0; t < tournament_rounds(n); ++t) {
+      std::vector<int32_t> partner(static_cast<size_t>(n), 0);
+      for (int32_t x = 0; x < n; ++x) partner[size_t(x)] = tournament_partner(n, t, x);
+      rounds.push_back(partner);
+    }
+    return rounds;
+  }, "partner[x] per ncclCommSplit round of the pair-communicator setup (>= n: sits out)");
 
   // Raw grouped-p2p endpoint (tests / microbenchmarks of the RCCL data plane).
   py::class_<P2P>(m, "P2PEndpoint")

@@ -55,6 +55,20 @@ void DataPlane::enable_staging(int32_t max_slots, std::function<bool(int32_t)> r
   max_slots_ = max_slots;
   reclaim_ = std::move(reclaim);
   staging_on_ = true;
+  // Preallocate the whole pool when it is small (<= 8 GiB): growing it while a
+  // peer lags would put hipMalloc/hipHostMalloc on the fast ranks' round path.
+  const size_t slot_bytes = (size_t(std::max<int64_t>(g_.S, 1)) + size_t(std::max<int64_t>(my_len_, 1))) * esize();
+  const int32_t pre = slot_bytes * size_t(max_slots) <= (size_t(8) << 30) ? max_slots : L_ + 2;
+  for (int32_t i = 0; i < pre; ++i) slots_.push_back(new_slot());
+}
+
+DataPlane::SendSlot DataPlane::new_slot() {
+  SendSlot s;
+  s.input = dev_->alloc(size_t(std::max<int64_t>(g_.S, 1)) * esize());
+  s.mine = dev_->alloc(size_t(std::max<int64_t>(my_len_, 1)) * esize());
+  s.wire = static_cast<int32_t*>(dev_->alloc(size_t(kmax_) * sizeof(int32_t)));
+  s.wire_h = static_cast<int32_t*>(dev_->alloc_pinned(size_t(kmax_) * sizeof(int32_t)));
+  return s;
 }
 
 int32_t DataPlane::slots_busy() const { return int32_t(slot_of_.size()); }
@@ -71,12 +85,7 @@ DataPlane::SendSlot& DataPlane::slot(int32_t round) {
     }
   if (idx == slots_.size()) {
     if (int32_t(slots_.size()) < max_slots_) {
-      SendSlot s;
-      s.input = dev_->alloc(size_t(std::max<int64_t>(g_.S, 1)) * esize());
-      s.mine = dev_->alloc(size_t(std::max<int64_t>(my_len_, 1)) * esize());
-      s.wire = static_cast<int32_t*>(dev_->alloc(size_t(kmax_) * sizeof(int32_t)));
-      s.wire_h = static_cast<int32_t*>(dev_->alloc_pinned(size_t(kmax_) * sizeof(int32_t)));
-      slots_.push_back(s);
+      slots_.push_back(new_slot());
     } else {
       // Pool exhausted (a peer is far behind): reclaim the oldest slot whose
       // round is over by making the compute stream wait for its transfers.

@@ -178,6 +178,7 @@ class DataPlane {
     int32_t* wire_h = nullptr;  // pinned [kmax]
   };
   SendSlot& slot(int32_t round);
+  SendSlot new_slot();
   bool staging_on_ = false;
   int32_t max_slots_ = 0;
   std::vector<SendSlot> slots_;

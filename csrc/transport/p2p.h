@@ -50,6 +50,18 @@ bool sim_step(const std::shared_ptr<SimHub>& hub, const std::vector<Device*>& de
 // ---- RCCL ---------------------------------------------------------------------
 std::vector<uint8_t> rccl_unique_id();
 std::unique_ptr<P2P> make_rccl_p2p(const std::vector<uint8_t>& uid, int32_t rank, int32_t nranks, int32_t device);
+// Round-robin tournament (circle method) used to split the global communicator
+// into pair communicators: in round t (0 <= t < P-1, P = N rounded up to even)
+// rank x is paired with tournament_partner(N, t, x); a partner >= N means x
+// sits this round out (odd N).  Every unordered pair meets exactly once.
+inline int32_t tournament_partner(int32_t n, int32_t t, int32_t x) {
+  const int32_t P = (n % 2) ? n + 1 : n;
+  if (x == P - 1) return t;
+  if (x == t) return P - 1;
+  return ((2 * t - x) % (P - 1) + (P - 1)) % (P - 1);
+}
+inline int32_t tournament_rounds(int32_t n) { return ((n % 2) ? n + 1 : n) - 1; }
+
 // Per-pair communicators (reactive transport): a group holds ops to one peer.
 std::unique_ptr<P2P> make_rccl_pair_p2p(const std::vector<uint8_t>& uid, int32_t rank, int32_t nranks,
                                         int32_t device);

@@ -93,12 +93,8 @@ class RcclPairP2P final : public P2P {
     AKKA_NCCL(ncclCommInitRank(&global_, nranks, id, rank));
     // Round-robin tournament (circle method): P-1 rounds of disjoint pairs,
     // one ncclCommSplit each; with odd N a dummy player sits one rank out.
-    const int32_t P = (nranks % 2) ? nranks + 1 : nranks;
-    for (int32_t t = 0; t + 1 < P; ++t) {
-      int32_t partner;
-      if (rank == P - 1) partner = t;
-      else if (rank == t) partner = P - 1;
-      else partner = ((2 * t - rank) % (P - 1) + (P - 1)) % (P - 1);
+    for (int32_t t = 0; t < tournament_rounds(nranks); ++t) {
+      const int32_t partner = tournament_partner(nranks, t, rank);
       const bool real = partner < nranks && partner != rank;
       ncclComm_t c = nullptr;
       AKKA_NCCL(ncclCommSplit(global_, real ? std::min(rank, partner) : NCCL_SPLIT_NOCOLOR, rank, &c, nullptr));

@@ -32,6 +32,7 @@ step hostovh 200 bash -c "python bench.py --steps 200 --warmup 20 --size-mb 0.06
 step bf16 300 bash -c "python bench.py --dtype bfloat16 --size-mb 1024 --chunk-mb 8 --steps 10 --warmup 3 > $O/bench_bf16_1g.json 2>&1; tail -1 $O/bench_bf16_1g.json"
 step mlp 300 bash -c "python examples/mlp_sgd.py > $O/mlp.json 2>&1; tail -1 $O/mlp.json"
 step rcclp2p 200 bash -c "python bench/rccl_p2p_overhead.py > $O/rccl_p2p.jsonl 2>&1; tail -4 $O/rccl_p2p.jsonl"
+step straggler 300 bash -c "python bench/straggler_gpu.py > $O/straggler_gpu.jsonl 2>&1; rc=\$?; tail -3 $O/straggler_gpu.jsonl; exit \$rc"
 step n1exp 200 bash -c "python bench/n1_experiments.py > $O/n1exp.json 2>&1; tail -2 $O/n1exp.json"
 step prof 400 bash -c "cd /tmp && export TMPDIR=/tmp && rocprofv3 --kernel-trace --stats -d $O/prof -o bench -- python $R/bench.py --steps 10 --warmup 3 > $O/prof.log 2>&1; tail -3 $O/prof.log; python $R/scripts/prof_summary.py $O/prof/bench_results.db 40 > $O/prof_summary.txt 2>&1; head -12 $O/prof_summary.txt"
 exit 0

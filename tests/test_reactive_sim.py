@@ -229,3 +229,34 @@ def test_slot_pool_exhaustion_is_bounded_wait_not_error():
     cl.run(lambda: all(cl.done(i, done_rounds) for i in fast))
     cl.settle()
     cl.drain()
+
+
+@pytest.mark.parametrize("n", range(2, 17))
+def test_pair_communicator_tournament(n):
+    """The ncclCommSplit schedule that builds one RCCL communicator per pair:
+    each round is a matching, every unordered pair meets exactly once."""
+    from akka_allreduce_amd._native_loader import load
+
+    rounds = load().tournament(n)
+    met = set()
+    for partner in rounds:
+        for x, p in enumerate(partner):
+            if p >= n:
+                continue
+            assert p != x and partner[p] == x  # symmetric matching
+            met.add((min(x, p), max(x, p)))
+    assert met == {(a, b) for a in range(n) for b in range(a + 1, n)}
+    assert len(rounds) == (n if n % 2 else n - 1)
+
+
+def test_threshold_allreduce_reactive_guards():
+    from akka_allreduce_amd.parallel import ThresholdAllreduce
+
+    with pytest.raises(ValueError):
+        ThresholdAllreduce(16, transport="bogus", rank=0, world_size=1, device="cpu")
+    with pytest.raises(ValueError):
+        ThresholdAllreduce(16, transport="reactive", rank=0, world_size=2, device="cpu")
+    # N = 1 needs no peers: the local path serves both transports
+    ar = ThresholdAllreduce(16, transport="reactive", rank=0, world_size=1, device="cpu")
+    o = ar(torch.arange(16.0))
+    assert torch.equal(o.data, torch.arange(16.0))
