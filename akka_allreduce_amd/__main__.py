@@ -50,6 +50,11 @@ def _master(a: argparse.Namespace) -> int:
 
 
 def _worker(a: argparse.Namespace) -> int:
+    import os
+
+    if a.transport == "reactive":
+        # one stream per peer: they must not share hardware queues (read at HIP init)
+        os.environ["GPU_MAX_HW_QUEUES"] = "32"
     import torch
 
     from .parallel.cluster import start_worker
@@ -63,7 +68,8 @@ def _worker(a: argparse.Namespace) -> int:
     if device == "auto":
         device = "cuda" if torch.cuda.is_available() else "cpu"
     w = start_worker(master, int(size), checkpoint=a.checkpoint if a.checkpoint is not None else cfg.checkpoint,
-                     assert_multiple=a.assert_multiple, port=int(port), device=device, dtype=dtype)
+                     assert_multiple=a.assert_multiple, port=int(port), device=device, dtype=dtype,
+                     transport=a.transport)
     try:
         while not w.wait(0.5):
             pass
@@ -136,6 +142,9 @@ def main(argv=None) -> int:
     w.add_argument("--assert-multiple", type=int, default=0)
     w.add_argument("--device", help="cpu | cuda | cuda:N | auto")
     w.add_argument("--dtype", default="float32")
+    w.add_argument("--transport", choices=["auto", "stream", "reactive", "outbox"], default="auto",
+                   help="GPU data path: stream (scheduled RCCL steps) or reactive (per-peer streams, straggler-"
+                        "tolerant); outbox = messages through the control plane (CPU)")
     w.set_defaults(fn=_worker)
 
     d = sub.add_parser("demo", help="master + N CPU workers on localhost")

@@ -73,6 +73,11 @@ class Node:
         self._threads: List[threading.Thread] = []
         self.on_send_failure: Optional[Callable[[str, BaseException], None]] = None
         self.on_message: Optional[Callable[[Any], None]] = None  # observer hook (failure detector)
+        # Progress hook run by the dispatcher thread between messages: returns
+        # None when there is nothing to drive (the dispatcher then blocks on the
+        # mailbox), True after progress, False while work is pending but idle
+        # (e.g. the reactive GPU transport's in-flight transfers).
+        self.poller: Optional[Callable[[], Optional[bool]]] = None
 
     # ---- references --------------------------------------------------------------
     def ref(self, address: Optional[str]) -> Any:
@@ -174,9 +179,27 @@ class Node:
         finally:
             conn.close()
 
+    def _next_message(self) -> Any:
+        poller = self.poller
+        while poller is not None and not self._stop.is_set():
+            try:
+                return self.mailbox.get_nowait()
+            except queue.Empty:
+                pass
+            try:
+                st = poller()
+            except Exception as e:  # keep the node alive (W:287-299)
+                log.exception("%s: error in poller: %s", self.name, e)
+                st = None
+            if st is None:
+                break  # nothing in flight: block on the mailbox
+            if not st:
+                time.sleep(20e-6)
+        return self.mailbox.get()
+
     def _dispatch_loop(self) -> None:
         while not self._stop.is_set():
-            msg = self.mailbox.get()
+            msg = self._next_message()
             if msg is None:
                 return
             if self.on_message:

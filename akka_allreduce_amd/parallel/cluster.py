@@ -184,14 +184,21 @@ def start_master(thresholds: ThresholdConfig, data: DataConfig, workers: WorkerC
 
 class WorkerProcess:
     def __init__(self, master_address: str, data_source, data_sink, *, host: str = "127.0.0.1", port: int = 0,
-                 device: Any = "cpu", dtype: torch.dtype = torch.float32, heartbeat_interval_s: float = 1.0):
+                 device: Any = "cpu", dtype: torch.dtype = torch.float32, heartbeat_interval_s: float = 1.0,
+                 transport: str = "auto"):
         self.node = Node(host, port, name="worker")
         dev = torch.device(device) if device not in (None, "cpu") else torch.device("cpu")
-        transport = "stream" if dev.type == "cuda" else "outbox"
+        if transport == "auto":
+            transport = "stream" if dev.type == "cuda" else "outbox"
+        if transport in ("stream", "reactive") and dev.type != "cuda":
+            raise ValueError(f"{transport} transport needs a GPU worker")
         self.worker = AllreduceWorker(data_source, data_sink, device=dev, dtype=dtype, transport=transport,
                                       name=f"worker@{self.node.address}")
         self.stopped = threading.Event()
         self.node.aliases.append(self.worker)
+        if transport == "reactive":
+            # the dispatcher thread drives the in-flight transfers between messages
+            self.node.poller = self._poll
         self.node.start(self)
         self.master = self.node.ref(master_address)
         self.master.tell(RegisterWorker(self.node.address, dev.index if dev.type == "cuda" else None,
@@ -211,6 +218,12 @@ class WorkerProcess:
             self.node.stop()
             return
         self.worker.receive(msg)
+
+    def _poll(self) -> Optional[bool]:
+        core = self.worker._core
+        if core is None or not self.worker.initialized or core.in_flight() == 0:
+            return None
+        return self.worker.poll()
 
     def _heartbeat(self, interval: float) -> None:
         while not self.stopped.is_set():

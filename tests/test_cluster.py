@@ -83,3 +83,51 @@ def test_cli_demo_processes():
                        cwd=ROOT, env=env, capture_output=True, text=True, timeout=180)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
     assert "failures=0" in r.stdout
+
+
+def test_node_poller_drives_progress_between_messages():
+    """The dispatcher thread runs the poller while it reports pending work
+    (the reactive GPU transport's in-flight transfers) and blocks on the
+    mailbox once it returns None."""
+    import threading
+    import time
+
+    from akka_allreduce_amd.parallel.actors import Node
+
+    got = []
+    pending = {"n": 5}
+    polled = threading.Event()
+
+    class A:
+        def receive(self, msg):
+            got.append(msg)
+
+    node = Node("127.0.0.1", 0, name="p")
+
+    def poller():
+        if pending["n"] == 0:
+            polled.set()
+            return None
+        pending["n"] -= 1
+        return pending["n"] % 2 == 0
+
+    node.poller = poller
+    node.start(A())
+    try:
+        node.send(node.address, "hello")
+        assert polled.wait(5)
+        node.send(node.address, "again")
+        t0 = time.time()
+        while len(got) < 2 and time.time() - t0 < 5:
+            time.sleep(0.01)
+        assert got == ["hello", "again"]
+        assert pending["n"] == 0
+    finally:
+        node.stop()
+
+
+def test_worker_process_rejects_gpu_transports_on_cpu():
+    from akka_allreduce_amd.parallel.cluster import WorkerProcess
+
+    with pytest.raises(ValueError):
+        WorkerProcess("127.0.0.1:1", None, None, device="cpu", transport="reactive")
