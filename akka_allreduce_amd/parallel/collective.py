@@ -94,9 +94,7 @@ class ThresholdAllreduce:
             device = torch.device("cuda", local % max(1, torch.cuda.device_count())) if torch.cuda.is_available() \
                 else torch.device("cpu")
         self.device = torch.device(device)
-        if transport == "reactive" and self.world_size > 1:
-            if self.device.type != "cuda":
-                raise ValueError("the reactive transport runs on GPUs (RCCL pair communicators)")
+        if transport == "reactive" and self.world_size > 1 and self.device.type == "cuda":
             need = self.world_size + 4
             have = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
             if have < need:
@@ -107,10 +105,16 @@ class ThresholdAllreduce:
             uid = share_unique_id(self.rank, self.world_size, store)
             spec = ("rccl", uid, self.rank, self.world_size) if self.world_size > 1 else ("local",)
         else:
-            # CPU processes: the same schedule over torch.distributed (gloo) p2p
-            from .gloo import make_group_fn
+            # CPU processes: the same schedules over torch.distributed (gloo) p2p
+            from .gloo import make_async_fns, make_group_fn
 
-            spec = ("callback", make_group_fn(), self.rank, self.world_size) if self.world_size > 1 else ("local",)
+            if self.world_size == 1:
+                spec = ("local",)
+            elif transport == "reactive":
+                post, test = make_async_fns()
+                spec = ("async_callback", post, test, self.rank, self.world_size)
+            else:
+                spec = ("callback", make_group_fn(), self.rank, self.world_size)
         self.transport = transport if self.world_size > 1 else "stream"
         self.worker = AllreduceWorker(None, data_sink, device=self.device, dtype=dtype, transport=self.transport,
                                       transport_spec=spec, broadcast_lag=broadcast_lag, strict=True,
@@ -135,3 +139,18 @@ class ThresholdAllreduce:
 
     def synchronize(self) -> None:
         self.worker.synchronize()
+
+    def drain(self, timeout: float = 60.0) -> None:
+        """Reactive transport: keep driving until none of this rank's transfers
+        is in flight (slow peers caught up).  Call before tearing down."""
+        import time
+
+        core = self.worker._core
+        if not core.reactive():
+            return
+        t0 = time.monotonic()
+        while core.in_flight():
+            if not self.worker.poll():
+                time.sleep(1e-4)
+            if time.monotonic() - t0 > timeout:
+                raise TimeoutError(f"rank {self.rank}: {core.in_flight()} transfers still in flight")

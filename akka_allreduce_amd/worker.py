@@ -91,7 +91,9 @@ class AllreduceWorker:
         self.strict = strict
         self.name = name
         n = _native()
-        deferred = bool(transport_spec and transport_spec[0] == "sim")
+        # host streams are queues this process runs: the simulator steps them,
+        # async-callback (gloo) workers step them in poll()
+        deferred = bool(transport_spec and transport_spec[0] in ("sim", "async_callback"))
         dev_index = self.device.index if self.device.type == "cuda" else -1
         self._core = n.WorkerCore(self, transport, dev_index, _DTYPES[dtype], deferred, broadcast_lag)
         self.id: int = -1
@@ -210,6 +212,9 @@ class AllreduceWorker:
         elif kind == "loopback_pair":
             _, hub, rank = spec
             self._core.connect_loopback_pair(hub, int(rank))
+        elif kind == "async_callback":
+            _, post, test, rank, nranks = spec
+            self._core.connect_async_callback(post, test, int(rank), int(nranks))
         elif kind == "callback":
             _, fn, rank, nranks = spec
             self._core.connect_callback(fn, int(rank), int(nranks))

@@ -26,6 +26,10 @@
 namespace py = pybind11;
 using namespace akka;
 
+namespace akka {
+bool host_device_step(Device* d, uint32_t rotate);  // host_device.cpp
+}
+
 namespace {
 
 struct PySimHub {
@@ -86,6 +90,47 @@ class PyCallbackP2P final : public P2P {
  private:
   py::function fn_;
   int32_t rank_, n_;
+};
+
+// Asynchronous grouped p2p through two Python callables (reactive transport
+// across CPU processes, torch.distributed gloo): when the stream reaches the
+// group, `post(ops)` starts the isend/irecv and returns a handle; the stream
+// op then completes once `test(handle)` is true.  Groups on one stream run in
+// order (one outstanding group per pair stream), different pair streams
+// overlap -- the same contract as RCCL pair communicators on MI355X.
+class PyAsyncCallbackP2P final : public P2P {
+ public:
+  PyAsyncCallbackP2P(py::function post, py::function test, int32_t rank, int32_t n, Device* dev)
+      : post_(std::move(post)), test_(std::move(test)), rank_(rank), n_(n), dev_(dev) {}
+  int32_t rank() const override { return rank_; }
+  int32_t nranks() const override { return n_; }
+  const char* name() const override { return "async-callback"; }
+  void group(StreamH stream, const std::vector<P2POp>& ops) override {
+    struct State {
+      py::list ops;
+      py::object handle;
+      bool posted = false;
+    };
+    auto st = std::make_shared<State>();
+    for (const auto& op : ops)
+      st->ops.append(py::make_tuple(op.send, op.peer, reinterpret_cast<uintptr_t>(op.buf), op.bytes));
+    py::function post = post_, test = test_;
+    // Runs from WorkerCore::poll / start (Python callers: the GIL is held).
+    dev_->enqueue_host_op(stream, [st, post, test]() {
+      if (!st->posted) {
+        st->handle = post(st->ops);
+        st->posted = true;
+      }
+      if (!test(st->handle).cast<bool>()) return false;
+      st->handle = py::none();
+      return true;
+    });
+  }
+
+ private:
+  py::function post_, test_;
+  int32_t rank_, n_;
+  Device* dev_;
 };
 
 // ---------------------------------------------------------------------------
@@ -390,6 +435,13 @@ class WorkerCore final : public EngineHost {
     p2p_ = std::make_unique<LoopbackPairP2P>(hub.hub, rank);
     make_reactive_link();
   }
+  void connect_async_callback(py::function post, py::function test, int32_t rank, int32_t nranks) {
+    AKKA_CHECK(dev_ && dev_->is_host() && deferred_, "async callback p2p runs on a deferred host device");
+    AKKA_CHECK(link_kind_ == "reactive", "async callback p2p serves the reactive link");
+    p2p_ = std::make_unique<PyAsyncCallbackP2P>(std::move(post), std::move(test), rank, nranks, dev_.get());
+    self_drive_ = true;
+    make_reactive_link();
+  }
   void connect_local() {  // N == 1: stream link without peers
     AKKA_CHECK(engine_->geometry().N == 1, "connect_local is for single-worker jobs");
     make_stream_link(/*any_kind=*/true);
@@ -403,7 +455,20 @@ class WorkerCore final : public EngineHost {
 
   void start(int32_t r) { engine_->start(r); }
   // Reactive transport: deliver completed transfers to the engine.
-  bool poll() { return reactive_link_ ? reactive_link_->poll() : false; }
+  bool poll() {
+    if (!reactive_link_) return false;
+    if (!self_drive_) return reactive_link_->poll();
+    // Host streams driven by this process (async callback p2p): run the
+    // stream queues and the link until neither moves.
+    bool any = false;
+    for (int i = 0; i < 64; ++i) {
+      bool moved = host_device_step(dev_.get(), 0);
+      moved |= reactive_link_->poll();
+      if (!moved) break;
+      any = true;
+    }
+    return any;
+  }
   int32_t in_flight() const { return reactive_link_ ? reactive_link_->in_flight() : 0; }
   bool reactive() const { return reactive_link_ != nullptr; }
   void scatter_in(int32_t src, int32_t dest, int32_t chunk, int32_t round, uintptr_t ptr, int64_t len, bool on_host) {
@@ -542,6 +607,7 @@ class WorkerCore final : public EngineHost {
   std::unique_ptr<P2P> p2p_;
   std::unique_ptr<StreamLink> stream_link_;
   std::unique_ptr<ReactiveLink> reactive_link_;
+  bool self_drive_ = false;
   std::unique_ptr<OutboxLink> outbox_;
   std::unique_ptr<Engine> engine_;
 };
@@ -595,6 +661,7 @@ PYBIND11_MODULE(_native, m) {
       .def("connect_callback", &WorkerCore::connect_callback)
       .def("connect_loopback", &WorkerCore::connect_loopback)
       .def("connect_loopback_pair", &WorkerCore::connect_loopback_pair)
+      .def("connect_async_callback", &WorkerCore::connect_async_callback)
       .def("attach", &WorkerCore::attach)
       .def("start", &WorkerCore::start)
       .def("poll", &WorkerCore::poll)
