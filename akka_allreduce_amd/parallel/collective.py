@@ -123,12 +123,19 @@ class ThresholdAllreduce:
         self.worker.tell(InitWorkers(peers, self.world_size, None, self.rank, th_reduce, th_complete, max_lag,
                                      int(data_size), int(max_chunk_size)))
         self.data_size = int(data_size)
+        from ..utils.faults import env_straggler_delay
+
+        self.fault_delay_s = env_straggler_delay(self.rank)  # AKKA_FAULT_RANK / AKKA_FAULT_DELAY_MS
 
     def __call__(self, x: torch.Tensor, async_op: bool = False, out: Optional[torch.Tensor] = None) -> AllReduceOutput:
         """One round.  ``async_op=True``: call ``.wait()`` before reading ``.data``.
         ``out``: preallocated output buffer (reused across rounds)."""
         if x.numel() != self.data_size:
             raise ValueError(f"expected {self.data_size} elements, got {x.numel()}")
+        if self.fault_delay_s:
+            import time
+
+            time.sleep(self.fault_delay_s)
         out = self.worker.allreduce(x, async_op=async_op, out=out)
         if out is None:
             raise RuntimeError("round did not complete (thresholds need every rank in the scheduled transport)")

@@ -7,9 +7,10 @@ maxLag 1) with one induced straggler.
    sleeps --delay-ms per round.  Reports rounds/s with and without the
    straggler and the mean contributor count: rounds complete without waiting
    for the slow worker (thAllreduce pacing + thresholds + maxLag catch-up).
---mode spmd (under torch.distributed.run on GPUs): the scheduled RCCL
-   transport; rank N-1 sleeps before each call.  RCCL p2p is a rendezvous, so
-   here the straggler's delay is paid by every rank -- reported as is.
+--mode spmd (under torch.distributed.run on GPUs): rank N-1 sleeps before each
+   call.  --transport stream (scheduled RCCL steps, a rendezvous: the delay is
+   paid by every rank) or --transport reactive (per-peer streams + pair
+   communicators: the fast ranks' own time per round is reported separately).
 """
 from __future__ import annotations
 
@@ -20,6 +21,9 @@ import sys
 import time
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+if "reactive" in sys.argv:
+    os.environ["GPU_MAX_HW_QUEUES"] = "32"  # per-peer streams (read at HIP init)
 
 import torch  # noqa: E402
 
@@ -76,7 +80,7 @@ def run_spmd(a) -> dict:
         dist.init_process_group("gloo", rank=rank, world_size=world)
     S = int(a.size_mb * (1 << 20)) // 4
     ar = ThresholdAllreduce(S, max_chunk_size=(4 << 20) // 4, th_reduce=a.th_reduce, th_complete=a.th_complete,
-                            max_lag=a.max_lag, device=dev)
+                            max_lag=a.max_lag, device=dev, transport=a.transport)
     x = torch.randn(S, device=dev)
     res = {}
     for straggle in (False, True):
@@ -91,12 +95,21 @@ def run_spmd(a) -> dict:
                 time.sleep(a.delay_ms / 1e3)
             out = ar(x)
         torch.cuda.synchronize()
+        own = time.perf_counter() - t0  # this rank's own time for the rounds
+        ar.drain()
         if world > 1:
             dist.barrier()
         dt = time.perf_counter() - t0
+        owns = [own]
+        if world > 1:
+            owns = [None] * world
+            dist.all_gather_object(owns, own)
+        fast = max(owns[:-1]) if world > 1 else own
         res["straggler" if straggle else "baseline"] = {
             "rounds_per_s": round(a.rounds / dt, 2), "algbw_GBps": round(S * 4 * a.rounds / dt / 1e9, 2),
+            "fast_ranks_ms_per_round": round(fast / a.rounds * 1e3, 3),
             "mean_contributors": float(out.count.float().mean())}
+    res["transport"] = a.transport
     return res
 
 
@@ -113,6 +126,7 @@ def main():
     p.add_argument("--th-reduce", type=float, default=0.75)
     p.add_argument("--th-complete", type=float, default=0.75)
     p.add_argument("--max-lag", type=int, default=1)
+    p.add_argument("--transport", choices=["stream", "reactive"], default="stream", help="spmd mode data path")
     a = p.parse_args()
     mode = a.mode
     if mode == "auto":
