@@ -269,6 +269,7 @@ class WorkerCore final : public EngineHost {
       ls["ops"] = stream_link_->stats().ops;
       ls["bytes_sent"] = stream_link_->stats().bytes_sent;
       ls["rounds"] = stream_link_->stats().rounds;
+      ls["unreduced_chunks"] = stream_link_->stats().unreduced_chunks;
       ls["lag"] = stream_link_->lag();
       d["link"] = ls;
     }

@@ -121,6 +121,7 @@ class Engine {
   int32_t max_round() const { return max_round_; }
   int32_t max_scattered() const { return max_scattered_; }
   std::vector<int32_t> completed() const { return {completed_.begin(), completed_.end()}; }
+  bool is_completed(int32_t r) const { return r < round_ || completed_.count(r) > 0; }
   std::vector<PeerEntry> peers() const { return peers_; }
   const InitParams& params() const { return params_; }
   const Geometry& geometry() const { return g_; }

@@ -78,12 +78,24 @@ void StreamLink::schedule(int32_t r) {
     ops.clear();
     const int32_t kb = s - lag_;
     bool bcast_step = kb >= 0 && kb < kme;
+    bool unreduced = false;
     if (bcast_step) {
       auto it = rq.bcast_ready.find(kb);
-      AKKA_CHECK(it != rq.bcast_ready.end(),
-                 "round " + std::to_string(r) + ": chunk " + std::to_string(kb) +
-                     " was not reduced by its broadcast step (threshold never reached?)");
-      dp_->comm_wait(it->second);
+      if (it == rq.bcast_ready.end()) {
+        // The round reached thComplete before this chunk reached thReduce:
+        // later scatters were outdated (W:172-173), so it is never reduced.
+        // The symmetric schedule still moves the bytes: zeros with in-band
+        // count 0 -- what the reference's output shows for a chunk that
+        // never arrived (RB:41-47).
+        AKKA_CHECK(engine_->is_completed(r), "round " + std::to_string(r) + ": chunk " + std::to_string(kb) +
+                                                 " was not reduced by its broadcast step (threshold never reached?)");
+        unreduced = true;
+        dp_->device()->zero(dp_->exec_stream(r), dp_->output_at(r, me, kb), size_t(g.chunk_len(me, kb)) * es);
+        dp_->comm_wait(dp_->record_compute());
+        ++stats_.unreduced_chunks;
+      } else {
+        dp_->comm_wait(it->second);
+      }
     }
     const bool last = (s == steps - 1);
     if (last) dp_->upload_counts(r, {me}, comm);
@@ -96,7 +108,9 @@ void StreamLink::schedule(int32_t r) {
         ops.push_back({true, peer, const_cast<void*>(it->second.ptr), size_t(it->second.len) * es});
       }
       if (s < kme) ops.push_back({false, peer, dp_->scatter_slot(r, peer, s), size_t(g.chunk_len(me, s)) * es});
-      if (bcast_step) {
+      if (bcast_step && unreduced) {
+        ops.push_back({true, peer, dp_->output_at(r, me, kb), size_t(g.chunk_len(me, kb)) * es});
+      } else if (bcast_step) {
         auto it = rq.bcast.find({kb, peer});
         AKKA_CHECK(it != rq.bcast.end(), "missing broadcast payload for peer " + std::to_string(peer));
         ops.push_back({true, peer, const_cast<void*>(it->second.ptr), size_t(it->second.len) * es});

@@ -33,7 +33,7 @@
 namespace akka {
 
 struct StreamLinkStats {
-  int64_t groups = 0, ops = 0, bytes_sent = 0, rounds = 0;
+  int64_t groups = 0, ops = 0, bytes_sent = 0, rounds = 0, unreduced_chunks = 0;
 };
 
 class StreamLink final : public Link {

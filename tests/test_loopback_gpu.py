@@ -68,3 +68,17 @@ def test_loopback_threshold_subset():
     for o in outs:
         assert torch.equal(o.data, want)
         assert bool((o.count == 3).all())
+
+
+def test_loopback_completion_before_late_chunks():
+    """Same as the simulator case: thComplete < 1 completes the round before
+    later chunks' broadcast steps; they go out as zeros with count 0."""
+    n, S, C, th = 3, 63 * 1024, 1024, 0.67
+    cl = LoopbackCluster(n, S, C, th_reduce=th, th_complete=th)
+    for _ in range(2):
+        outs = cl.allreduce([torch.full((S,), float(1 << i), device="cuda") for i in range(n)])
+        torch.cuda.synchronize()
+        for o in outs:
+            m = o.data.round().long()
+            pc = sum(((m >> b) & 1) for b in range(n))
+            assert torch.equal(pc.int(), o.count)

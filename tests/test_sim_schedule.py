@@ -105,3 +105,22 @@ def test_mismatched_schedule_is_detected():
     xs = _inputs(n, S, 0)
     with pytest.raises(RuntimeError, match="sim p2p"):
         cl.allreduce(xs)
+
+
+@pytest.mark.parametrize("n,S,C,th", [(3, 63 * 4, 4, 0.67), (4, 64 * 4, 4, 0.5), (8, 320, 5, 0.6), (3, 252, 4, 0.8)])
+def test_completion_before_late_chunks_are_reduced(n, S, C, th):
+    """thComplete < 1 with many chunks per block: the round completes while
+    later chunks are still ahead in the schedule; scatters for them are then
+    outdated (W:172-173), so they are never reduced, yet the symmetric
+    schedule must still send something at their broadcast step -- zeros with
+    count 0.  Every element's value must be a subset sum whose contributor
+    count equals the delivered count (inputs are 2^rank)."""
+    cl = SimCluster(n, S, C, th_reduce=th, th_complete=th)
+    for r in range(3):
+        outs = cl.allreduce([torch.full((S,), float(1 << i)) for i in range(n)])
+        for o in outs:
+            m = o.data.round().long()
+            pc = sum(((m >> b) & 1) for b in range(n))
+            assert torch.equal(pc.int(), o.count)
+            assert bool((o.count == 0).any())  # some chunks never made it: holes, not garbage
+    assert cl.workers[0].state()["link"]["unreduced_chunks"] > 0
