@@ -15,7 +15,15 @@ DataPlane::DataPlane(Device* dev, const Geometry& g, int32_t me, int32_t ring_ro
   kme_ = g_.num_chunks(me_);
   kmax_ = std::max(1, g_.max_block_len_chunks());
   my_len_ = g_.block_len(me_);
-  size_t ring_bytes = size_t(L_) * size_t(g_.N) * size_t(std::max<int64_t>(my_len_, 1)) * esize();
+  // 16-B vector loads need every pointer of a chunk reduce to share one
+  // alignment: slot data starts at the same offset mod 16 B as my block does
+  // in the caller's tensors (block_start * esize), and slot / row strides are
+  // multiples of 16 B (kernels.hip peels the common misaligned head).
+  const int64_t vec_el = int64_t(16 / esize());
+  mis_el_ = g_.block_start(me_) % vec_el;
+  slot_stride_ = (std::max<int64_t>(my_len_, 1) + mis_el_ + vec_el - 1) / vec_el * vec_el;
+  row_stride_ = (std::max<int64_t>(g_.S, 1) + vec_el - 1) / vec_el * vec_el;
+  size_t ring_bytes = size_t(L_) * size_t(g_.N) * size_t(slot_stride_) * esize();
   scatter_ring_ = dev_->alloc(ring_bytes);
   staging_ = static_cast<int32_t*>(dev_->alloc_pinned(size_t(L_) * g_.N * kmax_ * sizeof(int32_t)));
   std::memset(staging_, 0, size_t(L_) * g_.N * kmax_ * sizeof(int32_t));
@@ -51,13 +59,13 @@ DataPlane::~DataPlane() {
 void DataPlane::enable_staging(int32_t max_slots, std::function<bool(int32_t)> reclaim) {
   AKKA_CHECK(!staging_on_, "staging already enabled");
   AKKA_CHECK(max_slots >= L_ + 1, "send slot pool must exceed the ring depth");
-  land_ring_ = dev_->alloc(size_t(L_) * size_t(std::max<int64_t>(g_.S, 1)) * esize());
+  land_ring_ = dev_->alloc(size_t(L_) * size_t(row_stride_) * esize());
   max_slots_ = max_slots;
   reclaim_ = std::move(reclaim);
   staging_on_ = true;
   // Preallocate the whole pool when it is small (<= 8 GiB): growing it while a
   // peer lags would put hipMalloc/hipHostMalloc on the fast ranks' round path.
-  const size_t slot_bytes = (size_t(std::max<int64_t>(g_.S, 1)) + size_t(std::max<int64_t>(my_len_, 1))) * esize();
+  const size_t slot_bytes = (size_t(std::max<int64_t>(g_.S, 1)) + size_t(slot_stride_)) * esize();
   const int32_t pre = slot_bytes * size_t(max_slots) <= (size_t(8) << 30) ? max_slots : L_ + 2;
   for (int32_t i = 0; i < pre; ++i) slots_.push_back(new_slot());
 }
@@ -65,7 +73,7 @@ void DataPlane::enable_staging(int32_t max_slots, std::function<bool(int32_t)> r
 DataPlane::SendSlot DataPlane::new_slot() {
   SendSlot s;
   s.input = dev_->alloc(size_t(std::max<int64_t>(g_.S, 1)) * esize());
-  s.mine = dev_->alloc(size_t(std::max<int64_t>(my_len_, 1)) * esize());
+  s.mine = dev_->alloc(size_t(slot_stride_) * esize());
   s.wire = static_cast<int32_t*>(dev_->alloc(size_t(kmax_) * sizeof(int32_t)));
   s.wire_h = static_cast<int32_t*>(dev_->alloc_pinned(size_t(kmax_) * sizeof(int32_t)));
   return s;
@@ -125,7 +133,7 @@ const void* DataPlane::staged_input(int32_t round, int32_t block) {
 }
 
 void* DataPlane::mine_at(int32_t round, int32_t k) {
-  return static_cast<char*>(slot(round).mine) + size_t(k) * size_t(g_.C) * esize();
+  return static_cast<char*>(slot(round).mine) + (size_t(mis_el_) + size_t(k) * size_t(g_.C)) * esize();
 }
 
 int32_t* DataPlane::wire_dev(int32_t round) { return slot(round).wire; }
@@ -133,7 +141,7 @@ int32_t* DataPlane::wire_host(int32_t round) { return slot(round).wire_h; }
 
 void* DataPlane::landing_at(int32_t round, int32_t block, int32_t k) const {
   AKKA_CHECK(staging_on_, "landing_at: staging is off");
-  size_t off = size_t(round % L_) * size_t(std::max<int64_t>(g_.S, 1)) + size_t(g_.chunk_offset(block, k));
+  size_t off = size_t(round % L_) * size_t(row_stride_) + size_t(g_.chunk_offset(block, k));
   return static_cast<char*>(land_ring_) + off * esize();
 }
 
@@ -315,7 +323,7 @@ Payload DataPlane::output_chunk(int32_t round, int32_t block, int32_t k) const {
 
 void* DataPlane::scatter_slot(int32_t round, int32_t src, int32_t k) const {
   size_t row = size_t(round % L_);
-  size_t off = (row * size_t(g_.N) + size_t(src)) * size_t(std::max<int64_t>(my_len_, 1)) + size_t(k) * size_t(g_.C);
+  size_t off = (row * size_t(g_.N) + size_t(src)) * size_t(slot_stride_) + size_t(mis_el_) + size_t(k) * size_t(g_.C);
   return static_cast<char*>(scatter_ring_) + off * esize();
 }
 

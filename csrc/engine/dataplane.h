@@ -162,7 +162,10 @@ class DataPlane {
   int32_t kme_;
   int32_t kmax_;
   int64_t my_len_;
-  void* scatter_ring_ = nullptr;   // [L][N][my_len]
+  int64_t mis_el_ = 0;       // my block's offset mod 16 B, in elements
+  int64_t slot_stride_ = 0;  // scatter slot / own-block buffer stride (elements, 16-B multiple)
+  int64_t row_stride_ = 0;   // landing row stride (elements, 16-B multiple)
+  void* scatter_ring_ = nullptr;   // [L][N][slot_stride]
   int32_t* staging_ = nullptr;     // pinned [L][N][kmax]
   std::vector<Row> rows_;
   std::map<int32_t, Binding> bind_;

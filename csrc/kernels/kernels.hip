@@ -16,6 +16,8 @@
 // 64-lane waves throughout; blocks of 256 threads = 4 waves.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include <cstdlib>
 #include <cstring>
 
@@ -34,11 +36,47 @@ struct SrcTable {
   int32_t* fill;  // optional counts-row fill done by block 0 (saves a dispatch per round)
   int32_t fill_value;
   int32_t fill_n;
+  int32_t head_n;  // elements below the aligned body (vector kernels, block 0)
 };
 
 __device__ __forceinline__ void do_fill(const SrcTable& t) {
   if (blockIdx.x == 0)
     for (int i = threadIdx.x; i < t.fill_n; i += kBlock) t.fill[i] = t.fill_value;
+}
+
+template <typename T>
+__device__ __forceinline__ float to_f(T v);
+template <>
+__device__ __forceinline__ float to_f<float>(float v) {
+  return v;
+}
+template <>
+__device__ __forceinline__ float to_f<unsigned short>(unsigned short v) {
+  return __uint_as_float(uint32_t(v) << 16);
+}
+template <typename T>
+__device__ __forceinline__ T from_f(float v);
+template <>
+__device__ __forceinline__ float from_f<float>(float v) {
+  return v;
+}
+template <>
+__device__ __forceinline__ unsigned short from_f<unsigned short>(float v) {
+  return __builtin_bit_cast(unsigned short, static_cast<__bf16>(v));
+}
+
+// Misaligned head folded into a vector launch: the head_n elements just below
+// the (16-B aligned) body pointers, summed by block 0 (saves a dispatch per
+// chunk when the block offset is not a multiple of 16 B).
+template <typename T, int NSRC>
+__device__ __forceinline__ void do_head(const SrcTable& t, void* dst) {
+  if (blockIdx.x == 0 && int(threadIdx.x) < t.head_n) {
+    const int i = int(threadIdx.x) - t.head_n;
+    float acc = 0.f;
+#pragma unroll
+    for (int s = 0; s < NSRC; ++s) acc += to_f(static_cast<const T*>(t.p[s])[i]);
+    static_cast<T*>(dst)[i] = from_f<T>(acc);
+  }
 }
 
 __device__ __forceinline__ void add_vec(float (&acc)[4], const v4u& v, float) {
@@ -90,6 +128,7 @@ template <typename T, int NSRC, int UNROLL>
 __global__ __launch_bounds__(kBlock) void reduce_vec_kernel(SrcTable srcs, v4u* __restrict__ dst, int64_t nvec) {
   constexpr int E = VecTraits<T>::kElems;
   do_fill(srcs);
+  do_head<T, NSRC>(srcs, dst);
   const int64_t stride = int64_t(gridDim.x) * kBlock;
   for (int64_t base = int64_t(blockIdx.x) * kBlock + threadIdx.x; base < nvec; base += stride * UNROLL) {
     v4u v[UNROLL][NSRC];
@@ -128,6 +167,7 @@ __global__ __launch_bounds__(kBlock) void reduce_lds_kernel(SrcTable srcs, v4u* 
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   do_fill(srcs);
+  do_head<T, NSRC>(srcs, dst);
   const int64_t ntiles = nvec / 64;  // full wave tiles; the tail goes through VGPRs
   const int64_t wave_id = int64_t(blockIdx.x) * kWaves + wave;
   const int64_t wave_stride = int64_t(gridDim.x) * kWaves;
@@ -188,26 +228,6 @@ __global__ __launch_bounds__(kBlock) void reduce_lds_kernel(SrcTable srcs, v4u* 
 }
 
 // ---- Scalar: unaligned pointers / sub-vector tails --------------------------------
-template <typename T>
-__device__ __forceinline__ float to_f(T v);
-template <>
-__device__ __forceinline__ float to_f<float>(float v) {
-  return v;
-}
-template <>
-__device__ __forceinline__ float to_f<unsigned short>(unsigned short v) {
-  return __uint_as_float(uint32_t(v) << 16);
-}
-template <typename T>
-__device__ __forceinline__ T from_f(float v);
-template <>
-__device__ __forceinline__ float from_f<float>(float v) {
-  return v;
-}
-template <>
-__device__ __forceinline__ unsigned short from_f<unsigned short>(float v) {
-  return __builtin_bit_cast(unsigned short, static_cast<__bf16>(v));
-}
 
 template <typename T>
 __global__ __launch_bounds__(kBlock) void reduce_scalar_kernel(SrcTable srcs, int nsrc, T* __restrict__ dst,
@@ -330,54 +350,74 @@ const char* reduce_impl_name(ReduceImpl i) {
 void launch_reduce(hipStream_t s, const ReduceSpec& spec, DType dt, ReduceImpl impl) {
   if (spec.n <= 0) return;
   AKKA_CHECK(spec.nsrc >= 1 && spec.nsrc <= kMaxReduceSrc, "reduce: bad source count");
+  // Common misalignment (every pointer at the same offset mod 16 B, which the
+  // data plane's layout guarantees): the body runs on 16-B vectors from the
+  // first aligned element and block 0 also sums the few head elements.
+  int32_t head = 0;
+  ReduceSpec body = spec;
+  if (impl != ReduceImpl::Scalar) {
+    const uintptr_t mis = reinterpret_cast<uintptr_t>(spec.dst) & 15;
+    bool same = mis != 0;
+    for (int i = 0; i < spec.nsrc && same; ++i) same = (reinterpret_cast<uintptr_t>(spec.srcs[i]) & 15) == mis;
+    const size_t es = dt == DType::F32 ? 4 : 2;
+    const int64_t h = int64_t((16 - mis) / es);
+    if (same && mis % es == 0 && spec.n > h + 64) {
+      head = int32_t(h);
+      body.dst = static_cast<char*>(spec.dst) + h * es;
+      for (int i = 0; i < spec.nsrc; ++i) body.srcs[i] = static_cast<const char*>(spec.srcs[i]) + h * es;
+      body.n = spec.n - h;
+    }
+  }
+  const ReduceSpec& sp = body;
   SrcTable t{};
-  bool aligned = (reinterpret_cast<uintptr_t>(spec.dst) & 15) == 0;
-  for (int i = 0; i < spec.nsrc; ++i) {
-    t.p[i] = spec.srcs[i];
-    aligned &= (reinterpret_cast<uintptr_t>(spec.srcs[i]) & 15) == 0;
+  bool aligned = (reinterpret_cast<uintptr_t>(sp.dst) & 15) == 0;
+  for (int i = 0; i < sp.nsrc; ++i) {
+    t.p[i] = sp.srcs[i];
+    aligned &= (reinterpret_cast<uintptr_t>(sp.srcs[i]) & 15) == 0;
   }
   const int64_t per_vec = dt == DType::F32 ? 4 : 8;
-  const int64_t nvec = aligned ? spec.n / per_vec : 0;
+  const int64_t nvec = aligned ? sp.n / per_vec : 0;
   if (impl == ReduceImpl::Auto) {
     // Measured (profiles/README.md): LDS-DMA staging wins while the working set
     // sits in the 256 MiB Infinity Cache (chunk-sized reduces inside a round,
     // data just landed from xGMI); direct 16-B loads win for HBM-resident streams.
-    const int64_t bytes = int64_t(spec.nsrc + 1) * spec.n * (dt == DType::F32 ? 4 : 2);
-    impl = (bytes <= (int64_t(96) << 20) && spec.nsrc <= 8) ? ReduceImpl::Lds : ReduceImpl::Vec;
+    const int64_t bytes = int64_t(sp.nsrc + 1) * sp.n * (dt == DType::F32 ? 4 : 2);
+    impl = (bytes <= (int64_t(96) << 20) && sp.nsrc <= 8) ? ReduceImpl::Lds : ReduceImpl::Vec;
   }
   bool filled = false;
+  t.head_n = head;
   if (impl == ReduceImpl::Scalar) {
     // forced scalar path over everything
   } else if (nvec > 0) {
     const bool lds = impl == ReduceImpl::Lds;
-    t.fill = spec.fill;
-    t.fill_value = spec.fill_value;
-    t.fill_n = spec.fill ? spec.fill_n : 0;
+    t.fill = sp.fill;
+    t.fill_value = sp.fill_value;
+    t.fill_n = sp.fill ? sp.fill_n : 0;
     filled = true;
-    if (dt == DType::F32) launch_vec<float>(s, t, spec.nsrc, static_cast<v4u*>(spec.dst), nvec, lds);
-    else launch_vec<unsigned short>(s, t, spec.nsrc, static_cast<v4u*>(spec.dst), nvec, lds);
+    if (dt == DType::F32) launch_vec<float>(s, t, sp.nsrc, static_cast<v4u*>(sp.dst), nvec, lds);
+    else launch_vec<unsigned short>(s, t, sp.nsrc, static_cast<v4u*>(sp.dst), nvec, lds);
     check_launch("reduce_vec");
   }
   const int64_t done = impl == ReduceImpl::Scalar ? 0 : nvec * per_vec;
-  const int64_t rest = spec.n - done;
-  if (rest > 0 || (!filled && spec.fill && spec.fill_n > 0)) {
+  const int64_t rest = sp.n - done;
+  if (rest > 0 || (!filled && sp.fill && sp.fill_n > 0)) {
     const size_t es = dt == DType::F32 ? 4 : 2;
     SrcTable tt{};
     if (!filled) {
-      tt.fill = spec.fill;
-      tt.fill_value = spec.fill_value;
-      tt.fill_n = spec.fill ? spec.fill_n : 0;
+      tt.fill = sp.fill;
+      tt.fill_value = sp.fill_value;
+      tt.fill_n = sp.fill ? sp.fill_n : 0;
     }
-    for (int i = 0; i < spec.nsrc; ++i) tt.p[i] = static_cast<const char*>(spec.srcs[i]) + done * es;
+    for (int i = 0; i < sp.nsrc; ++i) tt.p[i] = static_cast<const char*>(sp.srcs[i]) + done * es;
     int64_t want = (rest + kBlock - 1) / kBlock;
     if (want < 1) want = 1;  // fill-only launch
     int grid = int(want < kMaxGrid ? want : kMaxGrid);
     if (dt == DType::F32) {
-      hipLaunchKernelGGL(reduce_scalar_kernel<float>, dim3(grid), dim3(kBlock), 0, s, tt, spec.nsrc,
-                         reinterpret_cast<float*>(static_cast<char*>(spec.dst) + done * es), rest);
+      hipLaunchKernelGGL(reduce_scalar_kernel<float>, dim3(grid), dim3(kBlock), 0, s, tt, sp.nsrc,
+                         reinterpret_cast<float*>(static_cast<char*>(sp.dst) + done * es), rest);
     } else {
-      hipLaunchKernelGGL(reduce_scalar_kernel<unsigned short>, dim3(grid), dim3(kBlock), 0, s, tt, spec.nsrc,
-                         reinterpret_cast<unsigned short*>(static_cast<char*>(spec.dst) + done * es), rest);
+      hipLaunchKernelGGL(reduce_scalar_kernel<unsigned short>, dim3(grid), dim3(kBlock), 0, s, tt, sp.nsrc,
+                         reinterpret_cast<unsigned short*>(static_cast<char*>(sp.dst) + done * es), rest);
     }
     check_launch("reduce_scalar");
   }

@@ -56,3 +56,20 @@ def test_count_expand(S, N, C):
     want = g.expand_counts(per)
     got = count_expand(per.cuda(), g).cpu()
     assert torch.equal(got, want)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("off", [1, 2, 3, 5, 7])
+@pytest.mark.parametrize("nsrc", [1, 3, 8])
+def test_chunk_reduce_common_misalignment(dtype, off, nsrc):
+    """All pointers at the same offset mod 16 B (the data plane's layout):
+    the launcher peels a scalar head and runs the vector body; results must
+    match the fp32 reference exactly for small-integer data."""
+    n = 100_003
+    base = [torch.randint(-8, 9, (n + 16,), device="cuda").to(dtype) for _ in range(nsrc)]
+    srcs = [b[off:off + n] for b in base]
+    out_base = torch.empty(n + 16, device="cuda", dtype=dtype)
+    out = out_base[off:off + n]
+    chunk_reduce(srcs, out=out)
+    want = torch.stack([x.float() for x in srcs]).sum(0).to(dtype)
+    assert torch.equal(out, want)
