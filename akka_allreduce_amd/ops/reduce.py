@@ -25,7 +25,9 @@ def _stream(t: torch.Tensor) -> int:
 def chunk_reduce(srcs: Sequence[torch.Tensor], out: Optional[torch.Tensor] = None, impl: str = "auto") -> torch.Tensor:
     """``out = sum(srcs)`` elementwise, fp32 accumulation, output in the inputs' dtype.
 
-    ``impl``: ``auto`` | ``vec`` (16-B loads to VGPRs) | ``lds`` (LDS-DMA staged)
+    ``impl``: ``auto`` | ``vec`` (16-B loads to VGPRs, cache policy picked from
+    the working set) | ``vec_nts`` / ``vec_ntl`` / ``vec_both`` (vec with a fixed
+    nontemporal-store / -load / both policy) | ``lds`` (LDS-DMA staged)
     | ``scalar``.  All sources must share shape, dtype and device.
     """
     if len(srcs) == 0:

@@ -34,6 +34,7 @@ def time_fn(fn, iters: int) -> float:
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--sizes-mb", default="4,32,256")
+    p.add_argument("--impls", default="vec,lds", help="comma list: auto,vec,lds,vec_nts,vec_ntl,vec_both")
     p.add_argument("--nsrc", default="1,2,4,8")
     p.add_argument("--dtypes", default="float32,bfloat16")
     p.add_argument("--iters", type=int, default=20)
@@ -50,7 +51,7 @@ def main():
                 out = torch.empty_like(srcs[0])
                 bytes_moved = (k + 1) * n * es
                 row = {"dtype": dt_name, "chunk_mb": mb, "nsrc": k}
-                for impl in ("vec", "lds"):
+                for impl in a.impls.split(","):
                     t = time_fn(lambda: chunk_reduce(srcs, out=out, impl=impl), a.iters)
                     row[f"{impl}_us"] = round(t * 1e6, 2)
                     row[f"{impl}_GBps"] = round(bytes_moved / t / 1e9, 1)

@@ -499,10 +499,7 @@ PYBIND11_MODULE(_native, m) {
   m.def("reduce", [](uintptr_t dst, std::vector<uintptr_t> srcs, int64_t n, std::string dtype, uintptr_t stream,
                      std::string impl) {
     DType dt = (dtype == "bfloat16" || dtype == "bf16") ? DType::BF16 : DType::F32;
-    ReduceImpl im = ReduceImpl::Auto;
-    if (impl == "vec") im = ReduceImpl::Vec;
-    else if (impl == "lds") im = ReduceImpl::Lds;
-    else if (impl == "scalar") im = ReduceImpl::Scalar;
+    ReduceImpl im = reduce_impl_from_name(impl.c_str());
     std::vector<const void*> ptrs;
     for (auto p : srcs) ptrs.push_back(reinterpret_cast<const void*>(p));
     AKKA_CHECK(!ptrs.empty(), "reduce: no sources");

@@ -8,11 +8,15 @@
 namespace akka {
 
 enum class ReduceImpl : int32_t {
-  Auto = 0,    // pick per call (currently: Vec)
-  Vec = 1,     // 16-B global loads straight to VGPRs, all sources in flight per thread
-  Lds = 2,     // global_load_lds (LDS-DMA) double-buffered staging, then ds_read + sum
-  Scalar = 3,  // unaligned fallback
+  Auto = 0,     // pick per call from the working set (profiles/README.md)
+  Vec = 1,      // 16-B global loads straight to VGPRs; load/store policy picked per call
+  Lds = 2,      // global_load_lds (LDS-DMA) double-buffered staging, then ds_read + sum
+  Scalar = 3,   // unaligned fallback
+  VecNts = 4,   // vec, plain loads + nontemporal stores (inputs stay in the Infinity Cache)
+  VecNtl = 5,   // vec, nontemporal loads + plain stores
+  VecBoth = 6,  // vec, nontemporal loads and stores, unroll 2 (large streams)
 };
+ReduceImpl reduce_impl_from_name(const char* name);
 
 // dst = sum(srcs) over n elements (fp32 accumulate).
 void launch_reduce(hipStream_t s, const ReduceSpec& spec, DType dt, ReduceImpl impl);

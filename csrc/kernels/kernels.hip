@@ -29,7 +29,8 @@ namespace {
 
 using v4u = unsigned int __attribute__((ext_vector_type(4)));
 constexpr int kBlock = 256;
-constexpr int kMaxGrid = 256 * 8;  // 256 CUs x 8 blocks
+constexpr int kCUs = 256;
+constexpr int kMaxGrid = kCUs * 8;  // 256 CUs x 8 blocks
 
 struct SrcTable {
   const void* p[kMaxReduceSrc];
@@ -124,7 +125,13 @@ struct VecTraits<unsigned short> {
 };
 
 // ---- Vec: loads straight to VGPRs ----------------------------------------------
-template <typename T, int NSRC, int UNROLL>
+// Load/store cache policy (measured by bench/stream_variants.hip, see
+// profiles/README.md): nontemporal stores keep a streamed output from
+// evicting the sources out of the 256 MiB Infinity Cache; nontemporal loads
+// help once the sources do not fit there anyway.
+enum VecPolicy : int { kNtl = 0, kNts = 1, kBoth = 2 };
+
+template <typename T, int NSRC, int UNROLL, int POL>
 __global__ __launch_bounds__(kBlock) void reduce_vec_kernel(SrcTable srcs, v4u* __restrict__ dst, int64_t nvec) {
   constexpr int E = VecTraits<T>::kElems;
   do_fill(srcs);
@@ -137,7 +144,10 @@ __global__ __launch_bounds__(kBlock) void reduce_vec_kernel(SrcTable srcs, v4u* 
       const int64_t i = base + u * stride;
       if (i < nvec) {
 #pragma unroll
-        for (int s = 0; s < NSRC; ++s) v[u][s] = __builtin_nontemporal_load(static_cast<const v4u*>(srcs.p[s]) + i);
+        for (int s = 0; s < NSRC; ++s) {
+          const v4u* src = static_cast<const v4u*>(srcs.p[s]) + i;
+          v[u][s] = POL == kNts ? *src : __builtin_nontemporal_load(src);
+        }
       }
     }
 #pragma unroll
@@ -149,7 +159,8 @@ __global__ __launch_bounds__(kBlock) void reduce_vec_kernel(SrcTable srcs, v4u* 
         for (int e = 0; e < E; ++e) acc[e] = 0.f;
 #pragma unroll
         for (int s = 0; s < NSRC; ++s) add_vec(acc, v[u][s], T{});
-        dst[i] = pack_vec(acc);
+        if constexpr (POL == kNtl) dst[i] = pack_vec(acc);
+        else __builtin_nontemporal_store(pack_vec(acc), dst + i);
       }
     }
   }
@@ -271,12 +282,21 @@ __global__ __launch_bounds__(kBlock) void count_expand_kernel(int32_t* __restric
   }
 }
 
-template <typename T, int NSRC>
-void launch_vec_n(hipStream_t s, const SrcTable& t, v4u* dst, int64_t nvec) {
-  constexpr int UNROLL = NSRC <= 4 ? 4 : (NSRC <= 8 ? 2 : 1);
+template <typename T, int NSRC, int POL>
+void launch_vec_pol(hipStream_t s, const SrcTable& t, v4u* dst, int64_t nvec, int blocks_per_cu) {
+  constexpr int U0 = NSRC <= 4 ? 4 : (NSRC <= 8 ? 2 : 1);
+  constexpr int UNROLL = POL == kBoth ? (U0 < 2 ? U0 : 2) : U0;
+  const int64_t cap = int64_t(kCUs) * blocks_per_cu;
   int64_t want = (nvec + int64_t(kBlock) * UNROLL - 1) / (int64_t(kBlock) * UNROLL);
-  int grid = int(want < kMaxGrid ? (want < 1 ? 1 : want) : kMaxGrid);
-  hipLaunchKernelGGL((reduce_vec_kernel<T, NSRC, UNROLL>), dim3(grid), dim3(kBlock), 0, s, t, dst, nvec);
+  int grid = int(want < cap ? (want < 1 ? 1 : want) : cap);
+  hipLaunchKernelGGL((reduce_vec_kernel<T, NSRC, UNROLL, POL>), dim3(grid), dim3(kBlock), 0, s, t, dst, nvec);
+}
+
+template <typename T, int NSRC>
+void launch_vec_n(hipStream_t s, const SrcTable& t, v4u* dst, int64_t nvec, int pol, int blocks_per_cu) {
+  if (pol == kNts) launch_vec_pol<T, NSRC, kNts>(s, t, dst, nvec, blocks_per_cu);
+  else if (pol == kBoth) launch_vec_pol<T, NSRC, kBoth>(s, t, dst, nvec, blocks_per_cu);
+  else launch_vec_pol<T, NSRC, kNtl>(s, t, dst, nvec, blocks_per_cu);
 }
 
 template <typename T, int NSRC>
@@ -289,11 +309,12 @@ void launch_lds_n(hipStream_t s, const SrcTable& t, v4u* dst, int64_t nvec) {
 }
 
 template <typename T>
-void launch_vec(hipStream_t s, const SrcTable& t, int nsrc, v4u* dst, int64_t nvec, bool lds) {
-#define AKKA_CASE(K)                                        \
-  case K:                                                   \
+void launch_vec(hipStream_t s, const SrcTable& t, int nsrc, v4u* dst, int64_t nvec, bool lds, int pol,
+                int blocks_per_cu) {
+#define AKKA_CASE(K)                                                       \
+  case K:                                                                  \
     if (lds && K <= 8) launch_lds_n<T, (K <= 8 ? K : 8)>(s, t, dst, nvec); \
-    else launch_vec_n<T, K>(s, t, dst, nvec);               \
+    else launch_vec_n<T, K>(s, t, dst, nvec, pol, blocks_per_cu);         \
     break;
   switch (nsrc) {
     AKKA_CASE(1)
@@ -325,14 +346,18 @@ inline void check_launch(const char* what) {
 
 }  // namespace
 
-ReduceImpl reduce_impl_from_env() {
-  const char* v = std::getenv("AKKA_REDUCE_IMPL");
+ReduceImpl reduce_impl_from_name(const char* v) {
   if (!v) return ReduceImpl::Auto;
   if (!std::strcmp(v, "vec")) return ReduceImpl::Vec;
   if (!std::strcmp(v, "lds")) return ReduceImpl::Lds;
   if (!std::strcmp(v, "scalar")) return ReduceImpl::Scalar;
+  if (!std::strcmp(v, "vec_nts")) return ReduceImpl::VecNts;
+  if (!std::strcmp(v, "vec_ntl")) return ReduceImpl::VecNtl;
+  if (!std::strcmp(v, "vec_both")) return ReduceImpl::VecBoth;
   return ReduceImpl::Auto;
 }
+
+ReduceImpl reduce_impl_from_env() { return reduce_impl_from_name(std::getenv("AKKA_REDUCE_IMPL")); }
 
 const char* reduce_impl_name(ReduceImpl i) {
   switch (i) {
@@ -342,6 +367,12 @@ const char* reduce_impl_name(ReduceImpl i) {
       return "lds";
     case ReduceImpl::Scalar:
       return "scalar";
+    case ReduceImpl::VecNts:
+      return "vec_nts";
+    case ReduceImpl::VecNtl:
+      return "vec_ntl";
+    case ReduceImpl::VecBoth:
+      return "vec_both";
     default:
       return "auto";
   }
@@ -377,12 +408,29 @@ void launch_reduce(hipStream_t s, const ReduceSpec& spec, DType dt, ReduceImpl i
   }
   const int64_t per_vec = dt == DType::F32 ? 4 : 8;
   const int64_t nvec = aligned ? sp.n / per_vec : 0;
+  const int64_t es_b = dt == DType::F32 ? 4 : 2;
+  const int64_t rbytes = int64_t(sp.nsrc) * sp.n * es_b, wbytes = sp.n * es_b;
   if (impl == ReduceImpl::Auto) {
     // Measured (profiles/README.md): LDS-DMA staging wins while the working set
     // sits in the 256 MiB Infinity Cache (chunk-sized reduces inside a round,
-    // data just landed from xGMI); direct 16-B loads win for HBM-resident streams.
-    const int64_t bytes = int64_t(sp.nsrc + 1) * sp.n * (dt == DType::F32 ? 4 : 2);
-    impl = (bytes <= (int64_t(96) << 20) && sp.nsrc <= 8) ? ReduceImpl::Lds : ReduceImpl::Vec;
+    // data just landed from xGMI); direct 16-B loads win for larger streams.
+    impl = (rbytes + wbytes <= (int64_t(96) << 20) && sp.nsrc <= 8) ? ReduceImpl::Lds : ReduceImpl::Vec;
+  }
+  // Vec load/store policy and grid (bench/stream_variants.hip sweep):
+  //   sources fit the Infinity Cache      -> plain loads, NT stores, 16 blocks/CU
+  //   big stream with a big output        -> NT loads + NT stores, unroll 2, 4 blocks/CU
+  //   otherwise (many sources, <=256 MiB) -> NT loads, plain stores, 4 blocks/CU
+  int pol = kNtl, bpc = 4;
+  if (impl == ReduceImpl::Vec) {
+    if (rbytes <= (int64_t(256) << 20)) pol = kNts, bpc = 16;
+    else if (wbytes >= (int64_t(512) << 20)) pol = kBoth, bpc = 4;
+    else pol = kNtl, bpc = 4;
+  } else if (impl == ReduceImpl::VecNts) {
+    pol = kNts, bpc = 16;
+  } else if (impl == ReduceImpl::VecBoth) {
+    pol = kBoth, bpc = 4;
+  } else if (impl == ReduceImpl::VecNtl) {
+    pol = kNtl, bpc = 8;
   }
   bool filled = false;
   t.head_n = head;
@@ -390,12 +438,13 @@ void launch_reduce(hipStream_t s, const ReduceSpec& spec, DType dt, ReduceImpl i
     // forced scalar path over everything
   } else if (nvec > 0) {
     const bool lds = impl == ReduceImpl::Lds;
+    if (const char* g = std::getenv("AKKA_VEC_BPC")) bpc = std::max(1, std::atoi(g));  // experiments
     t.fill = sp.fill;
     t.fill_value = sp.fill_value;
     t.fill_n = sp.fill ? sp.fill_n : 0;
     filled = true;
-    if (dt == DType::F32) launch_vec<float>(s, t, sp.nsrc, static_cast<v4u*>(sp.dst), nvec, lds);
-    else launch_vec<unsigned short>(s, t, sp.nsrc, static_cast<v4u*>(sp.dst), nvec, lds);
+    if (dt == DType::F32) launch_vec<float>(s, t, sp.nsrc, static_cast<v4u*>(sp.dst), nvec, lds, pol, bpc);
+    else launch_vec<unsigned short>(s, t, sp.nsrc, static_cast<v4u*>(sp.dst), nvec, lds, pol, bpc);
     check_launch("reduce_vec");
   }
   const int64_t done = impl == ReduceImpl::Scalar ? 0 : nvec * per_vec;
