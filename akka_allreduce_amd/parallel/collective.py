@@ -88,6 +88,12 @@ class ThresholdAllreduce:
         if transport not in ("stream", "reactive"):
             raise ValueError("transport must be 'stream' or 'reactive'")
         r, w, local = env_rank_world()
+        import torch.distributed as dist
+
+        if dist.is_available() and dist.is_initialized():
+            # an initialised process group is authoritative (mp.spawn sets no RANK/WORLD_SIZE env)
+            r, w = dist.get_rank(), dist.get_world_size()
+            local = int(os.environ.get("LOCAL_RANK", str(r)))
         self.rank = r if rank is None else int(rank)
         self.world_size = w if world_size is None else int(world_size)
         if device is None:

@@ -1,0 +1,54 @@
+"""torch DDP communication hook: gradient buckets through the threshold allreduce.
+
+    from akka_allreduce_amd.parallel.ddp import ThresholdHookState, threshold_allreduce_hook
+    model = DistributedDataParallel(model)
+    model.register_comm_hook(ThresholdHookState(th_reduce=0.75, th_complete=0.75), threshold_allreduce_hook)
+
+Every DDP bucket becomes one round of a ``ThresholdAllreduce`` (one per
+distinct bucket size, created lazily -- all ranks see the same bucket sequence,
+so creation is collective-safe).  The bucket is replaced by the mean over the
+contributors that made it into the round (per-element ``count``), which is
+what DDP's default hook computes at thresholds 1 (sum / world size) and stays
+unbiased when a straggler's gradients are missing (``count`` lets
+a consumer average partial sums).  With ``transport="reactive"`` on GPUs the
+fast ranks do not wait for slow ones.
+"""
+from typing import Dict, Tuple
+
+import torch
+import torch.distributed as dist
+
+from .collective import ThresholdAllreduce
+
+
+class ThresholdHookState:
+    def __init__(self, *, th_reduce: float = 1.0, th_complete: float = 1.0, max_lag: int = 2,
+                 max_chunk_size: int = 1 << 20, transport: str = "stream", broadcast_lag: int = 2):
+        self.kw = dict(th_reduce=th_reduce, th_complete=th_complete, max_lag=max_lag, max_chunk_size=max_chunk_size,
+                       transport=transport, broadcast_lag=broadcast_lag)
+        self.engines: Dict[Tuple[int, torch.dtype, torch.device], ThresholdAllreduce] = {}
+        self.rounds = 0
+
+    def engine(self, t: torch.Tensor) -> ThresholdAllreduce:
+        key = (t.numel(), t.dtype, t.device)
+        ar = self.engines.get(key)
+        if ar is None:
+            ar = ThresholdAllreduce(t.numel(), dtype=t.dtype, device=t.device, **self.kw)
+            self.engines[key] = ar
+        return ar
+
+
+# (real annotations, not postponed strings: DDP checks them)
+def threshold_allreduce_hook(state: ThresholdHookState, bucket: dist.GradBucket) -> torch.futures.Future[torch.Tensor]:
+    t = bucket.buffer()
+    flat = t.reshape(-1)
+    if flat.dtype not in (torch.float32, torch.bfloat16):
+        work = flat.float()
+    else:
+        work = flat
+    out = state.engine(work)(work.contiguous())
+    mean = out.mean().to(t.dtype).view_as(t)
+    state.rounds += 1
+    fut: torch.futures.Future[torch.Tensor] = torch.futures.Future()
+    fut.set_result(mean)
+    return fut

@@ -1,0 +1,72 @@
+"""DDP communication hook: the threshold allreduce replaces DDP's bucket
+allreduce.  Two CPU processes (gloo); at thresholds 1 training must match
+stock DDP (mean over all ranks), bucket by bucket."""
+import os
+import socket
+
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _train(use_hook, rank, world):
+    from torch.nn.parallel import DistributedDataParallel as DDP
+
+    from akka_allreduce_amd.parallel.ddp import ThresholdHookState, threshold_allreduce_hook
+
+    torch.manual_seed(0)
+    model = torch.nn.Sequential(torch.nn.Linear(32, 64), torch.nn.ReLU(), torch.nn.Linear(64, 8))
+    # small bucket cap -> several buckets of different sizes
+    ddp = DDP(model, bucket_cap_mb=0.004)
+    state = None
+    if use_hook:
+        state = ThresholdHookState(max_chunk_size=100)
+        ddp.register_comm_hook(state, threshold_allreduce_hook)
+    opt = torch.optim.SGD(ddp.parameters(), lr=0.1)
+    g = torch.Generator().manual_seed(100 + rank)
+    for _ in range(3):
+        x = torch.randn(16, 32, generator=g)
+        y = torch.randn(16, 8, generator=g)
+        opt.zero_grad()
+        torch.nn.functional.mse_loss(ddp(x), y).backward()
+        opt.step()
+    return [p.detach().clone() for p in model.parameters()], state
+
+
+def _main(rank, world, port, q):
+    try:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        torch.set_num_threads(1)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        ref, _ = _train(False, rank, world)
+        got, st = _train(True, rank, world)
+        ok = all(torch.allclose(a, b, rtol=1e-5, atol=1e-6) for a, b in zip(ref, got))
+        q.put((rank, ok, st.rounds, len(st.engines)))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover
+        q.put((rank, False, repr(e), 0))
+
+
+def test_ddp_hook_matches_stock_ddp():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_main, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+    for rank, ok, rounds, engines in res:
+        assert ok, (rank, rounds)
+        assert rounds >= 3 and engines >= 1  # one round per bucket per step
