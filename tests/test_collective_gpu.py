@@ -63,3 +63,29 @@ def test_mlp_dp_sgd_through_allreduce():
     x, y = synthetic_batch(256, 64, 10, device=dev)
     losses = [dp_sgd_step(model, x, y, 0.5, ar, bucket) for _ in range(60)]
     assert losses[-1] < 0.5 * losses[0], losses
+
+
+def test_round_captured_in_hip_graph():
+    """An exact-threshold round with fixed buffers captured with
+    torch.cuda.graph (relaxed mode) replays the same GPU work: new input
+    values written before replay() show up summed in the output."""
+    from akka_allreduce_amd.parallel import ThresholdAllreduce
+
+    S = 100_003
+    ar = ThresholdAllreduce(S, max_chunk_size=4096, device=torch.device("cuda", 0))
+    x = torch.randn(S, device="cuda")
+    buf = torch.empty(S, device="cuda")
+    ar(x, out=buf)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(g, stream=s, capture_error_mode="relaxed"):
+            for _ in range(3):
+                out = ar(x, out=buf)
+    for k in range(3):
+        x.copy_(torch.full((S,), float(k + 1), device="cuda"))
+        g.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(out.data, x) and bool((out.count == 1).all())
