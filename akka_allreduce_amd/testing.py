@@ -11,12 +11,12 @@ synchronous, so ``expect_no_msg`` needs no timeout (the reference's
 from __future__ import annotations
 
 from collections import deque
-from typing import Any, Callable, Dict, Iterable, List, Optional, Sequence
+from typing import Any, Callable, Dict, List, Optional, Sequence
 
 import torch
 
 from .data import AllReduceInput, AllReduceInputRequest, AllReduceOutput
-from .messages import CompleteAllreduce, ReduceBlock, ScatterBlock
+from .messages import ReduceBlock, ScatterBlock
 
 
 def _as_list(v: Any) -> List[float]:
