@@ -151,11 +151,18 @@ class ThresholdAllreduce:
         return self.worker.state()
 
     def synchronize(self) -> None:
+        """Drain the reactive transport's in-flight transfers, then wait for
+        this rank's queued device work."""
+        self.drain()
         self.worker.synchronize()
 
     def drain(self, timeout: float = 60.0) -> None:
         """Reactive transport: keep driving until none of this rank's transfers
-        is in flight (slow peers caught up).  Call before tearing down."""
+        is in flight (slow peers caught up).  Call before tearing down and
+        before any other blocking collective: on CPU processes (gloo) a rank's
+        sends are posted only while it polls, so a rank parked in a barrier
+        would stall a peer that still needs its data.  (GPU streams progress
+        on their own; there it only bounds the in-flight work.)"""
         import time
 
         core = self.worker._core

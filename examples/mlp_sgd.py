@@ -36,7 +36,13 @@ def main() -> int:
     p.add_argument("--th-reduce", type=float, default=1.0)
     p.add_argument("--th-complete", type=float, default=1.0)
     p.add_argument("--cpu", action="store_true")
+    p.add_argument("--transport", choices=["stream", "reactive"], default="stream",
+                   help="reactive: straggler-tolerant data path (pair with thresholds < 1)")
+    p.add_argument("--straggler-ms", type=float, default=0.0,
+                   help="the last rank sleeps this long before every step (BASELINE config 4)")
     a = p.parse_args()
+    if a.transport == "reactive" and not a.cpu:
+        os.environ["GPU_MAX_HW_QUEUES"] = "32"  # one stream per peer (read at HIP init)
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -57,11 +63,13 @@ def main() -> int:
     model = MLP(a.d_in, a.hidden, a.classes).to(dev)
     bucket = GradientBucket(list(model.parameters()))
     ar = ThresholdAllreduce(bucket.numel, max_chunk_size=int(a.chunk_mb * (1 << 20)) // 4, device=dev,
-                            th_reduce=a.th_reduce, th_complete=a.th_complete)
+                            th_reduce=a.th_reduce, th_complete=a.th_complete, transport=a.transport)
+    nap = a.straggler_ms / 1e3 if rank == world - 1 and world > 1 else 0.0
     gen = torch.Generator(device=dev).manual_seed(1000 + rank)
     x, y = synthetic_batch(a.batch, a.d_in, a.classes, device=dev, generator=gen)
 
     def sync():
+        ar.drain()  # reactive: finish transfers slower peers still need before a blocking collective
         if dev.type == "cuda":
             torch.cuda.synchronize()
         if world > 1:
@@ -73,9 +81,18 @@ def main() -> int:
     sync()
     t0 = time.perf_counter()
     for _ in range(a.steps):
+        if nap:
+            time.sleep(nap)
         losses.append(dp_sgd_step(model, x, y, a.lr, ar, bucket))
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    own = time.perf_counter() - t0  # this rank's own time (fast ranks vs the straggler)
     sync()
     dt = time.perf_counter() - t0
+    owns = [own]
+    if world > 1:
+        owns = [None] * world
+        dist.all_gather_object(owns, own)
     if world > 1:
         t = torch.tensor([dt], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -86,6 +103,8 @@ def main() -> int:
             "value": round(a.steps / dt, 3), "unit": "steps/s", "n_gpus": world,
             "samples_per_s": round(a.steps * a.batch * world / dt, 1),
             "grad_bytes": bucket.numel * 4, "loss_first": round(losses[0], 4), "loss_last": round(losses[-1], 4),
+            "fast_ranks_steps_per_s": round(a.steps / max(owns[:-1] if world > 1 else owns), 3),
+            "transport": a.transport, "straggler_ms": a.straggler_ms,
             "config": {"d_in": a.d_in, "hidden": a.hidden, "classes": a.classes, "batch_per_rank": a.batch},
         }), flush=True)
     if world > 1:
