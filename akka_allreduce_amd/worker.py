@@ -315,8 +315,11 @@ class AllreduceWorker:
         while round_ not in self._delivered:
             if not self.poll():
                 spins += 1
-                if spins > 64:
-                    _time.sleep(0)  # yield the GIL to other ranks' threads
+                if spins > 8:
+                    # sleep until a pair stream signals (GIL released), not spin
+                    self._core.wait_activity(200)
+                    if spins > 64:
+                        _time.sleep(0)  # CPU (gloo) transport: let other threads run
                 if deadline is not None and _time.monotonic() > deadline:
                     st = self._core.state()
                     raise TimeoutError(f"{self.name}: round {round_} did not complete within {timeout}s "

@@ -187,6 +187,11 @@ class WorkerCore final : public EngineHost {
     return any;
   }
   int32_t in_flight() const { return reactive_link_ ? reactive_link_->in_flight() : 0; }
+  void wait_activity(int64_t timeout_us) {
+    if (!reactive_link_ || self_drive_) return;
+    py::gil_scoped_release nogil;
+    reactive_link_->wait_activity(timeout_us);
+  }
   bool reactive() const { return reactive_link_ != nullptr; }
   void scatter_in(int32_t src, int32_t dest, int32_t chunk, int32_t round, uintptr_t ptr, int64_t len, bool on_host) {
     Payload p{reinterpret_cast<const void*>(ptr), len, PayloadKind::External, on_host};
@@ -384,6 +389,7 @@ PYBIND11_MODULE(_native, m) {
       .def("start", &WorkerCore::start)
       .def("poll", &WorkerCore::poll)
       .def("in_flight", &WorkerCore::in_flight)
+      .def("wait_activity", &WorkerCore::wait_activity)
       .def("reactive", &WorkerCore::reactive)
       .def("scatter_in", &WorkerCore::scatter_in)
       .def("reduce_in", &WorkerCore::reduce_in)

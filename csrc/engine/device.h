@@ -74,6 +74,10 @@ class Device {
   virtual void zero(StreamH s, void* dst, size_t bytes) = 0;
   virtual void fill_i32(StreamH s, int32_t* dst, int32_t value, size_t n) = 0;
 
+  // Run `fn` on a host thread once the stream reaches this point (HIP:
+  // hipLaunchHostFunc; `fn` must not call HIP).  Default: unsupported.
+  virtual bool host_notify(StreamH, std::function<void()>) { return false; }
+
   // Host-device only: deferred execution queue used by the p2p simulator.
   virtual void enqueue_host_op(StreamH, std::function<bool()>) {
     throw AkkaError("enqueue_host_op: not a host device");

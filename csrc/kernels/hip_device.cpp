@@ -149,6 +149,23 @@ class HipDevice final : public Device {
     }
     AKKA_HIP(hipMemcpyAsync(dst, src, bytes, k, static_cast<hipStream_t>(s)));
   }
+  bool host_notify(StreamH s, std::function<void()> fn) override {
+    flush_if(s);
+    auto* heap = new std::function<void()>(std::move(fn));
+    hipError_t e = hipLaunchHostFunc(
+        static_cast<hipStream_t>(s),
+        [](void* arg) {
+          auto* f = static_cast<std::function<void()>*>(arg);
+          (*f)();
+          delete f;
+        },
+        heap);
+    if (e != hipSuccess) {
+      delete heap;
+      return false;
+    }
+    return true;
+  }
   void zero(StreamH s, void* dst, size_t bytes) override {
     if (!bytes) return;
     flush_if(s);

@@ -1,6 +1,7 @@
 #include "reactive_link.h"
 
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 
 namespace akka {
@@ -166,6 +167,7 @@ void ReactiveLink::issue_p1(int32_t r) {
     pd.phase = 1;
     pd.ev = get_event();
     dev_->record(pd.ev, ps);
+    arm(ps);
     pending_.push_back(pd);
     ++s.open;
   }
@@ -226,6 +228,7 @@ void ReactiveLink::issue_p2(int32_t r) {
     }
     pd.ev = get_event();
     dev_->record(pd.ev, ps);
+    arm(ps);
     pending_.push_back(pd);
     ++s.open;
   }
@@ -255,6 +258,25 @@ void ReactiveLink::retire(int32_t r) {
   if (it == rounds_.end() || !it->second.p2_issued || it->second.open > 0 || !it->second.completed) return;
   rounds_.erase(it);
   dp_->release_slot(r);
+}
+
+void ReactiveLink::arm(StreamH s) {
+  if (!notify_ok_ || dev_->is_host()) return;
+  std::shared_ptr<Notifier> n = notifier_;  // outlives the link if a callback fires late
+  notify_ok_ = dev_->host_notify(s, [n]() {
+    {
+      std::lock_guard<std::mutex> lk(n->mu);
+      ++n->count;
+    }
+    n->cv.notify_all();
+  });
+}
+
+void ReactiveLink::wait_activity(int64_t timeout_us) {
+  if (!notify_ok_ || !dev_ || dev_->is_host() || pending_.empty()) return;
+  std::unique_lock<std::mutex> lk(notifier_->mu);
+  notifier_->cv.wait_for(lk, std::chrono::microseconds(timeout_us), [&] { return notifier_->count != seen_; });
+  seen_ = notifier_->count;
 }
 
 bool ReactiveLink::poll() {

@@ -33,8 +33,12 @@
 // host memory behind the receive so the host reads them at poll time.
 #pragma once
 
+#include <atomic>
+#include <condition_variable>
 #include <deque>
 #include <map>
+#include <memory>
+#include <mutex>
 #include <vector>
 
 #include "../engine/engine.h"
@@ -64,6 +68,10 @@ class ReactiveLink final : public Link {
   // Returns true if anything completed.
   bool poll();
   int32_t in_flight() const { return int32_t(pending_.size()); }
+  // Block (without spinning) until a transfer may have completed since the
+  // last call, or `timeout_us` elapsed.  Uses host notifications queued behind
+  // every group; returns immediately if the device cannot notify.
+  void wait_activity(int64_t timeout_us);
   const ReactiveLinkStats& stats() const { return stats_; }
   std::vector<StreamH> peer_streams() const { return streams_; }
 
@@ -110,6 +118,16 @@ class ReactiveLink final : public Link {
   std::vector<int32_t*> pinned_, free_pinned_;
   int32_t* recv_dev_ = nullptr;    // [L][N][kmax]
   ReactiveLinkStats stats_;
+  // completion notifications (host callbacks from the pair streams)
+  struct Notifier {
+    std::mutex mu;
+    std::condition_variable cv;
+    uint64_t count = 0;
+  };
+  std::shared_ptr<Notifier> notifier_ = std::make_shared<Notifier>();
+  uint64_t seen_ = 0;
+  bool notify_ok_ = true;
+  void arm(StreamH s);
 };
 
 }  // namespace akka
