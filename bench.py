@@ -53,6 +53,10 @@ def main() -> int:
     if args.transport == "reactive":
         # one stream per peer: must not share hardware queues (read at HIP init)
         os.environ["GPU_MAX_HW_QUEUES"] = "32"
+    elif int(os.environ.get("WORLD_SIZE", "1")) > 1 and int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 8:
+        # comm + compute + caller (+ RCCL's own) streams each on their own
+        # hardware queue, so chunk reduces never serialise behind transfers
+        os.environ["GPU_MAX_HW_QUEUES"] = "8"
     import torch
     import torch.distributed as dist
 
