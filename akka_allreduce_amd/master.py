@@ -73,6 +73,15 @@ class AllreduceMaster:
         return cls(workers.totalSize, thresholds.thAllreduce, thresholds.thReduce, thresholds.thComplete,
                    workers.maxLag, data.dataSize, data.maxRound, data.maxChunkSize, **kw)
 
+    @staticmethod
+    def startUp(port: int, thresholds: ThresholdConfig, dataConfig: DataConfig, workerConfig: WorkerConfig, **kw):
+        """Reference entry point ``AllreduceMaster.startUp(port, thresholds,
+        dataConfig, workerConfig)`` (M:138-144): a master process listening on
+        ``port`` (TCP control plane).  Returns the running ``MasterProcess``."""
+        from .parallel.cluster import start_master
+
+        return start_master(thresholds, dataConfig, workerConfig, port=int(port), **kw)
+
     # ---- actor API -------------------------------------------------------------
     def tell(self, msg: Any, sender: Any = None) -> None:
         self.receive(msg, sender)

@@ -116,6 +116,22 @@ class AllreduceWorker:
         self._core_reactive = transport == "reactive"
         self.reactive_timeout: Optional[float] = None  # reactive allreduce(): max seconds to wait
 
+    @staticmethod
+    def startUp(port: int, dataSize: int, checkpoint: int = 50, assertMultiple: int = 0,
+                master: Optional[str] = None, **kw):
+        """Reference entry point ``AllreduceWorker.startUp(port, dataSize,
+        checkpoint, assertMultiple)`` (W:348-362): a worker process joining the
+        master (default: the configured seed node, CONF:13-16) with the demo
+        data source and throughput/exactness sink.  Returns the ``WorkerProcess``."""
+        from .config import load_config
+        from .parallel.cluster import start_worker
+
+        if master is None:
+            cfg = load_config(None)
+            master = f"{cfg.cluster.host}:{cfg.cluster.port}"
+        return start_worker(master, int(dataSize), checkpoint=int(checkpoint), assert_multiple=int(assertMultiple),
+                            port=int(port), **kw)
+
     # ------------------------------------------------------------------ actor API
     def tell(self, msg: Any, sender: Any = None) -> None:
         self.receive(msg)

@@ -131,3 +131,22 @@ def test_worker_process_rejects_gpu_transports_on_cpu():
 
     with pytest.raises(ValueError):
         WorkerProcess("127.0.0.1:1", None, None, device="cpu", transport="reactive")
+
+
+def test_reference_startup_entry_points():
+    """AllreduceMaster.startUp / AllreduceWorker.startUp with the reference's
+    signatures (M:138-144, W:348-362) run the README demo shape."""
+    from akka_allreduce_amd import AllreduceMaster, AllreduceWorker
+
+    m = AllreduceMaster.startUp(0, ThresholdConfig(1.0, 1.0, 1.0), DataConfig(10, 2, 20), WorkerConfig(2, 1),
+                                transport="tcp")
+    ws = [AllreduceWorker.startUp(0, 10, 5, 2, master=m.address, printer=lambda *a: None) for _ in range(2)]
+    try:
+        assert m.wait(60)
+        for w in ws:
+            assert w.wait(30)
+            assert w.worker.dataSink.failures == 0 and w.worker.dataSink.rounds >= 20
+    finally:
+        m.stop()
+        for w in ws:
+            w.stop()
