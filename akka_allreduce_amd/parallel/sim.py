@@ -82,7 +82,11 @@ class ReactiveSimCluster:
 
     def start(self, rank: int, x: torch.Tensor) -> None:
         """Rank ``rank`` starts its next round with contribution ``x``."""
-        self.workers[rank].allreduce(x)
+        o = self.workers[rank].allreduce(x)
+        if o is not None:
+            # completed inside the call: keep it -- the simulated streams may
+            # still have ops queued that write its tensors
+            self.outputs[rank][o.iteration] = o
         self._collect(rank)
 
     def _collect(self, rank: int) -> None:

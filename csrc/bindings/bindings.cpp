@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <chrono>
 #include <condition_variable>
+#include <cstdlib>
 #include <cstring>
 #include <deque>
 #include <mutex>
@@ -308,7 +309,10 @@ class WorkerCore final : public EngineHost {
  private:
   void make_reactive_link() {
     AKKA_CHECK(engine_->geometry().N >= 2, "reactive link needs N >= 2");
-    reactive_link_ = std::make_unique<ReactiveLink>(engine_.get(), p2p_.get());
+    // send-slot pool depth = bounded staleness while a peer lags (default 16)
+    int32_t slots = 16;
+    if (const char* v = std::getenv("AKKA_REACTIVE_SLOTS")) slots = std::max(2, std::atoi(v));
+    reactive_link_ = std::make_unique<ReactiveLink>(engine_.get(), p2p_.get(), slots);
     reactive_link_->bind(dp_.get());
     engine_->set_link(reactive_link_.get());
   }

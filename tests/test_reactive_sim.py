@@ -258,3 +258,43 @@ def test_threshold_allreduce_reactive_guards():
     ar = ThresholdAllreduce(16, transport="reactive", rank=0, world_size=1, device="cpu")
     o = ar(torch.arange(16.0))
     assert torch.equal(o.data, torch.arange(16.0))
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_fuzz_small_pool_freezes_and_thresholds(seed, monkeypatch):
+    """Random freezes with a tiny send-slot pool (reclaim by stream wait),
+    random thresholds/lag/geometry: every round of every rank completes, the
+    contributor-mask/count invariant holds, nothing stays in flight."""
+    rng = random.Random(1000 + seed)
+    monkeypatch.setenv("AKKA_REACTIVE_SLOTS", str(rng.choice([2, 3, 4])))
+    n = rng.choice([2, 3, 4])
+    S = rng.choice([9, 64, 130])
+    C = rng.choice([1, 5, 16, 200])
+    th = rng.choice([1.0, 0.75, 0.5])
+    lag = rng.choice([1, 2])
+    cl = ReactiveSimCluster(n, S, C, th_reduce=th, th_complete=th, max_lag=lag, seed=seed)
+    R = 8
+    started = [0] * n
+    frozen_until = [0] * n
+    for step in range(200000):
+        if all(cl.done(i, R - 1) for i in range(n)):
+            break
+        if rng.random() < 0.02:
+            v = rng.randrange(n)
+            frozen_until[v] = step + rng.randrange(5, 200)
+        active = [i for i in range(n) if frozen_until[i] <= step] or [rng.randrange(n)]
+        for i in active:
+            if started[i] < R and (started[i] == 0 or cl.done(i, started[i] - 1)):
+                cl.start(i, _x(i, S))
+                started[i] += 1
+        cl.step(active, shuffle=True)
+    else:
+        raise AssertionError("fuzz run did not finish")
+    cl.settle()
+    for i in range(n):
+        for r in range(R):
+            mask = _check_masks(cl.outputs[i][r], S, n)
+            if th == 1.0:
+                assert bool((mask == (1 << n) - 1).all())
+    cl.drain()
+    assert all(w.state()["link"]["in_flight"] == 0 for w in cl.workers)
