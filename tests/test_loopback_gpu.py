@@ -82,3 +82,19 @@ def test_loopback_completion_before_late_chunks():
             m = o.data.round().long()
             pc = sum(((m >> b) & 1) for b in range(n))
             assert torch.equal(pc.int(), o.count)
+
+
+def test_loopback_n8_64mib_async():
+    """Headline-like shape at N=8 on one GPU: 64 MiB fp32, 4 MiB chunks,
+    async back-to-back rounds into one reused output buffer per rank."""
+    n, S, C = 8, (64 << 20) // 4, (4 << 20) // 4
+    cl = LoopbackCluster(n, S, C, max_lag=2)
+    for r in range(3):
+        xs = [torch.full((S,), float(r * 10 + i), device="cuda") for i in range(n)]
+        outs = cl.allreduce(xs, async_op=True)
+        want = float(sum(r * 10 + i for i in range(n)))
+        for o in outs:
+            o.wait()
+        torch.cuda.synchronize()
+        for o in outs:
+            assert bool((o.data == want).all()) and bool((o.count == n).all())
