@@ -123,10 +123,34 @@ class AllReduceOutput:
                 self._count = self.geometry.expand_counts(self.counts_per_chunk)
         return self._count
 
-    def mean(self) -> torch.Tensor:
-        """Element-wise average over the contributors that made it (0 where none)."""
-        c = self.count.to(self.data.dtype if self.data.is_floating_point() else torch.float32)
-        return torch.where(c > 0, self.data / c.clamp(min=1), torch.zeros_like(self.data))
+    def mean(self, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Element-wise average over the contributors that made it (0 where none).
+
+        On the GPU this is one fused pass (``count_mean`` kernel: each element
+        divided by its chunk's count from the tiny per-chunk table) instead of
+        expanding per-element counts; ``out`` may be any same-shape tensor,
+        including the buffer that was reduced (gradient buckets)."""
+        self.wait()
+        d = self.data
+        g = self.geometry
+        if (d.is_cuda and d.dtype in (torch.float32, torch.bfloat16) and self.counts_per_chunk is not None
+                and g is not None and self._count is None):
+            dst = torch.empty_like(d) if out is None else out
+            pc = self.counts_per_chunk.contiguous()
+            if (dst.is_contiguous() and dst.dtype == d.dtype and dst.device == d.device and dst.numel() == d.numel()
+                    and d.data_ptr() % 16 == 0 and dst.data_ptr() % 16 == 0):
+                from ._native_loader import load
+
+                load().count_mean(dst.data_ptr(), d.data_ptr(), pc.data_ptr(), g.dataSize, g.step, g.workerNum,
+                                  g.maxChunkSize, g.kmax, "bfloat16" if d.dtype == torch.bfloat16 else "float32",
+                                  torch.cuda.current_stream(d.device).cuda_stream)
+                return dst
+        c = self.count.to(d.dtype if d.is_floating_point() else torch.float32)
+        m = torch.where(c > 0, d / c.clamp(min=1), torch.zeros_like(d))
+        if out is None:
+            return m
+        out.copy_(m.view_as(out))
+        return out
 
     def __repr__(self) -> str:  # pragma: no cover - debugging aid
         return f"AllReduceOutput(iteration={self.iteration}, n={self.data.numel()}, dtype={self.data.dtype})"

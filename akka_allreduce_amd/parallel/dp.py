@@ -43,7 +43,10 @@ class GradientBucket:
         if allreduce is None:
             return None
         out = allreduce(self.flat)
-        self.flat.copy_(out.mean().to(self.flat.dtype))
+        if out.data.dtype == self.flat.dtype:
+            out.mean(out=self.flat)  # one fused pass on the GPU, straight into the bucket
+        else:
+            self.flat.copy_(out.mean().to(self.flat.dtype))
         return out
 
 

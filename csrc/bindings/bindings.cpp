@@ -223,6 +223,13 @@ class WorkerCore final : public EngineHost {
     dev_->sync_stream(dev_->compute_stream());
     dev_->sync_stream(dev_->comm_stream());
   }
+  void count_mean(uintptr_t dst, uintptr_t src, uintptr_t counts, uintptr_t stream) {
+    const Geometry& g = engine_->geometry();
+    AKKA_CHECK(dev_ && !dev_->is_host(), "count_mean: device path only");
+    launch_count_mean(reinterpret_cast<hipStream_t>(stream), reinterpret_cast<void*>(dst),
+                      reinterpret_cast<const void*>(src), reinterpret_cast<const int32_t*>(counts), g.S, g.step, g.N,
+                      g.C, dp_->kmax(), dt_);
+  }
   void expand_counts(uintptr_t out, uintptr_t counts, uintptr_t stream) {
     const Geometry& g = engine_->geometry();
     AKKA_CHECK(dev_ && !dev_->is_host(), "expand_counts: device path only");
@@ -406,6 +413,7 @@ PYBIND11_MODULE(_native, m) {
       .def("exec_on_producer", &WorkerCore::exec_on_producer)
       .def("sync_all", &WorkerCore::sync_all)
       .def("expand_counts", &WorkerCore::expand_counts)
+      .def("count_mean", &WorkerCore::count_mean)
       .def("drain", &WorkerCore::drain)
       .def("streams", &WorkerCore::streams)
       .def("state", &WorkerCore::state)
@@ -520,6 +528,12 @@ PYBIND11_MODULE(_native, m) {
                            int32_t kmax, uintptr_t stream) {
     launch_count_expand(as_stream(stream), reinterpret_cast<int32_t*>(out), reinterpret_cast<const int32_t*>(counts),
                         S, step, N, C, kmax);
+  });
+  m.def("count_mean", [](uintptr_t dst, uintptr_t src, uintptr_t counts, int64_t S, int64_t step, int32_t N,
+                         int64_t C, int32_t kmax, std::string dtype, uintptr_t stream) {
+    launch_count_mean(as_stream(stream), reinterpret_cast<void*>(dst), reinterpret_cast<const void*>(src),
+                      reinterpret_cast<const int32_t*>(counts), S, step, N, C, kmax,
+                      dtype == "bfloat16" ? DType::BF16 : DType::F32);
   });
   m.def("geometry", [](int64_t S, int32_t N, int64_t C) {
     Geometry g(S, N, C);

@@ -282,6 +282,48 @@ __global__ __launch_bounds__(kBlock) void count_expand_kernel(int32_t* __restric
   }
 }
 
+// dst[i] = src[i] / count(block(i), chunk(i)), 0 where the count is 0: the
+// count-weighted mean of an allreduce output (AllReduceOutput.mean) in one
+// pass, reading the tiny per-chunk count table instead of a per-element one.
+// Same region walk as count_expand (one wave-uniform count per region).
+template <typename T>
+__global__ __launch_bounds__(kBlock) void count_mean_kernel(T* __restrict__ dst, const T* __restrict__ src,
+                                                            const int32_t* __restrict__ counts, int64_t S,
+                                                            int64_t step, int32_t N, int64_t C, int32_t kmax) {
+  constexpr int E = VecTraits<T>::kElems;
+  const int64_t nregions = int64_t(N) * kmax;
+  for (int64_t reg = blockIdx.x; reg < nregions; reg += gridDim.x) {
+    const int32_t j = int32_t(reg / kmax);
+    const int64_t k = reg - int64_t(j) * kmax;
+    const int64_t bs = j * step < S ? j * step : S;
+    const int64_t be = j >= N - 1 ? S : ((j + 1) * step < S ? (j + 1) * step : S);
+    const int64_t s = bs + k * C;
+    if (s >= be) continue;
+    const int64_t e = s + C < be ? s + C : be;
+    const int32_t v = counts[reg];
+    const float fv = float(v);
+    int64_t a = (s + E - 1) & ~int64_t(E - 1);  // first 16-B aligned element
+    if (a > e) a = e;
+    const int64_t nv = (e - a) / E;
+    if (blockIdx.y == 0) {
+      for (int64_t i = s + threadIdx.x; i < a; i += kBlock) dst[i] = from_f<T>(v > 0 ? to_f(src[i]) / fv : 0.f);
+      for (int64_t i = a + nv * E + threadIdx.x; i < e; i += kBlock)
+        dst[i] = from_f<T>(v > 0 ? to_f(src[i]) / fv : 0.f);
+    }
+    const v4u* s4 = reinterpret_cast<const v4u*>(src + a);
+    v4u* d4 = reinterpret_cast<v4u*>(dst + a);
+    for (int64_t i = int64_t(blockIdx.y) * kBlock + threadIdx.x; i < nv; i += int64_t(kBlock) * gridDim.y) {
+      float acc[E];
+#pragma unroll
+      for (int q = 0; q < E; ++q) acc[q] = 0.f;
+      add_vec(acc, s4[i], T{});
+#pragma unroll
+      for (int q = 0; q < E; ++q) acc[q] = v > 0 ? acc[q] / fv : 0.f;
+      d4[i] = pack_vec(acc);
+    }
+  }
+}
+
 template <typename T, int NSRC, int POL>
 void launch_vec_pol(hipStream_t s, const SrcTable& t, v4u* dst, int64_t nvec, int blocks_per_cu) {
   constexpr int U0 = NSRC <= 4 ? 4 : (NSRC <= 8 ? 2 : 1);
@@ -486,6 +528,28 @@ void launch_count_expand(hipStream_t s, int32_t* out, const int32_t* counts, int
   if (split < 1) split = 1;
   hipLaunchKernelGGL(count_expand_kernel, dim3(grid, split), dim3(kBlock), 0, s, out, counts, S, step, N, C, kmax);
   check_launch("count_expand");
+}
+
+void launch_count_mean(hipStream_t s, void* dst, const void* src, const int32_t* counts, int64_t S, int64_t step,
+                       int32_t N, int64_t C, int32_t kmax, DType dt) {
+  if (S <= 0) return;
+  AKKA_CHECK((reinterpret_cast<uintptr_t>(dst) & 15) == 0 && (reinterpret_cast<uintptr_t>(src) & 15) == 0,
+             "count_mean: buffers must be 16-B aligned");
+  const int64_t regions = int64_t(N) * kmax;
+  int grid = int(regions < kMaxGrid ? regions : kMaxGrid);
+  int split = int(kMaxGrid / grid);
+  const int64_t per_region_vecs = (S / regions) / 4 + 1;
+  const int64_t useful = (per_region_vecs + kBlock - 1) / kBlock;
+  if (split > useful) split = int(useful);
+  if (split < 1) split = 1;
+  if (dt == DType::F32)
+    hipLaunchKernelGGL(count_mean_kernel<float>, dim3(grid, split), dim3(kBlock), 0, s, static_cast<float*>(dst),
+                       static_cast<const float*>(src), counts, S, step, N, C, kmax);
+  else
+    hipLaunchKernelGGL(count_mean_kernel<unsigned short>, dim3(grid, split), dim3(kBlock), 0, s,
+                       static_cast<unsigned short*>(dst), static_cast<const unsigned short*>(src), counts, S, step, N,
+                       C, kmax);
+  check_launch("count_mean");
 }
 
 }  // namespace akka

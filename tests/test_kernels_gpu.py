@@ -73,3 +73,22 @@ def test_chunk_reduce_common_misalignment(dtype, off, nsrc):
     chunk_reduce(srcs, out=out)
     want = torch.stack([x.float() for x in srcs]).sum(0).to(dtype)
     assert torch.equal(out, want)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("S,N,C", [(1000, 4, 64), (100_003, 3, 777), (5, 4, 1), (1 << 20, 8, 1 << 14), (77, 2, 100)])
+def test_count_mean_matches_torch(dtype, S, N, C):
+    """Fused AllReduceOutput.mean (count_mean kernel) == torch.where(c>0, x/c, 0)
+    with per-element counts expanded from the per-chunk table (incl. zeros)."""
+    from akka_allreduce_amd.data import AllReduceOutput
+
+    g = Geometry(S, N, C)
+    x = torch.randn(S, device="cuda").to(dtype)
+    pc = torch.randint(0, N + 1, (N, g.kmax), device="cuda", dtype=torch.int32)
+    o = AllReduceOutput(x, counts_per_chunk=pc, geometry=g)
+    got = o.mean()
+    c = g.expand_counts(pc.cpu()).cuda().to(dtype)
+    want = torch.where(c > 0, x / c.clamp(min=1), torch.zeros_like(x))
+    assert torch.equal(got, want)
+    buf = torch.empty_like(x)
+    assert o.mean(out=buf) is buf and torch.equal(buf, want)
