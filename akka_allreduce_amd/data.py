@@ -123,6 +123,31 @@ class AllReduceOutput:
                 self._count = self.geometry.expand_counts(self.counts_per_chunk)
         return self._count
 
+    def _fused_ok(self, dst: torch.Tensor) -> bool:
+        d, g = self.data, self.geometry
+        return (d.is_cuda and d.dtype in (torch.float32, torch.bfloat16) and self.counts_per_chunk is not None
+                and g is not None and self._count is None and dst.is_contiguous() and dst.dtype == d.dtype
+                and dst.device == d.device and dst.numel() == d.numel() and d.data_ptr() % 16 == 0
+                and dst.data_ptr() % 16 == 0)
+
+    def _count_mean(self, dst: torch.Tensor, axpy: bool, alpha: float) -> None:
+        from ._native_loader import load
+
+        d, g = self.data, self.geometry
+        pc = self.counts_per_chunk.contiguous()
+        load().count_mean(dst.data_ptr(), d.data_ptr(), pc.data_ptr(), g.dataSize, g.step, g.workerNum,
+                          g.maxChunkSize, g.kmax, "bfloat16" if d.dtype == torch.bfloat16 else "float32",
+                          torch.cuda.current_stream(d.device).cuda_stream, axpy, float(alpha))
+
+    def axpy_mean_(self, y: torch.Tensor, alpha: float) -> torch.Tensor:
+        """``y += alpha * mean()`` in one fused pass on the GPU (the SGD update
+        of a flat parameter buffer: alpha = -lr); ``y`` is updated in place."""
+        self.wait()
+        if self._fused_ok(y):
+            self._count_mean(y, True, alpha)
+            return y
+        return y.add_(self.mean().view_as(y).to(y.dtype), alpha=alpha)
+
     def mean(self, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Element-wise average over the contributors that made it (0 where none).
 
@@ -132,18 +157,10 @@ class AllReduceOutput:
         including the buffer that was reduced (gradient buckets)."""
         self.wait()
         d = self.data
-        g = self.geometry
-        if (d.is_cuda and d.dtype in (torch.float32, torch.bfloat16) and self.counts_per_chunk is not None
-                and g is not None and self._count is None):
+        if d.is_cuda:
             dst = torch.empty_like(d) if out is None else out
-            pc = self.counts_per_chunk.contiguous()
-            if (dst.is_contiguous() and dst.dtype == d.dtype and dst.device == d.device and dst.numel() == d.numel()
-                    and d.data_ptr() % 16 == 0 and dst.data_ptr() % 16 == 0):
-                from ._native_loader import load
-
-                load().count_mean(dst.data_ptr(), d.data_ptr(), pc.data_ptr(), g.dataSize, g.step, g.workerNum,
-                                  g.maxChunkSize, g.kmax, "bfloat16" if d.dtype == torch.bfloat16 else "float32",
-                                  torch.cuda.current_stream(d.device).cuda_stream)
+            if self._fused_ok(dst):
+                self._count_mean(dst, False, 0.0)
                 return dst
         c = self.count.to(d.dtype if d.is_floating_point() else torch.float32)
         m = torch.where(c > 0, d / c.clamp(min=1), torch.zeros_like(d))

@@ -14,7 +14,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
-from ..parallel.dp import AllreduceFn, GradientBucket, sgd_step
+from ..parallel.dp import AllreduceFn, GradientBucket
 
 
 class MLP(nn.Module):
@@ -28,8 +28,12 @@ class MLP(nn.Module):
 
 
 def dp_sgd_step(model: nn.Module, x: torch.Tensor, y: torch.Tensor, lr: float,
-                allreduce: Optional[AllreduceFn], bucket: Optional[GradientBucket] = None) -> float:
-    """forward + backward + gradient allreduce (mean over contributors) + SGD update."""
+                allreduce: Optional[AllreduceFn], bucket: Optional[GradientBucket] = None,
+                sync_loss: bool = True):
+    """forward + backward + gradient allreduce (mean over contributors) + SGD
+    update.  With a bucket built with ``flatten_params=True`` the averaging and
+    the update are one fused pass.  ``sync_loss=False`` returns the loss as a
+    device tensor (no host sync per step)."""
     if bucket is None:
         bucket = getattr(model, "_akka_bucket", None)
         if bucket is None:
@@ -38,9 +42,8 @@ def dp_sgd_step(model: nn.Module, x: torch.Tensor, y: torch.Tensor, lr: float,
     bucket.zero_()
     loss = F.cross_entropy(model(x), y)
     loss.backward()
-    bucket.average(allreduce)
-    sgd_step(bucket.params, lr)
-    return float(loss.detach())
+    bucket.sgd_from(allreduce, lr)
+    return float(loss.detach()) if sync_loss else loss.detach()
 
 
 def synthetic_batch(batch: int, d_in: int, n_classes: int, *, device, generator: Optional[torch.Generator] = None):

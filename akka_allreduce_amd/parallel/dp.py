@@ -21,7 +21,12 @@ AllreduceFn = Callable[[torch.Tensor], AllReduceOutput]
 
 
 class GradientBucket:
-    def __init__(self, params: List[torch.nn.Parameter], dtype: Optional[torch.dtype] = None):
+    """``flatten_params=True`` also moves the parameters into one flat buffer
+    with the gradients' layout, so the SGD update fuses into the averaging
+    (``sgd_from``: one pass ``p -= lr * sum / count`` on the GPU)."""
+
+    def __init__(self, params: List[torch.nn.Parameter], dtype: Optional[torch.dtype] = None,
+                 flatten_params: bool = False):
         self.params = [p for p in params if p.requires_grad]
         if not self.params:
             raise ValueError("no trainable parameters")
@@ -29,10 +34,17 @@ class GradientBucket:
         dt = dtype or self.params[0].dtype
         self.numel = sum(p.numel() for p in self.params)
         self.flat = torch.zeros(self.numel, dtype=dt, device=dev)
+        self.pflat: Optional[torch.Tensor] = None
+        if flatten_params and all(p.dtype == dt for p in self.params):
+            self.pflat = torch.empty(self.numel, dtype=dt, device=dev)
         off = 0
         for p in self.params:
             n = p.numel()
             p.grad = self.flat[off:off + n].view_as(p)
+            if self.pflat is not None:
+                view = self.pflat[off:off + n].view_as(p)
+                view.copy_(p.data)
+                p.data = view
             off += n
 
     def zero_(self) -> None:
@@ -43,11 +55,30 @@ class GradientBucket:
         if allreduce is None:
             return None
         out = allreduce(self.flat)
+        self.average_out(out)  # one fused pass on the GPU, straight into the bucket
+        return out
+
+
+    def sgd_from(self, allreduce: Optional[AllreduceFn], lr: float) -> Optional[AllReduceOutput]:
+        """Average the gradients over the contributors and apply SGD.  With
+        flattened parameters this is one fused pass over the allreduce output
+        (no averaged-gradient tensor is written)."""
+        if allreduce is None:
+            sgd_step(self.params, lr)
+            return None
+        out = allreduce(self.flat)
+        if self.pflat is not None and out.data.dtype == self.pflat.dtype:
+            out.axpy_mean_(self.pflat, -lr)
+        else:
+            self.average_out(out)
+            sgd_step(self.params, lr)
+        return out
+
+    def average_out(self, out: AllReduceOutput) -> None:
         if out.data.dtype == self.flat.dtype:
-            out.mean(out=self.flat)  # one fused pass on the GPU, straight into the bucket
+            out.mean(out=self.flat)
         else:
             self.flat.copy_(out.mean().to(self.flat.dtype))
-        return out
 
 
 def sgd_step(params: List[torch.nn.Parameter], lr: float) -> None:

@@ -530,11 +530,12 @@ PYBIND11_MODULE(_native, m) {
                         S, step, N, C, kmax);
   });
   m.def("count_mean", [](uintptr_t dst, uintptr_t src, uintptr_t counts, int64_t S, int64_t step, int32_t N,
-                         int64_t C, int32_t kmax, std::string dtype, uintptr_t stream) {
+                         int64_t C, int32_t kmax, std::string dtype, uintptr_t stream, bool axpy, float alpha) {
     launch_count_mean(as_stream(stream), reinterpret_cast<void*>(dst), reinterpret_cast<const void*>(src),
                       reinterpret_cast<const int32_t*>(counts), S, step, N, C, kmax,
-                      dtype == "bfloat16" ? DType::BF16 : DType::F32);
-  });
+                      dtype == "bfloat16" ? DType::BF16 : DType::F32, axpy, alpha);
+  }, py::arg("dst"), py::arg("src"), py::arg("counts"), py::arg("S"), py::arg("step"), py::arg("N"), py::arg("C"),
+     py::arg("kmax"), py::arg("dtype"), py::arg("stream"), py::arg("axpy") = false, py::arg("alpha") = 0.f);
   m.def("geometry", [](int64_t S, int32_t N, int64_t C) {
     Geometry g(S, N, C);
     py::dict d;

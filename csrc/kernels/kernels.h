@@ -23,9 +23,10 @@ void launch_reduce(hipStream_t s, const ReduceSpec& spec, DType dt, ReduceImpl i
 // counts[N][kmax] (per block, per chunk) -> out[S] (per element), RB:41-47.
 void launch_count_expand(hipStream_t s, int32_t* out, const int32_t* counts, int64_t S, int64_t step, int32_t N,
                          int64_t C, int32_t kmax);
-// dst = src / per-chunk count (0 where the count is 0), one pass.
+// dst = src / per-chunk count (0 where the count is 0), one pass; with
+// `axpy`: dst += alpha * that mean (fused SGD update).
 void launch_count_mean(hipStream_t s, void* dst, const void* src, const int32_t* counts, int64_t S, int64_t step,
-                       int32_t N, int64_t C, int32_t kmax, DType dt);
+                       int32_t N, int64_t C, int32_t kmax, DType dt, bool axpy = false, float alpha = 0.f);
 // Standalone kernels for tests/bench: out = a (+ b ...) via a pointer table on device.
 ReduceImpl reduce_impl_from_env();
 const char* reduce_impl_name(ReduceImpl i);

@@ -286,10 +286,13 @@ __global__ __launch_bounds__(kBlock) void count_expand_kernel(int32_t* __restric
 // count-weighted mean of an allreduce output (AllReduceOutput.mean) in one
 // pass, reading the tiny per-chunk count table instead of a per-element one.
 // Same region walk as count_expand (one wave-uniform count per region).
-template <typename T>
+// AXPY: dst[i] += alpha * mean[i] instead (the SGD update fused into the
+// averaging: one read of the sum, one read + write of the parameters).
+template <typename T, bool AXPY>
 __global__ __launch_bounds__(kBlock) void count_mean_kernel(T* __restrict__ dst, const T* __restrict__ src,
                                                             const int32_t* __restrict__ counts, int64_t S,
-                                                            int64_t step, int32_t N, int64_t C, int32_t kmax) {
+                                                            int64_t step, int32_t N, int64_t C, int32_t kmax,
+                                                            float alpha) {
   constexpr int E = VecTraits<T>::kElems;
   const int64_t nregions = int64_t(N) * kmax;
   for (int64_t reg = blockIdx.x; reg < nregions; reg += gridDim.x) {
@@ -305,10 +308,13 @@ __global__ __launch_bounds__(kBlock) void count_mean_kernel(T* __restrict__ dst,
     int64_t a = (s + E - 1) & ~int64_t(E - 1);  // first 16-B aligned element
     if (a > e) a = e;
     const int64_t nv = (e - a) / E;
+    auto one = [&](int64_t i) {
+      const float m = v > 0 ? to_f(src[i]) / fv : 0.f;
+      dst[i] = from_f<T>(AXPY ? to_f(dst[i]) + alpha * m : m);
+    };
     if (blockIdx.y == 0) {
-      for (int64_t i = s + threadIdx.x; i < a; i += kBlock) dst[i] = from_f<T>(v > 0 ? to_f(src[i]) / fv : 0.f);
-      for (int64_t i = a + nv * E + threadIdx.x; i < e; i += kBlock)
-        dst[i] = from_f<T>(v > 0 ? to_f(src[i]) / fv : 0.f);
+      for (int64_t i = s + threadIdx.x; i < a; i += kBlock) one(i);
+      for (int64_t i = a + nv * E + threadIdx.x; i < e; i += kBlock) one(i);
     }
     const v4u* s4 = reinterpret_cast<const v4u*>(src + a);
     v4u* d4 = reinterpret_cast<v4u*>(dst + a);
@@ -319,6 +325,14 @@ __global__ __launch_bounds__(kBlock) void count_mean_kernel(T* __restrict__ dst,
       add_vec(acc, s4[i], T{});
 #pragma unroll
       for (int q = 0; q < E; ++q) acc[q] = v > 0 ? acc[q] / fv : 0.f;
+      if constexpr (AXPY) {
+        float p[E];
+#pragma unroll
+        for (int q = 0; q < E; ++q) p[q] = 0.f;
+        add_vec(p, d4[i], T{});
+#pragma unroll
+        for (int q = 0; q < E; ++q) acc[q] = p[q] + alpha * acc[q];
+      }
       d4[i] = pack_vec(acc);
     }
   }
@@ -531,7 +545,7 @@ void launch_count_expand(hipStream_t s, int32_t* out, const int32_t* counts, int
 }
 
 void launch_count_mean(hipStream_t s, void* dst, const void* src, const int32_t* counts, int64_t S, int64_t step,
-                       int32_t N, int64_t C, int32_t kmax, DType dt) {
+                       int32_t N, int64_t C, int32_t kmax, DType dt, bool axpy, float alpha) {
   if (S <= 0) return;
   AKKA_CHECK((reinterpret_cast<uintptr_t>(dst) & 15) == 0 && (reinterpret_cast<uintptr_t>(src) & 15) == 0,
              "count_mean: buffers must be 16-B aligned");
@@ -542,13 +556,17 @@ void launch_count_mean(hipStream_t s, void* dst, const void* src, const int32_t*
   const int64_t useful = (per_region_vecs + kBlock - 1) / kBlock;
   if (split > useful) split = int(useful);
   if (split < 1) split = 1;
-  if (dt == DType::F32)
-    hipLaunchKernelGGL(count_mean_kernel<float>, dim3(grid, split), dim3(kBlock), 0, s, static_cast<float*>(dst),
-                       static_cast<const float*>(src), counts, S, step, N, C, kmax);
-  else
-    hipLaunchKernelGGL(count_mean_kernel<unsigned short>, dim3(grid, split), dim3(kBlock), 0, s,
-                       static_cast<unsigned short*>(dst), static_cast<const unsigned short*>(src), counts, S, step, N,
-                       C, kmax);
+#define AKKA_CM(T, AX)                                                                                       \
+  hipLaunchKernelGGL((count_mean_kernel<T, AX>), dim3(grid, split), dim3(kBlock), 0, s, static_cast<T*>(dst), \
+                     static_cast<const T*>(src), counts, S, step, N, C, kmax, alpha)
+  if (dt == DType::F32) {
+    if (axpy) AKKA_CM(float, true);
+    else AKKA_CM(float, false);
+  } else {
+    if (axpy) AKKA_CM(unsigned short, true);
+    else AKKA_CM(unsigned short, false);
+  }
+#undef AKKA_CM
   check_launch("count_mean");
 }
 

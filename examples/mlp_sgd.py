@@ -61,7 +61,7 @@ def main() -> int:
 
     torch.manual_seed(0)  # identical init on every rank
     model = MLP(a.d_in, a.hidden, a.classes).to(dev)
-    bucket = GradientBucket(list(model.parameters()))
+    bucket = GradientBucket(list(model.parameters()), flatten_params=True)  # fused average + SGD
     ar = ThresholdAllreduce(bucket.numel, max_chunk_size=int(a.chunk_mb * (1 << 20)) // 4, device=dev,
                             th_reduce=a.th_reduce, th_complete=a.th_complete, transport=a.transport)
     nap = a.straggler_ms / 1e3 if rank == world - 1 and world > 1 else 0.0
@@ -77,13 +77,13 @@ def main() -> int:
 
     losses = []
     for _ in range(a.warmup):
-        losses.append(dp_sgd_step(model, x, y, a.lr, ar, bucket))
+        losses.append(dp_sgd_step(model, x, y, a.lr, ar, bucket, sync_loss=False))
     sync()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         if nap:
             time.sleep(nap)
-        losses.append(dp_sgd_step(model, x, y, a.lr, ar, bucket))
+        losses.append(dp_sgd_step(model, x, y, a.lr, ar, bucket, sync_loss=False))
     if dev.type == "cuda":
         torch.cuda.synchronize()
     own = time.perf_counter() - t0  # this rank's own time (fast ranks vs the straggler)
@@ -102,7 +102,8 @@ def main() -> int:
             "metric": "2-layer MLP DP-SGD steps/s (gradient threshold allreduce)",
             "value": round(a.steps / dt, 3), "unit": "steps/s", "n_gpus": world,
             "samples_per_s": round(a.steps * a.batch * world / dt, 1),
-            "grad_bytes": bucket.numel * 4, "loss_first": round(losses[0], 4), "loss_last": round(losses[-1], 4),
+            "grad_bytes": bucket.numel * 4, "loss_first": round(float(losses[0]), 4),
+            "loss_last": round(float(losses[-1]), 4),
             "fast_ranks_steps_per_s": round(a.steps / max(owns[:-1] if world > 1 else owns), 3),
             "transport": a.transport, "straggler_ms": a.straggler_ms,
             "config": {"d_in": a.d_in, "hidden": a.hidden, "classes": a.classes, "batch_per_rank": a.batch},

@@ -89,3 +89,39 @@ def test_round_captured_in_hip_graph():
         g.replay()
         torch.cuda.synchronize()
         assert torch.equal(out.data, x) and bool((out.count == 1).all())
+
+
+def test_fused_average_sgd_matches_unfused():
+    """GradientBucket(flatten_params=True): the count-mean + SGD update in one
+    pass gives the same training trajectory as average() + sgd_step()."""
+    from akka_allreduce_amd.models.mlp import MLP, dp_sgd_step, synthetic_batch
+    from akka_allreduce_amd.parallel import ThresholdAllreduce
+    from akka_allreduce_amd.parallel.dp import GradientBucket
+
+    dev = torch.device("cuda", 0)
+    x, y = synthetic_batch(64, 256, 10, device=dev, generator=torch.Generator(device=dev).manual_seed(3))
+    params = []
+    for fused in (False, True):
+        torch.manual_seed(0)
+        model = MLP(256, 512, 10).to(dev)
+        bucket = GradientBucket(list(model.parameters()), flatten_params=fused)
+        ar = ThresholdAllreduce(bucket.numel, max_chunk_size=4096, device=dev)
+        for _ in range(5):
+            dp_sgd_step(model, x, y, 0.1, ar, bucket, sync_loss=False)
+        torch.cuda.synchronize()
+        params.append([p.detach().clone() for p in model.parameters()])
+    for a, b in zip(*params):
+        torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+
+
+def test_axpy_mean_matches_torch():
+    from akka_allreduce_amd.data import AllReduceOutput, Geometry
+
+    S, N, C = 100_003, 4, 999
+    g = Geometry(S, N, C)
+    d = torch.randn(S, device="cuda")
+    pc = torch.randint(0, N + 1, (N, g.kmax), device="cuda", dtype=torch.int32)
+    y = torch.randn(S, device="cuda")
+    want = y + (-0.05) * AllReduceOutput(d, counts_per_chunk=pc, geometry=g).mean()
+    got = AllReduceOutput(d, counts_per_chunk=pc, geometry=g).axpy_mean_(y.clone(), -0.05)
+    torch.testing.assert_close(got, want, rtol=1e-6, atol=1e-6)
