@@ -36,7 +36,9 @@ def parse():
     p.add_argument("--bcast-lag", type=int, default=2)
     p.add_argument("--th-reduce", type=float, default=1.0)
     p.add_argument("--th-complete", type=float, default=1.0)
-    p.add_argument("--compare-rccl", action="store_true", help="also time torch.distributed all_reduce (RCCL)")
+    p.add_argument("--compare-rccl", choices=["auto", "on", "off"], default="auto",
+                   help="also time torch.distributed all_reduce (RCCL) on the same buffer after the timed "
+                        "region -- auto: on for N>1")
     p.add_argument("--no-check", action="store_true")
     p.add_argument("--fresh-out", action="store_true", help="allocate a new output tensor every round")
     p.add_argument("--transport", choices=["stream", "reactive"], default="stream",
@@ -139,22 +141,30 @@ def main() -> int:
             dist.all_reduce(f, op=dist.ReduceOp.MIN)
             ok = bool(f.item())
 
+    # Comparator (outside the timed region): RCCL's own all_reduce on the same
+    # buffer, same N and step count, through a separate nccl (= RCCL) group.
     rccl = None
-    if args.compare_rccl and world > 1:
-        dist.destroy_process_group()
-        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
-        z = x.clone()
-        for _ in range(args.warmup):
-            dist.all_reduce(z)
-        torch.cuda.synchronize()
-        dist.barrier()
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            dist.all_reduce(z)
-        torch.cuda.synchronize()
-        dist.barrier()
-        t1 = time.perf_counter() - t0
-        rccl = nbytes / (t1 / args.steps) / 1e9
+    rccl_err = None
+    compare = (world > 1) if args.compare_rccl == "auto" else (args.compare_rccl == "on")
+    if compare and world > 1:
+        try:
+            grp = dist.new_group(backend="nccl")
+            z = x.clone()
+            for _ in range(args.warmup):
+                dist.all_reduce(z, group=grp)
+            torch.cuda.synchronize()
+            barrier()
+            t0 = time.perf_counter()
+            for _ in range(args.steps):
+                dist.all_reduce(z, group=grp)
+            torch.cuda.synchronize()
+            barrier()
+            t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            rccl = nbytes / (float(t.item()) / args.steps) / 1e9
+            del z
+        except Exception as e:  # the comparator must never cost the headline line
+            rccl_err = f"{type(e).__name__}: {e}"[:200]
 
     st = ar.state()
     if rank == 0:
@@ -192,6 +202,8 @@ def main() -> int:
                                  / max(1, st.get("link", {}).get("rounds", st["stats"]["rounds_completed"]) or 1)),
             "rccl_allreduce_algbw_GBps": round(rccl, 3) if rccl else None,
         }
+        if rccl_err:
+            line["rccl_compare_error"] = rccl_err
         print(json.dumps(line), flush=True)
     if world > 1 and dist.is_initialized():
         dist.barrier()
