@@ -40,6 +40,8 @@ def parse():
                    help="also time torch.distributed all_reduce (RCCL) on the same buffer after the timed "
                         "region -- auto: on for N>1")
     p.add_argument("--no-check", action="store_true")
+    p.add_argument("--watchdog-s", type=float, default=600.0,
+                   help="dump stacks and exit if the run is not done after this many seconds (0: off)")
     p.add_argument("--fresh-out", action="store_true", help="allocate a new output tensor every round")
     p.add_argument("--transport", choices=["stream", "reactive"], default="stream",
                    help="stream: symmetric step schedule on one comm stream (default); reactive: per-peer streams + "
@@ -76,6 +78,13 @@ def main() -> int:
     dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("gloo", rank=rank, world_size=world)
+    if args.watchdog_s > 0:
+        # A wedged rank (e.g. a p2p peer that never arrives) dumps every
+        # thread's stack and exits instead of holding the node until an outer
+        # limit kills it without a trace.
+        import faulthandler
+
+        faulthandler.dump_traceback_later(args.watchdog_s, exit=True)
 
     from akka_allreduce_amd.parallel import ThresholdAllreduce
 
