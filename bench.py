@@ -22,6 +22,7 @@ import sys
 import time
 
 BASELINE_METRIC = "allreduce algbw (GB/s) on 256 MB fp32 buffer at 1/2/4/8 MI355X"
+XGMI_LINK_GBPS = 153.0  # per-link figure used for the analytic bound, not measured here
 
 
 def parse():
@@ -213,6 +214,12 @@ def main() -> int:
         }
         if rccl_err:
             line["rccl_compare_error"] = rccl_err
+        if world == 1:
+            line["note"] = ("N=1 has no peer: the round is one local reduce pass (input -> output), HBM-bound; "
+                            "N>1 is xGMI-bound, compare it with rccl_allreduce_algbw_GBps")
+        else:
+            # direct scatter/broadcast moves S/N per link per phase: algbw <= N*L/2
+            line["xgmi_bound_algbw_GBps"] = round(world * XGMI_LINK_GBPS / 2, 1)
         print(json.dumps(line), flush=True)
     if world > 1 and dist.is_initialized():
         dist.barrier()
