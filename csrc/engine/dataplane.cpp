@@ -478,21 +478,34 @@ void DataPlane::finalize(int32_t round, const std::vector<uint8_t>& landed) {
       if (b.counts) dev_->zero(cs, b.counts + size_t(j) * kmax_ + k0, size_t(k - k0) * sizeof(int32_t));
     }
   }
-  dev_->record(b.done, cs);
+  if (b.exec_on_producer) {
+    dev_->flush(cs);  // the round's launch must not wait for the next round to merge into
+    b.done_lazy = true;
+  } else {
+    dev_->record(b.done, cs);
+  }
   b.finalized = true;
 }
 
+EventH DataPlane::done_event(Binding& b) {
+  if (b.done_lazy) {
+    dev_->record(b.done, b.exec);
+    b.done_lazy = false;
+  }
+  return b.done;
+}
+
 void DataPlane::stream_wait_done(int32_t round, StreamH stream) {
-  const Binding& b = binding(round);
+  Binding& b = binding_mut(round);
   AKKA_CHECK(b.finalized, "round not finalized");
   if (b.exec_on_producer && stream == b.exec) return;  // already in that stream's order
-  dev_->wait(stream, b.done);
+  dev_->wait(stream, done_event(b));
 }
 
 void DataPlane::sync_done(int32_t round) {
-  const Binding& b = binding(round);
+  Binding& b = binding_mut(round);
   AKKA_CHECK(b.finalized, "round not finalized");
-  dev_->sync_event(b.done);
+  dev_->sync_event(done_event(b));
 }
 
 void DataPlane::read_payload(const Payload& p, void* host_dst) const {

@@ -138,8 +138,14 @@ class DataPlane {
     StreamH exec = nullptr;  // stream running this round's compute when exec_on_producer
     bool exec_on_producer = false;
     EventH done = nullptr;
+    // Producer-stream rounds record `done` only when someone asks for it: the
+    // round is already in that stream's order, and a marker between two
+    // back-to-back reduce launches costs the command processor a few us.  A
+    // later record on the same stream covers this round (and possibly more).
+    bool done_lazy = false;
     bool finalized = false;
   };
+  EventH done_event(Binding& b);
   struct Row {
     int32_t round = -1;
     std::vector<uint8_t> self_alias;  // [K_me]: slot[me] of chunk k aliases the input

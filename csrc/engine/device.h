@@ -73,6 +73,8 @@ class Device {
   virtual void copy(StreamH s, void* dst, const void* src, size_t bytes, CopyKind kind) = 0;
   virtual void zero(StreamH s, void* dst, size_t bytes) = 0;
   virtual void fill_i32(StreamH s, int32_t* dst, int32_t value, size_t n) = 0;
+  // Issue any work held back on `s` (reduce launches kept open for merging).
+  virtual void flush(StreamH) {}
 
   // Run `fn` on a host thread once the stream reaches this point (HIP:
   // hipLaunchHostFunc; `fn` must not call HIP).  Default: unsupported.

@@ -185,6 +185,7 @@ class HipDevice final : public Device {
     flush_if(s);
     AKKA_HIP(hipMemsetD32Async(dst, value, n, static_cast<hipStream_t>(s)));
   }
+  void flush(StreamH s) override { flush_if(s); }
 
  private:
   bool mergeable(const ReduceSpec& a, const ReduceSpec& b) const {
