@@ -114,6 +114,8 @@ class AllreduceWorker:
         self._out_override: Dict[int, torch.Tensor] = {}
         self._delivered: set = set()
         self._core_reactive = transport == "reactive"
+        self._fast_source = dataSource is None  # rounds fed by allreduce(): eligible for the native fast path
+        self._fast_pending: Dict[int, Tuple[torch.Tensor, torch.Tensor]] = {}
         self.reactive_timeout: Optional[float] = None  # reactive allreduce(): max seconds to wait
 
     @staticmethod
@@ -279,6 +281,8 @@ class AllreduceWorker:
         order, so a buffer may be reused as soon as its previous round's result
         has been consumed in that order.
         """
+        if self._fast_ok(tensor):
+            return self._fast_allreduce(tensor, async_op, out)
         r = self._next_round
         self._next_round += 1
         self._feed[r] = tensor
@@ -299,6 +303,52 @@ class AllreduceWorker:
             self._async = False
         if self._core.reactive() and r not in self._outputs and not self._core_is_sim():
             self.progress_until(r, self.reactive_timeout)
+        return self._outputs.pop(r, None)
+
+    def _fast_ok(self, tensor: torch.Tensor) -> bool:
+        """Collective-style call on a GPU worker whose rounds complete inside
+        the call (scheduled transport): buffers can be bound natively."""
+        return (self.device.type == "cuda" and not self._core_reactive and self.initialized
+                and self.dataSink is None and self._fast_source and not self._pre_init and not self._rounds
+                and isinstance(tensor, torch.Tensor) and tensor.device == self.device and tensor.dtype == self.dtype
+                and tensor.is_contiguous() and tensor.numel() == self.geometry.dataSize)
+
+    def _fast_allreduce(self, x: torch.Tensor, async_op: bool, out: Optional[torch.Tensor]) -> Optional[AllReduceOutput]:
+        g = self.geometry
+        if out is None:
+            out = torch.empty(g.dataSize, dtype=self.dtype, device=self.device)
+        elif out.numel() != g.dataSize or out.dtype != self.dtype or out.device != self.device \
+                or not out.is_contiguous():
+            raise ValueError("out must be a contiguous tensor of dataSize elements, worker dtype and device")
+        counts = torch.empty(g.workerNum * g.kmax, dtype=torch.int32, device=self.device)
+        r = self._next_round
+        self._next_round += 1
+        stream = torch.cuda.current_stream(self.device)
+        local = g.workerNum == 1  # a purely local round runs on the caller's stream
+        if async_op and not local:
+            # the caller's stream will not wait: keep every buffer alive until
+            # the internal streams are past them
+            self._keep_alive_on_internal_streams(x, out, counts)
+        self._fast_pending[r] = (out, counts)
+        try:
+            with _tracing.range_(f"akka.round {r}"):
+                done = self._core.fast_round(r, x.data_ptr(), out.data_ptr(), counts.data_ptr(), stream.cuda_stream,
+                                             not async_op)
+        except Exception as e:  # tryCatch semantics as in receive()
+            self._fast_pending.pop(r, None)
+            self.errors.append(e)
+            log.error("%s: error in round %d: %s", self.name, r, e)
+            if self.strict:
+                raise
+            return None
+        for d in done:
+            o, c = self._fast_pending.pop(d)
+            event = None
+            if async_op:
+                event = torch.cuda.Event()
+                event.record(stream if local else self._internal_streams()[1])
+            self._outputs[d] = AllReduceOutput(o, iteration=d, counts_per_chunk=c.view(g.workerNum, g.kmax),
+                                               geometry=g, expander=self._expand_counts, event=event)
         return self._outputs.pop(r, None)
 
     # ------------------------------------------------------------------ reactive transport progress

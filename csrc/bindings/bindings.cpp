@@ -306,12 +306,66 @@ class WorkerCore final : public EngineHost {
   int32_t scatter_count(int32_t round, int32_t chunk) const { return engine_->scatter_count(round, chunk); }
   int32_t reduced_arrivals(int32_t round) const { return engine_->reduced_arrivals(round); }
 
+  // ---- fast path ---------------------------------------------------------------
+  // One collective-style round with caller-owned buffers: input, output and
+  // counts are bound natively, so the engine's fetch / alloc_output / deliver
+  // callbacks never enter Python.  Returns the rounds delivered during the call
+  // (the caller builds their outputs); they are already unbound.  With
+  // `stream_wait` the caller's stream is made to wait for each delivered round.
+  std::vector<int32_t> fast_round(int32_t r, uintptr_t in, uintptr_t out, uintptr_t counts, uintptr_t stream,
+                                  bool stream_wait) {
+    AKKA_CHECK(dp_ && dev_ && !dev_->is_host(), "fast_round: device workers only");
+    AKKA_CHECK(!reactive_link_, "fast_round: not for the reactive transport (rounds complete asynchronously)");
+    pre_[r] = Prebound{in, out, counts, stream, stream_wait};
+    fast_delivered_.clear();
+    try {
+      engine_->start(r);
+    } catch (...) {
+      pre_.erase(r);
+      throw;
+    }
+    std::vector<int32_t> got;
+    got.swap(fast_delivered_);
+    for (int32_t d : got) dp_->unbind(d);
+    return got;
+  }
+
   // ---- EngineHost -------------------------------------------------------------
-  void fetch(int32_t round) override { host_.attr("_fetch")(round); }
-  void alloc_output(int32_t round) override { host_.attr("_alloc_output")(round); }
-  void deliver(int32_t round) override { host_.attr("_deliver")(round); }
-  void notify_complete(int32_t round) override { host_.attr("_notify_complete")(round); }
-  void release(int32_t round) override { host_.attr("_release")(round); }
+  void fetch(int32_t round) override {
+    auto it = pre_.find(round);
+    if (it == pre_.end()) {
+      host_.attr("_fetch")(round);
+      return;
+    }
+    dp_->bind_input(round, reinterpret_cast<const void*>(it->second.in), reinterpret_cast<StreamH>(it->second.stream),
+                    true);
+  }
+  void alloc_output(int32_t round) override {
+    auto it = pre_.find(round);
+    if (it == pre_.end()) {
+      host_.attr("_alloc_output")(round);
+      return;
+    }
+    dp_->bind_output(round, reinterpret_cast<void*>(it->second.out), reinterpret_cast<int32_t*>(it->second.counts));
+  }
+  void deliver(int32_t round) override {
+    auto it = pre_.find(round);
+    if (it == pre_.end()) {
+      host_.attr("_deliver")(round);
+      return;
+    }
+    if (it->second.stream_wait) dp_->stream_wait_done(round, reinterpret_cast<StreamH>(it->second.stream));
+    pre_.erase(it);
+    fast_delivered_.push_back(round);
+  }
+  void notify_complete(int32_t round) override {
+    if (pre_.count(round) && host_.attr("master").is_none()) return;  // nobody to tell (collective use)
+    host_.attr("_notify_complete")(round);
+  }
+  void release(int32_t round) override {
+    if (pre_.count(round)) return;  // caller-owned input: nothing to drop
+    host_.attr("_release")(round);
+  }
 
  private:
   void make_reactive_link() {
@@ -329,6 +383,13 @@ class WorkerCore final : public EngineHost {
     stream_link_->bind(dp_.get());
     engine_->set_link(stream_link_.get());
   }
+
+  struct Prebound {
+    uintptr_t in, out, counts, stream;
+    bool stream_wait;
+  };
+  std::unordered_map<int32_t, Prebound> pre_;
+  std::vector<int32_t> fast_delivered_;
 
   py::object host_;
   std::string link_kind_;
@@ -405,6 +466,7 @@ PYBIND11_MODULE(_native, m) {
       .def("scatter_in", &WorkerCore::scatter_in)
       .def("reduce_in", &WorkerCore::reduce_in)
       .def("peer_terminated", &WorkerCore::peer_terminated)
+      .def("fast_round", &WorkerCore::fast_round)
       .def("bind_input", &WorkerCore::bind_input)
       .def("bind_output", &WorkerCore::bind_output)
       .def("unbind", &WorkerCore::unbind)

@@ -125,3 +125,31 @@ def test_axpy_mean_matches_torch():
     want = y + (-0.05) * AllReduceOutput(d, counts_per_chunk=pc, geometry=g).mean()
     got = AllReduceOutput(d, counts_per_chunk=pc, geometry=g).axpy_mean_(y.clone(), -0.05)
     torch.testing.assert_close(got, want, rtol=1e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("async_op", [False, True])
+def test_fast_path_matches_callback_path(async_op):
+    """ThresholdAllreduce rounds bind their buffers natively (no Python
+    callbacks per round); a worker with a user data source takes the callback
+    path.  Both give the same outputs and counts, round after round."""
+    from akka_allreduce_amd import AllreduceWorker, InitWorkers
+
+    dev = torch.device("cuda", 0)
+    S, C = (1 << 18) + 3, 1 << 14
+    xs = [torch.randn(S, device=dev) for _ in range(4)]
+    ar = ThresholdAllreduce(S, max_chunk_size=C, device=dev, rank=0, world_size=1)
+    assert ar.worker._fast_ok(xs[0])
+    fast = [ar(x, async_op=async_op) for x in xs]
+    assert not ar.worker._fast_pending
+
+    got = []
+    w = AllreduceWorker(lambda req: xs[req.iteration], got.append, device=dev, transport="stream", strict=True)
+    w.tell(InitWorkers({0: w}, 1, None, 0, 1.0, 1.0, 2, S, C))
+    assert not w._fast_ok(xs[0])  # user data source: callback path
+    for r in range(len(xs)):
+        w.allreduce(xs[r])
+    for r, (a, b) in enumerate(zip(fast, got)):
+        a.wait()
+        assert a.iteration == b.iteration == r
+        assert torch.equal(a.data, xs[r]) and torch.equal(b.data, xs[r])
+        assert torch.equal(a.count, b.count) and bool((a.count == 1).all())
