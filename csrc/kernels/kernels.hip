@@ -154,13 +154,19 @@ __global__ __launch_bounds__(kBlock) void reduce_vec_kernel(SrcTable srcs, v4u* 
     for (int u = 0; u < UNROLL; ++u) {
       const int64_t i = base + u * stride;
       if (i < nvec) {
-        float acc[E];
+        v4u o;
+        if constexpr (NSRC == 1) {
+          o = v[u][0];  // one contributor: the sum is the value itself, bit for bit (-0.0, NaN payloads)
+        } else {
+          float acc[E];
 #pragma unroll
-        for (int e = 0; e < E; ++e) acc[e] = 0.f;
+          for (int e = 0; e < E; ++e) acc[e] = 0.f;
 #pragma unroll
-        for (int s = 0; s < NSRC; ++s) add_vec(acc, v[u][s], T{});
-        if constexpr (POL == kNtl) dst[i] = pack_vec(acc);
-        else __builtin_nontemporal_store(pack_vec(acc), dst + i);
+          for (int s = 0; s < NSRC; ++s) add_vec(acc, v[u][s], T{});
+          o = pack_vec(acc);
+        }
+        if constexpr (POL == kNtl) dst[i] = o;
+        else __builtin_nontemporal_store(o, dst + i);
       }
     }
   }
