@@ -94,6 +94,7 @@ class AllreduceWorker:
         # host streams are queues this process runs: the simulator steps them,
         # async-callback (gloo) workers step them in poll()
         deferred = bool(transport_spec and transport_spec[0] in ("sim", "async_callback"))
+        self._deferred = deferred
         dev_index = self.device.index if self.device.type == "cuda" else -1
         self._core = n.WorkerCore(self, transport, dev_index, _DTYPES[dtype], deferred, broadcast_lag)
         self.id: int = -1
@@ -116,6 +117,7 @@ class AllreduceWorker:
         self._core_reactive = transport == "reactive"
         self._fast_source = dataSource is None  # rounds fed by allreduce(): eligible for the native fast path
         self._fast_pending: Dict[int, Tuple[torch.Tensor, torch.Tensor]] = {}
+        self.fast_rounds = 0  # rounds that took the native fast path
         self.reactive_timeout: Optional[float] = None  # reactive allreduce(): max seconds to wait
 
     @staticmethod
@@ -306,9 +308,9 @@ class AllreduceWorker:
         return self._outputs.pop(r, None)
 
     def _fast_ok(self, tensor: torch.Tensor) -> bool:
-        """Collective-style call on a GPU worker whose rounds complete inside
-        the call (scheduled transport): buffers can be bound natively."""
-        return (self.device.type == "cuda" and not self._core_reactive and self.initialized
+        """Collective-style call on the scheduled transport, whose rounds
+        complete inside the call: buffers can be bound natively."""
+        return (self.transport == "stream" and not self._deferred and self.initialized
                 and self.dataSink is None and self._fast_source and not self._pre_init and not self._rounds
                 and isinstance(tensor, torch.Tensor) and tensor.device == self.device and tensor.dtype == self.dtype
                 and tensor.is_contiguous() and tensor.numel() == self.geometry.dataSize)
@@ -323,7 +325,9 @@ class AllreduceWorker:
         counts = torch.empty(g.workerNum * g.kmax, dtype=torch.int32, device=self.device)
         r = self._next_round
         self._next_round += 1
-        stream = torch.cuda.current_stream(self.device)
+        cuda = self.device.type == "cuda"
+        async_op = bool(async_op) and cuda
+        stream = torch.cuda.current_stream(self.device) if cuda else None
         local = g.workerNum == 1  # a purely local round runs on the caller's stream
         if async_op and not local:
             # the caller's stream will not wait: keep every buffer alive until
@@ -332,8 +336,8 @@ class AllreduceWorker:
         self._fast_pending[r] = (out, counts)
         try:
             with _tracing.range_(f"akka.round {r}"):
-                done = self._core.fast_round(r, x.data_ptr(), out.data_ptr(), counts.data_ptr(), stream.cuda_stream,
-                                             not async_op)
+                done = self._core.fast_round(r, x.data_ptr(), out.data_ptr(), counts.data_ptr(),
+                                             stream.cuda_stream if cuda else 0, cuda and not async_op)
         except Exception as e:  # tryCatch semantics as in receive()
             self._fast_pending.pop(r, None)
             self.errors.append(e)
@@ -341,6 +345,7 @@ class AllreduceWorker:
             if self.strict:
                 raise
             return None
+        self.fast_rounds += 1
         for d in done:
             o, c = self._fast_pending.pop(d)
             event = None
@@ -348,7 +353,8 @@ class AllreduceWorker:
                 event = torch.cuda.Event()
                 event.record(stream if local else self._internal_streams()[1])
             self._outputs[d] = AllReduceOutput(o, iteration=d, counts_per_chunk=c.view(g.workerNum, g.kmax),
-                                               geometry=g, expander=self._expand_counts, event=event)
+                                               geometry=g, expander=self._expand_counts if cuda else None,
+                                               event=event)
         return self._outputs.pop(r, None)
 
     # ------------------------------------------------------------------ reactive transport progress

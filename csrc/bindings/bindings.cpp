@@ -314,8 +314,8 @@ class WorkerCore final : public EngineHost {
   // `stream_wait` the caller's stream is made to wait for each delivered round.
   std::vector<int32_t> fast_round(int32_t r, uintptr_t in, uintptr_t out, uintptr_t counts, uintptr_t stream,
                                   bool stream_wait) {
-    AKKA_CHECK(dp_ && dev_ && !dev_->is_host(), "fast_round: device workers only");
-    AKKA_CHECK(!reactive_link_, "fast_round: not for the reactive transport (rounds complete asynchronously)");
+    AKKA_CHECK(dp_ && dev_ && stream_link_, "fast_round: scheduled (stream) transport only");
+    AKKA_CHECK(!deferred_, "fast_round: deferred host streams complete rounds outside the call");
     pre_[r] = Prebound{in, out, counts, stream, stream_wait};
     fast_delivered_.clear();
     try {
@@ -338,7 +338,7 @@ class WorkerCore final : public EngineHost {
       return;
     }
     dp_->bind_input(round, reinterpret_cast<const void*>(it->second.in), reinterpret_cast<StreamH>(it->second.stream),
-                    true);
+                    !dev_->is_host());
   }
   void alloc_output(int32_t round) override {
     auto it = pre_.find(round);
