@@ -56,7 +56,8 @@ class ModelWorker:
         self.out = []
         self.sink = []
 
-    def init(self, id_, N, th_reduce, th_complete, max_lag, S, C):
+    def init(self, id_, N, th_reduce, th_complete, max_lag, S, C, peers=None):
+        self.peers = set(range(N)) if peers is None else set(peers)
         self.id, self.N, self.max_lag = id_, N, max_lag
         self.g = Geometry(S, N, C)
         self.kme = self.g.num_chunks(id_)
@@ -67,6 +68,12 @@ class ModelWorker:
         self.completed = set()
         self.rows = {}  # round -> state
         self.inputs = {}
+
+    def reinit(self, peers):
+        self.peers = set(peers)  # re-init only replaces the peer map (W:87-89)
+
+    def terminated(self, id_):
+        self.peers.discard(id_)
 
     # ---- per-round state (a ring row of the reference) ------------------------
     def row(self, r):
@@ -97,6 +104,8 @@ class ModelWorker:
         data = self.inputs[r]
         for i in range(self.N):
             idx = (i + self.id) % self.N
+            if idx not in self.peers:
+                continue
             for k in range(self.g.num_chunks(idx)):
                 o = self.g.chunk_offset(idx, k)
                 val = data[o:o + self.g.chunk_len(idx, k)]
@@ -135,6 +144,8 @@ class ModelWorker:
             rw["landed"][(self.id, chunk)] = (rw["landed"][(self.id, chunk)][0], val)
         for i in range(self.N):
             idx = (i + self.id) % self.N
+            if idx not in self.peers:
+                continue
             if idx == self.id and self.self_local:
                 self.on_reduce(self.id, idx, chunk, r, len(srcs), val)
             else:

@@ -16,7 +16,8 @@ import torch
 from hypothesis import HealthCheck, given, settings
 
 from akka_allreduce_amd import AllreduceWorker
-from akka_allreduce_amd.messages import CompleteAllreduce, InitWorkers, ReduceBlock, ScatterBlock, StartAllreduce
+from akka_allreduce_amd.messages import (CompleteAllreduce, InitWorkers, ReduceBlock, ScatterBlock, StartAllreduce,
+                                         WorkerTerminated)
 from akka_allreduce_amd.testing import TestProbe
 
 from model_worker import Geometry, ModelWorker
@@ -40,12 +41,19 @@ def scenarios(draw):
     owners = [j for j in range(N) if g.num_chunks(j) > 0]
     val = st.integers(-4, 4).map(float)
     rounds = st.integers(0, MAX_ROUND)
-    kinds = ["start", "reduce"] + (["scatter", "scatter"] if kme > 0 else [])
+    kinds = ["start", "reduce", "membership"] + (["scatter", "scatter"] if kme > 0 else [])
+    subset = st.sets(st.integers(0, N - 1)).map(lambda p: sorted(p | {me}))
     events = []
     for _ in range(draw(st.integers(1, 60))):
         kind = draw(st.sampled_from(kinds))
         if kind == "start":
             events.append(("start", draw(rounds)))
+        elif kind == "membership":  # re-InitWorkers with another peer map (T4/T5), or a peer death
+            others = [j for j in range(N) if j != me]
+            if draw(st.booleans()):
+                events.append(("reinit", draw(subset)))
+            else:
+                events.append(("terminated", draw(st.sampled_from(others))))
         elif kind == "scatter":
             k = draw(st.integers(0, kme - 1))
             vals = draw(st.lists(val, min_size=g.chunk_len(me, k), max_size=g.chunk_len(me, k)))
@@ -55,7 +63,7 @@ def scenarios(draw):
             k = draw(st.integers(0, g.num_chunks(j) - 1))
             vals = draw(st.lists(val, min_size=g.chunk_len(j, k), max_size=g.chunk_len(j, k)))
             events.append(("reduce", j, k, draw(rounds), draw(st.integers(0, N)), vals))
-    return dict(N=N, S=S, C=C, me=me, max_lag=draw(st.integers(0, 3)), th_reduce=draw(st.sampled_from(THRESHOLDS)),
+    return dict(N=N, S=S, C=C, me=me, peers=draw(subset), max_lag=draw(st.integers(0, 3)), th_reduce=draw(st.sampled_from(THRESHOLDS)),
                 th_complete=draw(st.sampled_from(THRESHOLDS)), self_local=draw(st.booleans()), events=events)
 
 
@@ -78,13 +86,21 @@ def run_native(sc, device="cpu"):
                         lambda o: sink.append((o.iteration, [float(v) for v in o.data.tolist()],
                                                [int(c) for c in o.count.tolist()])),
                         device=device, strict=True)
-    peers = {i: probe for i in range(sc["N"])}
-    if sc["self_local"]:
-        peers[sc["me"]] = w
-    w.tell(InitWorkers(peers, sc["N"], probe, sc["me"], sc["th_reduce"], sc["th_complete"], sc["max_lag"], S, sc["C"]))
+    def peer_map(ids):
+        m = {i: probe for i in ids}
+        if sc["self_local"]:
+            m[sc["me"]] = w
+        return m
+
+    w.tell(InitWorkers(peer_map(sc["peers"]), sc["N"], probe, sc["me"], sc["th_reduce"], sc["th_complete"], sc["max_lag"], S, sc["C"]))
     for ev in sc["events"]:
         if ev[0] == "start":
             w.tell(StartAllreduce(ev[1]))
+        elif ev[0] == "reinit":
+            w.tell(InitWorkers(peer_map(ev[1]), sc["N"], probe, sc["me"], sc["th_reduce"], sc["th_complete"],
+                               sc["max_lag"], S, sc["C"]))
+        elif ev[0] == "terminated":
+            w.tell(WorkerTerminated(ev[1]))
         elif ev[0] == "scatter":
             _, src, k, r, vals = ev
             w.tell(ScatterBlock(torch.tensor(vals), src, sc["me"], k, r))
@@ -97,10 +113,14 @@ def run_native(sc, device="cpu"):
 
 def run_model(sc):
     m = ModelWorker(lambda r: source_values(sc["S"], r), self_local=sc["self_local"])
-    m.init(sc["me"], sc["N"], sc["th_reduce"], sc["th_complete"], sc["max_lag"], sc["S"], sc["C"])
+    m.init(sc["me"], sc["N"], sc["th_reduce"], sc["th_complete"], sc["max_lag"], sc["S"], sc["C"], sc["peers"])
     for ev in sc["events"]:
         if ev[0] == "start":
             m.start(ev[1])
+        elif ev[0] == "reinit":
+            m.reinit(ev[1])
+        elif ev[0] == "terminated":
+            m.terminated(ev[1])
         elif ev[0] == "scatter":
             _, src, k, r, vals = ev
             m.on_scatter(src, sc["me"], k, r, vals)
