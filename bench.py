@@ -41,6 +41,9 @@ def parse():
                    help="also time torch.distributed all_reduce (RCCL) on the same buffer after the timed "
                         "region -- auto: on for N>1")
     p.add_argument("--no-check", action="store_true")
+    p.add_argument("--extras", choices=["auto", "on", "off"], default="auto",
+                   help="after the headline, also time BASELINE config 3 (bf16 1 GiB) and config 5 (MLP DP-SGD) "
+                        "-- auto: only for the default headline invocation")
     p.add_argument("--watchdog-s", type=float, default=600.0,
                    help="dump stacks and exit if the run is not done after this many seconds (0: off)")
     p.add_argument("--fresh-out", action="store_true", help="allocate a new output tensor every round")
@@ -51,6 +54,82 @@ def parse():
                    help="async rounds (event hand-off) -- auto: on for N>1 (saves a stream hop per round), off for "
                         "N=1 (local rounds run on the caller's stream, nothing to hop)")
     return p.parse_args()
+
+
+def timed(step, steps: int, warmup: int, world: int, barrier) -> float:
+    """Seconds for `steps` calls of step() (after `warmup`), barrier +
+    synchronize on both sides, max over ranks."""
+    import torch
+    import torch.distributed as dist
+
+    def finish(o):
+        if hasattr(o, "wait"):
+            o.wait()
+        torch.cuda.synchronize()
+        barrier()
+        torch.cuda.synchronize()
+
+    o = None
+    for _ in range(warmup):
+        o = step()
+    finish(o)
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        o = step()
+    finish(o)
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    return dt
+
+
+def run_extras(world: int, dev, barrier) -> dict:
+    """BASELINE config 3 (8-rank bf16, 1 GB buffer, link-sized chunks) and
+    config 5 (2-layer MLP DP-SGD step/s) at this N, on synthetic data."""
+    import torch
+
+    from akka_allreduce_amd.parallel import ThresholdAllreduce
+
+    res: dict = {}
+    keep = []  # communicators stay alive until exit (no per-rank teardown ordering)
+    try:
+        nbytes = 1 << 30
+        S = nbytes // 2
+        ar = ThresholdAllreduce(S, max_chunk_size=(8 << 20) // 2, dtype=torch.bfloat16, device=dev)
+        keep.append(ar)
+        x = torch.randn(S, device=dev, dtype=torch.bfloat16)
+        out = torch.empty_like(x)
+        steps = 10
+        dt = timed(lambda: ar(x, async_op=world > 1, out=out), steps, 3, world, barrier)
+        res["cfg3_bf16_1GiB_chunk8MiB"] = {"algbw_GBps": round(nbytes / (dt / steps) / 1e9, 3),
+                                           "ms_per_step": round(dt / steps * 1e3, 4)}
+        del x, out
+    except Exception as e:
+        res["cfg3_error"] = f"{type(e).__name__}: {e}"[:200]
+    try:
+        from akka_allreduce_amd.models.mlp import MLP, dp_sgd_step, synthetic_batch
+        from akka_allreduce_amd.parallel.dp import GradientBucket
+
+        torch.manual_seed(0)  # identical init on every rank
+        d_in, hidden, classes, batch = 4096, 8192, 1000, 256
+        model = MLP(d_in, hidden, classes).to(dev)
+        bucket = GradientBucket(list(model.parameters()), flatten_params=True)
+        ar = ThresholdAllreduce(bucket.numel, max_chunk_size=(4 << 20) // 4, device=dev)
+        keep.append(ar)
+        gen = torch.Generator(device=dev).manual_seed(1000 + (ar.rank or 0))
+        xb, yb = synthetic_batch(batch, d_in, classes, device=dev, generator=gen)
+        steps = 20
+        dt = timed(lambda: dp_sgd_step(model, xb, yb, 0.05, ar, bucket, sync_loss=False), steps, 5, world, barrier)
+        res["cfg5_mlp_dp_sgd"] = {"steps_per_s": round(steps / dt, 3),
+                                  "samples_per_s": round(steps * batch * world / dt, 1),
+                                  "grad_bytes": bucket.numel * 4,
+                                  "model": f"MLP {d_in}-{hidden}-{classes}, batch {batch}/rank"}
+    except Exception as e:
+        res["cfg5_error"] = f"{type(e).__name__}: {e}"[:200]
+    run_extras.keep = keep  # type: ignore[attr-defined]
+    return res
 
 
 def main() -> int:
@@ -176,6 +255,12 @@ def main() -> int:
         except Exception as e:  # the comparator must never cost the headline line
             rccl_err = f"{type(e).__name__}: {e}"[:200]
 
+    # The other BASELINE configs at the same N, measured after the headline
+    # (same scheduled transport; each guarded so it cannot cost the line).
+    run_extra = args.extras == "on" or (args.extras == "auto" and args.size_mb == 256.0 and args.dtype == "float32"
+                                        and args.transport == "stream")
+    extras = run_extras(world, dev, barrier) if run_extra else None
+
     st = ar.state()
     if rank == 0:
         line = {
@@ -214,6 +299,8 @@ def main() -> int:
         }
         if rccl_err:
             line["rccl_compare_error"] = rccl_err
+        if extras is not None:
+            line["extra_configs"] = extras
         if world == 1:
             line["note"] = ("N=1 has no peer: the round is one local reduce pass (input -> output), HBM-bound; "
                             "N>1 is xGMI-bound, compare it with rccl_allreduce_algbw_GBps")
