@@ -69,7 +69,7 @@ def _worker(a: argparse.Namespace) -> int:
         device = "cuda" if torch.cuda.is_available() else "cpu"
     w = start_worker(master, int(size), checkpoint=a.checkpoint if a.checkpoint is not None else cfg.checkpoint,
                      assert_multiple=a.assert_multiple, port=int(port), device=device, dtype=dtype,
-                     transport=a.transport)
+                     transport=a.transport, host=a.host or "127.0.0.1")
     try:
         while not w.wait(0.5):
             pass
@@ -136,6 +136,8 @@ def main(argv=None) -> int:
     w.add_argument("pos", nargs="*", type=int, help="[port] [dataSize]")
     w.add_argument("--config")
     w.add_argument("--port", type=int)
+    w.add_argument("--host", help="address this worker listens on and announces to the master (multi-machine: "
+                                  "this machine's IP; default 127.0.0.1)")
     w.add_argument("--data-size", type=int)
     w.add_argument("--master", help="host:port of the master")
     w.add_argument("--checkpoint", type=int)
