@@ -69,7 +69,8 @@ def _worker(a: argparse.Namespace) -> int:
         device = "cuda" if torch.cuda.is_available() else "cpu"
     w = start_worker(master, int(size), checkpoint=a.checkpoint if a.checkpoint is not None else cfg.checkpoint,
                      assert_multiple=a.assert_multiple, port=int(port), device=device, dtype=dtype,
-                     transport=a.transport, host=a.host or "127.0.0.1")
+                     transport=a.transport, host=a.host or "127.0.0.1",
+                     metrics_interval_s=cfg.cluster.metrics_interval_s)
     try:
         while not w.wait(0.5):
             pass

@@ -66,6 +66,8 @@ class ClusterSettings:
     heartbeat_interval_s: float = 1.0
     unreachable_after_s: float = 10.0
     registration_timeout_s: float = 5.0  # M:26
+    # Cluster metrics (CONF:26-34): node sample attached to a heartbeat this often (0: off)
+    metrics_interval_s: float = 10.0
 
 
 @dataclass

@@ -98,6 +98,7 @@ class WorkerTerminated:
 class Heartbeat:
     srcId: int
     round: int
+    metrics: Optional[Dict[str, Any]] = None  # node metrics sample (utils/node_metrics.py), when enabled
 
 
 @dataclass

@@ -101,6 +101,7 @@ class MasterProcess:
         self.unreachable_after_s = unreachable_after_s
         self.heartbeat_interval_s = heartbeat_interval_s
         self.last_seen: Dict[int, float] = {}
+        self.node_metrics: Dict[int, Dict[str, Any]] = {}  # latest sample per worker (cluster metrics)
         self.finished = threading.Event()
         self._lock = threading.Lock()
         self.node.on_send_failure = self._send_failed
@@ -137,6 +138,8 @@ class MasterProcess:
                 self.last_seen[wid] = time.time()
         elif isinstance(msg, Heartbeat):
             self.last_seen[int(msg.srcId)] = time.time()
+            if msg.metrics is not None:
+                self.node_metrics[int(msg.srcId)] = msg.metrics
         elif isinstance(msg, CompleteAllreduce):
             self.last_seen[int(msg.srcId)] = time.time()
             self.master.receive(msg)
@@ -185,7 +188,7 @@ def start_master(thresholds: ThresholdConfig, data: DataConfig, workers: WorkerC
 class WorkerProcess:
     def __init__(self, master_address: str, data_source, data_sink, *, host: str = "127.0.0.1", port: int = 0,
                  device: Any = "cpu", dtype: torch.dtype = torch.float32, heartbeat_interval_s: float = 1.0,
-                 transport: str = "auto"):
+                 transport: str = "auto", metrics_interval_s: float = 0.0):
         self.node = Node(host, port, name="worker")
         dev = torch.device(device) if device not in (None, "cpu") else torch.device("cpu")
         if transport == "auto":
@@ -203,6 +206,7 @@ class WorkerProcess:
         self.master = self.node.ref(master_address)
         self.master.tell(RegisterWorker(self.node.address, dev.index if dev.type == "cuda" else None,
                                         socket.gethostname()))
+        self.metrics_interval_s = metrics_interval_s
         self._hb = threading.Thread(target=self._heartbeat, args=(heartbeat_interval_s,), daemon=True,
                                     name="worker-hb")
         self._hb.start()
@@ -226,10 +230,17 @@ class WorkerProcess:
         return self.worker.poll()
 
     def _heartbeat(self, interval: float) -> None:
+        last_metrics = 0.0
         while not self.stopped.is_set():
             time.sleep(interval)
             if self.worker.initialized and not self.stopped.is_set():
-                self.master.tell(Heartbeat(self.worker.id, self.worker.round))
+                metrics = None
+                now = time.time()
+                if self.metrics_interval_s > 0 and now - last_metrics >= self.metrics_interval_s:
+                    from ..utils.node_metrics import sample
+
+                    metrics, last_metrics = sample(), now
+                self.master.tell(Heartbeat(self.worker.id, self.worker.round, metrics))
 
     def wait(self, timeout: Optional[float] = None) -> bool:
         return self.stopped.wait(timeout)

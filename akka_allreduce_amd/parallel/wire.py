@@ -79,7 +79,7 @@ def encode(msg: Any, ref_to_addr: Callable[[Any], Optional[str]]) -> bytes:
     elif isinstance(msg, WorkerTerminated):
         d = {"t": "WorkerTerminated", "workerId": msg.workerId}
     elif isinstance(msg, Heartbeat):
-        d = {"t": "Heartbeat", "srcId": msg.srcId, "round": msg.round}
+        d = {"t": "Heartbeat", "srcId": msg.srcId, "round": msg.round, "metrics": msg.metrics}
     elif isinstance(msg, Shutdown):
         d = {"t": "Shutdown", "reason": msg.reason}
     else:
@@ -112,7 +112,7 @@ def decode(body: bytes, addr_to_ref: Callable[[Optional[str]], Any]) -> Any:
     if t == "WorkerTerminated":
         return WorkerTerminated(d["workerId"])
     if t == "Heartbeat":
-        return Heartbeat(d["srcId"], d["round"])
+        return Heartbeat(d["srcId"], d["round"], d.get("metrics"))
     if t == "Shutdown":
         return Shutdown(d.get("reason", ""))
     raise ValueError(f"unknown message type {t!r}")

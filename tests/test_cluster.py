@@ -52,6 +52,35 @@ def test_scripts_config_four_workers_exact():
     assert sorted(w.worker.id for w in ws) == [0, 1, 2, 3]
 
 
+def test_node_metrics_on_heartbeats():
+    """Cluster metrics (CONF:26-34): workers attach a node sample to heartbeats; master keeps the latest."""
+    from akka_allreduce_amd.messages import Heartbeat
+    from akka_allreduce_amd.parallel.wire import decode, encode
+    from akka_allreduce_amd.utils.node_metrics import sample
+
+    s = sample(gpus=False)
+    assert s["mem_total_mb"] > 0 and s["mem_used_mb"] >= 0 and "cpu_pct" in s
+    hb = decode(encode(Heartbeat(3, 7, s), lambda r: None)[4:], lambda a: None)  # [4:]: frame header
+    assert (hb.srcId, hb.round, hb.metrics) == (3, 7, s)
+    assert decode(encode(Heartbeat(1, 2), lambda r: None)[4:], lambda a: None).metrics is None
+
+    size, rounds = 100, 200
+    m = start_master(ThresholdConfig(1.0, 1.0, 1.0), DataConfig(size, 10, rounds), WorkerConfig(2, 1), port=0,
+                     transport="tcp", unreachable_after_s=30.0, heartbeat_interval_s=0.1)
+    ws = [start_worker(m.address, size, checkpoint=1000, printer=lambda *_: None, heartbeat_interval_s=0.1,
+                       metrics_interval_s=0.05) for _ in range(2)]
+    try:
+        t0 = time.time()
+        while len(m.node_metrics) < 2 and time.time() - t0 < 20:
+            time.sleep(0.05)
+        assert sorted(m.node_metrics) == [0, 1]
+        assert all(v["mem_total_mb"] > 0 for v in m.node_metrics.values())
+    finally:
+        m.stop()
+        for w in ws:
+            w.stop()
+
+
 def test_worker_death_with_thresholds():
     n, size, chunk, rounds = 3, 300, 10, 400
     # thReduce .66 -> 1 of 3 copies, thComplete .3 of 30 chunks, thAllreduce .6 of live workers
