@@ -46,6 +46,8 @@ def parse():
                         "-- auto: only for the default headline invocation")
     p.add_argument("--watchdog-s", type=float, default=600.0,
                    help="dump stacks and exit if the run is not done after this many seconds (0: off)")
+    p.add_argument("--extras-deadline-s", type=float, default=240.0,
+                   help="give up on the extra configs after this many seconds (the headline line is still printed)")
     p.add_argument("--fresh-out", action="store_true", help="allocate a new output tensor every round")
     p.add_argument("--transport", choices=["stream", "reactive"], default="stream",
                    help="stream: symmetric step schedule on one comm stream (default); reactive: per-peer streams + "
@@ -255,58 +257,80 @@ def main() -> int:
         except Exception as e:  # the comparator must never cost the headline line
             rccl_err = f"{type(e).__name__}: {e}"[:200]
 
+    st = ar.state()
+    line = {
+        "metric": BASELINE_METRIC,
+        "value": round(algbw, 3),
+        "unit": "GB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "bf16" if dtype == torch.bfloat16 else "fp32",
+        "data": "synthetic random tensors (torch.randn), exact thresholds",
+        "config": {
+            "model": f"threshold-allreduce {args.size_mb:g}MiB {args.dtype}",
+            "global_batch": world,
+            "seq_len": S,
+            "parallelism": f"dp{world}",
+            "buffer_bytes": nbytes,
+            "chunk_bytes": C * esize,
+            "max_lag": args.max_lag,
+            "broadcast_lag": args.bcast_lag,
+            "thresholds": [1.0, args.th_reduce, args.th_complete],
+            "transport": ("rccl-pair-reactive" if ar.transport == "reactive" else "rccl-p2p-xgmi")
+            if world > 1 else "local",
+            "async_op": args.async_op,
+            "output": "fresh tensor per round" if args.fresh_out else "preallocated, reused",
+        },
+        "busbw_GBps": round(busbw, 3),
+        "exact": ok,
+        "groups_per_round": (st.get("link", {}).get("groups", 0)
+                             / max(1, st.get("link", {}).get("rounds", st["stats"]["rounds_completed"]) or 1)),
+        "rccl_allreduce_algbw_GBps": round(rccl, 3) if rccl else None,
+    }
+    if rccl_err:
+        line["rccl_compare_error"] = rccl_err
+    if world == 1:
+        line["note"] = ("N=1 has no peer: the round is one local reduce pass (input -> output), HBM-bound; "
+                        "N>1 is xGMI-bound, compare it with rccl_allreduce_algbw_GBps")
+    else:
+        # direct scatter/broadcast moves S/N per link per phase: algbw <= N*L/2
+        line["xgmi_bound_algbw_GBps"] = round(world * XGMI_LINK_GBPS / 2, 1)
+
     # The other BASELINE configs at the same N, measured after the headline
-    # (same scheduled transport; each guarded so it cannot cost the line).
+    # (same scheduled transport; each guarded so it cannot cost the line).  A
+    # deadline bounds them too: if they have not finished by then, every rank
+    # exits 0 and rank 0 prints the headline without them.
     run_extra = args.extras == "on" or (args.extras == "auto" and args.size_mb == 256.0 and args.dtype == "float32"
                                         and args.transport == "stream")
-    extras = run_extras(world, dev, barrier) if run_extra else None
+    if run_extra:
+        import threading
 
-    st = ar.state()
+        lock, done = threading.Lock(), []
+
+        def _give_up():
+            with lock:  # held through the exit: the main thread cannot print a second line
+                if done:
+                    return
+                if rank == 0:
+                    line["extras_error"] = f"extras not done after {args.extras_deadline_s:g} s; skipped"
+                    print(json.dumps(line), flush=True)
+                os._exit(0 if ok in (None, True) else 1)
+
+        timer = threading.Timer(args.extras_deadline_s, _give_up)
+        timer.daemon = True
+        timer.start()
+        extras = run_extras(world, dev, barrier)
+        with lock:
+            done.append(True)
+        timer.cancel()
+        line["extra_configs"] = extras
+
     if rank == 0:
-        line = {
-            "metric": BASELINE_METRIC,
-            "value": round(algbw, 3),
-            "unit": "GB/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(ms, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "bf16" if dtype == torch.bfloat16 else "fp32",
-            "data": "synthetic random tensors (torch.randn), exact thresholds",
-            "config": {
-                "model": f"threshold-allreduce {args.size_mb:g}MiB {args.dtype}",
-                "global_batch": world,
-                "seq_len": S,
-                "parallelism": f"dp{world}",
-                "buffer_bytes": nbytes,
-                "chunk_bytes": C * esize,
-                "max_lag": args.max_lag,
-                "broadcast_lag": args.bcast_lag,
-                "thresholds": [1.0, args.th_reduce, args.th_complete],
-                "transport": ("rccl-pair-reactive" if ar.transport == "reactive" else "rccl-p2p-xgmi")
-                if world > 1 else "local",
-                "async_op": args.async_op,
-                "output": "fresh tensor per round" if args.fresh_out else "preallocated, reused",
-            },
-            "busbw_GBps": round(busbw, 3),
-            "exact": ok,
-            "groups_per_round": (st.get("link", {}).get("groups", 0)
-                                 / max(1, st.get("link", {}).get("rounds", st["stats"]["rounds_completed"]) or 1)),
-            "rccl_allreduce_algbw_GBps": round(rccl, 3) if rccl else None,
-        }
-        if rccl_err:
-            line["rccl_compare_error"] = rccl_err
-        if extras is not None:
-            line["extra_configs"] = extras
-        if world == 1:
-            line["note"] = ("N=1 has no peer: the round is one local reduce pass (input -> output), HBM-bound; "
-                            "N>1 is xGMI-bound, compare it with rccl_allreduce_algbw_GBps")
-        else:
-            # direct scatter/broadcast moves S/N per link per phase: algbw <= N*L/2
-            line["xgmi_bound_algbw_GBps"] = round(world * XGMI_LINK_GBPS / 2, 1)
         print(json.dumps(line), flush=True)
     if world > 1 and dist.is_initialized():
         dist.barrier()

@@ -32,3 +32,16 @@ def test_bench_prints_one_baseline_line():
     ex = d["extra_configs"]
     assert ex["cfg3_bf16_1GiB_chunk8MiB"]["algbw_GBps"] > 0, ex
     assert ex["cfg5_mlp_dp_sgd"]["steps_per_s"] > 0, ex
+
+
+def test_bench_extras_deadline_keeps_headline():
+    """Extras that overrun their deadline are dropped; the headline line still prints once, rc 0."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "4", "--warmup", "2",
+                        "--size-mb", "16", "--extras", "on", "--extras-deadline-s", "0.01"],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["exact"] is True and d["value"] > 0
+    assert "extras_error" in d and "extra_configs" not in d
