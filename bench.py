@@ -48,6 +48,8 @@ def parse():
                    help="dump stacks and exit if the run is not done after this many seconds (0: off)")
     p.add_argument("--extras-deadline-s", type=float, default=240.0,
                    help="give up on the extra configs after this many seconds (the headline line is still printed)")
+    p.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
+                   help="cpu: rehearse the multi-rank flow on gloo (CPU tests); numbers are not the metric")
     p.add_argument("--fresh-out", action="store_true", help="allocate a new output tensor every round")
     p.add_argument("--transport", choices=["stream", "reactive"], default="stream",
                    help="stream: symmetric step schedule on one comm stream (default); reactive: per-peer streams + "
@@ -56,6 +58,14 @@ def parse():
                    help="async rounds (event hand-off) -- auto: on for N>1 (saves a stream hop per round), off for "
                         "N=1 (local rounds run on the caller's stream, nothing to hop)")
     return p.parse_args()
+
+
+def _sync() -> None:
+    """Device synchronize (no-op for the --device cpu rehearsal)."""
+    import torch
+
+    if torch.cuda.is_available() and torch.cuda.is_initialized():
+        torch.cuda.synchronize()
 
 
 def timed(step, steps: int, warmup: int, world: int, barrier) -> float:
@@ -67,9 +77,9 @@ def timed(step, steps: int, warmup: int, world: int, barrier) -> float:
     def finish(o):
         if hasattr(o, "wait"):
             o.wait()
-        torch.cuda.synchronize()
+        _sync()
         barrier()
-        torch.cuda.synchronize()
+        _sync()
 
     o = None
     for _ in range(warmup):
@@ -153,11 +163,14 @@ def main() -> int:
         if world == 1 and args.gpus > 1:
             print(f"bench.py: --gpus {args.gpus} needs torch.distributed.run (WORLD_SIZE unset)", file=sys.stderr)
             return 2
-    if not torch.cuda.is_available():
-        print("bench.py: no GPU visible", file=sys.stderr)
-        return 2
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    if args.device == "cpu":
+        dev = torch.device("cpu")
+    else:
+        if not torch.cuda.is_available():
+            print("bench.py: no GPU visible", file=sys.stderr)
+            return 2
+        torch.cuda.set_device(local)
+        dev = torch.device("cuda", local)
     if world > 1:
         dist.init_process_group("gloo", rank=rank, world_size=world)
     if args.watchdog_s > 0:
@@ -199,17 +212,17 @@ def main() -> int:
     for _ in range(args.warmup):
         out = ar(x, async_op=args.async_op, out=out_buf)
     out.wait()
-    torch.cuda.synchronize()
+    _sync()
     barrier()
-    torch.cuda.synchronize()
+    _sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         out = ar(x, async_op=args.async_op, out=out_buf)
     out.wait()
     outs = None
-    torch.cuda.synchronize()
+    _sync()
     barrier()
-    torch.cuda.synchronize()
+    _sync()
     dt = time.perf_counter() - t0
     del out, outs
     if world > 1:
@@ -239,16 +252,16 @@ def main() -> int:
     compare = (world > 1) if args.compare_rccl == "auto" else (args.compare_rccl == "on")
     if compare and world > 1:
         try:
-            grp = dist.new_group(backend="nccl")
+            grp = dist.new_group(backend="nccl" if dev.type == "cuda" else "gloo")
             z = x.clone()
             for _ in range(args.warmup):
                 dist.all_reduce(z, group=grp)
-            torch.cuda.synchronize()
+            _sync()
             barrier()
             t0 = time.perf_counter()
             for _ in range(args.steps):
                 dist.all_reduce(z, group=grp)
-            torch.cuda.synchronize()
+            _sync()
             barrier()
             t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -270,7 +283,8 @@ def main() -> int:
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "bf16" if dtype == torch.bfloat16 else "fp32",
-        "data": "synthetic random tensors (torch.randn), exact thresholds",
+        "data": "synthetic random tensors (torch.randn), exact thresholds"
+        + ("; CPU gloo rehearsal, not the metric" if dev.type == "cpu" else ""),
         "config": {
             "model": f"threshold-allreduce {args.size_mb:g}MiB {args.dtype}",
             "global_batch": world,
@@ -282,7 +296,7 @@ def main() -> int:
             "broadcast_lag": args.bcast_lag,
             "thresholds": [1.0, args.th_reduce, args.th_complete],
             "transport": ("rccl-pair-reactive" if ar.transport == "reactive" else "rccl-p2p-xgmi")
-            if world > 1 else "local",
+            if world > 1 and dev.type == "cuda" else ("gloo-p2p" if world > 1 else "local"),
             "async_op": args.async_op,
             "output": "fresh tensor per round" if args.fresh_out else "preallocated, reused",
         },
@@ -306,7 +320,7 @@ def main() -> int:
     # deadline bounds them too: if they have not finished by then, every rank
     # exits 0 and rank 0 prints the headline without them.
     run_extra = args.extras == "on" or (args.extras == "auto" and args.size_mb == 256.0 and args.dtype == "float32"
-                                        and args.transport == "stream")
+                                        and args.transport == "stream" and dev.type == "cuda")
     if run_extra:
         import threading
 

@@ -1,0 +1,48 @@
+"""bench.py's multi-rank flow rehearsed on CPU (gloo), the way the driver
+launches N>1: torch.distributed.run, one process per rank, rank 0 prints one
+JSON line, every rank exits 0.  Covers the barrier/max-over-ranks timing, the
+exactness check across ranks, the comparator group, and the extras deadline
+(every rank leaves through it).  The RCCL/xGMI data path itself is covered by
+the GPU loopback tests; these numbers are not the metric."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run(n, *extra):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", str(n), "--steps", "3", "--warmup", "1", "--size-mb", "0.5", "--chunk-mb", "0.0625",
+           "--device", "cpu", *extra]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip().startswith("{")]
+    assert len(lines) == 1, r.stdout
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("n,transport", [(2, "stream"), (3, "stream"), (2, "reactive")])
+def test_bench_multirank_line(n, transport):
+    d = _run(n, "--transport", transport)
+    assert d["n_gpus"] == n and d["steps"] == 3 and d["warmup"] == 1
+    assert d["exact"] is True and d["value"] > 0
+    assert d["config"]["parallelism"] == f"dp{n}" and d["config"]["transport"] == "gloo-p2p"
+    assert abs(d["busbw_GBps"] - d["value"] * 2 * (n - 1) / n) < 1e-2
+    assert d["rccl_allreduce_algbw_GBps"] and d["rccl_allreduce_algbw_GBps"] > 0
+
+
+def test_bench_multirank_extras_deadline():
+    d = _run(2, "--extras", "on", "--extras-deadline-s", "0.05")
+    assert d["exact"] is True and "extras_error" in d and "extra_configs" not in d
