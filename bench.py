@@ -169,6 +169,9 @@ def main() -> int:
         if not torch.cuda.is_available():
             print("bench.py: no GPU visible", file=sys.stderr)
             return 2
+        if os.environ.get("AKKA_SHARE_GPU") == "1":
+            # rehearsal only: several ranks on one card (1-GPU box)
+            local %= max(1, torch.cuda.device_count())
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
     if world > 1:
