@@ -29,18 +29,24 @@ class MLP(nn.Module):
 
 def dp_sgd_step(model: nn.Module, x: torch.Tensor, y: torch.Tensor, lr: float,
                 allreduce: Optional[AllreduceFn], bucket: Optional[GradientBucket] = None,
-                sync_loss: bool = True):
+                sync_loss: bool = True, compute_dtype: Optional[torch.dtype] = None):
     """forward + backward + gradient allreduce (mean over contributors) + SGD
     update.  With a bucket built with ``flatten_params=True`` the averaging and
     the update are one fused pass.  ``sync_loss=False`` returns the loss as a
-    device tensor (no host sync per step)."""
+    device tensor (no host sync per step).  ``compute_dtype=torch.bfloat16``
+    runs the forward/backward GEMMs on bf16 MFMA (autocast) while weights,
+    gradients, the allreduce and the update stay fp32."""
     if bucket is None:
         bucket = getattr(model, "_akka_bucket", None)
         if bucket is None:
             bucket = GradientBucket(list(model.parameters()))
             model._akka_bucket = bucket  # type: ignore[attr-defined]
     bucket.zero_()
-    loss = F.cross_entropy(model(x), y)
+    if compute_dtype is not None and compute_dtype != torch.float32:
+        with torch.autocast(device_type=x.device.type, dtype=compute_dtype):
+            loss = F.cross_entropy(model(x), y)
+    else:
+        loss = F.cross_entropy(model(x), y)
     loss.backward()
     bucket.sgd_from(allreduce, lr)
     return float(loss.detach()) if sync_loss else loss.detach()

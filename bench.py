@@ -137,7 +137,15 @@ def run_extras(world: int, dev, barrier) -> dict:
         res["cfg5_mlp_dp_sgd"] = {"steps_per_s": round(steps / dt, 3),
                                   "samples_per_s": round(steps * batch * world / dt, 1),
                                   "grad_bytes": bucket.numel * 4,
-                                  "model": f"MLP {d_in}-{hidden}-{classes}, batch {batch}/rank"}
+                                  "model": f"MLP {d_in}-{hidden}-{classes}, batch {batch}/rank",
+                                  "compute_dtype": "fp32"}
+        # same model/step with bf16 MFMA GEMMs (autocast); fp32 weights, grads,
+        # allreduce and update
+        dt = timed(lambda: dp_sgd_step(model, xb, yb, 0.05, ar, bucket, sync_loss=False,
+                                       compute_dtype=torch.bfloat16), steps, 5, world, barrier)
+        res["cfg5_mlp_dp_sgd_bf16"] = {"steps_per_s": round(steps / dt, 3),
+                                       "samples_per_s": round(steps * batch * world / dt, 1),
+                                       "compute_dtype": "bf16 autocast, fp32 master weights/grads"}
     except Exception as e:
         res["cfg5_error"] = f"{type(e).__name__}: {e}"[:200]
     run_extras.keep = keep  # type: ignore[attr-defined]

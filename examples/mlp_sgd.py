@@ -36,6 +36,8 @@ def main() -> int:
     p.add_argument("--th-reduce", type=float, default=1.0)
     p.add_argument("--th-complete", type=float, default=1.0)
     p.add_argument("--cpu", action="store_true")
+    p.add_argument("--compute-dtype", choices=["float32", "bfloat16"], default="float32",
+                   help="GEMM dtype (bfloat16: autocast onto bf16 MFMA; weights/grads/allreduce stay fp32)")
     p.add_argument("--transport", choices=["stream", "reactive"], default="stream",
                    help="reactive: straggler-tolerant data path (pair with thresholds < 1)")
     p.add_argument("--straggler-ms", type=float, default=0.0,
@@ -67,6 +69,7 @@ def main() -> int:
     nap = a.straggler_ms / 1e3 if rank == world - 1 and world > 1 else 0.0
     gen = torch.Generator(device=dev).manual_seed(1000 + rank)
     x, y = synthetic_batch(a.batch, a.d_in, a.classes, device=dev, generator=gen)
+    cdt = getattr(torch, a.compute_dtype)
 
     def sync():
         ar.drain()  # reactive: finish transfers slower peers still need before a blocking collective
@@ -77,13 +80,13 @@ def main() -> int:
 
     losses = []
     for _ in range(a.warmup):
-        losses.append(dp_sgd_step(model, x, y, a.lr, ar, bucket, sync_loss=False))
+        losses.append(dp_sgd_step(model, x, y, a.lr, ar, bucket, sync_loss=False, compute_dtype=cdt))
     sync()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         if nap:
             time.sleep(nap)
-        losses.append(dp_sgd_step(model, x, y, a.lr, ar, bucket, sync_loss=False))
+        losses.append(dp_sgd_step(model, x, y, a.lr, ar, bucket, sync_loss=False, compute_dtype=cdt))
     if dev.type == "cuda":
         torch.cuda.synchronize()
     own = time.perf_counter() - t0  # this rank's own time (fast ranks vs the straggler)
@@ -105,7 +108,7 @@ def main() -> int:
             "grad_bytes": bucket.numel * 4, "loss_first": round(float(losses[0]), 4),
             "loss_last": round(float(losses[-1]), 4),
             "fast_ranks_steps_per_s": round(a.steps / max(owns[:-1] if world > 1 else owns), 3),
-            "transport": a.transport, "straggler_ms": a.straggler_ms,
+            "transport": a.transport, "straggler_ms": a.straggler_ms, "compute_dtype": a.compute_dtype,
             "config": {"d_in": a.d_in, "hidden": a.hidden, "classes": a.classes, "batch_per_rank": a.batch},
         }), flush=True)
     if world > 1:

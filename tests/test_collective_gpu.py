@@ -65,6 +65,29 @@ def test_mlp_dp_sgd_through_allreduce():
     assert losses[-1] < 0.5 * losses[0], losses
 
 
+def test_mlp_dp_sgd_bf16_autocast_tracks_fp32():
+    """bf16 GEMMs (autocast) with fp32 weights/grads/allreduce: the fused
+    count-mean + SGD bucket still trains, and the first step's update matches
+    the fp32 step to bf16 tolerance."""
+    from akka_allreduce_amd.models.mlp import MLP, dp_sgd_step, synthetic_batch
+    from akka_allreduce_amd.parallel.dp import GradientBucket
+
+    dev = torch.device("cuda", 0)
+    runs = {}
+    for cdt in (torch.float32, torch.bfloat16):
+        torch.manual_seed(0)
+        model = MLP(64, 128, 10).to(dev)
+        bucket = GradientBucket(list(model.parameters()), flatten_params=True)
+        ar = ThresholdAllreduce(bucket.numel, max_chunk_size=4096, device=dev, rank=0, world_size=1)
+        x, y = synthetic_batch(256, 64, 10, device=dev)
+        losses = [dp_sgd_step(model, x, y, 0.5, ar, bucket, compute_dtype=cdt) for _ in range(60)]
+        assert all(p.dtype == torch.float32 for p in model.parameters())
+        runs[cdt] = losses
+    f32, b16 = runs[torch.float32], runs[torch.bfloat16]
+    assert abs(b16[0] - f32[0]) < 2e-2 * abs(f32[0]), (b16[0], f32[0])
+    assert b16[-1] < 0.5 * b16[0], b16
+
+
 def test_round_captured_in_hip_graph():
     """An exact-threshold round with fixed buffers captured with
     torch.cuda.graph (relaxed mode) replays the same GPU work: new input
