@@ -17,19 +17,69 @@ import torch.nn.functional as F
 from ..parallel.dp import AllreduceFn, GradientBucket
 
 
+def _mm_into(a: torch.Tensor, b: torch.Tensor, out: torch.Tensor) -> None:
+    """out <- a @ b, written in place (fp32 out from bf16 operands when the
+    GEMM library can; otherwise one cast pass)."""
+    if a.dtype == out.dtype:
+        torch.mm(a, b, out=out)
+        return
+    try:
+        torch.mm(a, b, out_dtype=out.dtype, out=out)
+    except (TypeError, RuntimeError):
+        out.copy_(torch.mm(a, b))
+
+
+class _LinearIntoBucket(torch.autograd.Function):
+    """Linear layer whose backward writes dW and db straight into the
+    gradient bucket's views (``p.grad``) instead of returning them to
+    autograd: no bucket zeroing and no AccumulateGrad read-modify-write pass
+    over the 167 MB of gradients per step.  Under autocast the GEMMs run in
+    the autocast dtype (bf16 MFMA) and the weight/bias stay fp32."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, gw, gb):
+        dt = torch.get_autocast_dtype(x.device.type) if torch.is_autocast_enabled(x.device.type) else None
+        with torch.autocast(device_type=x.device.type, enabled=False):
+            if dt is not None:
+                xc, wc, bc = x.to(dt), w.to(dt), b.to(dt)
+            else:
+                xc, wc, bc = x, w, b
+            y = F.linear(xc, wc, bc)
+        ctx.save_for_backward(xc, wc)
+        ctx.gw, ctx.gb = gw, gb
+        return y
+
+    @staticmethod
+    def backward(ctx, go):
+        xc, wc = ctx.saved_tensors
+        go2 = go.reshape(-1, go.shape[-1]).to(wc.dtype)
+        _mm_into(go2.t(), xc.reshape(-1, xc.shape[-1]), ctx.gw)
+        torch.sum(go2, 0, dtype=ctx.gb.dtype, out=ctx.gb)
+        gx = (go2 @ wc).reshape(*go.shape[:-1], wc.shape[1]) if ctx.needs_input_grad[0] else None
+        return gx, None, None, None, None
+
+
 class MLP(nn.Module):
     def __init__(self, d_in: int, d_hidden: int, d_out: int):
         super().__init__()
         self.fc1 = nn.Linear(d_in, d_hidden)
         self.fc2 = nn.Linear(d_hidden, d_out)
+        # set by dp_sgd_step when every parameter's .grad is a bucket view
+        self.direct_grads = False
+
+    def _linear(self, fc: nn.Linear, x: torch.Tensor) -> torch.Tensor:
+        if self.direct_grads and torch.is_grad_enabled():
+            return _LinearIntoBucket.apply(x, fc.weight, fc.bias, fc.weight.grad, fc.bias.grad)
+        return fc(x)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        return self.fc2(F.relu(self.fc1(x)))
+        return self._linear(self.fc2, F.relu(self._linear(self.fc1, x)))
 
 
 def dp_sgd_step(model: nn.Module, x: torch.Tensor, y: torch.Tensor, lr: float,
                 allreduce: Optional[AllreduceFn], bucket: Optional[GradientBucket] = None,
-                sync_loss: bool = True, compute_dtype: Optional[torch.dtype] = None):
+                sync_loss: bool = True, compute_dtype: Optional[torch.dtype] = None,
+                direct_grads: bool = True):
     """forward + backward + gradient allreduce (mean over contributors) + SGD
     update.  With a bucket built with ``flatten_params=True`` the averaging and
     the update are one fused pass.  ``sync_loss=False`` returns the loss as a
@@ -41,7 +91,12 @@ def dp_sgd_step(model: nn.Module, x: torch.Tensor, y: torch.Tensor, lr: float,
         if bucket is None:
             bucket = GradientBucket(list(model.parameters()))
             model._akka_bucket = bucket  # type: ignore[attr-defined]
-    bucket.zero_()
+    if isinstance(model, MLP):
+        # backward overwrites every bucket view directly: nothing to zero
+        model.direct_grads = direct_grads and all(p.grad is not None and p.grad._base is bucket.flat
+                                                  for p in model.parameters())
+    if not getattr(model, "direct_grads", False):
+        bucket.zero_()
     if compute_dtype is not None and compute_dtype != torch.float32:
         with torch.autocast(device_type=x.device.type, dtype=compute_dtype):
             loss = F.cross_entropy(model(x), y)

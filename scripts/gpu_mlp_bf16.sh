@@ -1,5 +1,5 @@
 set -o pipefail
-O=gpurun_out/s4b; mkdir -p $O
+O=gpurun_out/${OUTDIR:-s4b}; mkdir -p $O
 export HSA_ENABLE_IPC_MODE_LEGACY=0
 timeout -k 10 200 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_collective_gpu.py tests/test_mlp_cpu.py > $O/pytest.log 2>&1 || { tail -20 $O/pytest.log; exit 1; }
 tail -2 $O/pytest.log

@@ -18,6 +18,25 @@ def _train(cdt, steps=40):
     return losses
 
 
+def test_direct_bucket_grads_match_autograd():
+    """The backward that writes dW/db straight into the bucket views gives
+    the same gradients and update as autograd's zero + accumulate path."""
+    res = {}
+    for direct in (False, True):
+        torch.manual_seed(0)
+        model = MLP(32, 64, 8)
+        bucket = GradientBucket(list(model.parameters()), flatten_params=True)
+        ar = ThresholdAllreduce(bucket.numel, max_chunk_size=1024, device=torch.device("cpu"), rank=0, world_size=1)
+        x, y = synthetic_batch(128, 32, 8, device="cpu")
+        bucket.flat.fill_(123.0)  # stale garbage: the direct path must overwrite it
+        for _ in range(3):
+            dp_sgd_step(model, x, y, 0.1, ar, bucket, direct_grads=direct)
+        assert model.direct_grads == direct
+        res[direct] = (bucket.flat.clone(), torch.cat([p.detach().flatten() for p in model.parameters()]))
+    torch.testing.assert_close(res[True][0], res[False][0], rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(res[True][1], res[False][1], rtol=1e-5, atol=1e-6)
+
+
 def test_mlp_fp32_and_bf16_autocast_train():
     f32 = _train(torch.float32)
     b16 = _train(torch.bfloat16)
