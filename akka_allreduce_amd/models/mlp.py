@@ -64,8 +64,10 @@ class MLP(nn.Module):
         super().__init__()
         self.fc1 = nn.Linear(d_in, d_hidden)
         self.fc2 = nn.Linear(d_hidden, d_out)
-        # set by dp_sgd_step when every parameter's .grad is a bucket view
+        # set by dp_sgd_step for its own forward/backward only (every .grad is
+        # a bucket view); reset before it returns
         self.direct_grads = False
+        self.last_step_direct = False
 
     def _linear(self, fc: nn.Linear, x: torch.Tensor) -> torch.Tensor:
         if self.direct_grads and torch.is_grad_enabled():
@@ -91,18 +93,31 @@ def dp_sgd_step(model: nn.Module, x: torch.Tensor, y: torch.Tensor, lr: float,
         if bucket is None:
             bucket = GradientBucket(list(model.parameters()))
             model._akka_bucket = bucket  # type: ignore[attr-defined]
-    if isinstance(model, MLP):
-        # backward overwrites every bucket view directly: nothing to zero
-        model.direct_grads = direct_grads and all(p.grad is not None and p.grad._base is bucket.flat
-                                                  for p in model.parameters())
-    if not getattr(model, "direct_grads", False):
-        bucket.zero_()
-    if compute_dtype is not None and compute_dtype != torch.float32:
-        with torch.autocast(device_type=x.device.type, dtype=compute_dtype):
+    # zero_grad() (set_to_none) or a reassigned .grad detaches a parameter
+    # from the bucket: put the views back, or the allreduce would average a
+    # buffer autograd no longer writes
+    bucket.rebind()
+    direct = isinstance(model, MLP) and direct_grads and bucket.bound() \
+        and set(map(id, model.parameters())) == set(map(id, bucket.params))
+    try:
+        if direct:
+            # backward overwrites every bucket view directly: nothing to zero.
+            # Only for this step's single forward/backward: any other backward
+            # (micro-batch accumulation, a later plain loss.backward()) must
+            # accumulate as usual.
+            model.direct_grads = True
+        else:
+            bucket.zero_()
+        if compute_dtype is not None and compute_dtype != torch.float32:
+            with torch.autocast(device_type=x.device.type, dtype=compute_dtype):
+                loss = F.cross_entropy(model(x), y)
+        else:
             loss = F.cross_entropy(model(x), y)
-    else:
-        loss = F.cross_entropy(model(x), y)
-    loss.backward()
+        loss.backward()
+    finally:
+        if isinstance(model, MLP):
+            model.direct_grads = False
+            model.last_step_direct = direct
     bucket.sgd_from(allreduce, lr)
     return float(loss.detach()) if sync_loss else loss.detach()
 

@@ -50,6 +50,39 @@ class GradientBucket:
     def zero_(self) -> None:
         self.flat.zero_()
 
+    def bound(self) -> bool:
+        """Is every parameter's ``.grad`` still its view of ``flat``?"""
+        off = 0
+        es = self.flat.element_size()
+        base = self.flat.data_ptr()
+        for p in self.params:
+            g = p.grad
+            if g is None or g.data_ptr() != base + off * es or g.shape != p.shape:
+                return False
+            off += p.numel()
+        return True
+
+    def rebind(self) -> bool:
+        """Re-attach every ``.grad`` that is no longer a view of ``flat``
+        (``zero_grad()`` sets them to ``None`` by default; an optimizer or
+        user code may assign fresh tensors).  Any gradient held outside the
+        bucket is copied into its view first.  Returns True if anything had
+        to be re-attached."""
+        if self.bound():
+            return False
+        off = 0
+        for p in self.params:
+            n = p.numel()
+            view = self.flat[off:off + n].view_as(p)
+            g = p.grad
+            if g is None:
+                view.zero_()
+            elif g.data_ptr() != view.data_ptr():
+                view.copy_(g)
+            p.grad = view
+            off += n
+        return True
+
     def average(self, allreduce: Optional[AllreduceFn]) -> Optional[AllReduceOutput]:
         """flat <- mean over contributors (no-op without an allreduce)."""
         if allreduce is None:

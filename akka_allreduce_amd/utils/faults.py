@@ -112,3 +112,17 @@ def env_straggler_delay(rank: int) -> float:
     if want is None or int(want) != int(rank):
         return 0.0
     return float(os.environ.get("AKKA_FAULT_DELAY_MS", "0")) / 1e3
+
+
+def env_phase_stall(rank: int, phase: str) -> None:
+    """Hang forever at the start of ``phase`` if ``AKKA_FAULT_STALL_RANK`` names
+    this rank and ``AKKA_FAULT_STALL_PHASE`` names the phase: a rank that never
+    posts its side of a collective (tests the phase watchdog's failure line).
+    ``AKKA_FAULT_STALL_MODE=raise`` raises instead (a rank-local error)."""
+    want = os.environ.get("AKKA_FAULT_STALL_RANK")
+    if want is None or int(want) != int(rank) or os.environ.get("AKKA_FAULT_STALL_PHASE") != phase:
+        return
+    if os.environ.get("AKKA_FAULT_STALL_MODE") == "raise":
+        raise RuntimeError(f"injected fault on rank {rank} in phase {phase}")
+    while True:
+        time.sleep(3600)

@@ -44,8 +44,16 @@ def parse():
     p.add_argument("--extras", choices=["auto", "on", "off"], default="auto",
                    help="after the headline, also time BASELINE config 3 (bf16 1 GiB) and config 5 (MLP DP-SGD) "
                         "-- auto: only for the default headline invocation")
-    p.add_argument("--watchdog-s", type=float, default=600.0,
+    p.add_argument("--watchdog-s", type=float, default=900.0,
                    help="dump stacks and exit if the run is not done after this many seconds (0: off)")
+    p.add_argument("--phase-deadline-s", type=float, default=180.0,
+                   help="per-phase deadline (init, rccl_init, warmup, timed, ...): on expiry rank 0 prints one JSON "
+                        "line with failed_phase and the RCCL debug tail, and every rank exits non-zero")
+    p.add_argument("--preflight-deadline-s", type=float, default=120.0,
+                   help="deadline of the exact preflight round run before timing at N>1")
+    p.add_argument("--preflight", choices=["auto", "on"], default="auto",
+                   help="auto: preflight round only at N>1")
+    p.add_argument("--pg-timeout-s", type=float, default=300.0, help="host (gloo) process group timeout")
     p.add_argument("--extras-deadline-s", type=float, default=240.0,
                    help="give up on the extra configs after this many seconds (the headline line is still printed)")
     p.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
@@ -152,6 +160,23 @@ def run_extras(world: int, dev, barrier) -> dict:
     return res
 
 
+def _identity(ar, dev) -> dict:
+    """What this rank runs on, as the transport itself reports it (RCCL:
+    ncclCommCount / ncclCommUserRank / ncclCommCuDevice)."""
+    import torch
+
+    d = {"rank": ar.rank}
+    if dev.type == "cuda":
+        props = torch.cuda.get_device_properties(dev)
+        d["hip_device"] = dev.index
+        d["pci_bus_id"] = getattr(props, "pci_bus_id", None)
+        d["gpu"] = props.name
+    p2p = ar.worker._core.p2p_info()
+    if p2p is not None:
+        d["p2p"] = p2p
+    return d
+
+
 def main() -> int:
     args = parse()
     if args.transport == "reactive":
@@ -161,54 +186,125 @@ def main() -> int:
         # comm + compute + caller (+ RCCL's own) streams each on their own
         # hardware queue, so chunk reduces never serialise behind transfers
         os.environ["GPU_MAX_HW_QUEUES"] = "8"
-    import torch
-    import torch.distributed as dist
-
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            print(f"bench.py: --gpus {args.gpus} needs torch.distributed.run (WORLD_SIZE unset)", file=sys.stderr)
-            return 2
-    if args.device == "cpu":
-        dev = torch.device("cpu")
-    else:
-        if not torch.cuda.is_available():
-            print("bench.py: no GPU visible", file=sys.stderr)
-            return 2
-        if os.environ.get("AKKA_SHARE_GPU") == "1":
-            # rehearsal only: several ranks on one card (1-GPU box)
-            local %= max(1, torch.cuda.device_count())
-        torch.cuda.set_device(local)
-        dev = torch.device("cuda", local)
-    if world > 1:
-        dist.init_process_group("gloo", rank=rank, world_size=world)
-    if args.watchdog_s > 0:
-        # A wedged rank (e.g. a p2p peer that never arrives) dumps every
-        # thread's stack and exits instead of holding the node until an outer
-        # limit kills it without a trace.
-        import faulthandler
+    if world != args.gpus and world == 1 and args.gpus > 1:
+        print(f"bench.py: --gpus {args.gpus} needs torch.distributed.run (WORLD_SIZE unset)", file=sys.stderr)
+        return 2
+    from akka_allreduce_amd.utils.faults import env_phase_stall
+    from akka_allreduce_amd.utils.phases import PhaseGuard, enable_rccl_debug_log
 
-        faulthandler.dump_traceback_later(args.watchdog_s, exit=True)
-
-    from akka_allreduce_amd.parallel import ThresholdAllreduce
+    # RCCL warnings go to a per-rank file whose tail a failure line carries
+    debug_path = enable_rccl_debug_log(rank) if (world > 1 and args.device == "cuda") else ""
+    import torch
+    import torch.distributed as dist
 
     dtype = torch.float32 if args.dtype == "float32" else torch.bfloat16
     esize = 4 if dtype == torch.float32 else 2
     nbytes = int(args.size_mb * (1 << 20))
     S = nbytes // esize
     C = max(1, int(args.chunk_mb * (1 << 20)) // esize)
-    ar = ThresholdAllreduce(S, max_chunk_size=C, dtype=dtype, th_reduce=args.th_reduce, th_complete=args.th_complete,
-                            max_lag=args.max_lag, broadcast_lag=args.bcast_lag, device=dev, transport=args.transport)
+    base = {
+        "metric": BASELINE_METRIC, "value": None, "unit": "GB/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "higher_is_better": True,
+        # a fixed 256 MiB buffer whatever N is: total work is fixed (strong scaling)
+        "scaling": "strong", "vs_baseline": None,
+        "dtype": "bf16" if dtype == torch.bfloat16 else "fp32",
+        "data": "synthetic random tensors (torch.randn), exact thresholds"
+        + ("; CPU gloo rehearsal, not the metric" if args.device == "cpu" else ""),
+        "config": {
+            "model": f"threshold-allreduce {args.size_mb:g}MiB {args.dtype}",
+            "global_batch": world, "seq_len": S, "parallelism": f"dp{world}", "buffer_bytes": nbytes,
+            "chunk_bytes": C * esize, "max_lag": args.max_lag, "broadcast_lag": args.bcast_lag,
+            "thresholds": [1.0, args.th_reduce, args.th_complete],
+        },
+    }
+    guard = PhaseGuard(base, rank, world, debug_path)
+    dl = args.phase_deadline_s
 
-    g = torch.Generator(device=dev)
-    g.manual_seed(1234 + rank)
-    x = torch.randn(S, device=dev, dtype=torch.float32, generator=g).to(dtype)
+    def init():
+        env_phase_stall(rank, "init")
+        if args.device == "cpu":
+            dev = torch.device("cpu")
+        else:
+            if not torch.cuda.is_available():
+                raise RuntimeError("no GPU visible")
+            loc = local
+            if os.environ.get("AKKA_SHARE_GPU") == "1":
+                # rehearsal only: several ranks on one card (1-GPU box)
+                loc %= max(1, torch.cuda.device_count())
+            torch.cuda.set_device(loc)
+            dev = torch.device("cuda", loc)
+        if world > 1:
+            from datetime import timedelta
+
+            dist.init_process_group("gloo", rank=rank, world_size=world, timeout=timedelta(seconds=args.pg_timeout_s))
+        return dev
+
+    dev = guard.run("init", dl, init, agree=False)
+    if args.watchdog_s > 0:
+        # outer bound on the whole run (stacks + exit) on top of the phase deadlines
+        import faulthandler
+
+        faulthandler.dump_traceback_later(args.watchdog_s, exit=True)
+
+    from akka_allreduce_amd.parallel import ThresholdAllreduce
+
+    def rccl_init():
+        env_phase_stall(rank, "rccl_init")
+        return ThresholdAllreduce(S, max_chunk_size=C, dtype=dtype, th_reduce=args.th_reduce,
+                                  th_complete=args.th_complete, max_lag=args.max_lag, broadcast_lag=args.bcast_lag,
+                                  device=dev, transport=args.transport)
+
+    ar = guard.run("rccl_init", dl, rccl_init)
+
+    def identity():
+        me = _identity(ar, dev)
+        if world == 1:
+            return [me]
+        allv = [None] * world
+        dist.all_gather_object(allv, me)
+        for d in allv:
+            p2p = d.get("p2p") or {}
+            if p2p.get("kind", "").startswith("rccl") and (p2p.get("nranks") != world or p2p.get("rank") != d["rank"]):
+                raise RuntimeError(f"rank {d['rank']}: RCCL reports nranks={p2p.get('nranks')} rank={p2p.get('rank')}")
+        return allv
+
+    ranks = guard.run("identity", dl, identity)
+    p2p0 = ranks[0].get("p2p") or {}
+    rccl_kind = str(p2p0.get("kind", "")).startswith("rccl")
 
     def barrier():
         if world > 1:
             dist.barrier()
+
+    def exact_round(tag: str) -> bool:
+        # every rank contributes rank+1 -> sum = N(N+1)/2 exactly, count N
+        y = torch.full((S,), float(rank + 1), device=dev, dtype=dtype)
+        o = ar(y)
+        want = float(world * (world + 1) // 2)
+        ok = bool(torch.all(o.data == want).item()) and bool(torch.all(o.count == world).item())
+        if world > 1:
+            f = torch.tensor([1 if ok else 0])
+            dist.all_reduce(f, op=dist.ReduceOp.MIN)
+            ok = bool(f.item())
+        return ok
+
+    def preflight():
+        # one exact full-size round before anything is timed: a hang or a wrong
+        # sum shows up here, under its own deadline, with its own failure line
+        env_phase_stall(rank, "preflight")
+        if not exact_round("preflight"):
+            raise RuntimeError("preflight round is not exact (sum or counts differ on some rank)")
+        return True
+
+    if world > 1 or args.preflight == "on":
+        guard.run("preflight", args.preflight_deadline_s, preflight)
+
+    g = torch.Generator(device=dev)
+    g.manual_seed(1234 + rank)
+    x = torch.randn(S, device=dev, dtype=torch.float32, generator=g).to(dtype)
 
     # Rounds are issued back to back (async_op, like nccl-tests / torch's
     # async_op=True): every round's output is waited for on the current stream
@@ -220,48 +316,56 @@ def main() -> int:
     args.async_op = (world > 1) if args.async_op == "auto" else (args.async_op == "on")
     if ar.transport == "reactive":
         args.async_op = False  # reactive rounds return once complete (progress is host-polled)
-    for _ in range(args.warmup):
-        out = ar(x, async_op=args.async_op, out=out_buf)
-    out.wait()
-    _sync()
-    barrier()
-    _sync()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        out = ar(x, async_op=args.async_op, out=out_buf)
-    out.wait()
-    outs = None
-    _sync()
-    barrier()
-    _sync()
-    dt = time.perf_counter() - t0
-    del out, outs
-    if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
+
+    def warmup():
+        env_phase_stall(rank, "warmup")
+        out = None
+        for _ in range(args.warmup):
+            out = ar(x, async_op=args.async_op, out=out_buf)
+        if out is not None:
+            out.wait()
+        _sync()
+        barrier()
+        _sync()
+
+    guard.run("warmup", dl, warmup)
+
+    def timed_region():
+        env_phase_stall(rank, "timed")
+        host_s = 0.0
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            th = time.perf_counter()
+            out = ar(x, async_op=args.async_op, out=out_buf)
+            host_s += time.perf_counter() - th
+        out.wait()
+        _sync()
+        barrier()
+        _sync()
+        dt = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([dt, host_s], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            dt, host_s = float(t[0].item()), float(t[1].item())
+        return dt, host_s
+
+    dt, host_s = guard.run("timed", max(dl, args.steps * 2.0), timed_region)
     ms = dt / args.steps * 1e3
     algbw = nbytes / (dt / args.steps) / 1e9
-    busbw = algbw * (2 * (world - 1) / world) if world > 1 else 0.0
+    busbw = algbw * (2 * (world - 1) / world) if world > 1 else None
 
-    # Exactness check (untimed): every rank contributes rank+1 -> sum = N(N+1)/2 exactly.
+    # Exactness after the timed rounds (untimed).
     ok = None
     if not args.no_check:
-        y = torch.full((S,), float(rank + 1), device=dev, dtype=dtype)
-        o = ar(y)
-        want = float(world * (world + 1) // 2)
-        ok = bool(torch.all(o.data == want).item()) and bool(torch.all(o.count == world).item())
-        if world > 1:
-            f = torch.tensor([1 if ok else 0])
-            dist.all_reduce(f, op=dist.ReduceOp.MIN)
-            ok = bool(f.item())
+        ok = guard.run("check", dl, lambda: exact_round("check"))
 
     # Comparator (outside the timed region): RCCL's own all_reduce on the same
     # buffer, same N and step count, through a separate nccl (= RCCL) group.
-    rccl = None
-    rccl_err = None
     compare = (world > 1) if args.compare_rccl == "auto" else (args.compare_rccl == "on")
-    if compare and world > 1:
+
+    def comparator():
+        if not (compare and world > 1):
+            return None, None
         try:
             grp = dist.new_group(backend="nccl" if dev.type == "cuda" else "gloo")
             z = x.clone()
@@ -276,47 +380,39 @@ def main() -> int:
             barrier()
             t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            rccl = nbytes / (float(t.item()) / args.steps) / 1e9
             del z
+            return nbytes / (float(t.item()) / args.steps) / 1e9, None
         except Exception as e:  # the comparator must never cost the headline line
-            rccl_err = f"{type(e).__name__}: {e}"[:200]
+            return None, f"{type(e).__name__}: {e}"[:200]
+
+    rccl, rccl_err = guard.run("compare", dl, comparator)
 
     st = ar.state()
-    line = {
-        "metric": BASELINE_METRIC,
+    link = st.get("link", {})
+    rounds_done = max(1, link.get("rounds", st["stats"]["rounds_completed"]) or 1)
+    line = dict(base)
+    line.update({
         "value": round(algbw, 3),
-        "unit": "GB/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
         "ms_per_step": round(ms, 4),
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": "bf16" if dtype == torch.bfloat16 else "fp32",
-        "data": "synthetic random tensors (torch.randn), exact thresholds"
-        + ("; CPU gloo rehearsal, not the metric" if dev.type == "cpu" else ""),
-        "config": {
-            "model": f"threshold-allreduce {args.size_mb:g}MiB {args.dtype}",
-            "global_batch": world,
-            "seq_len": S,
-            "parallelism": f"dp{world}",
-            "buffer_bytes": nbytes,
-            "chunk_bytes": C * esize,
-            "max_lag": args.max_lag,
-            "broadcast_lag": args.bcast_lag,
-            "thresholds": [1.0, args.th_reduce, args.th_complete],
-            "transport": ("rccl-pair-reactive" if ar.transport == "reactive" else "rccl-p2p-xgmi")
-            if world > 1 and dev.type == "cuda" else ("gloo-p2p" if world > 1 else "local"),
-            "async_op": args.async_op,
-            "output": "fresh tensor per round" if args.fresh_out else "preallocated, reused",
-        },
-        "busbw_GBps": round(busbw, 3),
+        "busbw_GBps": round(busbw, 3) if busbw is not None else None,
         "exact": ok,
-        "groups_per_round": (st.get("link", {}).get("groups", 0)
-                             / max(1, st.get("link", {}).get("rounds", st["stats"]["rounds_completed"]) or 1)),
+        "preflight": "passed" if "preflight" in guard.history else "skipped",
+        "groups_per_round": round(link.get("groups", 0) / rounds_done, 3),
+        "host_us_per_round": round(host_s / args.steps * 1e6, 2),
+        "p2p_kind": p2p0.get("kind"),
+        "p2p_nranks": p2p0.get("nranks"),
+        "rccl_nranks": p2p0.get("nranks") if rccl_kind else None,
+        "rccl_version": _rccl_version() if rccl_kind else None,
+        "rank_devices": ranks,
         "rccl_allreduce_algbw_GBps": round(rccl, 3) if rccl else None,
-    }
+    })
+    line["config"] = dict(base["config"])
+    line["config"].update({
+        "transport": ("rccl-pair-reactive" if ar.transport == "reactive" else "rccl-p2p-xgmi")
+        if world > 1 and dev.type == "cuda" else ("gloo-p2p" if world > 1 else "local"),
+        "async_op": args.async_op,
+        "output": "fresh tensor per round" if args.fresh_out else "preallocated, reused",
+    })
     if rccl_err:
         line["rccl_compare_error"] = rccl_err
     if world == 1:
@@ -327,40 +423,29 @@ def main() -> int:
         line["xgmi_bound_algbw_GBps"] = round(world * XGMI_LINK_GBPS / 2, 1)
 
     # The other BASELINE configs at the same N, measured after the headline
-    # (same scheduled transport; each guarded so it cannot cost the line).  A
-    # deadline bounds them too: if they have not finished by then, every rank
-    # exits 0 and rank 0 prints the headline without them.
+    # (each guarded so it cannot cost the line).  The native watchdog bounds
+    # them: if they have not finished by the deadline, every rank exits and
+    # rank 0 writes the headline line with "extras_error" instead.
     run_extra = args.extras == "on" or (args.extras == "auto" and args.size_mb == 256.0 and args.dtype == "float32"
                                         and args.transport == "stream" and dev.type == "cuda")
     if run_extra:
-        import threading
-
-        lock, done = threading.Lock(), []
-
-        def _give_up():
-            with lock:  # held through the exit: the main thread cannot print a second line
-                if done:
-                    return
-                if rank == 0:
-                    line["extras_error"] = f"extras not done after {args.extras_deadline_s:g} s; skipped"
-                    print(json.dumps(line), flush=True)
-                os._exit(0 if ok in (None, True) else 1)
-
-        timer = threading.Timer(args.extras_deadline_s, _give_up)
-        timer.daemon = True
-        timer.start()
-        extras = run_extras(world, dev, barrier)
-        with lock:
-            done.append(True)
-        timer.cancel()
-        line["extra_configs"] = extras
+        late = dict(line)
+        late["extras_error"] = f"extras not done after {args.extras_deadline_s:g} s; skipped"
+        guard.arm(args.extras_deadline_s, late, exit_code=0 if ok in (None, True) else 1)
+        line["extra_configs"] = run_extras(world, dev, barrier)
+        guard.disarm()
 
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1 and dist.is_initialized():
-        dist.barrier()
-        dist.destroy_process_group()
+        guard.run("teardown", dl, lambda: (dist.barrier(), dist.destroy_process_group()), agree=False)
     return 0 if ok in (None, True) else 1
+
+
+def _rccl_version():
+    from akka_allreduce_amd._native_loader import load
+
+    return load().rccl_version()
 
 
 if __name__ == "__main__":

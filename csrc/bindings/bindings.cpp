@@ -20,6 +20,7 @@
 
 #include "../engine/engine.h"
 #include "../kernels/kernels.h"
+#include "../runtime/watchdog.h"
 #include "../transport/p2p.h"
 #include "../transport/reactive_link.h"
 #include "harness_p2p.h"
@@ -303,6 +304,22 @@ class WorkerCore final : public EngineHost {
     }
     return d;
   }
+  // What the transport reports about itself (RCCL: ncclCommCount/UserRank/
+  // CuDevice) -- None before a transport is connected.
+  py::object p2p_info() const {
+    if (!p2p_) return py::none();
+    P2PInfo i = p2p_->info();
+    py::dict d;
+    d["kind"] = i.kind;
+    d["nranks"] = i.nranks;
+    d["rank"] = i.rank;
+    d["device"] = i.device;
+    d["comms"] = i.comms;
+    return std::move(d);
+  }
+  void p2p_check() {
+    if (p2p_) p2p_->check();
+  }
   int32_t scatter_count(int32_t round, int32_t chunk) const { return engine_->scatter_count(round, chunk); }
   int32_t reduced_arrivals(int32_t round) const { return engine_->reduced_arrivals(round); }
 
@@ -479,6 +496,8 @@ PYBIND11_MODULE(_native, m) {
       .def("drain", &WorkerCore::drain)
       .def("streams", &WorkerCore::streams)
       .def("state", &WorkerCore::state)
+      .def("p2p_info", &WorkerCore::p2p_info)
+      .def("p2p_check", &WorkerCore::p2p_check)
       .def("scatter_count", &WorkerCore::scatter_count)
       .def("reduced_arrivals", &WorkerCore::reduced_arrivals);
 
@@ -498,6 +517,13 @@ PYBIND11_MODULE(_native, m) {
     return py::bytes(reinterpret_cast<const char*>(v.data()), v.size());
   });
   m.def("rccl_version", []() { return std::string(rccl_version_string()); });
+  m.def("watchdog_arm", &watchdog_arm, py::arg("seconds"), py::arg("line"), py::arg("to_stdout"),
+        py::arg("debug_path") = "", py::arg("exit_code") = 3, py::arg("tail_bytes") = 4096,
+        py::arg("beacon_path") = "",
+        "Native phase watchdog (runtime/watchdog.h): on expiry write `line` and _exit(exit_code)");
+  m.def("watchdog_disarm", &watchdog_disarm);
+  m.def("watchdog_install_sigterm", &watchdog_install_sigterm);
+  m.def("json_escape", &json_escape);
   m.def("hw_queue_probe", [](int32_t kmax, int32_t wait_ms) {
     // How many streams can be parked on a wait-value before a fresh stream
     // stops making progress (= the HW queues streams really get).  Returns the
@@ -563,6 +589,17 @@ PYBIND11_MODULE(_native, m) {
   py::class_<P2P>(m, "P2PEndpoint")
       .def("rank", &P2P::rank)
       .def("nranks", &P2P::nranks)
+      .def("info", [](const P2P& p) {
+        P2PInfo i = p.info();
+        py::dict d;
+        d["kind"] = i.kind;
+        d["nranks"] = i.nranks;
+        d["rank"] = i.rank;
+        d["device"] = i.device;
+        d["comms"] = i.comms;
+        return d;
+      })
+      .def("check", &P2P::check)
       .def("group", [](P2P& p, uintptr_t stream, const std::vector<std::tuple<bool, int32_t, uintptr_t, size_t>>& ops) {
         std::vector<P2POp> v;
         v.reserve(ops.size());
@@ -570,10 +607,11 @@ PYBIND11_MODULE(_native, m) {
           v.push_back({std::get<0>(o), std::get<1>(o), reinterpret_cast<void*>(std::get<2>(o)), std::get<3>(o)});
         p.group(reinterpret_cast<StreamH>(stream), v);
       });
-  m.def("rccl_endpoint", [](py::bytes uid, int32_t rank, int32_t nranks, int32_t device) {
+  m.def("rccl_endpoint", [](py::bytes uid, int32_t rank, int32_t nranks, int32_t device, bool pairs) {
     std::string s = uid;
-    return make_rccl_p2p(std::vector<uint8_t>(s.begin(), s.end()), rank, nranks, device);
-  });
+    std::vector<uint8_t> v(s.begin(), s.end());
+    return pairs ? make_rccl_pair_p2p(v, rank, nranks, device) : make_rccl_p2p(v, rank, nranks, device);
+  }, py::arg("uid"), py::arg("rank"), py::arg("nranks"), py::arg("device"), py::arg("pairs") = false);
 
   // ---- kernels (tests / microbench) ----------------------------------------------
   m.def("reduce", [](uintptr_t dst, std::vector<uintptr_t> srcs, int64_t n, std::string dtype, uintptr_t stream,

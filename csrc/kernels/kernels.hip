@@ -294,8 +294,10 @@ __global__ __launch_bounds__(kBlock) void count_expand_kernel(int32_t* __restric
 // Same region walk as count_expand (one wave-uniform count per region).
 // AXPY: dst[i] += alpha * mean[i] instead (the SGD update fused into the
 // averaging: one read of the sum, one read + write of the parameters).
+// dst may alias src (mean(out=data): a gradient bucket averaged in place);
+// each element is read before the same thread writes it, so no __restrict__.
 template <typename T, bool AXPY>
-__global__ __launch_bounds__(kBlock) void count_mean_kernel(T* __restrict__ dst, const T* __restrict__ src,
+__global__ __launch_bounds__(kBlock) void count_mean_kernel(T* dst, const T* src,
                                                             const int32_t* __restrict__ counts, int64_t S,
                                                             int64_t step, int32_t N, int64_t C, int32_t kmax,
                                                             float alpha) {

@@ -11,6 +11,7 @@
 #pragma once
 
 #include <memory>
+#include <string>
 #include <vector>
 
 #include "../engine/device.h"
@@ -24,6 +25,18 @@ struct P2POp {
   size_t bytes = 0;
 };
 
+// What the transport itself reports about its communicator(s): for RCCL the
+// values come from ncclCommCount / ncclCommUserRank / ncclCommCuDevice, not
+// from the arguments it was built with (the bench prints them as proof that
+// RCCL really saw N ranks).
+struct P2PInfo {
+  std::string kind;
+  int32_t nranks = 0;
+  int32_t rank = -1;
+  int32_t device = -1;
+  int32_t comms = 0;  // communicators held (global + pair comms)
+};
+
 class P2P {
  public:
   virtual ~P2P() = default;
@@ -32,6 +45,10 @@ class P2P {
   // Enqueue one group of ops on `stream` (RCCL: ncclGroupStart .. ncclGroupEnd).
   virtual void group(StreamH stream, const std::vector<P2POp>& ops) = 0;
   virtual const char* name() const = 0;
+  virtual P2PInfo info() const { return P2PInfo{name(), nranks(), rank(), -1, 0}; }
+  // Surface asynchronous transport errors (RCCL: ncclCommGetAsyncError on
+  // every communicator).  Links call it once per round, not per group.
+  virtual void check() {}
 };
 
 // ---- CPU simulator ------------------------------------------------------------

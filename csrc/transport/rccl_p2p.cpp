@@ -43,6 +43,30 @@ const char* rccl_version_string() {
 
 namespace {
 
+// Ask RCCL what it actually built: rank count, this rank, device.  A mismatch
+// (e.g. two ranks resolved to one card, or a stale unique id joining another
+// job) fails here, at init, instead of as a hang in the first group.
+void verify_comm(ncclComm_t c, int32_t want_n, int32_t want_rank, int32_t want_dev, const char* what) {
+  int n = -1, r = -1, d = -1;
+  AKKA_NCCL(ncclCommCount(c, &n));
+  AKKA_NCCL(ncclCommUserRank(c, &r));
+  AKKA_NCCL(ncclCommCuDevice(c, &d));
+  if (n != want_n || r != want_rank || (want_dev >= 0 && d != want_dev)) {
+    std::ostringstream os;
+    os << "akka: RCCL " << what << " communicator reports nranks=" << n << " rank=" << r << " device=" << d
+       << ", expected nranks=" << want_n << " rank=" << want_rank << " device=" << want_dev;
+    throw AkkaError(os.str());
+  }
+}
+
+void check_async(ncclComm_t c, const char* what) {
+  if (!c) return;
+  ncclResult_t async = ncclSuccess;
+  AKKA_NCCL(ncclCommGetAsyncError(c, &async));
+  if (async != ncclSuccess && async != ncclInProgress)
+    throw AkkaError(std::string("akka: RCCL async error on ") + what + " communicator: " + ncclGetErrorString(async));
+}
+
 class RcclP2P final : public P2P {
  public:
   RcclP2P(const std::vector<uint8_t>& uid, int32_t rank, int32_t nranks, int32_t device)
@@ -52,6 +76,8 @@ class RcclP2P final : public P2P {
     std::memcpy(&id, uid.data(), sizeof(id));
     if (hipSetDevice(device) != hipSuccess) throw AkkaError("akka: hipSetDevice failed");
     AKKA_NCCL(ncclCommInitRank(&comm_, nranks, id, rank));
+    verify_comm(comm_, nranks, rank, device, "global");
+    device_ = device;
   }
   ~RcclP2P() override {
     if (comm_) ncclCommDestroy(comm_);
@@ -68,13 +94,19 @@ class RcclP2P final : public P2P {
       else AKKA_NCCL(ncclRecv(op.buf, op.bytes, ncclUint8, op.peer, comm_, s));
     }
     AKKA_NCCL(ncclGroupEnd());
-    ncclResult_t async = ncclSuccess;
-    AKKA_NCCL(ncclCommGetAsyncError(comm_, &async));
-    AKKA_CHECK(async == ncclSuccess, std::string("RCCL async error: ") + ncclGetErrorString(async));
   }
+  P2PInfo info() const override {
+    int n = -1, r = -1, d = -1;
+    ncclCommCount(comm_, &n);
+    ncclCommUserRank(comm_, &r);
+    ncclCommCuDevice(comm_, &d);
+    return P2PInfo{name(), n, r, d, 1};
+  }
+  void check() override { check_async(comm_, "global"); }
 
  private:
   int32_t rank_, n_;
+  int32_t device_ = -1;
   ncclComm_t comm_ = nullptr;
 };
 
@@ -91,6 +123,7 @@ class RcclPairP2P final : public P2P {
     std::memcpy(&id, uid.data(), sizeof(id));
     if (hipSetDevice(device) != hipSuccess) throw AkkaError("akka: hipSetDevice failed");
     AKKA_NCCL(ncclCommInitRank(&global_, nranks, id, rank));
+    verify_comm(global_, nranks, rank, device, "global");
     // Round-robin tournament (circle method): P-1 rounds of disjoint pairs,
     // one ncclCommSplit each; with odd N a dummy player sits one rank out.
     for (int32_t t = 0; t < tournament_rounds(nranks); ++t) {
@@ -100,8 +133,12 @@ class RcclPairP2P final : public P2P {
       AKKA_NCCL(ncclCommSplit(global_, real ? std::min(rank, partner) : NCCL_SPLIT_NOCOLOR, rank, &c, nullptr));
       if (real) pair_[size_t(partner)] = c;
     }
-    for (int32_t p = 0; p < nranks; ++p)
-      AKKA_CHECK(p == rank || pair_[size_t(p)], "pair communicator missing for peer " + std::to_string(p));
+    for (int32_t p = 0; p < nranks; ++p) {
+      if (p == rank) continue;
+      AKKA_CHECK(pair_[size_t(p)], "pair communicator missing for peer " + std::to_string(p));
+      // split key = global rank: the lower global rank is pair rank 0
+      verify_comm(pair_[size_t(p)], 2, rank < p ? 0 : 1, device, "pair");
+    }
   }
   ~RcclPairP2P() override {
     for (ncclComm_t c : pair_)
@@ -126,6 +163,19 @@ class RcclPairP2P final : public P2P {
       else AKKA_NCCL(ncclRecv(op.buf, op.bytes, ncclUint8, prank, c, s));
     }
     AKKA_NCCL(ncclGroupEnd());
+  }
+  P2PInfo info() const override {
+    int n = -1, r = -1, d = -1;
+    ncclCommCount(global_, &n);
+    ncclCommUserRank(global_, &r);
+    ncclCommCuDevice(global_, &d);
+    int32_t comms = 1;
+    for (ncclComm_t c : pair_) comms += c ? 1 : 0;
+    return P2PInfo{name(), n, r, d, comms};
+  }
+  void check() override {
+    check_async(global_, "global");
+    for (ncclComm_t c : pair_) check_async(c, "pair");
   }
 
  private:

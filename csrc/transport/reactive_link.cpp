@@ -234,6 +234,7 @@ void ReactiveLink::issue_p2(int32_t r) {
   }
   put_event(ready);  // the waits above captured its record
   s.p2_issued = true;
+  p2p_->check();  // RCCL async errors on the pair communicators: once per round
 }
 
 bool ReactiveLink::reclaim(int32_t round) {

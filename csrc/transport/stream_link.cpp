@@ -154,6 +154,7 @@ void StreamLink::schedule(int32_t r) {
       }
     }
   }
+  p2p_->check();  // RCCL async errors: once per round, not per group
   in_flight_.erase(r);
   q_.erase(r);
   stats_.rounds++;

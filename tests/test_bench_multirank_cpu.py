@@ -21,15 +21,20 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def _run(n, *extra):
+def _run(n, *extra, env=None, expect_rc=0):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
            "--gpus", str(n), "--steps", "3", "--warmup", "1", "--size-mb", "0.5", "--chunk-mb", "0.0625",
            "--device", "cpu", *extra]
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT)
-    assert r.returncode == 0, r.stderr[-3000:]
+    e = dict(os.environ)
+    e.update(env or {})
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT, env=e)
+    if expect_rc == 0:
+        assert r.returncode == 0, r.stderr[-3000:]
+    else:
+        assert r.returncode != 0, r.stdout[-3000:]
     lines = [ln for ln in r.stdout.splitlines() if ln.strip().startswith("{")]
-    assert len(lines) == 1, r.stdout
+    assert len(lines) == 1, (r.stdout, r.stderr[-3000:])
     return json.loads(lines[0])
 
 
@@ -41,8 +46,39 @@ def test_bench_multirank_line(n, transport):
     assert d["config"]["parallelism"] == f"dp{n}" and d["config"]["transport"] == "gloo-p2p"
     assert abs(d["busbw_GBps"] - d["value"] * 2 * (n - 1) / n) < 1e-2
     assert d["rccl_allreduce_algbw_GBps"] and d["rccl_allreduce_algbw_GBps"] > 0
+    # self-proving fields: what the transport itself reports, per rank
+    assert d["scaling"] == "strong" and d["preflight"] == "passed"
+    assert d["p2p_nranks"] == n and "rccl_nranks" in d and "rccl_version" in d
+    assert [r["rank"] for r in d["rank_devices"]] == list(range(n))
+    assert all(r["p2p"]["nranks"] == n and r["p2p"]["rank"] == r["rank"] for r in d["rank_devices"])
+    assert d["groups_per_round"] > 0 and d["host_us_per_round"] > 0
 
 
 def test_bench_multirank_extras_deadline():
     d = _run(2, "--extras", "on", "--extras-deadline-s", "0.05")
     assert d["exact"] is True and "extras_error" in d and "extra_configs" not in d
+    assert d["value"] > 0
+
+
+def test_bench_stalled_rank_fails_legibly():
+    """A rank that never posts its side of the preflight round: rank 0 must
+    print ONE failure line naming the phase inside the preflight deadline and
+    the job must exit non-zero (no hang until an outer limit)."""
+    import time
+
+    t0 = time.monotonic()
+    d = _run(2, "--preflight-deadline-s", "8", env={"AKKA_FAULT_STALL_RANK": "1", "AKKA_FAULT_STALL_PHASE": "preflight"},
+             expect_rc=1)
+    assert time.monotonic() - t0 < 90
+    assert d["failed_phase"] == "preflight" and d["value"] is None
+    assert "deadline" in d["failure"] and "rccl_debug_tail" in d
+    assert d["phases_passed"] == ["init", "rccl_init", "identity"]
+
+
+def test_bench_rank_error_reported_by_rank0():
+    """A Python error on rank 1 reaches rank 0 through the agreement step."""
+    d = _run(2, env={"AKKA_FAULT_STALL_RANK": "1", "AKKA_FAULT_STALL_PHASE": "warmup", "AKKA_FAULT_STALL_MODE": "raise"},
+             expect_rc=1)
+    assert d["failed_phase"] == "warmup"
+    # either through the agreement step or through the failure beacon
+    assert "injected fault on rank 1" in json.dumps(d), d

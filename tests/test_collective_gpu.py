@@ -88,6 +88,30 @@ def test_mlp_dp_sgd_bf16_autocast_tracks_fp32():
     assert b16[-1] < 0.5 * b16[0], b16
 
 
+def test_mlp_bf16_direct_grads_match_autocast_autograd():
+    """The bf16 direct-into-bucket backward (_LinearIntoBucket under autocast,
+    fp32-out GEMM) gives the same fc1/fc2 weight AND bias gradients as
+    autocast + autograd's zero/accumulate path, to bf16 tolerance."""
+    from akka_allreduce_amd.models.mlp import MLP, dp_sgd_step, synthetic_batch
+    from akka_allreduce_amd.parallel.dp import GradientBucket
+
+    dev = torch.device("cuda", 0)
+    grads = {}
+    for direct in (True, False):
+        torch.manual_seed(0)
+        model = MLP(256, 512, 10).to(dev)
+        bucket = GradientBucket(list(model.parameters()), flatten_params=True)
+        x, y = synthetic_batch(128, 256, 10, device=dev)
+        bucket.flat.fill_(7.0)  # stale values: the direct path must overwrite every element
+        dp_sgd_step(model, x, y, 0.0, None, bucket, compute_dtype=torch.bfloat16, direct_grads=direct)
+        assert model.last_step_direct == direct
+        grads[direct] = {n: p.grad.detach().clone() for n, p in model.named_parameters()}
+    assert set(grads[True]) == {"fc1.weight", "fc1.bias", "fc2.weight", "fc2.bias"}
+    for name in grads[True]:
+        a, b = grads[True][name], grads[False][name]
+        torch.testing.assert_close(a, b, rtol=2e-2, atol=2e-3 * float(b.abs().max()) + 1e-6, msg=name)
+
+
 def test_round_captured_in_hip_graph():
     """An exact-threshold round with fixed buffers captured with
     torch.cuda.graph (relaxed mode) replays the same GPU work: new input

@@ -31,7 +31,7 @@ def test_direct_bucket_grads_match_autograd():
         bucket.flat.fill_(123.0)  # stale garbage: the direct path must overwrite it
         for _ in range(3):
             dp_sgd_step(model, x, y, 0.1, ar, bucket, direct_grads=direct)
-        assert model.direct_grads == direct
+        assert model.last_step_direct == direct and model.direct_grads is False
         res[direct] = (bucket.flat.clone(), torch.cat([p.detach().flatten() for p in model.parameters()]))
     torch.testing.assert_close(res[True][0], res[False][0], rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(res[True][1], res[False][1], rtol=1e-5, atol=1e-6)
@@ -43,3 +43,54 @@ def test_mlp_fp32_and_bf16_autocast_train():
     assert f32[-1] < 0.5 * f32[0], f32
     assert b16[-1] < 0.5 * b16[0], b16
     assert abs(b16[0] - f32[0]) < 2e-2 * abs(f32[0]), (b16[0], f32[0])
+
+
+def _fresh(seed=0):
+    torch.manual_seed(seed)
+    model = MLP(32, 64, 8)
+    bucket = GradientBucket(list(model.parameters()), flatten_params=True)
+    ar = ThresholdAllreduce(bucket.numel, max_chunk_size=1024, device=torch.device("cpu"), rank=0, world_size=1)
+    return model, bucket, ar
+
+
+def test_backward_after_dp_step_accumulates_like_autograd():
+    """Direct-into-bucket grads are scoped to dp_sgd_step: a later loss built
+    from two forwards (micro-batch accumulation) gets autograd's gradients."""
+    model, bucket, ar = _fresh()
+    x, y = synthetic_batch(64, 32, 8, device="cpu")
+    dp_sgd_step(model, x, y, 0.1, ar, bucket)
+    assert model.last_step_direct
+    ref = MLP(32, 64, 8)
+    ref.load_state_dict(model.state_dict())
+    for m in (model, ref):
+        for p in m.parameters():
+            p.grad = None
+        loss = torch.nn.functional.cross_entropy(m(x[:32]), y[:32]) + torch.nn.functional.cross_entropy(m(x[32:]), y[32:])
+        loss.backward()
+    for a, b in zip(model.parameters(), ref.parameters()):
+        torch.testing.assert_close(a.grad, b.grad, rtol=1e-5, atol=1e-6)
+
+
+def test_zero_grad_before_dp_step_still_trains():
+    """zero_grad() (set_to_none) detaches .grad from the bucket; dp_sgd_step
+    re-attaches the views, so the update uses the real gradients."""
+    model, bucket, ar = _fresh()
+    x, y = synthetic_batch(128, 32, 8, device="cpu")
+    w0 = model.fc1.weight.detach().clone()
+    losses = []
+    for _ in range(5):
+        model.zero_grad()
+        assert model.fc1.weight.grad is None
+        losses.append(dp_sgd_step(model, x, y, 0.5, ar, bucket))
+        assert bucket.bound()
+    assert not torch.equal(model.fc1.weight.detach(), w0)
+    assert losses[-1] < losses[0], losses
+
+
+def test_rebind_keeps_foreign_gradient_values():
+    model, bucket, _ = _fresh()
+    g = torch.randn_like(model.fc2.weight)
+    model.fc2.weight.grad = g.clone()
+    assert not bucket.bound()
+    assert bucket.rebind() and bucket.bound()
+    torch.testing.assert_close(model.fc2.weight.grad, g)
