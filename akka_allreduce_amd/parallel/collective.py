@@ -12,6 +12,13 @@ Usage::
     ar = ThresholdAllreduce(data_size=x.numel(), max_chunk_size=1 << 20)
     out = ar(x)          # AllReduceOutput; out.data is valid in stream order
 
+``lane`` picks how exact-threshold rounds (thReduce = thComplete = 1) move:
+``"auto"`` runs them as RCCL reduce-scatter + all-gather (two calls a round,
+RCCL's own xGMI schedules) when the buffer splits evenly, else the
+chunk-pipelined p2p schedule; ``"p2p"`` always uses the p2p schedule,
+``"collective"`` always the whole-round lane.  Rounds with thresholds < 1
+always take the p2p schedule (their outcome depends on arrival order).
+
 ``transport="reactive"`` selects the straggler-tolerant data path
 (csrc/transport/reactive_link.h): one stream + one RCCL pair communicator per
 peer, arrivals polled from events, so with thresholds < 1 a rank completes
@@ -84,6 +91,7 @@ class ThresholdAllreduce:
         store: Any = None,
         data_sink: Any = None,
         transport: str = "stream",
+        lane: str = "auto",
     ):
         if transport not in ("stream", "reactive"):
             raise ValueError("transport must be 'stream' or 'reactive'")
@@ -129,6 +137,8 @@ class ThresholdAllreduce:
         self.worker.tell(InitWorkers(peers, self.world_size, None, self.rank, th_reduce, th_complete, max_lag,
                                      int(data_size), int(max_chunk_size)))
         self.data_size = int(data_size)
+        if self.transport == "stream":
+            self.worker.set_lane(lane)
         from ..utils.faults import env_straggler_delay
 
         self.fault_delay_s = env_straggler_delay(self.rank)  # AKKA_FAULT_RANK / AKKA_FAULT_DELAY_MS
@@ -146,6 +156,13 @@ class ThresholdAllreduce:
         if out is None:
             raise RuntimeError("round did not complete (thresholds need every rank in the scheduled transport)")
         return out
+
+    def set_lane(self, lane: str) -> None:
+        """Switch the exact-round lane (``auto`` / ``p2p`` / ``collective``,
+        csrc/transport/stream_link.h) -- every rank must switch at the same round."""
+        if self.transport != "stream":
+            raise ValueError("lanes belong to the scheduled (stream) transport")
+        self.worker.set_lane(lane)
 
     def state(self) -> dict:
         return self.worker.state()

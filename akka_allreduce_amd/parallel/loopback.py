@@ -24,7 +24,7 @@ from .collective import _RemoteRank
 class LoopbackCluster:
     def __init__(self, n: int, data_size: int, max_chunk_size: int, *, dtype: torch.dtype = torch.float32,
                  th_reduce: float = 1.0, th_complete: float = 1.0, max_lag: int = 1, broadcast_lag: int = 2,
-                 device: Optional[torch.device] = None):
+                 device: Optional[torch.device] = None, lane: str = "auto"):
         self.n = n
         self.hub = _load().LoopbackHub(n)
         dev = device or torch.device("cuda", 0)
@@ -37,6 +37,7 @@ class LoopbackCluster:
         for r, w in enumerate(self.workers):
             peers = {i: (w if i == r else _RemoteRank(i)) for i in range(n)}
             w.tell(InitWorkers(peers, n, None, r, th_reduce, th_complete, max_lag, data_size, max_chunk_size))
+            w.set_lane(lane)
 
     def allreduce(self, inputs: Sequence[torch.Tensor], async_op: bool = False) -> List[AllReduceOutput]:
         assert len(inputs) == self.n

@@ -23,7 +23,8 @@ from .collective import _RemoteRank
 
 class SimCluster:
     def __init__(self, n: int, data_size: int, max_chunk_size: int, *, dtype: torch.dtype = torch.float32,
-                 th_reduce: float = 1.0, th_complete: float = 1.0, max_lag: int = 1, broadcast_lag=2):
+                 th_reduce: float = 1.0, th_complete: float = 1.0, max_lag: int = 1, broadcast_lag=2,
+                 lane: str = "auto"):
         nat = _load()
         self.n = n
         self.hub = nat.SimHub(n)
@@ -36,6 +37,7 @@ class SimCluster:
         for r, w in enumerate(self.workers):
             peers = {i: (w if i == r else _RemoteRank(i)) for i in range(n)}
             w.tell(InitWorkers(peers, n, None, r, th_reduce, th_complete, max_lag, data_size, max_chunk_size))
+            w.set_lane(lane)
 
     def allreduce(self, inputs: Sequence[torch.Tensor]) -> List[AllReduceOutput]:
         """One round on every rank; returns each rank's output (valid after the simulated run)."""

@@ -307,6 +307,14 @@ class AllreduceWorker:
             self.progress_until(r, self.reactive_timeout)
         return self._outputs.pop(r, None)
 
+    def set_lane(self, lane: str) -> None:
+        """Exact-round lane of the scheduled transport: ``"auto"`` (RCCL
+        reduce-scatter + all-gather when available and the geometry is even,
+        else the chunk-pipelined p2p schedule), ``"p2p"`` or ``"collective"``
+        (see csrc/transport/stream_link.h).  Threshold rounds (< 1) always run
+        the p2p schedule."""
+        self._core.set_lane(lane)
+
     def _fast_ok(self, tensor: torch.Tensor) -> bool:
         """Collective-style call on the scheduled transport, whose rounds
         complete inside the call: buffers can be bound natively."""

@@ -62,6 +62,9 @@ def parse():
     p.add_argument("--transport", choices=["stream", "reactive"], default="stream",
                    help="stream: symmetric step schedule on one comm stream (default); reactive: per-peer streams + "
                         "pair communicators, event-polled arrivals (straggler-tolerant)")
+    p.add_argument("--lane", choices=["auto", "p2p", "collective"], default="auto",
+                   help="exact-round lane of the stream transport (stream_link.h): auto = RCCL reduce-scatter + "
+                        "all-gather when the buffer splits evenly, else the chunk-pipelined p2p schedule")
     p.add_argument("--async-op", choices=["auto", "on", "off"], default="auto",
                    help="async rounds (event hand-off) -- auto: on for N>1 (saves a stream hop per round), off for "
                         "N=1 (local rounds run on the caller's stream, nothing to hop)")
@@ -255,7 +258,7 @@ def main() -> int:
         env_phase_stall(rank, "rccl_init")
         return ThresholdAllreduce(S, max_chunk_size=C, dtype=dtype, th_reduce=args.th_reduce,
                                   th_complete=args.th_complete, max_lag=args.max_lag, broadcast_lag=args.bcast_lag,
-                                  device=dev, transport=args.transport)
+                                  device=dev, transport=args.transport, lane=args.lane)
 
     ar = guard.run("rccl_init", dl, rccl_init)
 
@@ -387,7 +390,39 @@ def main() -> int:
 
     rccl, rccl_err = guard.run("compare", dl, comparator)
 
-    st = ar.state()
+    # The other exact-round lane on the same buffer (untimed for the headline):
+    # at N>1 the driver's run then records both the whole-round collective lane
+    # and the chunk-pipelined p2p schedule.
+    def other_lane():
+        st0 = ar.state().get("link", {})
+        used = "collective" if st0.get("bulk_rounds", 0) else "p2p"
+        if world == 1 or ar.transport != "stream":
+            return used, None
+        other = "p2p" if used == "collective" else "collective"
+        try:
+            ar.set_lane(other)
+            for _ in range(2):
+                o = ar(x, async_op=args.async_op, out=out_buf)
+            o.wait()
+            _sync()
+            barrier()
+            k = max(3, args.steps // 2)
+            t0 = time.perf_counter()
+            for _ in range(k):
+                o = ar(x, async_op=args.async_op, out=out_buf)
+            o.wait()
+            _sync()
+            barrier()
+            t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            return used, {"lane": other, "algbw_GBps": round(nbytes / (float(t.item()) / k) / 1e9, 3),
+                          "steps": k}
+        finally:
+            ar.set_lane(args.lane)
+
+    st = ar.state()  # headline rounds only (before the other lane runs)
+    lane_used, lane_other = guard.run("other_lane", dl, other_lane)
+
     link = st.get("link", {})
     rounds_done = max(1, link.get("rounds", st["stats"]["rounds_completed"]) or 1)
     line = dict(base)
@@ -404,6 +439,8 @@ def main() -> int:
         "rccl_nranks": p2p0.get("nranks") if rccl_kind else None,
         "rccl_version": _rccl_version() if rccl_kind else None,
         "rank_devices": ranks,
+        "lane": lane_used,
+        "other_lane": lane_other,
         "rccl_allreduce_algbw_GBps": round(rccl, 3) if rccl else None,
     })
     line["config"] = dict(base["config"])

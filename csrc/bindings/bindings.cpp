@@ -276,6 +276,7 @@ class WorkerCore final : public EngineHost {
     st["forced_reduces"] = s.forced_reduces;
     st["rounds_completed"] = s.rounds_completed;
     st["rounds_forced"] = s.rounds_forced;
+    st["bulk_rounds"] = s.bulk_rounds;
     d["stats"] = st;
     if (stream_link_) {
       py::dict ls;
@@ -285,6 +286,10 @@ class WorkerCore final : public EngineHost {
       ls["rounds"] = stream_link_->stats().rounds;
       ls["unreduced_chunks"] = stream_link_->stats().unreduced_chunks;
       ls["lag"] = stream_link_->lag();
+      ls["bulk_rounds"] = stream_link_->stats().bulk_rounds;
+      ls["collective_rounds"] = stream_link_->stats().collective_rounds;
+      const Lane ln = stream_link_->lane();
+      ls["lane"] = ln == Lane::Auto ? "auto" : ln == Lane::P2P ? "p2p" : "collective";
       d["link"] = ls;
     }
     if (reactive_link_) {
@@ -316,6 +321,14 @@ class WorkerCore final : public EngineHost {
     d["device"] = i.device;
     d["comms"] = i.comms;
     return std::move(d);
+  }
+  // Exact-round lane of the scheduled transport (stream_link.h Lane).
+  void set_lane(const std::string& lane) {
+    AKKA_CHECK(stream_link_, "set_lane: scheduled (stream) transport only");
+    if (lane == "auto") stream_link_->set_lane(Lane::Auto);
+    else if (lane == "p2p") stream_link_->set_lane(Lane::P2P);
+    else if (lane == "collective") stream_link_->set_lane(Lane::Collective);
+    else throw AkkaError("akka: lane must be 'auto', 'p2p' or 'collective'");
   }
   void p2p_check() {
     if (p2p_) p2p_->check();
@@ -498,6 +511,7 @@ PYBIND11_MODULE(_native, m) {
       .def("state", &WorkerCore::state)
       .def("p2p_info", &WorkerCore::p2p_info)
       .def("p2p_check", &WorkerCore::p2p_check)
+      .def("set_lane", &WorkerCore::set_lane)
       .def("scatter_count", &WorkerCore::scatter_count)
       .def("reduced_arrivals", &WorkerCore::reduced_arrivals);
 
@@ -600,6 +614,17 @@ PYBIND11_MODULE(_native, m) {
         return d;
       })
       .def("check", &P2P::check)
+      .def("has_collectives", &P2P::has_collectives)
+      .def("reduce_scatter", [](P2P& p, uintptr_t stream, uintptr_t send, uintptr_t recv, size_t count,
+                                const std::string& dtype) {
+        p.reduce_scatter(reinterpret_cast<StreamH>(stream), reinterpret_cast<const void*>(send),
+                         reinterpret_cast<void*>(recv), count, dtype == "bfloat16" ? DType::BF16 : DType::F32);
+      })
+      .def("all_gather", [](P2P& p, uintptr_t stream, uintptr_t send, uintptr_t recv, size_t count,
+                            const std::string& dtype) {
+        p.all_gather(reinterpret_cast<StreamH>(stream), reinterpret_cast<const void*>(send),
+                     reinterpret_cast<void*>(recv), count, dtype == "bfloat16" ? DType::BF16 : DType::F32);
+      })
       .def("group", [](P2P& p, uintptr_t stream, const std::vector<std::tuple<bool, int32_t, uintptr_t, size_t>>& ops) {
         std::vector<P2POp> v;
         v.reserve(ops.size());

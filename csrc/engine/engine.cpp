@@ -191,6 +191,11 @@ void Engine::do_start(int32_t r) {
     const int32_t next = max_scattered_ + 1;
     host_->fetch(next);
     AKKA_CHECK(dp_->has_input(next), "fetch did not bind an input for round " + std::to_string(next));
+    if (bulk_eligible(next) && link_->bulk_round(next)) {
+      max_scattered_ = next;
+      complete_bulk(next);
+      continue;
+    }
     scatter(next);
     max_scattered_ = next;
     if (link_) link_->on_scattered(next);
@@ -220,6 +225,36 @@ void Engine::scatter(int32_t r) {
       else if (link_) link_->send_scatter(idx, k, r, p);
     }
   }
+}
+
+bool Engine::bulk_eligible(int32_t r) const {
+  // The outcome of round r is fixed only with exact thresholds and the full
+  // membership, for the oldest open round (nothing to catch up, nothing of it
+  // received yet: its ring row still belongs to an older round).
+  if (!link_ || N_ < 2 || int32_t(peers_.size()) != N_) return false;
+  if (min_scatter_ != N_ || int64_t(min_reduced_) != g_.total_chunks()) return false;
+  if (r != round_ || r != max_round_ || completed_.count(r)) return false;
+  return find_row(r) == nullptr;
+}
+
+void Engine::complete_bulk(int32_t r) {
+  // Same end state as the message flow of an exact round: every chunk of my
+  // block reduced from all N sources, every reduced chunk landed with count N.
+  Row& rw = row(r);
+  std::fill(rw.sc_mask.begin(), rw.sc_mask.end(), uint8_t(1));
+  std::fill(rw.sc_count.begin(), rw.sc_count.end(), N_);
+  std::fill(rw.sc_reduced.begin(), rw.sc_reduced.end(), uint8_t(1));
+  for (int32_t j = 0; j < N_; ++j)
+    for (int32_t k = 0; k < g_.num_chunks(j); ++k) {
+      rw.rd_landed[size_t(j) * kmax_ + k] = 1;
+      dp_->set_count(r, j, k, N_);
+    }
+  rw.rd_arrivals = int32_t(g_.total_chunks());
+  stats_.scatters_in += int64_t(kme_) * N_;
+  stats_.reduces_in += g_.total_chunks();
+  stats_.chunks_reduced += kme_;
+  ++stats_.bulk_rounds;
+  complete(r);
 }
 
 void Engine::do_scatter_msg(int32_t src, int32_t dest, int32_t chunk, int32_t r, const Payload& p) {

@@ -67,6 +67,13 @@ class Link {
   // no while receives for the round are still being issued; it then calls
   // Engine::flush_deferred(round) itself.
   virtual bool may_finalize(int32_t /*round*/) { return true; }
+  // Exact-threshold fast lane: the engine offers a round whose outcome is
+  // fixed (thReduce = thComplete = 1, all N peers known, no state of the round
+  // seen yet): every chunk is the sum of all N inputs with count N.  A link
+  // that can move and reduce the whole round by itself (collectives) does so
+  // and returns true; the engine then completes the round without per-chunk
+  // bookkeeping.  False: the engine runs the ordinary message flow.
+  virtual bool bulk_round(int32_t /*round*/) { return false; }
 };
 
 // Embedding layer callbacks (Python, CLI, bench).
@@ -91,6 +98,7 @@ struct EngineStats {
   int64_t scatters_in = 0, reduces_in = 0, outdated_dropped = 0, future_started = 0;
   int64_t chunks_reduced = 0, forced_reduces = 0, rounds_completed = 0, rounds_forced = 0;
   int64_t errors = 0;
+  int64_t bulk_rounds = 0;  // rounds run through Link::bulk_round
 };
 
 class Engine {
@@ -159,6 +167,8 @@ class Engine {
   void do_scatter_msg(int32_t src, int32_t dest, int32_t chunk, int32_t round, const Payload& p);
   void do_reduce_msg(int32_t src, int32_t dest, int32_t chunk, int32_t round, int32_t count, const Payload& p);
   void scatter(int32_t r);
+  bool bulk_eligible(int32_t r) const;
+  void complete_bulk(int32_t r);
   void reduce_and_broadcast(int32_t r, int32_t chunk, bool forced);
   void complete(int32_t r);
   void finalize_round(int32_t r);

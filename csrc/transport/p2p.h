@@ -49,6 +49,18 @@ class P2P {
   // Surface asynchronous transport errors (RCCL: ncclCommGetAsyncError on
   // every communicator).  Links call it once per round, not per group.
   virtual void check() {}
+
+  // Whole-buffer collectives over all ranks (the exact-threshold fast lane,
+  // stream_link.h): `count` elements per rank.  reduce_scatter: recv = sum
+  // over ranks of send[rank*count ..]; all_gather: recv[r*count ..] = rank r's
+  // send (in place when send == recv + rank*count).  Default: unsupported.
+  virtual bool has_collectives() const { return false; }
+  virtual void reduce_scatter(StreamH, const void*, void*, size_t, DType) {
+    throw AkkaError(std::string("akka: ") + name() + " p2p has no reduce_scatter");
+  }
+  virtual void all_gather(StreamH, const void*, void*, size_t, DType) {
+    throw AkkaError(std::string("akka: ") + name() + " p2p has no all_gather");
+  }
 };
 
 // ---- CPU simulator ------------------------------------------------------------

@@ -104,7 +104,16 @@ class RcclP2P final : public P2P {
   }
   void check() override { check_async(comm_, "global"); }
 
+  bool has_collectives() const override { return true; }
+  void reduce_scatter(StreamH stream, const void* send, void* recv, size_t count, DType dt) override {
+    AKKA_NCCL(ncclReduceScatter(send, recv, count, nccl_type(dt), ncclSum, comm_, static_cast<hipStream_t>(stream)));
+  }
+  void all_gather(StreamH stream, const void* send, void* recv, size_t count, DType dt) override {
+    AKKA_NCCL(ncclAllGather(send, recv, count, nccl_type(dt), comm_, static_cast<hipStream_t>(stream)));
+  }
+
  private:
+  static ncclDataType_t nccl_type(DType dt) { return dt == DType::BF16 ? ncclBfloat16 : ncclFloat32; }
   int32_t rank_, n_;
   int32_t device_ = -1;
   ncclComm_t comm_ = nullptr;

@@ -161,6 +161,82 @@ void StreamLink::schedule(int32_t r) {
   mark_scheduled(r);
 }
 
+bool StreamLink::bulk_round(int32_t r) {
+  if (lane_ == Lane::P2P || !dp_) return false;
+  const Geometry& g = dp_->geometry();
+  const int32_t N = g.N;
+  const int32_t me = dp_->me();
+  if (N < 2) return false;  // a local round is already one pass
+  const bool native = p2p_->has_collectives() && g.S == int64_t(N) * g.step;
+  if (lane_ == Lane::Auto && !native) return false;
+  AKKA_CHECK(p2p_->nranks() == N && p2p_->rank() == me, "p2p communicator does not match the worker geometry");
+  const size_t es = dp_->esize();
+  Device* dev = dp_->device();
+  engine_->ensure_output(r);
+  StreamH comm = dev->comm_stream();
+  dp_->comm_wait(dp_->row_release_event(r));  // the direct exchange lands in ring row r%L
+  dp_->wait_input(r, comm);
+  dp_->mark_comm_used(r);
+  const char* in = static_cast<const char*>(dp_->input_chunk(r, 0, 0).ptr);
+  char* out = static_cast<char*>(dp_->output_at(r, 0, 0));
+  char* mine = out + size_t(g.block_start(me)) * es;
+  const int64_t my_len = g.block_len(me);
+  if (native) {
+    // phase 1 = reduce-scatter of the N blocks, phase 2 = all-gather of the
+    // reduced blocks (in place): RCCL's own xGMI schedules, two calls a round
+    p2p_->reduce_scatter(comm, in, mine, size_t(g.step), dp_->dtype());
+    p2p_->all_gather(comm, mine, out, size_t(g.step), dp_->dtype());
+    stats_.groups += 2;
+    stats_.bytes_sent += int64_t(2) * (N - 1) * g.step * int64_t(es);
+    ++stats_.collective_rounds;
+  } else {
+    // Whole-block direct exchange: the reference's scatter / reduce /
+    // broadcast (W:212-268) with one message per peer and phase.
+    std::vector<P2POp> ops;
+    for (int32_t i = 1; i < N; ++i) {
+      const int32_t peer = (me + i) % N;
+      const int64_t plen = g.block_len(peer);
+      if (plen > 0) ops.push_back({true, peer, const_cast<char*>(in) + size_t(g.block_start(peer)) * es, size_t(plen) * es});
+      if (my_len > 0) ops.push_back({false, peer, dp_->scatter_slot(r, peer, 0), size_t(my_len) * es});
+    }
+    if (!ops.empty()) {
+      p2p_->group(comm, ops);
+      stats_.groups++;
+      stats_.ops += int64_t(ops.size());
+    }
+    if (my_len > 0) {
+      StreamH cs = dev->compute_stream();
+      dp_->compute_wait(dp_->record_comm());
+      dp_->wait_input(r, cs);
+      std::vector<const void*> srcs;
+      srcs.push_back(in + size_t(g.block_start(me)) * es);
+      for (int32_t i = 1; i < N; ++i) srcs.push_back(dp_->scatter_slot(r, (me + i) % N, 0));
+      auto specs = split_reduce(mine, srcs, my_len);
+      dev->reduce(cs, specs.data(), int32_t(specs.size()), dp_->dtype());
+      dp_->comm_wait(dp_->record_compute());
+    }
+    ops.clear();
+    for (int32_t i = 1; i < N; ++i) {
+      const int32_t peer = (me + i) % N;
+      const int64_t plen = g.block_len(peer);
+      if (my_len > 0) ops.push_back({true, peer, mine, size_t(my_len) * es});
+      if (plen > 0) ops.push_back({false, peer, out + size_t(g.block_start(peer)) * es, size_t(plen) * es});
+    }
+    if (!ops.empty()) {
+      p2p_->group(comm, ops);
+      stats_.groups++;
+      stats_.ops += int64_t(ops.size());
+    }
+    for (int32_t i = 1; i < N; ++i)
+      stats_.bytes_sent += (g.block_len((me + i) % N) + my_len) * int64_t(es);
+  }
+  p2p_->check();
+  stats_.rounds++;
+  stats_.bulk_rounds++;
+  mark_scheduled(r);
+  return true;
+}
+
 void StreamLink::mark_scheduled(int32_t r) {
   scheduled_.insert(r);
   while (scheduled_.size() > 4096) scheduled_.erase(scheduled_.begin());

@@ -34,7 +34,19 @@ namespace akka {
 
 struct StreamLinkStats {
   int64_t groups = 0, ops = 0, bytes_sent = 0, rounds = 0, unreduced_chunks = 0;
+  int64_t bulk_rounds = 0, collective_rounds = 0;
 };
+
+// Which schedule runs an exact-threshold round (thReduce = thComplete = 1):
+//  P2P        the chunk-pipelined step schedule below, like every other round;
+//  Collective the bulk lane: RCCL reduce-scatter + all-gather over the whole
+//             buffer when the geometry is even (S == N * step), otherwise a
+//             whole-block direct exchange (one grouped p2p per phase around
+//             one N-way reduce);
+//  Auto       Collective when the transport has native collectives and the
+//             geometry is even, else P2P.
+// Threshold rounds (< 1) always take the step schedule.
+enum class Lane : int32_t { Auto = 0, P2P = 1, Collective = 2 };
 
 class StreamLink final : public Link {
  public:
@@ -46,7 +58,10 @@ class StreamLink final : public Link {
   void on_scattered(int32_t round) override;
   void pump() override;
   bool may_finalize(int32_t round) override;
+  bool bulk_round(int32_t round) override;
 
+  void set_lane(Lane l) { lane_ = l; }
+  Lane lane() const { return lane_; }
   const StreamLinkStats& stats() const { return stats_; }
   int32_t lag() const { return lag_; }
 
@@ -72,6 +87,7 @@ class StreamLink final : public Link {
   std::set<int32_t> in_flight_;
   std::set<int32_t> scheduled_;
   bool pumping_ = false;
+  Lane lane_ = Lane::Auto;
   StreamLinkStats stats_;
 };
 

@@ -52,6 +52,17 @@ def test_bench_multirank_line(n, transport):
     assert [r["rank"] for r in d["rank_devices"]] == list(range(n))
     assert all(r["p2p"]["nranks"] == n and r["p2p"]["rank"] == r["rank"] for r in d["rank_devices"])
     assert d["groups_per_round"] > 0 and d["host_us_per_round"] > 0
+    # gloo has no native collectives: auto keeps the chunk schedule, and the
+    # whole-round lane is measured as the other lane (stream transport only)
+    assert d["lane"] == "p2p"
+    if transport == "stream":
+        assert d["other_lane"]["lane"] == "collective" and d["other_lane"]["algbw_GBps"] > 0
+
+
+def test_bench_collective_lane_line():
+    d = _run(3, "--lane", "collective")
+    assert d["exact"] is True and d["lane"] == "collective" and d["other_lane"]["lane"] == "p2p"
+    assert d["groups_per_round"] == 2.0
 
 
 def test_bench_multirank_extras_deadline():

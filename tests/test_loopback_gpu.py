@@ -98,3 +98,22 @@ def test_loopback_n8_64mib_async():
         torch.cuda.synchronize()
         for o in outs:
             assert bool((o.data == want).all()) and bool((o.count == n).all())
+
+
+@pytest.mark.parametrize("n", [2, 3, 8])
+@pytest.mark.parametrize("S,C", [(1 << 16, 1 << 12), (100_003, 777), (5, 1)])
+def test_loopback_collective_lane(n, S, C):
+    """Exact rounds on the whole-round lane with real HIP streams: whole-block
+    direct exchange (the loopback endpoint has no native collectives) around
+    one gfx950 N-way reduce, several rounds through the ring, async hand-off."""
+    cl = LoopbackCluster(n, S, C, max_lag=1, lane="collective")
+    rounds = [_inputs(n, S, r) for r in range(4)]
+    outs = [cl.allreduce(xs, async_op=True) for xs in rounds]
+    for xs, os_ in zip(rounds, outs):
+        want = torch.stack(xs).sum(0)
+        for o in os_:
+            o.wait()
+            assert torch.equal(o.data, want)
+            assert bool((o.count == n).all())
+    st = cl.workers[0].state()
+    assert st["link"]["bulk_rounds"] == 4 and st["stats"]["bulk_rounds"] == 4

@@ -66,3 +66,22 @@ def test_rccl_n8_step_shape_exact(ep):
     ep.group(torch.cuda.current_stream(dev).cuda_stream, ops)
     torch.cuda.synchronize()
     assert all(torch.equal(a, b) for a, b in zip(src, dst))
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_rccl_collective_lane_calls(ep, dtype):
+    """The whole-round lane's two RCCL calls (reduce-scatter, then in-place
+    all-gather) with the types the engine passes; on a 1-rank communicator
+    both are copies, so the result must equal the input bit for bit."""
+    dev = torch.device("cuda", 0)
+    assert ep.has_collectives()
+    n = (1 << 20) + 16
+    x = torch.randn(n, device=dev).to(dtype)
+    out = torch.empty_like(x)
+    s = torch.cuda.current_stream(dev).cuda_stream
+    name = "bfloat16" if dtype == torch.bfloat16 else "float32"
+    ep.reduce_scatter(s, x.data_ptr(), out.data_ptr(), n, name)
+    ep.all_gather(s, out.data_ptr(), out.data_ptr(), n, name)
+    torch.cuda.synchronize()
+    assert torch.equal(out, x)
+    ep.check()

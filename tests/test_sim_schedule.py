@@ -124,3 +124,63 @@ def test_completion_before_late_chunks_are_reduced(n, S, C, th):
             assert torch.equal(pc.int(), o.count)
             assert bool((o.count == 0).any())  # some chunks never made it: holes, not garbage
     assert cl.workers[0].state()["link"]["unreduced_chunks"] > 0
+
+
+@pytest.mark.parametrize("n", [2, 3, 4, 8])
+@pytest.mark.parametrize("S,C", [(64, 8), (1000, 7), (5, 1), (4096, 4096), (333, 1000)])
+def test_collective_lane_exact(n, S, C):
+    """Exact rounds on the whole-round lane (stream_link.cpp bulk_round): the
+    simulator has no native collectives, so this is the whole-block direct
+    exchange -- two grouped p2p per round around one N-way reduce.  Same sums
+    and counts as the chunk schedule, traffic = 2(N-1)/N*S per rank, no
+    separate counts exchange (every count is N)."""
+    cl = SimCluster(n, S, C, max_lag=1, lane="collective")
+    g = Geometry(S, n, C)
+    before = 0
+    for r in range(4):
+        xs = _inputs(n, S, r)
+        outs = cl.allreduce(xs)
+        want = torch.stack(xs).sum(0)
+        for rank, o in enumerate(outs):
+            assert o.iteration == r
+            assert torch.equal(o.data, want), (rank, r)
+            assert bool((o.count == n).all()), (rank, r)
+        moved = cl.bytes_moved() - before
+        before = cl.bytes_moved()
+        assert moved == 2 * (n - 1) * S * 4
+    for w in cl.workers:
+        st = w.state()
+        assert st["round"] == 4 and st["stats"]["rounds_completed"] == 4
+        assert st["stats"]["bulk_rounds"] == 4 and st["link"]["bulk_rounds"] == 4
+        assert st["link"]["groups"] == 4 * 2 and st["link"]["lane"] == "collective"
+        assert st["stats"]["chunks_reduced"] == 4 * g.num_chunks(st["id"])
+
+
+def test_collective_lane_only_for_exact_rounds():
+    """Thresholds < 1 depend on arrival order: the lane is not taken."""
+    n, S, C = 4, 400, 50
+    cl = SimCluster(n, S, C, th_reduce=0.75, lane="collective")
+    cl.allreduce(_inputs(n, S, 0))
+    assert all(w.state()["link"]["bulk_rounds"] == 0 for w in cl.workers)
+
+
+def test_auto_lane_without_native_collectives_keeps_chunk_schedule():
+    n, S, C = 4, 4096, 100
+    cl = SimCluster(n, S, C)
+    cl.allreduce(_inputs(n, S, 0))
+    st = cl.workers[0].state()
+    assert st["link"]["bulk_rounds"] == 0 and st["link"]["lane"] == "auto"
+    assert st["link"]["groups"] == Geometry(S, n, C).kmax + 2
+
+
+def test_lane_switch_between_rounds():
+    n, S, C = 3, 999, 10
+    cl = SimCluster(n, S, C, max_lag=2)
+    for r, lane in enumerate(["p2p", "collective", "p2p", "collective", "collective"]):
+        for w in cl.workers:
+            w.set_lane(lane)
+        xs = _inputs(n, S, r)
+        outs = cl.allreduce(xs)
+        want = torch.stack(xs).sum(0)
+        assert all(torch.equal(o.data, want) and bool((o.count == n).all()) for o in outs), (r, lane)
+    assert cl.workers[0].state()["link"]["bulk_rounds"] == 3
