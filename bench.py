@@ -54,6 +54,10 @@ def parse():
     p.add_argument("--preflight", choices=["auto", "on"], default="auto",
                    help="auto: preflight round only at N>1")
     p.add_argument("--pg-timeout-s", type=float, default=300.0, help="host (gloo) process group timeout")
+    p.add_argument("--extras-only", default="", help="comma list of extra configs to run (cfg3,cfg4,cfg5)")
+    p.add_argument("--cfg4-size-mb", type=float, default=64.0, help="config 4 buffer (MiB)")
+    p.add_argument("--cfg4-delay-ms", type=float, default=50.0, help="config 4 straggler delay per round")
+    p.add_argument("--cfg4-rounds", type=int, default=10)
     p.add_argument("--extras-deadline-s", type=float, default=240.0,
                    help="give up on the extra configs after this many seconds (the headline line is still printed)")
     p.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
@@ -108,16 +112,89 @@ def timed(step, steps: int, warmup: int, world: int, barrier) -> float:
     return dt
 
 
-def run_extras(world: int, dev, barrier) -> dict:
-    """BASELINE config 3 (8-rank bf16, 1 GB buffer, link-sized chunks) and
-    config 5 (2-layer MLP DP-SGD step/s) at this N, on synthetic data."""
+class _Skip(Exception):
+    pass
+
+
+def run_cfg4(world: int, rank: int, dev, barrier, size_mb: float, delay_ms: float, rounds: int) -> dict:
+    """BASELINE config 4: threshold allreduce at thReduce = thComplete = 0.75,
+    maxLag 1, with rank N-1 an induced straggler (sleeps ``delay_ms`` before
+    each round), on the straggler-tolerant reactive transport (one pair
+    communicator + stream per peer, reactive_link.h).  Reports the fast ranks'
+    time per round with and without the straggler (max over the fast ranks),
+    the mean contributor count they saw, and the forced (catch-up) rounds.
+    Reference: thresholds SB:9-13 / RB:13-17, catch-up W:100-106, pacing M:58.
+    With N < 4, 0.75 of the chunks cannot complete without the straggler's
+    block, so the fast ranks wait for it -- the reported times show that."""
+    import torch
+    import torch.distributed as dist
+
+    from akka_allreduce_amd.parallel import ThresholdAllreduce
+
+    esize = 4
+    S = int(size_mb * (1 << 20)) // esize
+    C = max(1, min(S, (4 << 20) // esize))
+    ar = ThresholdAllreduce(S, max_chunk_size=C, th_reduce=0.75, th_complete=0.75, max_lag=1, device=dev,
+                            transport="reactive")
+    run_cfg4.keep = ar  # type: ignore[attr-defined]
+    straggler = world - 1
+    g = torch.Generator(device=dev).manual_seed(77 + rank)
+    x = torch.randn(S, device=dev, generator=g)
+    res = {"thresholds": [1.0, 0.75, 0.75], "max_lag": 1, "straggler_rank": straggler,
+           "straggler_delay_ms": delay_ms, "rounds": rounds, "buffer_bytes": S * esize, "transport": "reactive"}
+
+    def phase(delay_s: float):
+        ar.fault_delay_s = delay_s if rank == straggler else 0.0
+        outs = []
+        t0 = time.perf_counter()
+        for _ in range(rounds):
+            outs.append(ar(x))
+        _sync()
+        dt = time.perf_counter() - t0
+        cnt = [float(o.count.float().mean()) for o in outs]
+        ar.fault_delay_s = 0.0
+        ar.drain()  # every transfer of this rank done before the blocking collectives
+        _sync()
+        barrier()
+        return dt, sum(cnt) / len(cnt)
+
+    phase(0.0)  # warm-up: pair connections, send-slot pool
+    for key, delay_s in (("no_straggler", 0.0), ("with_straggler", delay_ms / 1e3)):
+        forced0 = ar.state()["stats"]["rounds_forced"]
+        dt, mean_count = phase(delay_s)
+        forced = ar.state()["stats"]["rounds_forced"] - forced0
+        t = torch.tensor([dt / rounds * 1e3, mean_count, float(forced)], dtype=torch.float64)
+        allv = [torch.zeros_like(t) for _ in range(world)] if world > 1 else [t]
+        if world > 1:
+            dist.all_gather(allv, t)
+        fast = [v for i, v in enumerate(allv) if i != straggler] or allv
+        res[f"fast_rank_ms_per_round_{key}"] = round(max(float(v[0]) for v in fast), 3)
+        res[f"straggler_ms_per_round_{key}"] = round(float(allv[straggler][0]), 3)
+        res[f"fast_rank_mean_count_{key}"] = round(sum(float(v[1]) for v in fast) / len(fast), 4)
+        res[f"forced_rounds_{key}"] = int(sum(float(v[2]) for v in allv))
+    return res
+
+
+def run_extras(world: int, dev, barrier, which=("cfg3", "cfg4", "cfg5"), rank: int = 0,
+               cfg4_size_mb: float = 64.0, cfg4_delay_ms: float = 50.0, cfg4_rounds: int = 10) -> dict:
+    """BASELINE config 3 (8-rank bf16, 1 GB buffer, link-sized chunks),
+    config 4 (threshold 0.75/0.75 + straggler, N>1 only) and config 5 (2-layer
+    MLP DP-SGD step/s) at this N, on synthetic data."""
     import torch
 
     from akka_allreduce_amd.parallel import ThresholdAllreduce
 
     res: dict = {}
     keep = []  # communicators stay alive until exit (no per-rank teardown ordering)
+    if "cfg4" in which and world > 1:
+        try:
+            res["cfg4_threshold_straggler"] = run_cfg4(world, rank, dev, barrier, cfg4_size_mb, cfg4_delay_ms,
+                                                       cfg4_rounds)
+        except Exception as e:
+            res["cfg4_error"] = f"{type(e).__name__}: {e}"[:300]
     try:
+        if "cfg3" not in which:
+            raise _Skip()
         nbytes = 1 << 30
         S = nbytes // 2
         ar = ThresholdAllreduce(S, max_chunk_size=(8 << 20) // 2, dtype=torch.bfloat16, device=dev)
@@ -129,9 +206,13 @@ def run_extras(world: int, dev, barrier) -> dict:
         res["cfg3_bf16_1GiB_chunk8MiB"] = {"algbw_GBps": round(nbytes / (dt / steps) / 1e9, 3),
                                            "ms_per_step": round(dt / steps * 1e3, 4)}
         del x, out
+    except _Skip:
+        pass
     except Exception as e:
         res["cfg3_error"] = f"{type(e).__name__}: {e}"[:200]
     try:
+        if "cfg5" not in which:
+            raise _Skip()
         from akka_allreduce_amd.models.mlp import MLP, dp_sgd_step, synthetic_batch
         from akka_allreduce_amd.parallel.dp import GradientBucket
 
@@ -157,6 +238,8 @@ def run_extras(world: int, dev, barrier) -> dict:
         res["cfg5_mlp_dp_sgd_bf16"] = {"steps_per_s": round(steps / dt, 3),
                                        "samples_per_s": round(steps * batch * world / dt, 1),
                                        "compute_dtype": "bf16 autocast, fp32 master weights/grads"}
+    except _Skip:
+        pass
     except Exception as e:
         res["cfg5_error"] = f"{type(e).__name__}: {e}"[:200]
     run_extras.keep = keep  # type: ignore[attr-defined]
@@ -185,10 +268,13 @@ def main() -> int:
     if args.transport == "reactive":
         # one stream per peer: must not share hardware queues (read at HIP init)
         os.environ["GPU_MAX_HW_QUEUES"] = "32"
-    elif int(os.environ.get("WORLD_SIZE", "1")) > 1 and int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 8:
+    elif int(os.environ.get("WORLD_SIZE", "1")) > 1:
         # comm + compute + caller (+ RCCL's own) streams each on their own
-        # hardware queue, so chunk reduces never serialise behind transfers
-        os.environ["GPU_MAX_HW_QUEUES"] = "8"
+        # hardware queue, so chunk reduces never serialise behind transfers;
+        # config 4 (reactive transport) needs one more per peer: N + 4
+        need = min(32, max(8, int(os.environ["WORLD_SIZE"]) + 4))
+        if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < need:
+            os.environ["GPU_MAX_HW_QUEUES"] = str(need)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -469,7 +555,9 @@ def main() -> int:
         late = dict(line)
         late["extras_error"] = f"extras not done after {args.extras_deadline_s:g} s; skipped"
         guard.arm(args.extras_deadline_s, late, exit_code=0 if ok in (None, True) else 1)
-        line["extra_configs"] = run_extras(world, dev, barrier)
+        which = tuple(args.extras_only.split(",")) if args.extras_only else ("cfg3", "cfg4", "cfg5")
+        line["extra_configs"] = run_extras(world, dev, barrier, which, rank, args.cfg4_size_mb,
+                                           args.cfg4_delay_ms, args.cfg4_rounds)
         guard.disarm()
 
     if rank == 0:

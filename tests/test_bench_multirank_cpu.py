@@ -93,3 +93,21 @@ def test_bench_rank_error_reported_by_rank0():
     assert d["failed_phase"] == "warmup"
     # either through the agreement step or through the failure beacon
     assert "injected fault on rank 1" in json.dumps(d), d
+
+
+def test_bench_cfg4_threshold_straggler():
+    """BASELINE config 4 in the bench extras (reactive transport, 0.75/0.75,
+    maxLag 1, rank N-1 sleeps before each round).  At N=4 three of four
+    contributions reduce a chunk and 3/4 of the chunks complete a round, so
+    the fast ranks must not wait for the straggler: their time per round stays
+    well below its delay.  (At N=2/3, 0.75 of the chunks always includes the
+    straggler's block, so there the fast ranks do wait -- the reference's
+    semantics.)"""
+    delay = 150.0
+    d = _run(4, "--extras", "on", "--extras-only", "cfg4", "--cfg4-size-mb", "1", "--cfg4-delay-ms", str(delay),
+             "--cfg4-rounds", "6")
+    c = d["extra_configs"]["cfg4_threshold_straggler"]
+    assert c["straggler_rank"] == 3 and c["thresholds"] == [1.0, 0.75, 0.75] and c["max_lag"] == 1
+    assert c["straggler_ms_per_round_with_straggler"] >= delay
+    assert c["fast_rank_ms_per_round_with_straggler"] < delay / 3, c
+    assert 0 < c["fast_rank_mean_count_with_straggler"] <= 3
