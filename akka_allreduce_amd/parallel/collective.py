@@ -164,6 +164,12 @@ class ThresholdAllreduce:
             raise ValueError("lanes belong to the scheduled (stream) transport")
         self.worker.set_lane(lane)
 
+    def set_graphs(self, on: bool = True) -> None:
+        """HIP-graph replay of exact p2p-lane rounds (see AllreduceWorker.set_graphs)."""
+        if self.transport != "stream":
+            raise ValueError("graphs belong to the scheduled (stream) transport")
+        self.worker.set_graphs(on)
+
     def state(self) -> dict:
         return self.worker.state()
 

@@ -221,6 +221,9 @@ class AllreduceWorker:
         if kind == "rccl":
             _, uid, rank, nranks = spec
             self._core.connect_rccl(uid, int(rank), int(nranks))
+        elif kind == "rccl_shape":
+            _, rank, nranks = spec
+            self._core.connect_rccl_shape(int(rank), int(nranks))
         elif kind == "sim":
             _, hub, rank = spec
             self._core.connect_sim(hub, int(rank))
@@ -314,6 +317,12 @@ class AllreduceWorker:
         (see csrc/transport/stream_link.h).  Threshold rounds (< 1) always run
         the p2p schedule."""
         self._core.set_lane(lane)
+
+    def set_graphs(self, on: bool = True) -> None:
+        """Replay exact p2p-lane rounds from captured HIP graphs: a round whose
+        buffers (input, ring row, output) were seen before is captured once,
+        later ones are one graph launch (stream_link.h).  GPU only."""
+        self._core.set_graphs(bool(on))
 
     def _fast_ok(self, tensor: torch.Tensor) -> bool:
         """Collective-style call on the scheduled transport, whose rounds

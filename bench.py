@@ -481,7 +481,7 @@ def main() -> int:
     # and the chunk-pipelined p2p schedule.
     def other_lane():
         st0 = ar.state().get("link", {})
-        used = "collective" if st0.get("bulk_rounds", 0) else "p2p"
+        used = "collective" if st0.get("bulk_rounds", 0) > st0.get("exact_step_rounds", 0) else "p2p"
         if world == 1 or ar.transport != "stream":
             return used, None
         other = "p2p" if used == "collective" else "collective"

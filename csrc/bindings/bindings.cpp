@@ -132,6 +132,14 @@ class WorkerCore final : public EngineHost {
     p2p_ = make_rccl_p2p(v, rank, nranks, device_idx_);
     make_stream_link();
   }
+  // Host-cost rehearsal of the N-rank schedule on one GPU (rccl_p2p.cpp
+  // RcclShapeP2P): the bytes are meaningless, the host path is the real one.
+  void connect_rccl_shape(int32_t rank, int32_t nranks) {
+    AKKA_CHECK(dev_ && !dev_->is_host(), "RCCL transport needs a HIP device");
+    AKKA_CHECK(link_kind_ == "stream", "shape rehearsal runs the scheduled transport");
+    p2p_ = make_rccl_shape_p2p(rank, nranks, device_idx_);
+    make_stream_link();
+  }
   void connect_sim(const PySimHub& hub, int32_t rank) {
     AKKA_CHECK(dev_ && dev_->is_host() && deferred_, "sim transport needs a deferred host device");
     p2p_ = make_sim_p2p(hub.hub, rank, dev_.get());
@@ -288,6 +296,11 @@ class WorkerCore final : public EngineHost {
       ls["lag"] = stream_link_->lag();
       ls["bulk_rounds"] = stream_link_->stats().bulk_rounds;
       ls["collective_rounds"] = stream_link_->stats().collective_rounds;
+      ls["exact_step_rounds"] = stream_link_->stats().exact_step_rounds;
+      ls["graph_captures"] = stream_link_->stats().graph_captures;
+      ls["graph_replays"] = stream_link_->stats().graph_replays;
+      ls["graphs"] = stream_link_->graphs();
+      if (!stream_link_->graph_error().empty()) ls["graph_error"] = stream_link_->graph_error();
       const Lane ln = stream_link_->lane();
       ls["lane"] = ln == Lane::Auto ? "auto" : ln == Lane::P2P ? "p2p" : "collective";
       d["link"] = ls;
@@ -329,6 +342,10 @@ class WorkerCore final : public EngineHost {
     else if (lane == "p2p") stream_link_->set_lane(Lane::P2P);
     else if (lane == "collective") stream_link_->set_lane(Lane::Collective);
     else throw AkkaError("akka: lane must be 'auto', 'p2p' or 'collective'");
+  }
+  void set_graphs(bool on) {
+    AKKA_CHECK(stream_link_, "set_graphs: scheduled (stream) transport only");
+    stream_link_->set_graphs(on);
   }
   void p2p_check() {
     if (p2p_) p2p_->check();
@@ -482,6 +499,7 @@ PYBIND11_MODULE(_native, m) {
       .def("init", &WorkerCore::init)
       .def("connect_rccl", &WorkerCore::connect_rccl)
       .def("connect_sim", &WorkerCore::connect_sim)
+      .def("connect_rccl_shape", &WorkerCore::connect_rccl_shape)
       .def("connect_local", &WorkerCore::connect_local)
       .def("connect_callback", &WorkerCore::connect_callback)
       .def("connect_loopback", &WorkerCore::connect_loopback)
@@ -512,6 +530,7 @@ PYBIND11_MODULE(_native, m) {
       .def("p2p_info", &WorkerCore::p2p_info)
       .def("p2p_check", &WorkerCore::p2p_check)
       .def("set_lane", &WorkerCore::set_lane)
+      .def("set_graphs", &WorkerCore::set_graphs)
       .def("scatter_count", &WorkerCore::scatter_count)
       .def("reduced_arrivals", &WorkerCore::reduced_arrivals);
 

@@ -20,6 +20,7 @@ namespace akka {
 
 using StreamH = void*;
 using EventH = void*;
+using GraphH = void*;  // an instantiated (executable) graph
 
 // Sources per reduce launch; more sources are folded in extra passes.
 constexpr int kMaxReduceSrc = 16;
@@ -75,6 +76,15 @@ class Device {
   virtual void fill_i32(StreamH s, int32_t* dst, int32_t value, size_t n) = 0;
   // Issue any work held back on `s` (reduce launches kept open for merging).
   virtual void flush(StreamH) {}
+
+  // Stream capture into graphs (HIP graphs).  While capturing, wait() must
+  // never be elided and nothing may synchronize.  Host devices: unsupported.
+  virtual bool begin_capture(StreamH) { return false; }
+  // Ends the capture on `s`; returns the instantiated graph, or nullptr (and
+  // discards the capture) if `discard` or the capture failed.
+  virtual GraphH end_capture(StreamH, bool /*discard*/) { return nullptr; }
+  virtual void launch_graph(GraphH, StreamH) { throw AkkaError("launch_graph: unsupported device"); }
+  virtual void destroy_graph(GraphH) {}
 
   // Run `fn` on a host thread once the stream reaches this point (HIP:
   // hipLaunchHostFunc; `fn` must not call HIP).  Default: unsupported.

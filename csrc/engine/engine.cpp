@@ -228,13 +228,23 @@ void Engine::scatter(int32_t r) {
 }
 
 bool Engine::bulk_eligible(int32_t r) const {
-  // The outcome of round r is fixed only with exact thresholds and the full
-  // membership, for the oldest open round (nothing to catch up, nothing of it
-  // received yet: its ring row still belongs to an older round).
+  // The outcome of round r is fixed with exact thresholds and the full
+  // membership.  The decision must not depend on local timing: a scheduled
+  // link runs exact rounds with their own pairwise-matched schedule, so every
+  // rank has to take it for the same rounds.  Local state that would make
+  // this rank deviate (older rounds still open, part of r already received)
+  // is an error rather than a silent switch to a different schedule.
   if (!link_ || N_ < 2 || int32_t(peers_.size()) != N_) return false;
   if (min_scatter_ != N_ || int64_t(min_reduced_) != g_.total_chunks()) return false;
-  if (r != round_ || r != max_round_ || completed_.count(r)) return false;
-  return find_row(r) == nullptr;
+  const bool clean = r == round_ && r == max_round_ && !completed_.count(r) && find_row(r) == nullptr;
+  if (!clean) {
+    // outbox / reactive links run the message flow for every round anyway
+    AKKA_CHECK(!link_->takes_exact_rounds(),
+               "round " + std::to_string(r) + " is exact but cannot run as a whole (older rounds open or part of it "
+               "already received): the scheduled transport needs rounds started in order");
+    return false;
+  }
+  return true;
 }
 
 void Engine::complete_bulk(int32_t r) {

@@ -74,6 +74,9 @@ class Link {
   // and returns true; the engine then completes the round without per-chunk
   // bookkeeping.  False: the engine runs the ordinary message flow.
   virtual bool bulk_round(int32_t /*round*/) { return false; }
+  // True if bulk_round always takes exact rounds (its schedule for them
+  // differs from the message flow's, so every rank must take it).
+  virtual bool takes_exact_rounds() const { return false; }
 };
 
 // Embedding layer callbacks (Python, CLI, bench).

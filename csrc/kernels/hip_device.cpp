@@ -95,8 +95,10 @@ class HipDevice final : public Device {
   void wait(StreamH s, EventH e) override {
     flush_if(s);
     // An event that already completed needs no barrier packet on the stream
-    // (each cross-stream wait costs the command processor several us).
-    if (hipEventQuery(static_cast<hipEvent_t>(e)) == hipSuccess) return;
+    // (each cross-stream wait costs the command processor several us).  Not
+    // while capturing: an event recorded inside the capture has no eager
+    // record, so it would read as complete and the graph would lose an edge.
+    if (!capturing_ && hipEventQuery(static_cast<hipEvent_t>(e)) == hipSuccess) return;
     AKKA_HIP(hipStreamWaitEvent(static_cast<hipStream_t>(s), static_cast<hipEvent_t>(e), 0));
   }
   bool query(EventH e) override {
@@ -114,6 +116,36 @@ class HipDevice final : public Device {
   void sync_stream(StreamH s) override {
     flush_if(s);
     AKKA_HIP(hipStreamSynchronize(static_cast<hipStream_t>(s)));
+  }
+
+  bool begin_capture(StreamH s) override {
+    flush_all();
+    AKKA_HIP(hipStreamBeginCapture(static_cast<hipStream_t>(s), hipStreamCaptureModeRelaxed));
+    capturing_ = true;
+    return true;
+  }
+  GraphH end_capture(StreamH s, bool discard) override {
+    flush_all();
+    capturing_ = false;
+    hipGraph_t g = nullptr;
+    hipError_t e = hipStreamEndCapture(static_cast<hipStream_t>(s), &g);
+    if (e != hipSuccess || !g || discard) {
+      if (g) hipGraphDestroy(g);
+      if (e != hipSuccess && !discard) AKKA_HIP(e);
+      return nullptr;
+    }
+    hipGraphExec_t ex = nullptr;
+    e = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
+    hipGraphDestroy(g);
+    AKKA_HIP(e);
+    return ex;
+  }
+  void launch_graph(GraphH g, StreamH s) override {
+    flush_if(s);
+    AKKA_HIP(hipGraphLaunch(static_cast<hipGraphExec_t>(g), static_cast<hipStream_t>(s)));
+  }
+  void destroy_graph(GraphH g) override {
+    if (g) hipGraphExecDestroy(static_cast<hipGraphExec_t>(g));
   }
 
   void reduce(StreamH s, const ReduceSpec* specs, int32_t n, DType dt) override {
@@ -214,6 +246,7 @@ class HipDevice final : public Device {
   hipStream_t compute_ = nullptr;
   bool exported_ = false;
   ReduceImpl impl_;
+  bool capturing_ = false;
   std::vector<ReduceSpec> pending_;
   StreamH pending_stream_ = nullptr;
   DType pending_dt_ = DType::F32;

@@ -95,5 +95,7 @@ inline int32_t tournament_rounds(int32_t n) { return ((n % 2) ? n + 1 : n) - 1; 
 std::unique_ptr<P2P> make_rccl_pair_p2p(const std::vector<uint8_t>& uid, int32_t rank, int32_t nranks,
                                         int32_t device);
 const char* rccl_version_string();
+// One-GPU shape rehearsal (1-rank comm posing as rank/nranks, ops to self).
+std::unique_ptr<P2P> make_rccl_shape_p2p(int32_t rank, int32_t nranks, int32_t device);
 
 }  // namespace akka

@@ -193,7 +193,49 @@ class RcclPairP2P final : public P2P {
   std::vector<ncclComm_t> pair_;
 };
 
+// Shape rehearsal on ONE GPU: a 1-rank RCCL communicator that presents
+// itself as rank `rank` of `nranks` and sends every op to itself.  In an
+// exact round of an even geometry the k-th send and the k-th receive of a
+// group have the same size, so RCCL matches them pairwise; the bytes are
+// meaningless but the host path (engine, link, ncclGroupStart/End with the
+// N-rank group shape) and the GPU p2p kernels are the real ones.  Used to
+// measure the host cost per round of the N=8 schedule on a 1-GPU box.
+class RcclShapeP2P final : public P2P {
+ public:
+  RcclShapeP2P(int32_t rank, int32_t nranks, int32_t device) : rank_(rank), n_(nranks) {
+    if (hipSetDevice(device) != hipSuccess) throw AkkaError("akka: hipSetDevice failed");
+    ncclUniqueId id;
+    AKKA_NCCL(ncclGetUniqueId(&id));
+    AKKA_NCCL(ncclCommInitRank(&comm_, 1, id, 0));
+    verify_comm(comm_, 1, 0, device, "shape");
+  }
+  ~RcclShapeP2P() override {
+    if (comm_) ncclCommDestroy(comm_);
+  }
+  int32_t rank() const override { return rank_; }
+  int32_t nranks() const override { return n_; }
+  const char* name() const override { return "rccl-shape"; }
+  void group(StreamH stream, const std::vector<P2POp>& ops) override {
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    AKKA_NCCL(ncclGroupStart());
+    for (const auto& op : ops) {
+      if (op.send) AKKA_NCCL(ncclSend(op.buf, op.bytes, ncclUint8, 0, comm_, s));
+      else AKKA_NCCL(ncclRecv(op.buf, op.bytes, ncclUint8, 0, comm_, s));
+    }
+    AKKA_NCCL(ncclGroupEnd());
+  }
+  void check() override { check_async(comm_, "shape"); }
+
+ private:
+  int32_t rank_, n_;
+  ncclComm_t comm_ = nullptr;
+};
+
 }  // namespace
+
+std::unique_ptr<P2P> make_rccl_shape_p2p(int32_t rank, int32_t nranks, int32_t device) {
+  return std::make_unique<RcclShapeP2P>(rank, nranks, device);
+}
 
 std::unique_ptr<P2P> make_rccl_pair_p2p(const std::vector<uint8_t>& uid, int32_t rank, int32_t nranks,
                                         int32_t device) {

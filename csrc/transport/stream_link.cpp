@@ -8,6 +8,26 @@ StreamLink::StreamLink(Engine* engine, P2P* p2p, int32_t lag) : engine_(engine),
   AKKA_CHECK(lag >= 1, "broadcast lag must be >= 1 (a chunk is reduced after its scatter step)");
 }
 
+StreamLink::~StreamLink() {
+  if (graphs_map_.empty() || !dp_) return;
+  Device* dev = dp_->device();
+  try {
+    dev->sync_stream(dev->comm_stream());
+  } catch (...) {
+  }
+  for (auto& kv : graphs_map_) dev->destroy_graph(kv.second.exec);
+}
+
+void StreamLink::set_graphs(bool on) {
+  graphs_ = on && dp_ && !dp_->device()->is_host();
+  if (!graphs_ && !graphs_map_.empty()) {
+    Device* dev = dp_->device();
+    dev->sync_stream(dev->comm_stream());
+    for (auto& kv : graphs_map_) dev->destroy_graph(kv.second.exec);
+    graphs_map_.clear();
+  }
+}
+
 void StreamLink::send_scatter(int32_t dest, int32_t chunk, int32_t round, const Payload& p) {
   q_[round].scatter[{chunk, dest}] = Out{p.ptr, p.len};
 }
@@ -162,14 +182,25 @@ void StreamLink::schedule(int32_t r) {
 }
 
 bool StreamLink::bulk_round(int32_t r) {
-  if (lane_ == Lane::P2P || !dp_) return false;
+  AKKA_CHECK(dp_, "stream link has no data plane");
+  const Geometry& g = dp_->geometry();
+  const int32_t N = g.N;
+  if (N < 2) return false;  // a local round is already one pass
+  AKKA_CHECK(p2p_->nranks() == N && p2p_->rank() == dp_->me(), "p2p communicator does not match the worker geometry");
+  const bool native = p2p_->has_collectives() && g.S == int64_t(N) * g.step;
+  if (lane_ == Lane::Collective || (lane_ == Lane::Auto && native)) collective_round(r, native);
+  else exact_steps(r);
+  p2p_->check();
+  stats_.rounds++;
+  stats_.bulk_rounds++;
+  mark_scheduled(r);
+  return true;
+}
+
+void StreamLink::collective_round(int32_t r, bool native) {
   const Geometry& g = dp_->geometry();
   const int32_t N = g.N;
   const int32_t me = dp_->me();
-  if (N < 2) return false;  // a local round is already one pass
-  const bool native = p2p_->has_collectives() && g.S == int64_t(N) * g.step;
-  if (lane_ == Lane::Auto && !native) return false;
-  AKKA_CHECK(p2p_->nranks() == N && p2p_->rank() == me, "p2p communicator does not match the worker geometry");
   const size_t es = dp_->esize();
   Device* dev = dp_->device();
   engine_->ensure_output(r);
@@ -189,52 +220,191 @@ bool StreamLink::bulk_round(int32_t r) {
     stats_.groups += 2;
     stats_.bytes_sent += int64_t(2) * (N - 1) * g.step * int64_t(es);
     ++stats_.collective_rounds;
-  } else {
-    // Whole-block direct exchange: the reference's scatter / reduce /
-    // broadcast (W:212-268) with one message per peer and phase.
-    std::vector<P2POp> ops;
-    for (int32_t i = 1; i < N; ++i) {
-      const int32_t peer = (me + i) % N;
-      const int64_t plen = g.block_len(peer);
-      if (plen > 0) ops.push_back({true, peer, const_cast<char*>(in) + size_t(g.block_start(peer)) * es, size_t(plen) * es});
-      if (my_len > 0) ops.push_back({false, peer, dp_->scatter_slot(r, peer, 0), size_t(my_len) * es});
-    }
-    if (!ops.empty()) {
-      p2p_->group(comm, ops);
-      stats_.groups++;
-      stats_.ops += int64_t(ops.size());
-    }
-    if (my_len > 0) {
-      StreamH cs = dev->compute_stream();
-      dp_->compute_wait(dp_->record_comm());
-      dp_->wait_input(r, cs);
-      std::vector<const void*> srcs;
-      srcs.push_back(in + size_t(g.block_start(me)) * es);
-      for (int32_t i = 1; i < N; ++i) srcs.push_back(dp_->scatter_slot(r, (me + i) % N, 0));
-      auto specs = split_reduce(mine, srcs, my_len);
-      dev->reduce(cs, specs.data(), int32_t(specs.size()), dp_->dtype());
-      dp_->comm_wait(dp_->record_compute());
-    }
-    ops.clear();
-    for (int32_t i = 1; i < N; ++i) {
-      const int32_t peer = (me + i) % N;
-      const int64_t plen = g.block_len(peer);
-      if (my_len > 0) ops.push_back({true, peer, mine, size_t(my_len) * es});
-      if (plen > 0) ops.push_back({false, peer, out + size_t(g.block_start(peer)) * es, size_t(plen) * es});
-    }
-    if (!ops.empty()) {
-      p2p_->group(comm, ops);
-      stats_.groups++;
-      stats_.ops += int64_t(ops.size());
-    }
-    for (int32_t i = 1; i < N; ++i)
-      stats_.bytes_sent += (g.block_len((me + i) % N) + my_len) * int64_t(es);
+    return;
   }
-  p2p_->check();
-  stats_.rounds++;
-  stats_.bulk_rounds++;
-  mark_scheduled(r);
-  return true;
+  // Whole-block direct exchange: the reference's scatter / reduce / broadcast
+  // (W:212-268) with one message per peer and phase.
+  std::vector<P2POp>& ops = scratch_;
+  ops.clear();
+  for (int32_t i = 1; i < N; ++i) {
+    const int32_t peer = (me + i) % N;
+    const int64_t plen = g.block_len(peer);
+    if (plen > 0) ops.push_back({true, peer, const_cast<char*>(in) + size_t(g.block_start(peer)) * es, size_t(plen) * es});
+    if (my_len > 0) ops.push_back({false, peer, dp_->scatter_slot(r, peer, 0), size_t(my_len) * es});
+  }
+  if (!ops.empty()) {
+    p2p_->group(comm, ops);
+    stats_.groups++;
+    stats_.ops += int64_t(ops.size());
+  }
+  if (my_len > 0) {
+    StreamH cs = dev->compute_stream();
+    dp_->compute_wait(dp_->record_comm());
+    dp_->wait_input(r, cs);
+    std::vector<const void*> srcs;
+    for (int32_t src = 0; src < N; ++src)  // ascending source id, like the message flow
+      srcs.push_back(src == me ? static_cast<const void*>(in + size_t(g.block_start(me)) * es)
+                               : dp_->scatter_slot(r, src, 0));
+    auto specs = split_reduce(mine, srcs, my_len);
+    dev->reduce(cs, specs.data(), int32_t(specs.size()), dp_->dtype());
+    dp_->comm_wait(dp_->record_compute());
+  }
+  ops.clear();
+  for (int32_t i = 1; i < N; ++i) {
+    const int32_t peer = (me + i) % N;
+    const int64_t plen = g.block_len(peer);
+    if (my_len > 0) ops.push_back({true, peer, mine, size_t(my_len) * es});
+    if (plen > 0) ops.push_back({false, peer, out + size_t(g.block_start(peer)) * es, size_t(plen) * es});
+  }
+  if (!ops.empty()) {
+    p2p_->group(comm, ops);
+    stats_.groups++;
+    stats_.ops += int64_t(ops.size());
+  }
+  for (int32_t i = 1; i < N; ++i) stats_.bytes_sent += (g.block_len((me + i) % N) + my_len) * int64_t(es);
+}
+
+void StreamLink::build_exact_template() {
+  // The exact round's step schedule depends only on the geometry and the lag:
+  // built once, then every round only adds three base pointers.  Same groups
+  // and per-pair order as schedule() minus the counts exchange (all N).
+  const Geometry& g = dp_->geometry();
+  const int32_t me = dp_->me();
+  const int32_t N = g.N;
+  const size_t es = dp_->esize();
+  const int32_t kme = g.num_chunks(me);
+  const int32_t steps = g.max_block_len_chunks() + lag_;
+  const char* ring0 = static_cast<const char*>(dp_->scatter_slot(0, 0, 0));
+  exact_.assign(size_t(steps), {});
+  for (int32_t s = 0; s < steps; ++s) {
+    auto& v = exact_[size_t(s)];
+    const int32_t kb = s - lag_;
+    const bool bcast = kb >= 0 && kb < kme;
+    for (int32_t i = 1; i < N; ++i) {
+      const int32_t peer = (me + i) % N;
+      const int32_t kp = g.num_chunks(peer);
+      if (s < kp) v.push_back({true, peer, 0, g.chunk_offset(peer, s) * int64_t(es), size_t(g.chunk_len(peer, s)) * es});
+      if (s < kme)
+        v.push_back({false, peer, 1, static_cast<const char*>(dp_->scatter_slot(0, peer, s)) - ring0,
+                     size_t(g.chunk_len(me, s)) * es});
+      if (bcast) v.push_back({true, peer, 2, g.chunk_offset(me, kb) * int64_t(es), size_t(g.chunk_len(me, kb)) * es});
+      if (kb >= 0 && kb < kp)
+        v.push_back({false, peer, 2, g.chunk_offset(peer, kb) * int64_t(es), size_t(g.chunk_len(peer, kb)) * es});
+    }
+  }
+  reduced_ev_.assign(size_t(std::max(kme, 1)), nullptr);
+  exact_groups_ = exact_ops_ = exact_bytes_ = 0;
+  for (const auto& v : exact_) {
+    if (!v.empty()) ++exact_groups_;
+    exact_ops_ += int64_t(v.size());
+    for (const auto& t : v)
+      if (t.send) exact_bytes_ += int64_t(t.bytes);
+  }
+}
+
+void StreamLink::exact_steps(int32_t r) {
+  if (exact_.empty()) build_exact_template();
+  Device* dev = dp_->device();
+  engine_->ensure_output(r);
+  StreamH comm = dev->comm_stream();
+  dp_->comm_wait(dp_->row_release_event(r));  // ring row r%L was last read by round r-L's reduces
+  dp_->wait_input(r, comm);
+  dp_->mark_comm_used(r);
+  char* base[3] = {const_cast<char*>(static_cast<const char*>(dp_->input_chunk(r, 0, 0).ptr)),
+                   static_cast<char*>(dp_->scatter_slot(r, 0, 0)), static_cast<char*>(dp_->output_at(r, 0, 0))};
+  ++stats_.exact_step_rounds;
+  if (graphs_) {
+    auto key = std::make_tuple(base[0], base[1], base[2]);
+    GraphEntry& ge = graphs_map_[key];
+    ge.last_use = ++tick_;
+    if (ge.exec) {
+      // the whole round is in comm-stream order: everything after it (the
+      // next round's ring reuse, finalize's join) orders behind the launch
+      dev->launch_graph(ge.exec, comm);
+      ++stats_.graph_replays;
+      stats_.groups += exact_groups_;
+      stats_.ops += exact_ops_;
+      stats_.bytes_sent += exact_bytes_;
+      return;
+    }
+    if (++ge.seen >= 2) {
+      if (graphs_map_.size() > 16) {  // LRU: keep the cache bounded (fresh buffers every round never repeat)
+        auto victim = graphs_map_.end();
+        for (auto it = graphs_map_.begin(); it != graphs_map_.end(); ++it)
+          if (it->first != key && (victim == graphs_map_.end() || it->second.last_use < victim->second.last_use))
+            victim = it;
+        if (victim != graphs_map_.end()) {
+          if (victim->second.exec) {
+            dev->sync_stream(comm);
+            dev->destroy_graph(victim->second.exec);
+          }
+          graphs_map_.erase(victim);
+        }
+      }
+      GraphEntry& g2 = graphs_map_[key];
+      GraphH exec = nullptr;
+      dev->begin_capture(comm);
+      try {
+        exact_body(r, base, /*captured=*/true);
+        exec = dev->end_capture(comm, false);
+      } catch (const std::exception& e) {
+        dev->end_capture(comm, true);
+        graph_error_ = e.what();
+        set_graphs(false);  // capture unsupported here: stay eager from now on
+        exact_body(r, base, false);
+        return;
+      }
+      g2.exec = exec;
+      ++stats_.graph_captures;
+      dev->launch_graph(exec, comm);
+      stats_.groups += exact_groups_;
+      stats_.ops += exact_ops_;
+      stats_.bytes_sent += exact_bytes_;
+      return;
+    }
+  }
+  exact_body(r, base, false);
+  stats_.groups += exact_groups_;
+  stats_.ops += exact_ops_;
+  stats_.bytes_sent += exact_bytes_;
+}
+
+void StreamLink::exact_body(int32_t r, char* const base[3], bool captured) {
+  const Geometry& g = dp_->geometry();
+  const int32_t me = dp_->me();
+  const int32_t N = g.N;
+  const size_t es = dp_->esize();
+  const int32_t kme = g.num_chunks(me);
+  Device* dev = dp_->device();
+  StreamH comm = dev->comm_stream();
+  StreamH cs = dev->compute_stream();
+  // Eager: the compute stream waits for the input's producer.  Captured: the
+  // compute branch forks from the comm stream inside the graph, which starts
+  // after the comm stream's (eager) input wait.
+  if (!captured && kme > 0) dp_->wait_input(r, cs);
+  std::vector<P2POp>& ops = scratch_;
+  std::vector<const void*> srcs(static_cast<size_t>(N), nullptr);
+  for (size_t s = 0; s < exact_.size(); ++s) {
+    const int32_t kb = int32_t(s) - lag_;
+    if (kb >= 0 && kb < kme) dp_->comm_wait(reduced_ev_[size_t(kb)]);
+    ops.clear();
+    for (const OpT& t : exact_[s]) ops.push_back({t.send, t.peer, base[t.base] + t.off, t.bytes});
+    if (!ops.empty()) p2p_->group(comm, ops);
+    if (int32_t(s) < kme) {
+      // chunk s of my block landed from every peer: reduce it (compute stream)
+      dp_->compute_wait(dp_->record_comm());
+      const int32_t k = int32_t(s);
+      for (int32_t src = 0; src < N; ++src)  // ascending source id, like the message flow
+        srcs[size_t(src)] = src == me ? static_cast<const void*>(base[0] + g.chunk_offset(me, k) * int64_t(es))
+                                      : dp_->scatter_slot(r, src, k);
+      auto specs = split_reduce(base[2] + g.chunk_offset(me, k) * int64_t(es), srcs, g.chunk_len(me, k));
+      dev->reduce(cs, specs.data(), int32_t(specs.size()), dp_->dtype());
+      reduced_ev_[size_t(k)] = dp_->record_compute();
+    }
+  }
+  // A capture must end with every forked stream joined back (the last
+  // broadcast step already waited for the last reduce; this covers kme == 0).
+  if (captured && kme > 0) dp_->comm_wait(dp_->record_compute());
 }
 
 void StreamLink::mark_scheduled(int32_t r) {

@@ -26,6 +26,8 @@
 #include <deque>
 #include <map>
 #include <set>
+#include <string>
+#include <tuple>
 
 #include "../engine/engine.h"
 #include "p2p.h"
@@ -34,7 +36,7 @@ namespace akka {
 
 struct StreamLinkStats {
   int64_t groups = 0, ops = 0, bytes_sent = 0, rounds = 0, unreduced_chunks = 0;
-  int64_t bulk_rounds = 0, collective_rounds = 0;
+  int64_t bulk_rounds = 0, collective_rounds = 0, exact_step_rounds = 0, graph_captures = 0, graph_replays = 0;
 };
 
 // Which schedule runs an exact-threshold round (thReduce = thComplete = 1):
@@ -45,12 +47,19 @@ struct StreamLinkStats {
 //             one N-way reduce);
 //  Auto       Collective when the transport has native collectives and the
 //             geometry is even, else P2P.
-// Threshold rounds (< 1) always take the step schedule.
+// Exact rounds never go through the engine's per-chunk message flow: their
+// outcome is fixed (every chunk = sum of all N, count N), so the link runs
+// them from a per-geometry op template with no engine callbacks, no op maps
+// and no counts exchange (exact_steps).  Threshold rounds (< 1) take the
+// message-driven step schedule (schedule()).  Which path a round takes is a
+// function of the round's parameters only, identical on every rank (the
+// schedules must match pairwise).
 enum class Lane : int32_t { Auto = 0, P2P = 1, Collective = 2 };
 
 class StreamLink final : public Link {
  public:
   StreamLink(Engine* engine, P2P* p2p, int32_t lag);
+  ~StreamLink() override;
   void bind(DataPlane* dp) { dp_ = dp; }
 
   void send_scatter(int32_t dest, int32_t chunk, int32_t round, const Payload& p) override;
@@ -59,8 +68,13 @@ class StreamLink final : public Link {
   void pump() override;
   bool may_finalize(int32_t round) override;
   bool bulk_round(int32_t round) override;
+  bool takes_exact_rounds() const override { return dp_ && dp_->geometry().N > 1; }
 
   void set_lane(Lane l) { lane_ = l; }
+  // Replay exact p2p-lane rounds from captured HIP graphs (off by default).
+  void set_graphs(bool on);
+  bool graphs() const { return graphs_; }
+  const std::string& graph_error() const { return graph_error_; }
   Lane lane() const { return lane_; }
   const StreamLinkStats& stats() const { return stats_; }
   int32_t lag() const { return lag_; }
@@ -70,6 +84,36 @@ class StreamLink final : public Link {
     const void* ptr = nullptr;
     int64_t len = 0;
   };
+  // One op of the exact step template: base 0 = round input, 1 = ring row
+  // of the round, 2 = round output; `off` in bytes from that base.
+  struct OpT {
+    bool send;
+    int32_t peer;
+    int8_t base;
+    int64_t off;
+    size_t bytes;
+  };
+  void build_exact_template();
+  void exact_steps(int32_t round);
+  void exact_body(int32_t round, char* const base[3], bool captured);
+  // HIP-graph cache of exact rounds, keyed by their three base pointers
+  // (input, ring row, output): a round seen twice is captured, later rounds
+  // with the same buffers replay the graph (one launch instead of one RCCL
+  // group + two event hops + one reduce launch per step).
+  struct GraphEntry {
+    GraphH exec = nullptr;
+    int32_t seen = 0;
+    uint64_t last_use = 0;
+  };
+  std::map<std::tuple<char*, char*, char*>, GraphEntry> graphs_map_;
+  bool graphs_ = false;
+  uint64_t tick_ = 0;
+  int64_t exact_groups_ = 0, exact_ops_ = 0, exact_bytes_ = 0;
+  std::string graph_error_;
+  void collective_round(int32_t round, bool native);
+  std::vector<std::vector<OpT>> exact_;  // [step] -> ops
+  std::vector<P2POp> scratch_;
+  std::vector<EventH> reduced_ev_;
   struct RoundQ {
     std::map<std::pair<int32_t, int32_t>, Out> scatter;  // (chunk, dest)
     std::map<std::pair<int32_t, int32_t>, Out> bcast;    // (chunk, dest)

@@ -85,3 +85,36 @@ def test_rccl_collective_lane_calls(ep, dtype):
     torch.cuda.synchronize()
     assert torch.equal(out, x)
     ep.check()
+
+
+@pytest.mark.parametrize("graphs", [False, True])
+def test_shape_rehearsal_exact_schedule_and_graph_replay(graphs):
+    """The N=8 exact step schedule through real RCCL on one GPU
+    (RcclShapeP2P: rank 0 of 8 posing, every op to itself).  With a constant
+    input every slot and every broadcast carries that constant whatever the
+    pairing, so the output must be 8*c with count 8 -- round after round,
+    also when the rounds replay a captured HIP graph with new input values."""
+    from akka_allreduce_amd import AllreduceWorker, InitWorkers
+    from akka_allreduce_amd.parallel.collective import _RemoteRank
+
+    dev = torch.device("cuda", 0)
+    n, C = 8, 1024
+    S = n * 4 * C + n * 8  # even split, short last chunk in every block
+    w = AllreduceWorker(None, None, device=dev, transport="stream", transport_spec=("rccl_shape", 0, n),
+                        strict=True, name="shape")
+    w.tell(InitWorkers({i: (w if i == 0 else _RemoteRank(i)) for i in range(n)}, n, None, 0, 1.0, 1.0, 2, S, C))
+    w.set_lane("p2p")
+    w.set_graphs(graphs)
+    x = torch.empty(S, device=dev)
+    out = torch.empty(S, device=dev)
+    for r in range(12):  # 3 ring rows: each key is captured at its 2nd round, replayed from its 3rd
+        x.fill_(float(r + 1))
+        o = w.allreduce(x, out=out)
+        torch.cuda.synchronize()
+        assert torch.equal(o.data, torch.full_like(x, 8.0 * (r + 1))), r
+        assert bool((o.count == n).all())
+    st = w.state()["link"]
+    assert st["exact_step_rounds"] == 12 and "graph_error" not in st, st
+    if graphs:
+        assert st["graph_captures"] == 3 and st["graph_replays"] == 6, st
+    w.close()

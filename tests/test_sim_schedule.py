@@ -58,13 +58,21 @@ def test_bf16():
 
 
 def test_traffic_volume_matches_direct_algorithm():
+    """Exact rounds move exactly the direct algorithm's payload (every count
+    is N by construction: no counts exchange); threshold rounds also carry
+    each owner's per-chunk counts (the ReduceBlock.count field)."""
     n, S, C = 8, 8192, 128
-    cl = SimCluster(n, S, C)
-    cl.allreduce(_inputs(n, S, 0))
     g = Geometry(S, n, C)
     payload = 2 * (n - 1) * S * 4  # each rank: (N-1)/N*S out in phase 1 and phase 2
     counts = sum((n - 1) * g.num_chunks(j) * 4 for j in range(n))  # each owner -> N-1 peers
+    cl = SimCluster(n, S, C)
+    cl.allreduce(_inputs(n, S, 0))
+    assert cl.bytes_moved() == payload
+    assert cl.workers[0].state()["link"]["exact_step_rounds"] == 1
+    cl = SimCluster(n, S, C, th_reduce=0.99)
+    cl.allreduce(_inputs(n, S, 0))
     assert cl.bytes_moved() == payload + counts
+    assert cl.workers[0].state()["link"]["exact_step_rounds"] == 0
 
 
 def test_many_rounds_ring_reuse():
@@ -162,6 +170,7 @@ def test_collective_lane_only_for_exact_rounds():
     cl = SimCluster(n, S, C, th_reduce=0.75, lane="collective")
     cl.allreduce(_inputs(n, S, 0))
     assert all(w.state()["link"]["bulk_rounds"] == 0 for w in cl.workers)
+    assert all(w.state()["link"]["exact_step_rounds"] == 0 for w in cl.workers)
 
 
 def test_auto_lane_without_native_collectives_keeps_chunk_schedule():
@@ -169,7 +178,8 @@ def test_auto_lane_without_native_collectives_keeps_chunk_schedule():
     cl = SimCluster(n, S, C)
     cl.allreduce(_inputs(n, S, 0))
     st = cl.workers[0].state()
-    assert st["link"]["bulk_rounds"] == 0 and st["link"]["lane"] == "auto"
+    assert st["link"]["collective_rounds"] == 0 and st["link"]["lane"] == "auto"
+    assert st["link"]["exact_step_rounds"] == 1
     assert st["link"]["groups"] == Geometry(S, n, C).kmax + 2
 
 
@@ -183,4 +193,5 @@ def test_lane_switch_between_rounds():
         outs = cl.allreduce(xs)
         want = torch.stack(xs).sum(0)
         assert all(torch.equal(o.data, want) and bool((o.count == n).all()) for o in outs), (r, lane)
-    assert cl.workers[0].state()["link"]["bulk_rounds"] == 3
+    st = cl.workers[0].state()["link"]
+    assert st["bulk_rounds"] == 5 and st["exact_step_rounds"] == 2
