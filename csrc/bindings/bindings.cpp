@@ -315,6 +315,8 @@ class WorkerCore final : public EngineHost {
       ls["unreduced_chunks"] = rs.unreduced_chunks;
       ls["polls"] = rs.polls;
       ls["reclaim_waits"] = rs.reclaim_waits;
+      ls["peers_lost"] = rs.peers_lost;
+      ls["transfers_dropped"] = rs.transfers_dropped;
       ls["slots"] = dp_->slots_allocated();
       ls["slots_busy"] = dp_->slots_busy();
       ls["in_flight"] = reactive_link_->in_flight();

@@ -18,6 +18,7 @@
 #include <deque>
 #include <memory>
 #include <mutex>
+#include <set>
 #include <vector>
 
 #include "../transport/p2p.h"
@@ -245,6 +246,7 @@ struct PairHub {
   std::vector<uint32_t> seq;            // [a*n+b]: groups a posted towards b
   void* block = nullptr;
   std::vector<hipEvent_t> events, free_events;
+  std::set<std::pair<int32_t, int32_t>> dead;  // (me, peer) aborted by me
   int64_t bytes = 0;
 };
 
@@ -258,6 +260,20 @@ class LoopbackPairP2P final : public P2P {
   int32_t rank() const override { return rank_; }
   int32_t nranks() const override { return hub_->n; }
   const char* name() const override { return "loopback-pair"; }
+  bool abort_peer(int32_t peer) override {
+    // Release both directions of the pair for good: a stream parked on the
+    // dead peer moves on (its copies never happen), and the unmatched posts
+    // are dropped.
+    PairHub& h = *hub_;
+    std::lock_guard<std::mutex> lk(h.mu);
+    const size_t key = size_t(std::min(rank_, peer)) * h.n + size_t(std::max(rank_, peer));
+    for (auto& p : h.posts[key]) h.free_events.push_back(p.posted);
+    h.posts[key].clear();
+    __atomic_store_n(h.flags[size_t(rank_) * h.n + peer], 0x7fffffffu, __ATOMIC_SEQ_CST);
+    __atomic_store_n(h.flags[size_t(peer) * h.n + rank_], 0x7fffffffu, __ATOMIC_SEQ_CST);
+    h.dead.insert({rank_, peer});
+    return true;
+  }
   void group(StreamH stream, const std::vector<P2POp>& ops) override {
     if (ops.empty()) return;
     PairHub& h = *hub_;
@@ -265,6 +281,7 @@ class LoopbackPairP2P final : public P2P {
     for (const auto& op : ops) AKKA_CHECK(op.peer == peer, "pair group holds ops to more than one peer");
     hipStream_t s = static_cast<hipStream_t>(stream);
     std::lock_guard<std::mutex> lk(h.mu);
+    AKKA_CHECK(!h.dead.count({rank_, peer}), "pair loopback: group to an aborted peer");
     const size_t key = size_t(std::min(rank_, peer)) * h.n + size_t(std::max(rank_, peer));
     auto& q = h.posts[key];
     if (q.empty() || q.front().rank == rank_) {

@@ -155,6 +155,10 @@ void Engine::on_peer_terminated(int32_t id) {
   // reference's handler never fires because workers never watch peers (W:141-146).
   peers_.erase(std::remove_if(peers_.begin(), peers_.end(), [id](const PeerEntry& p) { return p.id == id; }),
                peers_.end());
+  if (link_ && id != id_) {
+    Scope s(this);  // the link may deliver / retire rounds: pump afterwards
+    link_->on_peer_lost(id);
+  }
 }
 
 void Engine::flush_deferred(int32_t r) {

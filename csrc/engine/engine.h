@@ -77,6 +77,9 @@ class Link {
   // True if bulk_round always takes exact rounds (its schedule for them
   // differs from the message flow's, so every rank must take it).
   virtual bool takes_exact_rounds() const { return false; }
+  // The control plane reported peer `id` dead (WorkerTerminated): end the
+  // transfers owed to / expected from it; it is no longer in the peer map.
+  virtual void on_peer_lost(int32_t /*id*/) {}
 };
 
 // Embedding layer callbacks (Python, CLI, bench).

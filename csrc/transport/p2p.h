@@ -54,6 +54,13 @@ class P2P {
   // stream_link.h): `count` elements per rank.  reduce_scatter: recv = sum
   // over ranks of send[rank*count ..]; all_gather: recv[r*count ..] = rank r's
   // send (in place when send == recv + rank*count).  Default: unsupported.
+  // A peer died (the control plane said so): end every transfer with it that
+  // is queued or in flight, so streams parked on it move on, and never match
+  // with it again.  RCCL pair communicators: ncclCommAbort of that pair's
+  // communicator.  Transports whose communicator spans all ranks cannot
+  // abort one peer (they are rebuilt over the survivors instead): false.
+  virtual bool abort_peer(int32_t /*peer*/) { return false; }
+
   virtual bool has_collectives() const { return false; }
   virtual void reduce_scatter(StreamH, const void*, void*, size_t, DType) {
     throw AkkaError(std::string("akka: ") + name() + " p2p has no reduce_scatter");

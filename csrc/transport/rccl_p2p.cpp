@@ -163,6 +163,7 @@ class RcclPairP2P final : public P2P {
     const int32_t peer = ops.front().peer;
     AKKA_CHECK(peer >= 0 && peer < n_ && peer != rank_, "pair group: bad peer");
     ncclComm_t c = pair_[size_t(peer)];
+    AKKA_CHECK(c, "pair group to peer " + std::to_string(peer) + " after its communicator was aborted");
     const int32_t prank = peer < rank_ ? 0 : 1;  // split key = global rank
     hipStream_t s = static_cast<hipStream_t>(stream);
     AKKA_NCCL(ncclGroupStart());
@@ -172,6 +173,18 @@ class RcclPairP2P final : public P2P {
       else AKKA_NCCL(ncclRecv(op.buf, op.bytes, ncclUint8, prank, c, s));
     }
     AKKA_NCCL(ncclGroupEnd());
+  }
+  bool abort_peer(int32_t peer) override {
+    if (peer < 0 || peer >= n_ || peer == rank_) return false;
+    ncclComm_t& c = pair_[size_t(peer)];
+    if (c) {
+      // Kernels parked on the dead peer exit; the pair stream moves on.  The
+      // communicator is gone: every later group to that peer is an error.
+      ncclCommAbort(c);
+      c = nullptr;
+    }
+    aborted_.push_back(peer);
+    return true;
   }
   P2PInfo info() const override {
     int n = -1, r = -1, d = -1;
@@ -183,7 +196,9 @@ class RcclPairP2P final : public P2P {
     return P2PInfo{name(), n, r, d, comms};
   }
   void check() override {
-    check_async(global_, "global");
+    // the global communicator spans the dead rank too: only the pairs matter
+    // once a peer was aborted
+    if (aborted_.empty()) check_async(global_, "global");
     for (ncclComm_t c : pair_) check_async(c, "pair");
   }
 
@@ -191,6 +206,7 @@ class RcclPairP2P final : public P2P {
   int32_t rank_, n_;
   ncclComm_t global_ = nullptr;
   std::vector<ncclComm_t> pair_;
+  std::vector<int32_t> aborted_;
 };
 
 // Shape rehearsal on ONE GPU: a 1-rank RCCL communicator that presents

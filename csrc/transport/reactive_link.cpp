@@ -11,13 +11,15 @@ ReactiveLink::ReactiveLink(Engine* engine, P2P* p2p, int32_t max_slots)
 
 ReactiveLink::~ReactiveLink() {
   if (!dev_) return;
+  // A lost peer's stream is left alone (never synchronized or destroyed):
+  // whatever it still holds can only wait for a rank that is gone.
   try {
-    for (StreamH s : streams_)
-      if (s) dev_->sync_stream(s);
+    for (size_t p = 0; p < streams_.size(); ++p)
+      if (streams_[p] && !lost_[p]) dev_->sync_stream(streams_[p]);
   } catch (...) {
   }
-  for (StreamH s : streams_)
-    if (s) dev_->destroy_stream(s);
+  for (size_t p = 0; p < streams_.size(); ++p)
+    if (streams_[p] && !lost_[p]) dev_->destroy_stream(streams_[p]);
   for (EventH e : events_) dev_->destroy_event(e);
   for (int32_t* p : pinned_) dev_->release_pinned(p);
   if (recv_dev_) dev_->release(recv_dev_);
@@ -36,6 +38,7 @@ void ReactiveLink::bind(DataPlane* dp) {
   AKKA_CHECK(N_ >= 2, "the reactive transport needs at least two workers");
   AKKA_CHECK(p2p_->nranks() == N_ && p2p_->rank() == me_, "p2p endpoint does not match the worker geometry");
   streams_.assign(size_t(N_), nullptr);
+  lost_.assign(size_t(N_), 0);
   for (int32_t p = 0; p < N_; ++p)
     if (p != me_) streams_[size_t(p)] = dev_->create_stream();
   recv_dev_ = static_cast<int32_t*>(dev_->alloc(size_t(L_) * N_ * kmax_ * sizeof(int32_t)));
@@ -138,8 +141,41 @@ void ReactiveLink::issue_ready() {
   issuing_ = false;
 }
 
+bool ReactiveLink::exchanges_with(int32_t p) const {
+  if (p == me_ || lost_[size_t(p)]) return false;
+  for (const auto& pe : engine_->peers())
+    if (pe.id == p) return true;
+  return false;
+}
+
+void ReactiveLink::on_peer_lost(int32_t id) {
+  if (id < 0 || id >= N_ || id == me_ || lost_[size_t(id)]) return;
+  lost_[size_t(id)] = 1;
+  ++stats_.peers_lost;
+  // End what is queued / in flight with the dead peer (RCCL: abort of the
+  // pair communicator), then forget it: its arrivals are never delivered, so
+  // its contributions count as missing (the thresholds decide), and nothing
+  // -- slot reclaim included -- ever waits for its transfers again.
+  p2p_->abort_peer(id);
+  for (auto it = pending_.begin(); it != pending_.end();) {
+    if (it->peer != id) {
+      ++it;
+      continue;
+    }
+    auto rs = rounds_.find(it->round);
+    if (rs != rounds_.end()) --rs->second.open;
+    // the event / pinned row may still be referenced by the dead stream: not recycled
+    ++stats_.transfers_dropped;
+    it = pending_.erase(it);
+  }
+  for (auto it = rounds_.begin(); it != rounds_.end() && it->first < next_round_;) {
+    const int32_t r = it->first;
+    ++it;
+    retire(r);
+  }
+}
+
 void ReactiveLink::issue_p1(int32_t r) {
-  AKKA_CHECK(int32_t(engine_->peers().size()) == N_, "reactive transport needs the full peer map (all N workers)");
   const Geometry& g = dp_->geometry();
   const size_t es = dp_->esize();
   const int64_t my_len = g.block_len(me_);
@@ -150,6 +186,7 @@ void ReactiveLink::issue_p1(int32_t r) {
   std::vector<P2POp> ops;
   for (int32_t i = 1; i < N_; ++i) {
     const int32_t p = (me_ + i) % N_;
+    if (!exchanges_with(p)) continue;
     StreamH ps = streams_[size_t(p)];
     dev_->wait(ps, rel);
     ops.clear();
@@ -199,6 +236,7 @@ void ReactiveLink::issue_p2(int32_t r) {
   std::vector<P2POp> ops;
   for (int32_t i = 1; i < N_; ++i) {
     const int32_t p = (me_ + i) % N_;
+    if (!exchanges_with(p)) continue;
     StreamH ps = streams_[size_t(p)];
     dev_->wait(ps, ready);
     const int32_t kp = g.num_chunks(p);

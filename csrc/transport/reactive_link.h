@@ -48,7 +48,7 @@ namespace akka {
 
 struct ReactiveLinkStats {
   int64_t groups = 0, bytes_sent = 0, p1_arrivals = 0, p2_arrivals = 0, unreduced_chunks = 0, polls = 0,
-          reclaim_waits = 0;
+          reclaim_waits = 0, peers_lost = 0, transfers_dropped = 0;
 };
 
 class ReactiveLink final : public Link {
@@ -63,6 +63,7 @@ class ReactiveLink final : public Link {
   void on_scattered(int32_t round) override;
   void pump() override;
   bool may_finalize(int32_t round) override;
+  void on_peer_lost(int32_t id) override;
 
   // Query in-flight transfers and deliver the completed ones to the engine.
   // Returns true if anything completed.
@@ -94,6 +95,11 @@ class ReactiveLink final : public Link {
   };
 
   RoundState& st(int32_t r);
+  // Peers this rank exchanges with in a round: in the engine's peer map at
+  // issue time and not lost.  (Both sides of a pair must agree, which holds
+  // when membership changes at a round boundary: InitWorkers / death.)
+  bool exchanges_with(int32_t p) const;
+  std::vector<uint8_t> lost_;  // [N]
   void issue_ready();
   void issue_p1(int32_t r);
   void issue_p2(int32_t r);

@@ -4,6 +4,7 @@
 #include <cstdlib>
 #include <deque>
 #include <map>
+#include <set>
 #include <sstream>
 
 #include "p2p.h"
@@ -25,6 +26,8 @@ class SimHub {
   int32_t n_;
   // fifo[src][dst]: sends posted by src to dst not yet consumed, in order.
   std::map<std::pair<int32_t, int32_t>, std::deque<std::shared_ptr<SimSend>>> fifo;
+  // (me, peer): `me` aborted its transfers with `peer` (abort_peer).
+  std::set<std::pair<int32_t, int32_t>> aborted;
   int64_t bytes = 0;
   int64_t groups = 0;
   int64_t events = 0;  // posts + matches: progress that completes no queue op yet
@@ -42,6 +45,13 @@ class SimP2P final : public P2P {
   int32_t rank() const override { return rank_; }
   int32_t nranks() const override { return hub_->n_; }
   const char* name() const override { return "sim"; }
+  bool abort_peer(int32_t peer) override {
+    // like ncclCommAbort of the pair communicator: queued and future ops
+    // with `peer` complete at once without moving data
+    hub_->aborted.insert({rank_, peer});
+    hub_->events++;
+    return true;
+  }
 
   void group(StreamH s, const std::vector<P2POp>& ops) override {
     for (const auto& op : ops) {
@@ -78,6 +88,10 @@ class SimP2P final : public P2P {
       for (size_t i = 0; i < ops.size(); ++i) {
         const auto& op = ops[i];
         if (op.send || st->recv_done[i]) continue;
+        if (hub->aborted.count({me, op.peer})) {
+          st->recv_done[i] = true;
+          continue;
+        }
         // Earlier recvs from the same peer in this group must match first.
         bool blocked = false;
         for (size_t j = 0; j < i; ++j)
@@ -105,8 +119,12 @@ class SimP2P final : public P2P {
         st->recv_done[i] = true;
         hub->events++;
       }
-      for (const auto& snd : st->sends)
-        if (!snd->consumed) all = false;
+      size_t si = 0;
+      for (const auto& op : ops) {
+        if (!op.send) continue;
+        const auto& snd = st->sends[si++];
+        if (!snd->consumed && !hub->aborted.count({me, op.peer})) all = false;
+      }
       return all;
     });
   }

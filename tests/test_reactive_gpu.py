@@ -101,3 +101,57 @@ def _sleeping(cl, n, S, C, R):
         _check_masks(outs[3][k], S, n)
     cl.drain()
     assert all(w.state()["link"]["slots_busy"] == 0 for w in cl.workers)
+
+
+def test_reactive_loopback_dead_peer(monkeypatch):
+    """Rank 3 is gone for good (never posts).  The survivors are told after
+    two rounds (WorkerTerminated): their pair transfers with it are aborted
+    (pair loopback: both directions released, queued posts dropped) and they
+    run far more rounds than the 4-slot send pool holds, summing only each
+    other's data; rank 3's block arrives as zeros with count 0."""
+    import threading
+
+    from akka_allreduce_amd.messages import WorkerTerminated
+
+    monkeypatch.setenv("AKKA_REACTIVE_SLOTS", "4")
+    n, S, C, R = 4, 1 << 14, 1 << 10, 12
+    cl = ReactiveLoopbackCluster(n, S, C, th_reduce=0.75, th_complete=0.75, max_lag=1)
+    alive = [0, 1, 2]
+    outs = {r: [] for r in alive}
+    errs = []
+
+    def run(r):
+        try:
+            w = cl.workers[r]
+            w.reactive_timeout = 30.0
+            for k in range(R):
+                if k == 2:
+                    w.receive(WorkerTerminated(3))
+                outs[r].append(w.allreduce(_w(S) * float(1 << r)))
+            torch.cuda.current_stream().synchronize()
+        except BaseException as e:  # pragma: no cover - surfaced below
+            errs.append(e)
+
+    ts = [threading.Thread(target=run, args=(r,)) for r in alive]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    try:
+        assert not errs, errs
+        g = Geometry(S, n, C)
+        s3, e3 = g.block_range(3)
+        for r in alive:
+            assert len(outs[r]) == R
+            for k in range(R):
+                o = outs[r][k]
+                _check_masks(o, S, n, allowed=set(alive))
+                assert int(o.count[s3:e3].abs().sum()) == 0
+            st = cl.workers[r].state()["link"]
+            assert st["peers_lost"] == 1
+        for r in alive:
+            cl.workers[r].synchronize()
+    finally:
+        cl.hub.release_all()
+        for w in cl.workers:
+            w.close()

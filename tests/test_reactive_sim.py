@@ -298,3 +298,79 @@ def test_fuzz_small_pool_freezes_and_thresholds(seed, monkeypatch):
                 assert bool((mask == (1 << n) - 1).all())
     cl.drain()
     assert all(w.state()["link"]["in_flight"] == 0 for w in cl.workers)
+
+
+def _dead_rank_run(n, dead, S, C, rounds, warm, slots, monkeypatch, th=0.75):
+    monkeypatch.setenv("AKKA_REACTIVE_SLOTS", str(slots))
+    from akka_allreduce_amd.messages import WorkerTerminated
+
+    cl = ReactiveSimCluster(n, S, C, th_reduce=th, th_complete=th, max_lag=1)
+    alive = [i for i in range(n) if i != dead]
+    for r in range(warm):  # everyone together first
+        for i in range(n):
+            cl.start(i, _x(i, S))
+        cl.run(lambda: all(cl.done(i, r) for i in range(n)))
+    # `dead` stops for good; the survivors keep starting rounds until the
+    # send-slot pool would stall them, then the control plane reports the death
+    told = False
+    for r in range(warm, warm + rounds):
+        for i in alive:
+            cl.start(i, _x(i, S))
+        try:
+            cl.run(lambda: all(cl.done(i, r) for i in alive), active=alive, max_idle=30)
+        except RuntimeError:
+            assert not told, f"survivors stalled at round {r} after the death was reported"
+            for i in alive:
+                cl.workers[i].receive(WorkerTerminated(dead))
+            told = True
+            cl.run(lambda: all(cl.done(i, r) for i in alive), active=alive)
+    cl.settle(alive)
+    return cl, alive, told
+
+
+@pytest.mark.parametrize("warm", [0, 3])
+def test_dead_peer_survivors_keep_going(warm, monkeypatch):
+    """A rank that dies for good (never steps again): once the survivors are
+    told (WorkerTerminated, the reference's Terminated handler W:141-146 made
+    reachable), their transfers with it are aborted and forgotten, so they
+    complete far more rounds than the send-slot pool holds (the pool would
+    otherwise park them on the dead rank forever).  Its contributions are
+    missing: no output element ever contains it afterwards, and the block it
+    owned arrives as zeros with count 0."""
+    n, dead, S, C, slots = 4, 3, 64, 8, 4
+    rounds = 2 * slots + 4
+    cl, alive, told = _dead_rank_run(n, dead, S, C, rounds, warm, slots, monkeypatch)
+    assert told  # without the report the pool would have stalled them
+    g = Geometry(S, n, C)
+    s3, e3 = g.block_range(dead)
+    for i in alive:
+        for r in range(warm + 2, warm + rounds):  # rounds after the death settled
+            o = cl.outputs[i][r]
+            _check_masks(o, S, n, allowed=set(alive))
+            assert int(o.count[s3:e3].abs().sum()) == 0  # its block: zeros, count 0
+            assert bool((o.count[:s3] <= n - 1).all())
+        st = cl.workers[i].state()["link"]
+        assert st["peers_lost"] == 1
+    cl.drain(alive)
+    assert all(cl.workers[i].state()["link"]["in_flight"] == 0 for i in alive)
+
+
+def test_dead_peer_reported_up_front_never_exchanged(monkeypatch):
+    """Told before the first round: nothing is ever posted to the dead rank."""
+    from akka_allreduce_amd.messages import WorkerTerminated
+
+    monkeypatch.setenv("AKKA_REACTIVE_SLOTS", "3")
+    n, S, C = 4, 40, 5
+    cl = ReactiveSimCluster(n, S, C, th_reduce=0.75, th_complete=0.75, max_lag=1)
+    alive = [0, 1, 2]
+    for i in alive:
+        cl.workers[i].receive(WorkerTerminated(3))
+    for r in range(10):
+        for i in alive:
+            cl.start(i, _x(i, S))
+        cl.run(lambda: all(cl.done(i, r) for i in alive), active=alive)
+    cl.settle(alive)
+    for i in alive:
+        for r in range(10):
+            _check_masks(cl.outputs[i][r], S, n, allowed=set(alive))
+    assert cl.workers[0].state()["link"]["transfers_dropped"] == 0
