@@ -16,7 +16,10 @@ Reference gaps fixed:
     ``thAllreduce = 1`` no longer stalls forever after a death;
   * ids are the smallest free id in ``[0, totalWorkers)`` (the reference's
     ``workers.size`` collides after a removal);
-  * surviving workers are told about the death (``WorkerTerminated``), and a
+  * surviving workers are told about the death (``WorkerTerminated``); on a
+    device (RCCL) data plane they also get a re-``InitWorkers`` carrying a new
+    unique id and the survivor list, from which they build a new communicator
+    (a membership epoch); and a
     worker joining after the start takes a free id, gets ``InitWorkers`` and the
     current ``StartAllreduce`` (it catches up through the worker's catch-up
     path); the survivors get a re-``InitWorkers`` with the new peer map.
@@ -134,6 +137,11 @@ class AllreduceMaster:
         log.warning("master: worker %d terminated, %d alive", worker_id, len(self.workers))
         for ref in list(self.workers.values()):
             ref.tell(WorkerTerminated(worker_id))
+        if self.round >= 0 and self.transport_info is not None and self.workers:
+            # device data plane: the survivors build a new communicator over
+            # themselves (new unique id, members = survivors) -- a worker
+            # cannot leave an RCCL communicator it shares with a dead rank
+            self._init_workers(list(self.workers))
         if self.round >= 0:
             self._maybe_advance()
 
@@ -146,6 +154,9 @@ class AllreduceMaster:
     # ---- rounds --------------------------------------------------------------------
     def _init_workers(self, ids: List[int]) -> None:
         extra = self.transport_info() if self.transport_info else None
+        if extra is not None:
+            extra = dict(extra)
+            extra.setdefault("members", sorted(self.workers))
         for idx in ids:
             msg = InitWorkers(dict(self.workers), self.totalWorkers, self, idx, self.thReduce, self.thComplete,
                               self.maxLag, self.dataSize, self.maxChunkSize)

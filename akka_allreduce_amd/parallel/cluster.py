@@ -122,11 +122,15 @@ class MasterProcess:
         want_rccl = self.transport == "rccl" or (self.transport == "auto" and all_gpu)
         if not want_rccl:
             return None
-        if not hasattr(self, "_uid"):
+        # one unique id per membership: a death or a join starts a new epoch
+        # (every member builds a fresh communicator over the new member list)
+        members = tuple(sorted(self.master.workers))
+        if getattr(self, "_uid_members", None) != members:
             from .._native_loader import load
 
             self._uid = load().rccl_unique_id()
-        return {"kind": "rccl", "uid": self._uid}
+            self._uid_members = members
+        return {"kind": "rccl", "uid": self._uid, "members": list(members)}
 
     def receive(self, msg: Any) -> None:
         if isinstance(msg, RegisterWorker):

@@ -118,6 +118,7 @@ class AllreduceWorker:
         self._fast_source = dataSource is None  # rounds fed by allreduce(): eligible for the native fast path
         self._fast_pending: Dict[int, Tuple[torch.Tensor, torch.Tensor]] = {}
         self.fast_rounds = 0  # rounds that took the native fast path
+        self.epochs = 0  # RCCL membership epochs after the first (re-InitWorkers with a new unique id)
         self.reactive_timeout: Optional[float] = None  # reactive allreduce(): max seconds to wait
 
     @staticmethod
@@ -190,14 +191,24 @@ class AllreduceWorker:
         # a reference to this worker itself (or a local wrapper of it) short-circuits (W:228)
         peers = [(int(i), ref is self or getattr(ref, "actor", None) is self) for i, ref in m.workers.items()]
         tinfo = getattr(m, "transport", None)
-        if tinfo and tinfo.get("kind") == "rccl" and self.transport in ("stream", "reactive") \
-                and self.transport_spec is None:
-            self.transport_spec = ("rccl", tinfo["uid"], int(m.destId), int(m.workerNum))
+        rccl = bool(tinfo and tinfo.get("kind") == "rccl" and self.transport in ("stream", "reactive"))
+        if rccl and self.transport_spec is None:
+            self.transport_spec = ("rccl", tinfo["uid"], int(m.destId), int(m.workerNum),
+                                   list(tinfo.get("members") or []))
         first = self._core.init(int(m.destId), int(m.workerNum), float(m.thReduce), float(m.thComplete),
                                 int(m.maxLag), int(m.dataSize), int(m.maxChunkSize), peers)
         self.peers = dict(m.workers)
         if not first:
-            return  # re-init only replaces the peer map (W:87-89)
+            # re-init only replaces the peer map (W:87-89) -- and, on the RCCL
+            # data plane, starts a new membership epoch: a communicator over
+            # the listed members from the new unique id (after a death / join)
+            if rccl and self.transport_spec and self.transport_spec[0] == "rccl" \
+                    and bytes(tinfo["uid"]) != bytes(self.transport_spec[1]):
+                members = sorted(int(i) for i in (tinfo.get("members") or m.workers))
+                self._core.rebuild_transport(tinfo["uid"], members)
+                self.transport_spec = ("rccl", tinfo["uid"], self.id, int(m.workerNum), members)
+                self.epochs += 1
+            return
         self.id = int(m.destId)
         self.master = m.master
         self.geometry = Geometry(int(m.dataSize), int(m.workerNum), int(m.maxChunkSize))
@@ -219,8 +230,9 @@ class AllreduceWorker:
             raise RuntimeError("stream transport needs transport_spec=('rccl', uid, rank, nranks) or ('sim', hub, rank)")
         kind = spec[0]
         if kind == "rccl":
-            _, uid, rank, nranks = spec
-            self._core.connect_rccl(uid, int(rank), int(nranks))
+            _, uid, rank, nranks = spec[:4]
+            members = [int(i) for i in spec[4]] if len(spec) > 4 and spec[4] else []
+            self._core.connect_rccl(uid, int(rank), int(nranks), members)
         elif kind == "rccl_shape":
             _, rank, nranks = spec
             self._core.connect_rccl_shape(int(rank), int(nranks))

@@ -120,17 +120,27 @@ class WorkerCore final : public EngineHost {
     return true;
   }
   // Must be called after init for link == "stream", before attach.
-  void connect_rccl(py::bytes uid, int32_t rank, int32_t nranks) {
+  void connect_rccl(py::bytes uid, int32_t rank, int32_t nranks, std::vector<int32_t> members) {
     std::string s = uid;
     std::vector<uint8_t> v(s.begin(), s.end());
     AKKA_CHECK(dev_ && !dev_->is_host(), "RCCL transport needs a HIP device");
     if (link_kind_ == "reactive") {
+      AKKA_CHECK(members.empty() || int32_t(members.size()) == nranks,
+                 "the reactive transport's pair communicators are built over all workers");
       p2p_ = make_rccl_pair_p2p(v, rank, nranks, device_idx_);
       make_reactive_link();
       return;
     }
-    p2p_ = make_rccl_p2p(v, rank, nranks, device_idx_);
+    p2p_ = make_rccl_p2p(v, rank, nranks, device_idx_, members);
     make_stream_link();
+  }
+  // Membership epoch from a re-InitWorkers (new unique id + member list).
+  bool rebuild_transport(py::bytes uid, std::vector<int32_t> members) {
+    AKKA_CHECK(p2p_, "rebuild_transport before the transport was connected");
+    std::string s = uid;
+    std::vector<uint8_t> v(s.begin(), s.end());
+    py::gil_scoped_release nogil;  // ncclCommInitRank waits for every member
+    return p2p_->rebuild(v, members);
   }
   // Host-cost rehearsal of the N-rank schedule on one GPU (rccl_p2p.cpp
   // RcclShapeP2P): the bytes are meaningless, the host path is the real one.
@@ -499,7 +509,9 @@ PYBIND11_MODULE(_native, m) {
            py::arg("link") = "outbox", py::arg("device") = -1, py::arg("dtype") = "float32",
            py::arg("deferred") = false, py::arg("lag") = 2)
       .def("init", &WorkerCore::init)
-      .def("connect_rccl", &WorkerCore::connect_rccl)
+      .def("connect_rccl", &WorkerCore::connect_rccl, py::arg("uid"), py::arg("rank"), py::arg("nranks"),
+           py::arg("members") = std::vector<int32_t>{})
+      .def("rebuild_transport", &WorkerCore::rebuild_transport)
       .def("connect_sim", &WorkerCore::connect_sim)
       .def("connect_rccl_shape", &WorkerCore::connect_rccl_shape)
       .def("connect_local", &WorkerCore::connect_local)
@@ -636,6 +648,10 @@ PYBIND11_MODULE(_native, m) {
       })
       .def("check", &P2P::check)
       .def("has_collectives", &P2P::has_collectives)
+      .def("rebuild", [](P2P& p, py::bytes uid, std::vector<int32_t> members) {
+        std::string s = uid;
+        return p.rebuild(std::vector<uint8_t>(s.begin(), s.end()), members);
+      })
       .def("reduce_scatter", [](P2P& p, uintptr_t stream, uintptr_t send, uintptr_t recv, size_t count,
                                 const std::string& dtype) {
         p.reduce_scatter(reinterpret_cast<StreamH>(stream), reinterpret_cast<const void*>(send),
@@ -653,11 +669,13 @@ PYBIND11_MODULE(_native, m) {
           v.push_back({std::get<0>(o), std::get<1>(o), reinterpret_cast<void*>(std::get<2>(o)), std::get<3>(o)});
         p.group(reinterpret_cast<StreamH>(stream), v);
       });
-  m.def("rccl_endpoint", [](py::bytes uid, int32_t rank, int32_t nranks, int32_t device, bool pairs) {
+  m.def("rccl_endpoint", [](py::bytes uid, int32_t rank, int32_t nranks, int32_t device, bool pairs,
+                            std::vector<int32_t> members) {
     std::string s = uid;
     std::vector<uint8_t> v(s.begin(), s.end());
-    return pairs ? make_rccl_pair_p2p(v, rank, nranks, device) : make_rccl_p2p(v, rank, nranks, device);
-  }, py::arg("uid"), py::arg("rank"), py::arg("nranks"), py::arg("device"), py::arg("pairs") = false);
+    return pairs ? make_rccl_pair_p2p(v, rank, nranks, device) : make_rccl_p2p(v, rank, nranks, device, members);
+  }, py::arg("uid"), py::arg("rank"), py::arg("nranks"), py::arg("device"), py::arg("pairs") = false,
+     py::arg("members") = std::vector<int32_t>{});
 
   // ---- kernels (tests / microbench) ----------------------------------------------
   m.def("reduce", [](uintptr_t dst, std::vector<uintptr_t> srcs, int64_t n, std::string dtype, uintptr_t stream,

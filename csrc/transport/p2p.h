@@ -60,6 +60,13 @@ class P2P {
   // communicator.  Transports whose communicator spans all ranks cannot
   // abort one peer (they are rebuilt over the survivors instead): false.
   virtual bool abort_peer(int32_t /*peer*/) { return false; }
+  // New membership epoch (the control plane's re-InitWorkers after a death or
+  // a join): drop the old communicator and build one over `members` (engine
+  // ids, ascending; comm rank = index) from a fresh unique id.  Transports
+  // keyed by engine ids directly need nothing: false.
+  virtual bool rebuild(const std::vector<uint8_t>& /*uid*/, const std::vector<int32_t>& /*members*/) {
+    return false;
+  }
 
   virtual bool has_collectives() const { return false; }
   virtual void reduce_scatter(StreamH, const void*, void*, size_t, DType) {
@@ -85,7 +92,10 @@ bool sim_step(const std::shared_ptr<SimHub>& hub, const std::vector<Device*>& de
 
 // ---- RCCL ---------------------------------------------------------------------
 std::vector<uint8_t> rccl_unique_id();
-std::unique_ptr<P2P> make_rccl_p2p(const std::vector<uint8_t>& uid, int32_t rank, int32_t nranks, int32_t device);
+// `members`: engine ids in the communicator (empty = all nranks); the
+// communicator rank of engine id m is its index in `members`.
+std::unique_ptr<P2P> make_rccl_p2p(const std::vector<uint8_t>& uid, int32_t rank, int32_t nranks, int32_t device,
+                                   const std::vector<int32_t>& members = {});
 // Round-robin tournament (circle method) used to split the global communicator
 // into pair communicators: in round t (0 <= t < P-1, P = N rounded up to even)
 // rank x is paired with tournament_partner(N, t, x); a partner >= N means x

@@ -69,15 +69,11 @@ void check_async(ncclComm_t c, const char* what) {
 
 class RcclP2P final : public P2P {
  public:
-  RcclP2P(const std::vector<uint8_t>& uid, int32_t rank, int32_t nranks, int32_t device)
-      : rank_(rank), n_(nranks) {
-    AKKA_CHECK(uid.size() == sizeof(ncclUniqueId), "bad RCCL unique id size");
-    ncclUniqueId id;
-    std::memcpy(&id, uid.data(), sizeof(id));
+  RcclP2P(const std::vector<uint8_t>& uid, int32_t rank, int32_t nranks, int32_t device,
+          const std::vector<int32_t>& members)
+      : rank_(rank), n_(nranks), device_(device) {
     if (hipSetDevice(device) != hipSuccess) throw AkkaError("akka: hipSetDevice failed");
-    AKKA_NCCL(ncclCommInitRank(&comm_, nranks, id, rank));
-    verify_comm(comm_, nranks, rank, device, "global");
-    device_ = device;
+    connect(uid, members);
   }
   ~RcclP2P() override {
     if (comm_) ncclCommDestroy(comm_);
@@ -90,8 +86,9 @@ class RcclP2P final : public P2P {
     hipStream_t s = static_cast<hipStream_t>(stream);
     AKKA_NCCL(ncclGroupStart());
     for (const auto& op : ops) {
-      if (op.send) AKKA_NCCL(ncclSend(op.buf, op.bytes, ncclUint8, op.peer, comm_, s));
-      else AKKA_NCCL(ncclRecv(op.buf, op.bytes, ncclUint8, op.peer, comm_, s));
+      const int32_t cr = comm_rank(op.peer);
+      if (op.send) AKKA_NCCL(ncclSend(op.buf, op.bytes, ncclUint8, cr, comm_, s));
+      else AKKA_NCCL(ncclRecv(op.buf, op.bytes, ncclUint8, cr, comm_, s));
     }
     AKKA_NCCL(ncclGroupEnd());
   }
@@ -104,19 +101,59 @@ class RcclP2P final : public P2P {
   }
   void check() override { check_async(comm_, "global"); }
 
-  bool has_collectives() const override { return true; }
+  bool rebuild(const std::vector<uint8_t>& uid, const std::vector<int32_t>& members) override {
+    if (comm_) {
+      // A member may be dead with kernels of ours still parked on it: abort
+      // (destroy would wait for them).  Rounds in flight at that moment are lost.
+      ncclCommAbort(comm_);
+      comm_ = nullptr;
+    }
+    connect(uid, members);
+    return true;
+  }
+
+  bool has_collectives() const override { return int32_t(members_.size()) == n_; }
   void reduce_scatter(StreamH stream, const void* send, void* recv, size_t count, DType dt) override {
+    AKKA_CHECK(has_collectives(), "reduce_scatter needs every rank in the communicator");
     AKKA_NCCL(ncclReduceScatter(send, recv, count, nccl_type(dt), ncclSum, comm_, static_cast<hipStream_t>(stream)));
   }
   void all_gather(StreamH stream, const void* send, void* recv, size_t count, DType dt) override {
+    AKKA_CHECK(has_collectives(), "all_gather needs every rank in the communicator");
     AKKA_NCCL(ncclAllGather(send, recv, count, nccl_type(dt), comm_, static_cast<hipStream_t>(stream)));
   }
 
  private:
+  void connect(const std::vector<uint8_t>& uid, const std::vector<int32_t>& members) {
+    AKKA_CHECK(uid.size() == sizeof(ncclUniqueId), "bad RCCL unique id size");
+    members_ = members;
+    if (members_.empty())
+      for (int32_t i = 0; i < n_; ++i) members_.push_back(i);
+    comm_rank_.assign(size_t(n_), -1);
+    int32_t mine = -1;
+    for (size_t i = 0; i < members_.size(); ++i) {
+      const int32_t m = members_[i];
+      AKKA_CHECK(m >= 0 && m < n_ && comm_rank_[size_t(m)] < 0, "bad communicator member list");
+      comm_rank_[size_t(m)] = int32_t(i);
+      if (m == rank_) mine = int32_t(i);
+    }
+    AKKA_CHECK(mine >= 0, "this rank is not a member of the communicator it should join");
+    ncclUniqueId id;
+    std::memcpy(&id, uid.data(), sizeof(id));
+    if (hipSetDevice(device_) != hipSuccess) throw AkkaError("akka: hipSetDevice failed");
+    AKKA_NCCL(ncclCommInitRank(&comm_, int(members_.size()), id, mine));
+    verify_comm(comm_, int32_t(members_.size()), mine, device_, "global");
+  }
+  int32_t comm_rank(int32_t peer) const {
+    AKKA_CHECK(peer >= 0 && peer < n_ && comm_rank_[size_t(peer)] >= 0,
+               "p2p op to worker " + std::to_string(peer) + ", which is not in the communicator");
+    return comm_rank_[size_t(peer)];
+  }
   static ncclDataType_t nccl_type(DType dt) { return dt == DType::BF16 ? ncclBfloat16 : ncclFloat32; }
   int32_t rank_, n_;
   int32_t device_ = -1;
   ncclComm_t comm_ = nullptr;
+  std::vector<int32_t> members_;
+  std::vector<int32_t> comm_rank_;  // [n] engine id -> communicator rank (-1: not a member)
 };
 
 // One two-rank communicator per peer pair, split off the global one.  A group
@@ -258,8 +295,9 @@ std::unique_ptr<P2P> make_rccl_pair_p2p(const std::vector<uint8_t>& uid, int32_t
   return std::make_unique<RcclPairP2P>(uid, rank, nranks, device);
 }
 
-std::unique_ptr<P2P> make_rccl_p2p(const std::vector<uint8_t>& uid, int32_t rank, int32_t nranks, int32_t device) {
-  return std::make_unique<RcclP2P>(uid, rank, nranks, device);
+std::unique_ptr<P2P> make_rccl_p2p(const std::vector<uint8_t>& uid, int32_t rank, int32_t nranks, int32_t device,
+                                   const std::vector<int32_t>& members) {
+  return std::make_unique<RcclP2P>(uid, rank, nranks, device, members);
 }
 
 }  // namespace akka

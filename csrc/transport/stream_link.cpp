@@ -77,8 +77,12 @@ void StreamLink::schedule(int32_t r) {
     return;
   }
   AKKA_CHECK(p2p_->nranks() == N && p2p_->rank() == me, "p2p communicator does not match the worker geometry");
-  auto peers = engine_->peers();
-  AKKA_CHECK(int32_t(peers.size()) == N, "scheduled transport needs the full peer map (all N workers)");
+  // Partial membership (W:213-216, SPEC:141-172): the step schedule runs over
+  // the peers in the current peer map.  Both sides of a pair must agree, which
+  // holds when the map changes at a round boundary (InitWorkers, death).
+  std::vector<uint8_t> present(size_t(N), 0);
+  for (const auto& pe : engine_->peers())
+    if (pe.id >= 0 && pe.id < N) present[size_t(pe.id)] = 1;
   const size_t es = dp_->esize();
   const int32_t kme = g.num_chunks(me);
   const int32_t kmax = dp_->kmax();
@@ -121,6 +125,7 @@ void StreamLink::schedule(int32_t r) {
     if (last) dp_->upload_counts(r, {me}, comm);
     for (int32_t i = 1; i < N; ++i) {
       const int32_t peer = (me + i) % N;
+      if (!present[size_t(peer)]) continue;
       const int32_t kp = g.num_chunks(peer);
       if (s < kp) {
         auto it = rq.scatter.find({s, peer});
@@ -155,6 +160,7 @@ void StreamLink::schedule(int32_t r) {
       dp_->compute_wait(landed);
       for (int32_t i = 1; i < N; ++i) {
         const int32_t peer = (me + i) % N;
+        if (!present[size_t(peer)]) continue;
         Payload p;
         p.kind = PayloadKind::Landed;
         p.len = g.chunk_len(me, s);
@@ -165,7 +171,7 @@ void StreamLink::schedule(int32_t r) {
     if (kb >= 0) {
       for (int32_t i = 1; i < N; ++i) {
         const int32_t peer = (me + i) % N;
-        if (kb >= g.num_chunks(peer)) continue;
+        if (!present[size_t(peer)] || kb >= g.num_chunks(peer)) continue;
         Payload p;
         p.kind = PayloadKind::Landed;
         p.len = g.chunk_len(peer, kb);

@@ -374,3 +374,43 @@ def test_dead_peer_reported_up_front_never_exchanged(monkeypatch):
         for r in range(10):
             _check_masks(cl.outputs[i][r], S, n, allowed=set(alive))
     assert cl.workers[0].state()["link"]["transfers_dropped"] == 0
+
+
+def test_partial_membership_islands_reactive():
+    """T4/T5 across real ranks on the reactive transport: two islands {0,1}
+    and {2,3} exchange only within themselves, then a re-InitWorkers with the
+    full map (at a round boundary) makes every pair exchange."""
+    import random as _random
+
+    from akka_allreduce_amd._native_loader import load
+    from akka_allreduce_amd.worker import AllreduceWorker
+
+    import tests.test_sim_schedule as ts
+
+    n, S, C = 4, 64, 4
+    cl = ReactiveSimCluster.__new__(ReactiveSimCluster)
+    cl._nat = load()
+    cl.n = n
+    cl.hub = cl._nat.SimHub(n)
+    cl.rng = _random.Random(0)
+    cl.workers = [AllreduceWorker(None, None, device="cpu", transport="reactive", transport_spec=("sim", cl.hub, r),
+                                  strict=True, name=f"risl{r}") for r in range(n)]
+    cl.outputs = [dict() for _ in range(n)]
+    rounds = [0]
+
+    def run_round(xs):
+        r = rounds[0]
+        for i in range(n):
+            cl.start(i, xs[i])
+        cl.run(lambda: all(cl.done(i, r) for i in range(n)))
+        cl.settle()
+        cl.drain()
+        rounds[0] += 1
+        return [cl.outputs[i][r] for i in range(n)]
+
+    ts._islands(cl, n, S, C, 0.5, run_round, chunk_order=False)
+    # round 0: phase 1 from the one island peer; round 1: from all three
+    # (whole-block P1/P2 per pair -- which blocks make the 50% is timing)
+    for w in cl.workers:
+        st = w.state()["link"]
+        assert st["p1_arrivals"] == 1 + 3 and st["p2_arrivals"] == 1 + 3, st

@@ -195,3 +195,67 @@ def test_lane_switch_between_rounds():
         assert all(torch.equal(o.data, want) and bool((o.count == n).all()) for o in outs), (r, lane)
     st = cl.workers[0].state()["link"]
     assert st["bulk_rounds"] == 5 and st["exact_step_rounds"] == 2
+
+
+def _islands(cl, n, S, C, th, run_round, chunk_order=True):
+    """T4/T5 across real ranks: start as two islands {0,1} and {2,3} (each
+    rank's InitWorkers lists only its island, SPEC:141-162), then a
+    re-InitWorkers with the full map at a round boundary (W:87-89,
+    SPEC:164-170).  Inputs 2^rank reveal who contributed to each element."""
+    from akka_allreduce_amd.messages import InitWorkers
+    from akka_allreduce_amd.parallel.collective import _RemoteRank
+
+    isl = {0: [0, 1], 1: [0, 1], 2: [2, 3], 3: [2, 3]}
+    for r, w in enumerate(cl.workers):
+        peers = {i: (w if i == r else _RemoteRank(i)) for i in isl[r]}
+        w.tell(InitWorkers(peers, n, None, r, th, th, 1, S, C))
+    xs = [torch.full((S,), float(1 << i)) for i in range(n)]
+    outs0 = run_round(xs)
+    g = Geometry(S, n, C)
+    for r, o in enumerate(outs0):
+        for j in range(n):
+            s, e = g.block_range(j)
+            if j in isl[r]:  # my island's blocks: reduced from the island only
+                want = float(sum(1 << i for i in isl[r]))
+                assert torch.equal(o.data[s:e], torch.full((e - s,), want)), (r, j)
+                assert bool((o.count[s:e] == 2).all())
+            else:  # the other island's blocks never reach me: zeros, count 0
+                assert int(o.count[s:e].abs().sum()) == 0 and int(o.data[s:e].abs().sum()) == 0
+    for r, w in enumerate(cl.workers):  # re-init: the full map (only the peers change)
+        peers = {i: (w if i == r else _RemoteRank(i)) for i in range(n)}
+        w.tell(InitWorkers(peers, n, None, r, th, th, 1, S, C))
+    outs1 = run_round(xs)
+    for r, o in enumerate(outs1):
+        got = o.count > 0
+        # thReduce 0.5: reduced from the first two arrivals; thComplete 0.5:
+        # the round completes with half of the chunks, the rest read 0/0
+        assert bool((o.count[got] == 2).all())
+        m = o.data.long()[got]
+        assert bool(((m & (m - 1)) != 0).all())  # two distinct contributors
+        if chunk_order:  # scheduled transport: every block's first chunk arrives first
+            for j in range(n):
+                s, _ = g.block_range(j)
+                assert int(o.count[s]) == 2, (r, j)
+    return outs0, outs1
+
+
+def test_partial_membership_islands_stream_transport():
+    n, S, C = 4, 64, 4
+    hub_before = []
+    cl = SimCluster.__new__(SimCluster)
+    from akka_allreduce_amd._native_loader import load
+    from akka_allreduce_amd.worker import AllreduceWorker
+
+    cl.n = n
+    cl.hub = load().SimHub(n)
+    cl.workers = [AllreduceWorker(None, None, device="cpu", transport="stream", transport_spec=("sim", cl.hub, r),
+                                  strict=True, name=f"isl{r}") for r in range(n)]
+
+    def run_round(xs):
+        hub_before.append(cl.bytes_moved())
+        return cl.allreduce(xs)
+
+    _islands(cl, n, S, C, 0.5, run_round)
+    # round 0 moved island traffic only; round 1 the full direct volume
+    r0 = cl.bytes_moved() - hub_before[1]
+    assert hub_before[1] < r0
