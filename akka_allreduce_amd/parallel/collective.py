@@ -4,7 +4,8 @@
 (``stream``) transport.  Every rank starts round r when it calls the object
 (each rank is its own master for pacing; with ``thAllreduce = 1`` and
 lock-step callers this is exactly the reference's master behaviour, M:54-63,
-without a control-plane round trip per round).  The RCCL unique id is shared
+without a control-plane round trip per round -- or, with ``th_allreduce``,
+paced through the store like the reference's master).  The RCCL unique id is shared
 through ``torch.distributed`` (any backend; gloo is enough) or a TCPStore.
 
 Usage::
@@ -18,6 +19,11 @@ RCCL's own xGMI schedules) when the buffer splits evenly, else the
 chunk-pipelined p2p schedule; ``"p2p"`` always uses the p2p schedule,
 ``"collective"`` always the whole-round lane.  Rounds with thresholds < 1
 always take the p2p schedule (their outcome depends on arrival order).
+
+``th_allreduce`` adds the reference's third straggler knob, the master's
+round pacing (M:54-63): a rank starts round r only once ``thAllreduce * N``
+ranks completed round r-1 (counters in the job's TCPStore, no master
+process).  ``None`` (default): each rank paces itself.
 
 ``transport="reactive"`` selects the straggler-tolerant data path
 (csrc/transport/reactive_link.h): one stream + one RCCL pair communicator per
@@ -74,7 +80,56 @@ def share_unique_id(rank: int, world: int, store: Any = None) -> bytes:
     return obj[0]
 
 
+class RoundPacer:
+    """The master's round pacing (M:54-63) without a master process: round r
+    may start on a rank once at least ``thAllreduce * N`` ranks (float32
+    product, like the reference) completed round r-1.  Completions are
+    counters in the job's key-value store (torch.distributed's TCPStore,
+    hosted by rank 0), so pacing costs one store add per round plus polls
+    while a rank is ahead of the threshold."""
+
+    def __init__(self, store: Any, prefix: str, world: int, th_allreduce: float, timeout: float = 300.0):
+        import numpy as np
+
+        self.store = store
+        self.prefix = prefix
+        self.need = float(np.float32(world) * np.float32(th_allreduce))
+        self.timeout = timeout
+        self.waited_s = 0.0
+        self.waits = 0
+
+    def completed(self, r: int) -> None:
+        self.store.add(f"{self.prefix}/{r}", 1)
+
+    def wait_start(self, r: int, progress: Any = None) -> None:
+        """Block until round ``r`` may start (always for r = 0).  ``progress``
+        (e.g. the reactive worker's poll) keeps this rank's own transfers
+        moving while it waits: the ranks being waited for may need them."""
+        if r <= 0:
+            return
+        import time
+
+        key = f"{self.prefix}/{r - 1}"
+        t0 = time.monotonic()
+        nap = 2e-5
+        while self.store.add(key, 0) < self.need:
+            if time.monotonic() - t0 > self.timeout:
+                raise TimeoutError(f"round {r}: fewer than {self.need:g} ranks completed round {r - 1} "
+                                   f"within {self.timeout:g} s (thAllreduce pacing)")
+            if progress is not None and progress():
+                nap = 2e-5
+                continue
+            time.sleep(nap)
+            nap = min(nap * 2, 2e-3)
+        dt = time.monotonic() - t0
+        if dt > 1e-4:
+            self.waits += 1
+        self.waited_s += dt
+
+
 class ThresholdAllreduce:
+    _instances = 0  # creation order is the same on every rank: names pacing keys
+
     def __init__(
         self,
         data_size: int,
@@ -92,6 +147,7 @@ class ThresholdAllreduce:
         data_sink: Any = None,
         transport: str = "stream",
         lane: str = "auto",
+        th_allreduce: Optional[float] = None,
     ):
         if transport not in ("stream", "reactive"):
             raise ValueError("transport must be 'stream' or 'reactive'")
@@ -142,6 +198,19 @@ class ThresholdAllreduce:
         from ..utils.faults import env_straggler_delay
 
         self.fault_delay_s = env_straggler_delay(self.rank)  # AKKA_FAULT_RANK / AKKA_FAULT_DELAY_MS
+        ThresholdAllreduce._instances += 1
+        self.pacer: Optional[RoundPacer] = None
+        if th_allreduce is not None and self.world_size > 1:
+            pstore = store
+            if pstore is None:
+                import torch.distributed as dist
+
+                if not dist.is_initialized():
+                    raise RuntimeError("thAllreduce pacing needs torch.distributed initialised or a store")
+                pstore = dist.distributed_c10d._get_default_store()
+            self.pacer = RoundPacer(pstore, f"akka/pace/{ThresholdAllreduce._instances}", self.world_size,
+                                    float(th_allreduce))
+        self._round = 0
 
     def __call__(self, x: torch.Tensor, async_op: bool = False, out: Optional[torch.Tensor] = None) -> AllReduceOutput:
         """One round.  ``async_op=True``: call ``.wait()`` before reading ``.data``.
@@ -152,9 +221,15 @@ class ThresholdAllreduce:
             import time
 
             time.sleep(self.fault_delay_s)
+        r = self._round
+        if self.pacer is not None:
+            self.pacer.wait_start(r, self.worker.poll if self.transport == "reactive" else None)
         out = self.worker.allreduce(x, async_op=async_op, out=out)
         if out is None:
             raise RuntimeError("round did not complete (thresholds need every rank in the scheduled transport)")
+        self._round += 1
+        if self.pacer is not None:
+            self.pacer.completed(r)  # CompleteAllreduce(id, r) to the "master" (W:276)
         return out
 
     def set_lane(self, lane: str) -> None:

@@ -22,12 +22,22 @@ from .collective import ThresholdAllreduce
 
 
 class ThresholdHookState:
+    """``async_op`` (default True): on GPUs the hook returns before the round
+    ran -- the round, the count-weighted mean and the future's ready event are
+    all queued in stream order (DDP waits on the future's CUDA event, not on
+    the host), so bucket communication overlaps the rest of the backward pass
+    like DDP's own allreduce hook.  ``th_allreduce``: master-style round
+    pacing across ranks (see ThresholdAllreduce)."""
+
     def __init__(self, *, th_reduce: float = 1.0, th_complete: float = 1.0, max_lag: int = 2,
-                 max_chunk_size: int = 1 << 20, transport: str = "stream", broadcast_lag: int = 2):
+                 max_chunk_size: int = 1 << 20, transport: str = "stream", broadcast_lag: int = 2,
+                 async_op: bool = True, th_allreduce=None):
         self.kw = dict(th_reduce=th_reduce, th_complete=th_complete, max_lag=max_lag, max_chunk_size=max_chunk_size,
-                       transport=transport, broadcast_lag=broadcast_lag)
+                       transport=transport, broadcast_lag=broadcast_lag, th_allreduce=th_allreduce)
         self.engines: Dict[Tuple[int, torch.dtype, torch.device], ThresholdAllreduce] = {}
         self.rounds = 0
+        self.async_op = async_op
+        self.async_rounds = 0
 
     def engine(self, t: torch.Tensor) -> ThresholdAllreduce:
         key = (t.numel(), t.dtype, t.device)
@@ -46,9 +56,20 @@ def threshold_allreduce_hook(state: ThresholdHookState, bucket: dist.GradBucket)
         work = flat.float()
     else:
         work = flat
-    out = state.engine(work)(work.contiguous())
+    ar = state.engine(work)
+    cuda = work.is_cuda
+    async_op = bool(state.async_op and cuda and ar.transport == "stream")
+    out = ar(work.contiguous(), async_op=async_op)
+    # async: mean() makes the current stream wait for the round's done event
+    # (a stream wait, not a host wait) and queues the count-mean kernel behind it
     mean = out.mean().to(t.dtype).view_as(t)
     state.rounds += 1
-    fut: torch.futures.Future[torch.Tensor] = torch.futures.Future()
+    state.async_rounds += int(async_op)
+    if cuda:
+        # CUDA-aware future: set_result records an event on the current stream;
+        # DDP's wait() makes its stream wait on that event
+        fut: torch.futures.Future[torch.Tensor] = torch.futures.Future(devices=[work.device])
+    else:
+        fut = torch.futures.Future()
     fut.set_result(mean)
     return fut

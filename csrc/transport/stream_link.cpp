@@ -81,8 +81,12 @@ void StreamLink::schedule(int32_t r) {
   // the peers in the current peer map.  Both sides of a pair must agree, which
   // holds when the map changes at a round boundary (InitWorkers, death).
   std::vector<uint8_t> present(size_t(N), 0);
+  bool any_peer = false;
   for (const auto& pe : engine_->peers())
-    if (pe.id >= 0 && pe.id < N) present[size_t(pe.id)] = 1;
+    if (pe.id >= 0 && pe.id < N) {
+      present[size_t(pe.id)] = 1;
+      any_peer |= pe.id != me;
+    }
   const size_t es = dp_->esize();
   const int32_t kme = g.num_chunks(me);
   const int32_t kmax = dp_->kmax();
@@ -101,7 +105,8 @@ void StreamLink::schedule(int32_t r) {
   for (int32_t s = 0; s < steps; ++s) {
     ops.clear();
     const int32_t kb = s - lag_;
-    bool bcast_step = kb >= 0 && kb < kme;
+    // (no remote peer in the map: my reduced chunks have nobody to go to)
+    bool bcast_step = any_peer && kb >= 0 && kb < kme;
     bool unreduced = false;
     if (bcast_step) {
       auto it = rq.bcast_ready.find(kb);

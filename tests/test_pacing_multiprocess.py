@@ -1,0 +1,79 @@
+"""thAllreduce pacing in the SPMD front end (the reference master's third
+straggler knob, M:54-63): round r starts on a rank once thAllreduce*N ranks
+completed round r-1 (counters in the job's TCPStore).  Four CPU processes on
+the reactive transport (gloo), rank 3 sleeps before every round:
+  * thAllreduce = 0.75 -- the pacing advances on ranks 0-2 alone;
+  * thAllreduce = 1.0  -- every round waits for the sleeper."""
+import os
+import socket
+import time
+
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _rank_main(rank, world, port, th_allreduce, rounds, nap, q):
+    try:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        torch.set_num_threads(1)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        from akka_allreduce_amd.parallel import ThresholdAllreduce
+
+        S = 4096
+        ar = ThresholdAllreduce(S, max_chunk_size=256, rank=rank, world_size=world, device=torch.device("cpu"),
+                                th_reduce=0.75, th_complete=0.75, max_lag=2, transport="reactive",
+                                th_allreduce=th_allreduce)
+        ar.worker.reactive_timeout = 60.0
+        t0 = time.monotonic()
+        for _ in range(rounds):
+            if rank == world - 1:
+                time.sleep(nap)
+            ar(torch.full((S,), float(rank + 1)))
+        elapsed = time.monotonic() - t0
+        ar.drain(60.0)
+        q.put((rank, elapsed, ar.pacer.waits, None))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover
+        q.put((rank, -1.0, -1, repr(e)))
+
+
+def _run(th_allreduce, rounds=5, nap=0.3, world=4):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main, args=(r, world, port, th_allreduce, rounds, nap, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in range(world))
+    for p in procs:
+        p.join(timeout=60)
+    for r in res:
+        assert r[3] is None, r
+    return res
+
+
+def test_pacing_advances_without_the_slow_rank():
+    rounds, nap = 5, 0.3
+    res = _run(0.75, rounds, nap)
+    for rank, elapsed, waits, _ in res[:3]:
+        assert elapsed < nap * rounds / 2, (rank, elapsed)
+
+
+def test_full_pacing_waits_for_every_rank():
+    rounds, nap = 4, 0.3
+    res = _run(1.0, rounds, nap)
+    for rank, elapsed, waits, _ in res[:3]:
+        # round r+1 starts only after the sleeper completed round r
+        assert elapsed > nap * (rounds - 1), (rank, elapsed)
+        assert waits >= rounds - 2

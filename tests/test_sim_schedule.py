@@ -259,3 +259,24 @@ def test_partial_membership_islands_stream_transport():
     # round 0 moved island traffic only; round 1 the full direct volume
     r0 = cl.bytes_moved() - hub_before[1]
     assert hub_before[1] < r0
+
+
+def test_lone_member_completes_from_itself():
+    """Every other worker gone (peer map = {me}), thresholds 0.5: my block is
+    reduced from my own contribution and delivered -- not mistaken for an
+    unreduced chunk because nobody needs its broadcast."""
+    from akka_allreduce_amd._native_loader import load
+    from akka_allreduce_amd.messages import InitWorkers
+    from akka_allreduce_amd.worker import AllreduceWorker
+
+    hub = load().SimHub(2)
+    w = AllreduceWorker(None, None, device="cpu", transport="stream", transport_spec=("sim", hub, 0), strict=True)
+    S, C = 4096, 256
+    w.tell(InitWorkers({0: w}, 2, None, 0, 0.5, 0.5, 1, S, C))
+    for r in range(3):
+        x = torch.full((S,), float(r + 3))
+        o = w.allreduce(x)
+        load().sim_run(hub, [w._core])
+        assert torch.equal(o.data[:S // 2], x[:S // 2]) and bool((o.count[:S // 2] == 1).all())
+        assert int(o.count[S // 2:].abs().sum()) == 0
+    assert w.state()["link"]["unreduced_chunks"] == 0
