@@ -60,16 +60,20 @@ def threshold_allreduce_hook(state: ThresholdHookState, bucket: dist.GradBucket)
     cuda = work.is_cuda
     async_op = bool(state.async_op and cuda and ar.transport == "stream")
     out = ar(work.contiguous(), async_op=async_op)
-    # async: mean() makes the current stream wait for the round's done event
-    # (a stream wait, not a host wait) and queues the count-mean kernel behind it
-    mean = out.mean().to(t.dtype).view_as(t)
     state.rounds += 1
     state.async_rounds += int(async_op)
-    if cuda:
-        # CUDA-aware future: set_result records an event on the current stream;
-        # DDP's wait() makes its stream wait on that event
-        fut: torch.futures.Future[torch.Tensor] = torch.futures.Future(devices=[work.device])
-    else:
-        fut = torch.futures.Future()
-    fut.set_result(mean)
+    if not cuda:
+        fut: torch.futures.Future[torch.Tensor] = torch.futures.Future()
+        fut.set_result(out.mean().to(t.dtype).view_as(t))
+        return fut
+    # CUDA-aware future: set_result records an event on the stream current at
+    # that point, and DDP's wait() makes ITS stream wait on that event (and
+    # record_streams the result).  Async: the count-mean runs on the engine's
+    # compute stream behind the round, so the caller's stream -- the rest of
+    # the backward pass -- only waits where DDP consumes the bucket.
+    side = ar.worker._internal_streams()[1] if async_op else torch.cuda.current_stream(work.device)
+    with torch.cuda.stream(side):
+        mean = out.mean().to(t.dtype).view_as(t)
+        fut = torch.futures.Future(devices=[work.device])
+        fut.set_result(mean)
     return fut
