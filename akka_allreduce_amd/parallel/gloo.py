@@ -19,7 +19,7 @@ from typing import Callable, List, Tuple
 import torch
 import torch.distributed as dist
 
-Op = Tuple[bool, int, int, int]
+Op = Tuple[bool, int, int, int, int]  # (send, peer, ptr, nbytes, channel) -- channel = gloo tag
 
 
 def _view(ptr: int, nbytes: int) -> torch.Tensor:
@@ -30,11 +30,12 @@ def _view(ptr: int, nbytes: int) -> torch.Tensor:
 def make_group_fn(group=None) -> Callable[[List[Op]], None]:
     def run(ops: List[Op]) -> None:
         reqs = []
-        for send, peer, ptr, nbytes in ops:
+        for send, peer, ptr, nbytes, *ch in ops:
             if nbytes == 0:
                 continue
             t = _view(ptr, nbytes)
-            reqs.append(dist.isend(t, peer, group=group) if send else dist.irecv(t, peer, group=group))
+            tag = ch[0] if ch else 0
+            reqs.append(dist.isend(t, peer, group=group, tag=tag) if send else dist.irecv(t, peer, group=group, tag=tag))
         for r in reqs:
             r.wait()
 
@@ -50,11 +51,13 @@ def make_async_fns(group=None) -> Tuple[Callable[[List[Op]], object], Callable[[
 
     def post(ops: List[Op]) -> object:
         works = []
-        for send, peer, ptr, nbytes in ops:
+        for send, peer, ptr, nbytes, *ch in ops:
             if nbytes == 0:
                 continue
             t = _view(ptr, nbytes)
-            works.append((t, dist.isend(t, peer, group=group) if send else dist.irecv(t, peer, group=group)))
+            tag = ch[0] if ch else 0  # independent matching order per channel, like one RCCL comm each
+            works.append((t, dist.isend(t, peer, group=group, tag=tag) if send
+                          else dist.irecv(t, peer, group=group, tag=tag)))
         done = threading.Event()
         if not works:
             done.set()

@@ -327,6 +327,7 @@ class WorkerCore final : public EngineHost {
       ls["reclaim_waits"] = rs.reclaim_waits;
       ls["peers_lost"] = rs.peers_lost;
       ls["transfers_dropped"] = rs.transfers_dropped;
+      ls["p2_overlapped"] = rs.p2_overlapped;
       ls["slots"] = dp_->slots_allocated();
       ls["slots_busy"] = dp_->slots_busy();
       ls["in_flight"] = reactive_link_->in_flight();

@@ -39,7 +39,7 @@ class PyCallbackP2P final : public P2P {
   void group(StreamH, const std::vector<P2POp>& ops) override {
     py::list l;
     for (const auto& op : ops)
-      l.append(py::make_tuple(op.send, op.peer, reinterpret_cast<uintptr_t>(op.buf), op.bytes));
+      l.append(py::make_tuple(op.send, op.peer, reinterpret_cast<uintptr_t>(op.buf), op.bytes, op.channel));
     fn_(l);
   }
 
@@ -69,7 +69,7 @@ class PyAsyncCallbackP2P final : public P2P {
     };
     auto st = std::make_shared<State>();
     for (const auto& op : ops)
-      st->ops.append(py::make_tuple(op.send, op.peer, reinterpret_cast<uintptr_t>(op.buf), op.bytes));
+      st->ops.append(py::make_tuple(op.send, op.peer, reinterpret_cast<uintptr_t>(op.buf), op.bytes, op.channel));
     py::function post = post_, test = test_;
     // Runs from WorkerCore::poll / start (Python callers: the GIL is held).
     dev_->enqueue_host_op(stream, [st, post, test]() {
@@ -209,13 +209,20 @@ class LoopbackP2P final : public P2P {
 // only its own pair's streams, which is exactly what the reactive link has to
 // tolerate.
 struct PairHub {
-  explicit PairHub(int32_t n) : n(n), posts(size_t(n) * n), flags(size_t(n) * n, nullptr), seq(size_t(n) * n, 0) {
+  static constexpr int32_t kCh = 2;  // channels (independent matching orders) per pair
+  explicit PairHub(int32_t n)
+      : n(n), posts(size_t(n) * n * kCh), flags(size_t(n) * n * kCh, nullptr), seq(size_t(n) * n * kCh, 0) {
     // One coherent pinned block, one 64-byte line per signal word: the CP's
     // wait-value packets poll it, the peer stream's write-value packet sets it.
-    if (hipHostMalloc(&block, size_t(n) * n * 64, hipHostMallocCoherent) != hipSuccess)
+    if (hipHostMalloc(&block, flags.size() * 64, hipHostMallocCoherent) != hipSuccess)
       throw AkkaError("akka: pair loopback: cannot allocate signal memory");
-    std::memset(block, 0, size_t(n) * n * 64);
+    std::memset(block, 0, flags.size() * 64);
     for (size_t i = 0; i < flags.size(); ++i) flags[i] = reinterpret_cast<uint32_t*>(static_cast<char*>(block) + i * 64);
+  }
+  // index of (a, b, channel) in flags/seq, and of the unordered pair in posts
+  size_t dir(int32_t a, int32_t b, int32_t ch) const { return (size_t(a) * n + size_t(b)) * kCh + size_t(ch); }
+  size_t pair(int32_t a, int32_t b, int32_t ch) const {
+    return (size_t(std::min(a, b)) * n + size_t(std::max(a, b))) * kCh + size_t(ch);
   }
   ~PairHub() {
     for (auto* e : events) hipEventDestroy(e);
@@ -241,9 +248,9 @@ struct PairHub {
   }
   int32_t n;
   std::mutex mu;
-  std::vector<std::deque<Post>> posts;  // [lo*n+hi] unmatched posts of that pair (one side at a time)
-  std::vector<uint32_t*> flags;         // [a*n+b]: a's stream waits here for its groups with b
-  std::vector<uint32_t> seq;            // [a*n+b]: groups a posted towards b
+  std::vector<std::deque<Post>> posts;  // [pair(lo,hi,ch)] unmatched posts of that pair (one side at a time)
+  std::vector<uint32_t*> flags;         // [dir(a,b,ch)]: a's stream waits here for its groups with b
+  std::vector<uint32_t> seq;            // [dir(a,b,ch)]: groups a posted towards b
   void* block = nullptr;
   std::vector<hipEvent_t> events, free_events;
   std::set<std::pair<int32_t, int32_t>> dead;  // (me, peer) aborted by me
@@ -266,11 +273,13 @@ class LoopbackPairP2P final : public P2P {
     // are dropped.
     PairHub& h = *hub_;
     std::lock_guard<std::mutex> lk(h.mu);
-    const size_t key = size_t(std::min(rank_, peer)) * h.n + size_t(std::max(rank_, peer));
-    for (auto& p : h.posts[key]) h.free_events.push_back(p.posted);
-    h.posts[key].clear();
-    __atomic_store_n(h.flags[size_t(rank_) * h.n + peer], 0x7fffffffu, __ATOMIC_SEQ_CST);
-    __atomic_store_n(h.flags[size_t(peer) * h.n + rank_], 0x7fffffffu, __ATOMIC_SEQ_CST);
+    for (int32_t ch = 0; ch < PairHub::kCh; ++ch) {
+      const size_t key = h.pair(rank_, peer, ch);
+      for (auto& p : h.posts[key]) h.free_events.push_back(p.posted);
+      h.posts[key].clear();
+      __atomic_store_n(h.flags[h.dir(rank_, peer, ch)], 0x7fffffffu, __ATOMIC_SEQ_CST);
+      __atomic_store_n(h.flags[h.dir(peer, rank_, ch)], 0x7fffffffu, __ATOMIC_SEQ_CST);
+    }
     h.dead.insert({rank_, peer});
     return true;
   }
@@ -278,16 +287,18 @@ class LoopbackPairP2P final : public P2P {
     if (ops.empty()) return;
     PairHub& h = *hub_;
     const int32_t peer = ops.front().peer;
-    for (const auto& op : ops) AKKA_CHECK(op.peer == peer, "pair group holds ops to more than one peer");
+    const int32_t ch = ops.front().channel;
+    for (const auto& op : ops)
+      AKKA_CHECK(op.peer == peer && op.channel == ch, "pair group holds ops to more than one peer / channel");
+    AKKA_CHECK(ch >= 0 && ch < PairHub::kCh, "pair loopback: bad channel");
     hipStream_t s = static_cast<hipStream_t>(stream);
     std::lock_guard<std::mutex> lk(h.mu);
     AKKA_CHECK(!h.dead.count({rank_, peer}), "pair loopback: group to an aborted peer");
-    const size_t key = size_t(std::min(rank_, peer)) * h.n + size_t(std::max(rank_, peer));
-    auto& q = h.posts[key];
+    auto& q = h.posts[h.pair(rank_, peer, ch)];
     if (q.empty() || q.front().rank == rank_) {
-      PairHub::Post p{rank_, stream, ops, h.event(), ++h.seq[size_t(rank_) * h.n + peer]};
+      PairHub::Post p{rank_, stream, ops, h.event(), ++h.seq[h.dir(rank_, peer, ch)]};
       check(hipEventRecord(p.posted, s));
-      check(hipStreamWaitValue32(s, h.flags[size_t(rank_) * h.n + peer], p.seq, hipStreamWaitValueGte, 0xFFFFFFFFu));
+      check(hipStreamWaitValue32(s, h.flags[h.dir(rank_, peer, ch)], p.seq, hipStreamWaitValueGte, 0xFFFFFFFFu));
       q.push_back(std::move(p));
       return;
     }
@@ -298,7 +309,7 @@ class LoopbackPairP2P final : public P2P {
     int64_t moved = 0;
     moved += copy_dir(other.ops, ops, s);  // other's sends -> my recvs
     moved += copy_dir(ops, other.ops, s);  // my sends -> other's recvs
-    check(hipStreamWriteValue32(s, h.flags[size_t(other.rank) * h.n + rank_], other.seq, 0));
+    check(hipStreamWriteValue32(s, h.flags[h.dir(other.rank, rank_, ch)], other.seq, 0));
     h.bytes += moved;
   }
 

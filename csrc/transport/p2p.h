@@ -23,6 +23,10 @@ struct P2POp {
   int32_t peer = -1;
   void* buf = nullptr;
   size_t bytes = 0;
+  // Independent ordering domain (pair transports): channel 0 and 1 of a pair
+  // match separately, so phase-2 chunks never queue behind phase-1 chunks
+  // (RCCL: one pair communicator per channel).  Global transports: 0 only.
+  int32_t channel = 0;
 };
 
 // What the transport itself reports about its communicator(s): for RCCL the
@@ -108,7 +112,9 @@ inline int32_t tournament_partner(int32_t n, int32_t t, int32_t x) {
 }
 inline int32_t tournament_rounds(int32_t n) { return ((n % 2) ? n + 1 : n) - 1; }
 
-// Per-pair communicators (reactive transport): a group holds ops to one peer.
+// Per-pair communicators (reactive transport): a group holds ops to one peer
+// on one channel; two communicators per pair (channel 0: phase 1, channel 1:
+// phase 2).
 std::unique_ptr<P2P> make_rccl_pair_p2p(const std::vector<uint8_t>& uid, int32_t rank, int32_t nranks,
                                         int32_t device);
 const char* rccl_version_string();

@@ -163,7 +163,7 @@ class RcclP2P final : public P2P {
 class RcclPairP2P final : public P2P {
  public:
   RcclPairP2P(const std::vector<uint8_t>& uid, int32_t rank, int32_t nranks, int32_t device)
-      : rank_(rank), n_(nranks), pair_(size_t(nranks), nullptr) {
+      : rank_(rank), n_(nranks) {
     AKKA_CHECK(uid.size() == sizeof(ncclUniqueId), "bad RCCL unique id size");
     ncclUniqueId id;
     std::memcpy(&id, uid.data(), sizeof(id));
@@ -171,24 +171,29 @@ class RcclPairP2P final : public P2P {
     AKKA_NCCL(ncclCommInitRank(&global_, nranks, id, rank));
     verify_comm(global_, nranks, rank, device, "global");
     // Round-robin tournament (circle method): P-1 rounds of disjoint pairs,
-    // one ncclCommSplit each; with odd N a dummy player sits one rank out.
-    for (int32_t t = 0; t < tournament_rounds(nranks); ++t) {
-      const int32_t partner = tournament_partner(nranks, t, rank);
-      const bool real = partner < nranks && partner != rank;
-      ncclComm_t c = nullptr;
-      AKKA_NCCL(ncclCommSplit(global_, real ? std::min(rank, partner) : NCCL_SPLIT_NOCOLOR, rank, &c, nullptr));
-      if (real) pair_[size_t(partner)] = c;
-    }
-    for (int32_t p = 0; p < nranks; ++p) {
-      if (p == rank) continue;
-      AKKA_CHECK(pair_[size_t(p)], "pair communicator missing for peer " + std::to_string(p));
-      // split key = global rank: the lower global rank is pair rank 0
-      verify_comm(pair_[size_t(p)], 2, rank < p ? 0 : 1, device, "pair");
+    // one ncclCommSplit per channel each; with odd N a dummy player sits one
+    // rank out.  Every rank runs the same sequence of splits.
+    for (int32_t ch = 0; ch < kChannels; ++ch) {
+      pair_[ch].assign(size_t(nranks), nullptr);
+      for (int32_t t = 0; t < tournament_rounds(nranks); ++t) {
+        const int32_t partner = tournament_partner(nranks, t, rank);
+        const bool real = partner < nranks && partner != rank;
+        ncclComm_t c = nullptr;
+        AKKA_NCCL(ncclCommSplit(global_, real ? std::min(rank, partner) : NCCL_SPLIT_NOCOLOR, rank, &c, nullptr));
+        if (real) pair_[ch][size_t(partner)] = c;
+      }
+      for (int32_t p = 0; p < nranks; ++p) {
+        if (p == rank) continue;
+        AKKA_CHECK(pair_[ch][size_t(p)], "pair communicator missing for peer " + std::to_string(p));
+        // split key = global rank: the lower global rank is pair rank 0
+        verify_comm(pair_[ch][size_t(p)], 2, rank < p ? 0 : 1, device, "pair");
+      }
     }
   }
   ~RcclPairP2P() override {
-    for (ncclComm_t c : pair_)
-      if (c) ncclCommDestroy(c);
+    for (auto& v : pair_)
+      for (ncclComm_t c : v)
+        if (c) ncclCommDestroy(c);
     if (global_) ncclCommDestroy(global_);
   }
   int32_t rank() const override { return rank_; }
@@ -198,14 +203,16 @@ class RcclPairP2P final : public P2P {
   void group(StreamH stream, const std::vector<P2POp>& ops) override {
     if (ops.empty()) return;
     const int32_t peer = ops.front().peer;
+    const int32_t ch = ops.front().channel;
     AKKA_CHECK(peer >= 0 && peer < n_ && peer != rank_, "pair group: bad peer");
-    ncclComm_t c = pair_[size_t(peer)];
+    AKKA_CHECK(ch >= 0 && ch < kChannels, "pair group: bad channel");
+    ncclComm_t c = pair_[ch][size_t(peer)];
     AKKA_CHECK(c, "pair group to peer " + std::to_string(peer) + " after its communicator was aborted");
     const int32_t prank = peer < rank_ ? 0 : 1;  // split key = global rank
     hipStream_t s = static_cast<hipStream_t>(stream);
     AKKA_NCCL(ncclGroupStart());
     for (const auto& op : ops) {
-      AKKA_CHECK(op.peer == peer, "pair group holds ops to more than one peer");
+      AKKA_CHECK(op.peer == peer && op.channel == ch, "pair group holds ops to more than one peer / channel");
       if (op.send) AKKA_NCCL(ncclSend(op.buf, op.bytes, ncclUint8, prank, c, s));
       else AKKA_NCCL(ncclRecv(op.buf, op.bytes, ncclUint8, prank, c, s));
     }
@@ -213,12 +220,14 @@ class RcclPairP2P final : public P2P {
   }
   bool abort_peer(int32_t peer) override {
     if (peer < 0 || peer >= n_ || peer == rank_) return false;
-    ncclComm_t& c = pair_[size_t(peer)];
-    if (c) {
-      // Kernels parked on the dead peer exit; the pair stream moves on.  The
-      // communicator is gone: every later group to that peer is an error.
-      ncclCommAbort(c);
-      c = nullptr;
+    for (auto& v : pair_) {
+      ncclComm_t& c = v[size_t(peer)];
+      if (c) {
+        // Kernels parked on the dead peer exit; the pair streams move on.  The
+        // communicators are gone: every later group to that peer is an error.
+        ncclCommAbort(c);
+        c = nullptr;
+      }
     }
     aborted_.push_back(peer);
     return true;
@@ -229,20 +238,23 @@ class RcclPairP2P final : public P2P {
     ncclCommUserRank(global_, &r);
     ncclCommCuDevice(global_, &d);
     int32_t comms = 1;
-    for (ncclComm_t c : pair_) comms += c ? 1 : 0;
+    for (const auto& v : pair_)
+      for (ncclComm_t c : v) comms += c ? 1 : 0;
     return P2PInfo{name(), n, r, d, comms};
   }
   void check() override {
     // the global communicator spans the dead rank too: only the pairs matter
     // once a peer was aborted
     if (aborted_.empty()) check_async(global_, "global");
-    for (ncclComm_t c : pair_) check_async(c, "pair");
+    for (const auto& v : pair_)
+      for (ncclComm_t c : v) check_async(c, "pair");
   }
 
  private:
+  static constexpr int32_t kChannels = 2;
   int32_t rank_, n_;
   ncclComm_t global_ = nullptr;
-  std::vector<ncclComm_t> pair_;
+  std::vector<ncclComm_t> pair_[kChannels];  // [channel][peer]
   std::vector<int32_t> aborted_;
 };
 

@@ -6,22 +6,34 @@
 
 namespace akka {
 
+namespace {
+constexpr int32_t kPhase1 = 0;  // pair channel of phase 1 (scatter)
+constexpr int32_t kPhase2 = 1;  // pair channel of phase 2 (reduced chunks + counts)
+constexpr int32_t kCountBlock = 1024;  // pinned count slots allocated at a time
+}  // namespace
+
 ReactiveLink::ReactiveLink(Engine* engine, P2P* p2p, int32_t max_slots)
     : engine_(engine), p2p_(p2p), max_slots_(max_slots) {}
 
 ReactiveLink::~ReactiveLink() {
   if (!dev_) return;
-  // A lost peer's stream is left alone (never synchronized or destroyed):
-  // whatever it still holds can only wait for a rank that is gone.
+  // A lost peer's streams are left alone (never synchronized or destroyed):
+  // whatever they still hold can only wait for a rank that is gone.
   try {
-    for (size_t p = 0; p < streams_.size(); ++p)
-      if (streams_[p] && !lost_[p]) dev_->sync_stream(streams_[p]);
+    for (size_t p = 0; p < s1_.size(); ++p) {
+      if (lost_[p]) continue;
+      if (s1_[p]) dev_->sync_stream(s1_[p]);
+      if (s2_[p]) dev_->sync_stream(s2_[p]);
+    }
   } catch (...) {
   }
-  for (size_t p = 0; p < streams_.size(); ++p)
-    if (streams_[p] && !lost_[p]) dev_->destroy_stream(streams_[p]);
+  for (size_t p = 0; p < s1_.size(); ++p) {
+    if (lost_[p]) continue;
+    if (s1_[p]) dev_->destroy_stream(s1_[p]);
+    if (s2_[p]) dev_->destroy_stream(s2_[p]);
+  }
   for (EventH e : events_) dev_->destroy_event(e);
-  for (int32_t* p : pinned_) dev_->release_pinned(p);
+  for (int32_t* p : pinned_blocks_) dev_->release_pinned(p);
   if (recv_dev_) dev_->release(recv_dev_);
 }
 
@@ -37,10 +49,14 @@ void ReactiveLink::bind(DataPlane* dp) {
   kmax_ = dp->kmax();
   AKKA_CHECK(N_ >= 2, "the reactive transport needs at least two workers");
   AKKA_CHECK(p2p_->nranks() == N_ && p2p_->rank() == me_, "p2p endpoint does not match the worker geometry");
-  streams_.assign(size_t(N_), nullptr);
+  s1_.assign(size_t(N_), nullptr);
+  s2_.assign(size_t(N_), nullptr);
   lost_.assign(size_t(N_), 0);
   for (int32_t p = 0; p < N_; ++p)
-    if (p != me_) streams_[size_t(p)] = dev_->create_stream();
+    if (p != me_) {
+      s1_[size_t(p)] = dev_->create_stream();
+      s2_[size_t(p)] = dev_->create_stream();
+    }
   recv_dev_ = static_cast<int32_t*>(dev_->alloc(size_t(L_) * N_ * kmax_ * sizeof(int32_t)));
   dp->enable_staging(std::max(max_slots_, L_ + 1), [this](int32_t round) { return reclaim(round); });
 }
@@ -50,8 +66,12 @@ ReactiveLink::RoundState& ReactiveLink::st(int32_t r) {
   if (it != rounds_.end()) return it->second;
   RoundState& s = rounds_[r];
   s.wire.assign(size_t(std::max(kme_, 1)), 0);
-  if (kme_ == 0) s.closable = true;  // empty block: nothing of mine to reduce
+  s.ready.assign(size_t(std::max(kme_, 1)), nullptr);
   return s;
+}
+
+int32_t ReactiveLink::chunks_with(int32_t p) const {
+  return std::max(kme_, dp_->geometry().num_chunks(p));
 }
 
 EventH ReactiveLink::get_event() {
@@ -66,50 +86,45 @@ EventH ReactiveLink::get_event() {
 }
 void ReactiveLink::put_event(EventH e) { free_events_.push_back(e); }
 
-int32_t* ReactiveLink::get_pinned() {
-  if (!free_pinned_.empty()) {
-    int32_t* p = free_pinned_.back();
-    free_pinned_.pop_back();
-    return p;
+int32_t* ReactiveLink::get_count_slot() {
+  if (free_counts_.empty()) {
+    int32_t* b = static_cast<int32_t*>(dev_->alloc_pinned(size_t(kCountBlock) * sizeof(int32_t)));
+    pinned_blocks_.push_back(b);
+    for (int32_t i = kCountBlock - 1; i >= 0; --i) free_counts_.push_back(b + i);
   }
-  int32_t* p = static_cast<int32_t*>(dev_->alloc_pinned(size_t(kmax_) * sizeof(int32_t)));
-  pinned_.push_back(p);
+  int32_t* p = free_counts_.back();
+  free_counts_.pop_back();
   return p;
 }
 
 void ReactiveLink::send_reduce(int32_t /*dest*/, int32_t chunk, int32_t round, int32_t count, const Payload&) {
-  // Called once per (chunk, remote peer); the data already sits in the landing
-  // row (DataPlane staged mode) -- only record the chunk's count once.
-  if (round < next_round_) return;  // P2 already out (cannot happen: no reduces after completion)
+  // Called once per (chunk, remote peer) right after the engine reduced the
+  // chunk into the round's send slot: record its count once -- written into
+  // the slot's device count row by a 4-byte fill that merges into the reduce
+  // launch -- and the point the chunk's P2 groups wait for.
+  if (round < p2_round_) return;  // P2 of the round already out (cannot happen: no reduces after completion)
   RoundState& s = st(round);
-  if (s.p2_issued) return;
-  int32_t& w = s.wire[size_t(chunk)];
-  if (w == 0) {
-    w = count + 1;
-    if (++s.reduced == kme_) s.closable = true;
-  }
+  if (chunk < s.p2_next || s.wire[size_t(chunk)] != 0) return;
+  s.wire[size_t(chunk)] = count + 1;
+  StreamH cs = dev_->compute_stream();
+  dev_->fill_i32(cs, dp_->wire_dev(round) + chunk, count + 1, 1);
+  s.ready[size_t(chunk)] = get_event();
+  dev_->record(s.ready[size_t(chunk)], cs);
 }
 
 void ReactiveLink::on_scattered(int32_t round) { st(round).scattered = true; }
 
 bool ReactiveLink::may_finalize(int32_t round) {
-  // The round completed: P2 goes out with whatever is reduced by now.  (Its
-  // send slot is released at the next pump, after finalize read it.)
-  auto it = rounds_.find(round);
-  if (it != rounds_.end()) {
-    it->second.closable = true;
-    it->second.completed = true;
-  } else if (round >= next_round_) {
-    RoundState& s = st(round);
-    s.closable = true;
-    s.completed = true;
-  }
+  // The round completed: its remaining P2 chunks go out with whatever is
+  // reduced by now (count 0 for the rest).  Its send slot is released once
+  // every transfer of the round finished.
+  if (round >= p2_round_ || rounds_.count(round)) st(round).completed = true;
   return true;
 }
 
 void ReactiveLink::pump() {
   issue_ready();
-  for (auto it = rounds_.begin(); it != rounds_.end() && it->first < next_round_;) {
+  for (auto it = rounds_.begin(); it != rounds_.end() && it->first < p2_round_;) {
     const int32_t r = it->first;
     ++it;
     retire(r);
@@ -120,19 +135,18 @@ void ReactiveLink::issue_ready() {
   if (issuing_ || !dp_) return;
   issuing_ = true;
   try {
+    // Phase 1 in round order, each round as soon as it was scattered.
     for (;;) {
-      auto it = rounds_.find(next_round_);
-      if (it == rounds_.end()) break;
-      if (!next_is_p2_) {
-        if (!it->second.scattered) break;
-        issue_p1(next_round_);
-        next_is_p2_ = true;
-      } else {
-        if (!it->second.closable) break;
-        issue_p2(next_round_);
-        next_is_p2_ = false;
-        ++next_round_;
-      }
+      auto it = rounds_.find(p1_round_);
+      if (it == rounds_.end() || !it->second.scattered) break;
+      issue_p1(p1_round_);
+      ++p1_round_;
+    }
+    // Phase 2 in (round, chunk) order, each chunk as soon as it is ready.
+    for (;;) {
+      if (!rounds_.count(p2_round_)) break;
+      if (!issue_p2(p2_round_)) break;
+      ++p2_round_;
     }
   } catch (...) {
     issuing_ = false;
@@ -153,7 +167,7 @@ void ReactiveLink::on_peer_lost(int32_t id) {
   lost_[size_t(id)] = 1;
   ++stats_.peers_lost;
   // End what is queued / in flight with the dead peer (RCCL: abort of the
-  // pair communicator), then forget it: its arrivals are never delivered, so
+  // pair communicators), then forget it: its arrivals are never delivered, so
   // its contributions count as missing (the thresholds decide), and nothing
   // -- slot reclaim included -- ever waits for its transfers again.
   p2p_->abort_peer(id);
@@ -163,12 +177,15 @@ void ReactiveLink::on_peer_lost(int32_t id) {
       continue;
     }
     auto rs = rounds_.find(it->round);
-    if (rs != rounds_.end()) --rs->second.open;
-    // the event / pinned row may still be referenced by the dead stream: not recycled
+    if (rs != rounds_.end()) {
+      --rs->second.open;
+      if (it->phase == 1) --rs->second.p1_open;
+    }
+    // the event / pinned count may still be referenced by the dead stream: not recycled
     ++stats_.transfers_dropped;
     it = pending_.erase(it);
   }
-  for (auto it = rounds_.begin(); it != rounds_.end() && it->first < next_round_;) {
+  for (auto it = rounds_.begin(); it != rounds_.end() && it->first < p2_round_;) {
     const int32_t r = it->first;
     ++it;
     retire(r);
@@ -178,7 +195,6 @@ void ReactiveLink::on_peer_lost(int32_t id) {
 void ReactiveLink::issue_p1(int32_t r) {
   const Geometry& g = dp_->geometry();
   const size_t es = dp_->esize();
-  const int64_t my_len = g.block_len(me_);
   // Covers the staging copy of r and every reduce that read ring row r%L for
   // an older round.
   EventH rel = dp_->row_release_event(r);
@@ -187,101 +203,126 @@ void ReactiveLink::issue_p1(int32_t r) {
   for (int32_t i = 1; i < N_; ++i) {
     const int32_t p = (me_ + i) % N_;
     if (!exchanges_with(p)) continue;
-    StreamH ps = streams_[size_t(p)];
+    StreamH ps = s1_[size_t(p)];
     dev_->wait(ps, rel);
-    ops.clear();
-    const int64_t plen = g.block_len(p);
-    if (plen > 0) ops.push_back({true, p, const_cast<void*>(dp_->staged_input(r, p)), size_t(plen) * es});
-    if (my_len > 0) ops.push_back({false, p, dp_->scatter_slot(r, p, 0), size_t(my_len) * es});
-    if (!ops.empty()) {
+    const int32_t kp = g.num_chunks(p);
+    const char* in = static_cast<const char*>(dp_->staged_input(r, p));
+    for (int32_t k = 0; k < chunks_with(p); ++k) {
+      ops.clear();
+      if (k < kp) {
+        ops.push_back({true, p, const_cast<char*>(in) + size_t(g.chunk_start(p, k)) * es,
+                       size_t(g.chunk_len(p, k)) * es, kPhase1});
+        stats_.bytes_sent += g.chunk_len(p, k) * int64_t(es);
+      }
+      if (k < kme_) ops.push_back({false, p, dp_->scatter_slot(r, p, k), size_t(g.chunk_len(me_, k)) * es, kPhase1});
       p2p_->group(ps, ops);
       ++stats_.groups;
-      if (plen > 0) stats_.bytes_sent += plen * int64_t(es);
+      Pending pd;
+      pd.round = r;
+      pd.peer = p;
+      pd.phase = 1;
+      pd.chunk = k;
+      pd.ev = get_event();
+      dev_->record(pd.ev, ps);
+      arm(ps);
+      pending_.push_back(pd);
+      ++s.open;
+      ++s.p1_open;
     }
-    Pending pd;
-    pd.round = r;
-    pd.peer = p;
-    pd.phase = 1;
-    pd.ev = get_event();
-    dev_->record(pd.ev, ps);
-    arm(ps);
-    pending_.push_back(pd);
-    ++s.open;
   }
+  s.p1_issued = true;
 }
 
-void ReactiveLink::issue_p2(int32_t r) {
+bool ReactiveLink::issue_p2(int32_t r) {
+  RoundState& s = st(r);
+  if (s.p2_done) return true;
+  // The landing row r%L was last read by round r-L's finalize (compute
+  // stream): that round must have completed (it has, whenever one of my
+  // chunks of r was reduced; with an empty block of my own this is the check).
+  if (r - L_ >= 0 && !engine_->is_completed(r - L_)) return false;
   const Geometry& g = dp_->geometry();
   const size_t es = dp_->esize();
-  const int64_t my_len = g.block_len(me_);
-  const size_t row = size_t(r % L_);
-  RoundState& s = st(r);
   StreamH cs = dev_->compute_stream();
-  int32_t* wdev = dp_->wire_dev(r);
-  void* mine = dp_->mine_at(r, 0);
-  if (kme_ > 0) {
-    // The slot's pinned row is only rewritten after its previous round's
-    // transfers (which follow this upload in stream order) finished.
-    int32_t* wh = dp_->wire_host(r);
-    std::memcpy(wh, s.wire.data(), size_t(kme_) * sizeof(int32_t));
-    for (int32_t k = 0; k < kme_; ++k)
-      if (s.wire[size_t(k)] == 0) ++stats_.unreduced_chunks;
-    dev_->copy(cs, wdev, wh, size_t(kme_) * sizeof(int32_t), CopyKind::HostToDevice);
+  const size_t row = size_t(r % L_);
+  if (s.p2_next == 0) {
+    // receive-only groups (chunks past the end of my block) wait on this
+    EventH landing = get_event();
+    dev_->record(landing, cs);
+    for (int32_t i = 1; i < N_; ++i) {
+      const int32_t p = (me_ + i) % N_;
+      if (exchanges_with(p)) dev_->wait(s2_[size_t(p)], landing);
+    }
+    put_event(landing);
   }
-  // Everything my block's sends read (reduces, wire counts) and everything
-  // that read the landing row for round r-L (its finalize) is on the compute
-  // stream before this point.
-  EventH ready = get_event();
-  dev_->record(ready, cs);
   std::vector<P2POp> ops;
-  for (int32_t i = 1; i < N_; ++i) {
-    const int32_t p = (me_ + i) % N_;
-    if (!exchanges_with(p)) continue;
-    StreamH ps = streams_[size_t(p)];
-    dev_->wait(ps, ready);
-    const int32_t kp = g.num_chunks(p);
-    const int64_t plen = g.block_len(p);
-    int32_t* rdev = recv_dev_ + (row * N_ + size_t(p)) * kmax_;
-    ops.clear();
-    if (my_len > 0) {
-      ops.push_back({true, p, mine, size_t(my_len) * es});
-      ops.push_back({true, p, wdev, size_t(kme_) * sizeof(int32_t)});
+  while (s.p2_next < kmax_) {
+    const int32_t k = s.p2_next;
+    if (k < kme_) {
+      if (s.wire[size_t(k)] == 0) {
+        if (!s.completed) break;  // not reduced yet: later chunks wait too (per-pair order)
+        // round completed before this chunk reached its threshold: count 0
+        dev_->fill_i32(cs, dp_->wire_dev(r) + k, 0, 1);
+        s.ready[size_t(k)] = get_event();
+        dev_->record(s.ready[size_t(k)], cs);
+        ++stats_.unreduced_chunks;
+      }
     }
-    if (plen > 0) {
-      ops.push_back({false, p, dp_->landing_at(r, p, 0), size_t(plen) * es});
-      ops.push_back({false, p, rdev, size_t(kp) * sizeof(int32_t)});
-    }
-    if (!ops.empty()) {
+    bool issued = false;
+    for (int32_t i = 1; i < N_; ++i) {
+      const int32_t p = (me_ + i) % N_;
+      if (!exchanges_with(p) || k >= chunks_with(p)) continue;
+      StreamH ps = s2_[size_t(p)];
+      const int32_t kp = g.num_chunks(p);
+      int32_t* rdev = recv_dev_ + (row * size_t(N_) + size_t(p)) * size_t(kmax_);
+      ops.clear();
+      if (k < kme_) {
+        dev_->wait(ps, s.ready[size_t(k)]);
+        ops.push_back({true, p, dp_->mine_at(r, k), size_t(g.chunk_len(me_, k)) * es, kPhase2});
+        ops.push_back({true, p, dp_->wire_dev(r) + k, sizeof(int32_t), kPhase2});
+        stats_.bytes_sent += g.chunk_len(me_, k) * int64_t(es) + int64_t(sizeof(int32_t));
+      }
+      if (k < kp) {
+        ops.push_back({false, p, dp_->landing_at(r, p, k), size_t(g.chunk_len(p, k)) * es, kPhase2});
+        ops.push_back({false, p, rdev + k, sizeof(int32_t), kPhase2});
+      }
       p2p_->group(ps, ops);
       ++stats_.groups;
-      if (my_len > 0) stats_.bytes_sent += my_len * int64_t(es) + kme_ * int64_t(sizeof(int32_t));
+      Pending pd;
+      pd.round = r;
+      pd.peer = p;
+      pd.phase = 2;
+      pd.chunk = k;
+      if (k < kp) {
+        pd.count = get_count_slot();
+        dev_->copy(ps, pd.count, rdev + k, sizeof(int32_t), CopyKind::DeviceToHost);
+      }
+      pd.ev = get_event();
+      dev_->record(pd.ev, ps);
+      arm(ps);
+      pending_.push_back(pd);
+      ++s.open;
+      issued = true;
     }
-    Pending pd;
-    pd.round = r;
-    pd.peer = p;
-    pd.phase = 2;
-    if (kp > 0) {
-      pd.counts = get_pinned();
-      dev_->copy(ps, pd.counts, rdev, size_t(kp) * sizeof(int32_t), CopyKind::DeviceToHost);
+    if (issued && s.p1_open > 0) ++stats_.p2_overlapped;
+    if (k < kme_) {
+      put_event(s.ready[size_t(k)]);  // the waits above captured its record
+      s.ready[size_t(k)] = nullptr;
     }
-    pd.ev = get_event();
-    dev_->record(pd.ev, ps);
-    arm(ps);
-    pending_.push_back(pd);
-    ++s.open;
+    ++s.p2_next;
   }
-  put_event(ready);  // the waits above captured its record
-  s.p2_issued = true;
+  if (s.p2_next < kmax_) return false;
+  s.p2_done = true;
   p2p_->check();  // RCCL async errors on the pair communicators: once per round
+  return true;
 }
 
 bool ReactiveLink::reclaim(int32_t round) {
   // The data plane wants to reuse `round`'s send slot for a newer round: make
   // the compute stream (which writes the slot next) wait for the transfers
   // that still read it.  Everything issuable is issued first so those waits
-  // exist; a round whose P2 cannot be issued yet is not reclaimable.
+  // exist; a round whose P2 is not fully issued yet is not reclaimable.
   issue_ready();
-  if (round >= next_round_) return false;
+  if (round >= p2_round_ || round >= p1_round_) return false;
   for (const Pending& pd : pending_) {
     if (pd.round == round) {
       dev_->wait(dev_->compute_stream(), pd.ev);
@@ -294,7 +335,9 @@ bool ReactiveLink::reclaim(int32_t round) {
 
 void ReactiveLink::retire(int32_t r) {
   auto it = rounds_.find(r);
-  if (it == rounds_.end() || !it->second.p2_issued || it->second.open > 0 || !it->second.completed) return;
+  if (it == rounds_.end()) return;
+  const RoundState& s = it->second;
+  if (!s.p2_done || !s.p1_issued || s.open > 0 || !s.completed) return;
   rounds_.erase(it);
   dp_->release_slot(r);
 }
@@ -336,38 +379,39 @@ bool ReactiveLink::poll() {
     put_event(pd.ev);
     {
       auto rs = rounds_.find(pd.round);
-      if (rs != rounds_.end()) --rs->second.open;
+      if (rs != rounds_.end()) {
+        --rs->second.open;
+        if (pd.phase == 1) --rs->second.p1_open;
+      }
     }
     if (pd.phase == 1) {
-      ++stats_.p1_arrivals;
-      for (int32_t k = 0; k < kme_; ++k) {
+      if (pd.chunk < kme_) {
+        ++stats_.p1_arrivals;
         Payload p;
         p.kind = PayloadKind::Landed;
-        p.len = g.chunk_len(me_, k);
+        p.len = g.chunk_len(me_, pd.chunk);
         p.on_host = dev_->is_host();
-        engine_->on_scatter(pd.peer, me_, k, pd.round, p);
+        engine_->on_scatter(pd.peer, me_, pd.chunk, pd.round, p);
       }
-    } else {
+    } else if (pd.count) {
       ++stats_.p2_arrivals;
-      const int32_t kp = g.num_chunks(pd.peer);
-      std::vector<int32_t> counts(pd.counts, pd.counts + kp);
-      if (pd.counts) free_pinned_.push_back(pd.counts);
-      for (int32_t k = 0; k < kp; ++k) {
-        const int32_t w = counts[size_t(k)];
-        if (w <= 0) continue;  // the owner never reduced this chunk
+      const int32_t w = *pd.count;
+      free_counts_.push_back(pd.count);
+      if (w > 0) {  // 0: the owner never reduced this chunk
         Payload p;
         p.kind = PayloadKind::Landed;
-        p.len = g.chunk_len(pd.peer, k);
+        p.len = g.chunk_len(pd.peer, pd.chunk);
         p.on_host = dev_->is_host();
         if (w == 1 && pd.round >= engine_->round()) {
           // Reduced from zero contributions: reads as zeros (a forced reduce of
           // a round whose landing row may already have been reused).
-          dev_->zero(dev_->compute_stream(), dp_->landing_at(pd.round, pd.peer, k), size_t(p.len) * dp_->esize());
+          dev_->zero(dev_->compute_stream(), dp_->landing_at(pd.round, pd.peer, pd.chunk),
+                     size_t(p.len) * dp_->esize());
         }
-        engine_->on_reduce(pd.peer, me_, k, pd.round, w - 1, p);
+        engine_->on_reduce(pd.peer, me_, pd.chunk, pd.round, w - 1, p);
       }
     }
-    if (pd.round < next_round_) retire(pd.round);
+    if (pd.round < p2_round_) retire(pd.round);
   }
   return true;
 }

@@ -5,32 +5,39 @@
 // slowest peer: fast on a healthy node, but the threshold parameters
 // (thReduce / thComplete) only decide *what* is summed, never *when*.
 // The reference's point is the opposite: each ScatterBlock / ReduceBlock is an
-// independent message (W:212-238, W:252-268) and a worker reduces / completes
-// as soon as the threshold number of them arrived (SB:9-13, RB:60-66), so a
-// slow or dead peer does not stall the others.
+// independent message of at most maxChunkSize floats (W:212-238, W:252-268),
+// and a worker reduces a chunk the moment its threshold number of copies
+// arrived and broadcasts it at once (W:177-181, SB:9-13); a round completes
+// when enough reduced chunks arrived (RB:60-66).  A slow or dead peer does
+// not stall the others.
 //
 // MI355X mapping of that message model:
-//   * one HIP stream per peer and one point-to-point RCCL communicator per
-//     pair (rccl_pair_p2p.cpp): transfers to different peers never wait for
-//     each other, and each xGMI link carries its own peer's traffic;
-//   * per (round, peer) two grouped exchanges on that pair's stream:
-//       P1(r): my input slice of block p -> p,  p's slice of my block -> ring
-//       P2(r): my reduced block + wire counts -> p,  p's reduced block -> landing
-//     issued in the same order by both sides of every pair
-//     (P1(0), P2(0), P1(1), P2(1), ...), so matching never depends on timing;
-//   * arrival is an event completing on the pair stream: poll() queries the
-//     in-flight events and hands completed arrivals to the unchanged Engine,
-//     which applies the reference's thresholds, reduces on the compute stream,
-//     completes rounds and runs catch-up -- without waiting for stragglers;
-//   * P2(r) is issued once my block is fully reduced or the round completed
-//     (then unreduced chunks go out with wire count 0 = "not reduced");
+//   * per peer two HIP streams and two point-to-point RCCL communicators
+//     (rccl_p2p.cpp, channel 0 = phase 1, channel 1 = phase 2): transfers to
+//     different peers never wait for each other, each xGMI link carries its
+//     own peer's traffic, and phase-2 chunks never queue behind phase-1 chunks;
+//   * every chunk is its own grouped exchange on its pair channel:
+//       P1(r,k): chunk k of my input slice of block p -> p,
+//                chunk k of p's slice of my block -> ring slot     (channel 0)
+//       P2(r,k): my reduced chunk k + its count -> p,
+//                p's reduced chunk k + count -> landing row        (channel 1)
+//     Both sides of a pair issue P1 in (round, chunk) order at scatter time,
+//     and P2 in (round, chunk) order as chunks get reduced, so matching never
+//     depends on timing;
+//   * arrival is an event completing on the pair stream, per chunk: poll()
+//     hands completed arrivals to the unchanged Engine, which applies the
+//     reference's thresholds, reduces chunk k on the compute stream, completes
+//     rounds and runs catch-up -- without waiting for stragglers;
+//   * P2(r,k) is issued as soon as my chunk k is reduced (its count rides in
+//     the same launch: a 4-byte fill merged into the reduce), or once the
+//     round completed (then unreduced chunks go out with count 0);
 //   * the data plane runs in staged mode (per-round send slots + a landing
 //     row), so transfers still in flight after a round completed never touch
 //     memory the caller owns.  A frozen peer pins one send slot per round; the
 //     pool grows up to `max_slots`, after which the oldest finished round's
 //     slot is reclaimed by a GPU-side wait (the bounded-staleness limit).
 // Counts travel in-band as count+1 (0 = chunk not reduced), copied to pinned
-// host memory behind the receive so the host reads them at poll time.
+// host memory behind each receive so the host reads them at poll time.
 #pragma once
 
 #include <atomic>
@@ -49,6 +56,9 @@ namespace akka {
 struct ReactiveLinkStats {
   int64_t groups = 0, bytes_sent = 0, p1_arrivals = 0, p2_arrivals = 0, unreduced_chunks = 0, polls = 0,
           reclaim_waits = 0, peers_lost = 0, transfers_dropped = 0;
+  // P2 chunks issued while P1 chunks of the same round were still in flight
+  // (the per-chunk pipeline at work)
+  int64_t p2_overlapped = 0;
 };
 
 class ReactiveLink final : public Link {
@@ -58,7 +68,7 @@ class ReactiveLink final : public Link {
   // Creates the per-peer streams and switches the data plane to staged mode.
   void bind(DataPlane* dp);
 
-  void send_scatter(int32_t, int32_t, int32_t, const Payload&) override {}  // whole-block P1 from the staged input
+  void send_scatter(int32_t, int32_t, int32_t, const Payload&) override {}  // P1 chunks come from the staged input
   void send_reduce(int32_t dest, int32_t chunk, int32_t round, int32_t count, const Payload& p) override;
   void on_scattered(int32_t round) override;
   void pump() override;
@@ -71,27 +81,30 @@ class ReactiveLink final : public Link {
   int32_t in_flight() const { return int32_t(pending_.size()); }
   // Block (without spinning) until a transfer may have completed since the
   // last call, or `timeout_us` elapsed.  Uses host notifications queued behind
-  // every group; returns immediately if the device cannot notify.
+  // the groups; returns immediately if the device cannot notify.
   void wait_activity(int64_t timeout_us);
   const ReactiveLinkStats& stats() const { return stats_; }
-  std::vector<StreamH> peer_streams() const { return streams_; }
+  std::vector<StreamH> peer_streams() const { return s1_; }
 
  private:
   struct RoundState {
     bool scattered = false;
-    bool closable = false;  // my block fully reduced, or the round completed
-    std::vector<int32_t> wire;  // [kme] count+1, 0 = not reduced
-    int32_t reduced = 0;
-    int32_t open = 0;  // in-flight transfers of this round
-    bool p2_issued = false;
     bool completed = false;
+    bool p1_issued = false;
+    std::vector<int32_t> wire;    // [kme] count+1, 0 = not reduced
+    std::vector<EventH> ready;    // [kme] compute event after chunk k's reduce + count fill
+    int32_t p2_next = 0;          // first chunk index whose P2 groups are not issued
+    int32_t open = 0;             // in-flight transfers of this round
+    int32_t p1_open = 0;          // of which phase 1
+    bool p2_done = false;         // every P2 chunk issued
   };
   struct Pending {
     int32_t round = 0;
     int32_t peer = 0;
     int32_t phase = 0;
+    int32_t chunk = 0;
     EventH ev = nullptr;
-    int32_t* counts = nullptr;  // pinned, phase 2
+    int32_t* count = nullptr;  // pinned, phase 2
   };
 
   RoundState& st(int32_t r);
@@ -99,30 +112,32 @@ class ReactiveLink final : public Link {
   // issue time and not lost.  (Both sides of a pair must agree, which holds
   // when membership changes at a round boundary: InitWorkers / death.)
   bool exchanges_with(int32_t p) const;
-  std::vector<uint8_t> lost_;  // [N]
   void issue_ready();
   void issue_p1(int32_t r);
-  void issue_p2(int32_t r);
+  // Issue P2 chunks of round r that are ready; true once all are issued.
+  bool issue_p2(int32_t r);
   bool reclaim(int32_t round);
   void retire(int32_t r);
   EventH get_event();
   void put_event(EventH e);
-  int32_t* get_pinned();
+  int32_t* get_count_slot();
+  int32_t chunks_with(int32_t p) const;  // P1/P2 chunk groups per round with peer p
 
   Engine* engine_;
   P2P* p2p_;
   DataPlane* dp_ = nullptr;
   Device* dev_ = nullptr;
   int32_t N_ = 0, me_ = 0, L_ = 0, kme_ = 0, kmax_ = 0, max_slots_ = 16;
-  std::vector<StreamH> streams_;  // [N], null for me
+  std::vector<StreamH> s1_, s2_;  // [N] phase-1 / phase-2 pair streams, null for me
+  std::vector<uint8_t> lost_;     // [N]
   std::map<int32_t, RoundState> rounds_;
-  int32_t next_round_ = 0;
-  bool next_is_p2_ = false;
+  int32_t p1_round_ = 0;  // next round whose P1 is not issued
+  int32_t p2_round_ = 0;  // round whose P2 chunks are being issued
   bool issuing_ = false;
   std::deque<Pending> pending_;
   std::vector<EventH> events_, free_events_;
-  std::vector<int32_t*> pinned_, free_pinned_;
-  int32_t* recv_dev_ = nullptr;    // [L][N][kmax]
+  std::vector<int32_t*> pinned_blocks_, free_counts_;
+  int32_t* recv_dev_ = nullptr;  // [L][N][kmax]
   ReactiveLinkStats stats_;
   // completion notifications (host callbacks from the pair streams)
   struct Notifier {

@@ -5,6 +5,7 @@
 #include <deque>
 #include <map>
 #include <set>
+#include <tuple>
 #include <sstream>
 
 #include "p2p.h"
@@ -24,8 +25,8 @@ class SimHub {
  public:
   explicit SimHub(int32_t n) : n_(n) {}
   int32_t n_;
-  // fifo[src][dst]: sends posted by src to dst not yet consumed, in order.
-  std::map<std::pair<int32_t, int32_t>, std::deque<std::shared_ptr<SimSend>>> fifo;
+  // fifo[src, dst, channel]: sends posted by src to dst not yet consumed, in order.
+  std::map<std::tuple<int32_t, int32_t, int32_t>, std::deque<std::shared_ptr<SimSend>>> fifo;
   // (me, peer): `me` aborted its transfers with `peer` (abort_peer).
   std::set<std::pair<int32_t, int32_t>> aborted;
   int64_t bytes = 0;
@@ -70,7 +71,7 @@ class SimP2P final : public P2P {
         for (const auto& op : ops) {
           if (!op.send) continue;
           auto snd = std::make_shared<SimSend>(SimSend{op.buf, op.bytes});
-          hub->fifo[{me, op.peer}].push_back(snd);
+          hub->fifo[{me, op.peer, op.channel}].push_back(snd);
           st->sends.push_back(snd);
         }
         st->recv_done.assign(ops.size(), false);
@@ -95,12 +96,13 @@ class SimP2P final : public P2P {
         // Earlier recvs from the same peer in this group must match first.
         bool blocked = false;
         for (size_t j = 0; j < i; ++j)
-          if (!ops[j].send && ops[j].peer == op.peer && !st->recv_done[j]) blocked = true;
+          if (!ops[j].send && ops[j].peer == op.peer && ops[j].channel == op.channel && !st->recv_done[j])
+            blocked = true;
         if (blocked) {
           all = false;
           continue;
         }
-        auto& q = hub->fifo[{op.peer, me}];
+        auto& q = hub->fifo[{op.peer, me, op.channel}];
         if (q.empty()) {
           all = false;
           continue;
@@ -163,7 +165,9 @@ void sim_run(const std::shared_ptr<SimHub>& hub, const std::vector<Device*>& dev
       std::ostringstream os;
       os << "sim p2p: deadlock - no rank can progress; pending sends per pair:";
       for (auto& kv : hub->fifo)
-        if (!kv.second.empty()) os << " " << kv.first.first << "->" << kv.first.second << ":" << kv.second.size();
+        if (!kv.second.empty())
+          os << " " << std::get<0>(kv.first) << "->" << std::get<1>(kv.first) << "/c" << std::get<2>(kv.first) << ":"
+             << kv.second.size();
       for (size_t i = 0; i < devices.size(); ++i)
         if (!host_device_idle(devices[i])) os << " [rank " << i << " blocked]";
       throw AkkaError(os.str());

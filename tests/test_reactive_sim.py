@@ -410,7 +410,31 @@ def test_partial_membership_islands_reactive():
 
     ts._islands(cl, n, S, C, 0.5, run_round, chunk_order=False)
     # round 0: phase 1 from the one island peer; round 1: from all three
-    # (whole-block P1/P2 per pair -- which blocks make the 50% is timing)
+    # (4 chunks per block, one arrival per chunk and peer; which chunks make
+    # the 50% is timing)
+    k = Geometry(S, n, C).num_chunks(0)
     for w in cl.workers:
         st = w.state()["link"]
-        assert st["p1_arrivals"] == 1 + 3 and st["p2_arrivals"] == 1 + 3, st
+        assert st["p1_arrivals"] == k * (1 + 3) and st["p2_arrivals"] == k * (1 + 3), st
+
+
+def test_chunk_granular_phase2_overlaps_phase1():
+    """maxChunkSize is the transfer unit (W:218-232): every chunk is its own
+    P1 / P2 exchange, and a chunk is broadcast the moment it is reduced
+    (W:177-181) -- chunk 0's phase-2 groups go out while later phase-1 chunks
+    of the same round are still in flight (phase 2 has its own pair channel,
+    so it never queues behind them)."""
+    n, S, C = 3, 3 * 8 * 16, 16  # 8 chunks per block
+    cl = ReactiveSimCluster(n, S, C, max_lag=1)
+    xs = [torch.randint(-8, 9, (S,), generator=torch.Generator().manual_seed(i)).float() for i in range(n)]
+    for i in range(n):
+        cl.start(i, xs[i])
+    cl.run(lambda: all(cl.done(i, 0) for i in range(n)))
+    cl.settle()
+    want = torch.stack(xs).sum(0)
+    for i in range(n):
+        assert torch.equal(cl.outputs[i][0].data, want)
+        st = cl.workers[i].state()["link"]
+        assert st["p2_overlapped"] > 0, st
+        assert st["p1_arrivals"] == (n - 1) * 8 and st["p2_arrivals"] == (n - 1) * 8
+    cl.drain()
