@@ -29,8 +29,7 @@ process).  ``None`` (default): each rank paces itself.
 (csrc/transport/reactive_link.h): one stream + one RCCL pair communicator per
 peer, arrivals polled from events, so with thresholds < 1 a rank completes
 rounds without waiting for slow peers (the reference's semantics).  It runs
-2N streams per process (two per peer: phase 1 and phase 2): set
-``GPU_MAX_HW_QUEUES`` (<= 32) to at least 2N+4
+N+2 streams per process: set ``GPU_MAX_HW_QUEUES`` (<= 32) to at least N+4
 before the first HIP call, or parked streams share hardware queues.
 """
 from __future__ import annotations
@@ -166,7 +165,7 @@ class ThresholdAllreduce:
                 else torch.device("cpu")
         self.device = torch.device(device)
         if transport == "reactive" and self.world_size > 1 and self.device.type == "cuda":
-            need = min(32, 2 * self.world_size + 4)
+            need = min(32, self.world_size + 4)
             have = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
             if have < need:
                 raise RuntimeError(f"reactive transport at N={self.world_size} needs GPU_MAX_HW_QUEUES >= {need} "

@@ -271,8 +271,8 @@ def main() -> int:
     elif int(os.environ.get("WORLD_SIZE", "1")) > 1:
         # comm + compute + caller (+ RCCL's own) streams each on their own
         # hardware queue, so chunk reduces never serialise behind transfers;
-        # config 4 (reactive transport) needs two more per peer: 2N + 4
-        need = min(32, max(8, 2 * int(os.environ["WORLD_SIZE"]) + 4))
+        # config 4 (reactive transport) needs one more per peer: N + 4
+        need = min(32, max(8, int(os.environ["WORLD_SIZE"]) + 4))
         if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < need:
             os.environ["GPU_MAX_HW_QUEUES"] = str(need)
     rank = int(os.environ.get("RANK", "0"))

@@ -205,14 +205,17 @@ class RcclPairP2P final : public P2P {
     const int32_t peer = ops.front().peer;
     const int32_t ch = ops.front().channel;
     AKKA_CHECK(peer >= 0 && peer < n_ && peer != rank_, "pair group: bad peer");
-    AKKA_CHECK(ch >= 0 && ch < kChannels, "pair group: bad channel");
-    ncclComm_t c = pair_[ch][size_t(peer)];
+    AKKA_CHECK(ch >= 0, "pair group: bad channel");
+    // The reactive link issues both phases of a pair on ONE stream in one
+    // total order both sides share, so one communicator per pair serves both
+    // channels (fewer RCCL communicators to build at N = 8).
+    ncclComm_t c = pair_[std::min(ch, kChannels - 1)][size_t(peer)];
     AKKA_CHECK(c, "pair group to peer " + std::to_string(peer) + " after its communicator was aborted");
     const int32_t prank = peer < rank_ ? 0 : 1;  // split key = global rank
     hipStream_t s = static_cast<hipStream_t>(stream);
     AKKA_NCCL(ncclGroupStart());
     for (const auto& op : ops) {
-      AKKA_CHECK(op.peer == peer && op.channel == ch, "pair group holds ops to more than one peer / channel");
+      AKKA_CHECK(op.peer == peer, "pair group holds ops to more than one peer");
       if (op.send) AKKA_NCCL(ncclSend(op.buf, op.bytes, ncclUint8, prank, c, s));
       else AKKA_NCCL(ncclRecv(op.buf, op.bytes, ncclUint8, prank, c, s));
     }
@@ -251,7 +254,7 @@ class RcclPairP2P final : public P2P {
   }
 
  private:
-  static constexpr int32_t kChannels = 2;
+  static constexpr int32_t kChannels = 1;
   int32_t rank_, n_;
   ncclComm_t global_ = nullptr;
   std::vector<ncclComm_t> pair_[kChannels];  // [channel][peer]

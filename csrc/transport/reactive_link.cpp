@@ -23,14 +23,14 @@ ReactiveLink::~ReactiveLink() {
     for (size_t p = 0; p < s1_.size(); ++p) {
       if (lost_[p]) continue;
       if (s1_[p]) dev_->sync_stream(s1_[p]);
-      if (s2_[p]) dev_->sync_stream(s2_[p]);
+      if (s2_[p] && s2_[p] != s1_[p]) dev_->sync_stream(s2_[p]);
     }
   } catch (...) {
   }
   for (size_t p = 0; p < s1_.size(); ++p) {
     if (lost_[p]) continue;
     if (s1_[p]) dev_->destroy_stream(s1_[p]);
-    if (s2_[p]) dev_->destroy_stream(s2_[p]);
+    if (s2_[p] && s2_[p] != s1_[p]) dev_->destroy_stream(s2_[p]);
   }
   for (EventH e : events_) dev_->destroy_event(e);
   for (int32_t* p : pinned_blocks_) dev_->release_pinned(p);
@@ -52,11 +52,15 @@ void ReactiveLink::bind(DataPlane* dp) {
   s1_.assign(size_t(N_), nullptr);
   s2_.assign(size_t(N_), nullptr);
   lost_.assign(size_t(N_), 0);
+  // One stream per peer for both phases: a second stream per peer doubles the
+  // hardware queues a process needs, and past ~16 mapped queues per device
+  // the scheduler time-slices them (measured on the 3-rank loopback: ~1.5 ms
+  // per parked group).  Phase-2 chunks therefore run behind the pair's
+  // phase-1 chunks of the same round in stream order (they are still issued,
+  // reduced and delivered per chunk); the two phases keep separate matching
+  // channels.
   for (int32_t p = 0; p < N_; ++p)
-    if (p != me_) {
-      s1_[size_t(p)] = dev_->create_stream();
-      s2_[size_t(p)] = dev_->create_stream();
-    }
+    if (p != me_) s1_[size_t(p)] = s2_[size_t(p)] = dev_->create_stream();
   recv_dev_ = static_cast<int32_t*>(dev_->alloc(size_t(L_) * N_ * kmax_ * sizeof(int32_t)));
   dp->enable_staging(std::max(max_slots_, L_ + 1), [this](int32_t round) { return reclaim(round); });
 }
@@ -135,15 +139,16 @@ void ReactiveLink::issue_ready() {
   if (issuing_ || !dp_) return;
   issuing_ = true;
   try {
-    // Phase 1 in round order, each round as soon as it was scattered.
+    // Per pair stream: P1(r) chunks, then P2(r) chunks as they get ready,
+    // then P1(r+1) ...  -- one total order both sides of every pair share,
+    // so the pair's stream never waits on a group its peer queued later.
     for (;;) {
-      auto it = rounds_.find(p1_round_);
-      if (it == rounds_.end() || !it->second.scattered) break;
-      issue_p1(p1_round_);
-      ++p1_round_;
-    }
-    // Phase 2 in (round, chunk) order, each chunk as soon as it is ready.
-    for (;;) {
+      if (p1_round_ == p2_round_) {
+        auto it = rounds_.find(p1_round_);
+        if (it == rounds_.end() || !it->second.scattered) break;
+        issue_p1(p1_round_);
+        ++p1_round_;
+      }
       if (!rounds_.count(p2_round_)) break;
       if (!issue_p2(p2_round_)) break;
       ++p2_round_;
@@ -224,7 +229,11 @@ void ReactiveLink::issue_p1(int32_t r) {
       pd.chunk = k;
       pd.ev = get_event();
       dev_->record(pd.ev, ps);
-      arm(ps);
+      // one host notification per pair and round (the last chunk): a host
+      // callback blocks its stream until it ran, and hundreds per round
+      // serialise on the runtime's callback thread; earlier chunks are
+      // picked up by the waiter's periodic poll
+      if (k + 1 == chunks_with(p)) arm(ps);
       pending_.push_back(pd);
       ++s.open;
       ++s.p1_open;
@@ -298,7 +307,7 @@ bool ReactiveLink::issue_p2(int32_t r) {
       }
       pd.ev = get_event();
       dev_->record(pd.ev, ps);
-      arm(ps);
+      if (k + 1 == chunks_with(p)) arm(ps);  // see issue_p1
       pending_.push_back(pd);
       ++s.open;
       issued = true;

@@ -12,18 +12,18 @@
 // not stall the others.
 //
 // MI355X mapping of that message model:
-//   * per peer two HIP streams and two point-to-point RCCL communicators
-//     (rccl_p2p.cpp, channel 0 = phase 1, channel 1 = phase 2): transfers to
-//     different peers never wait for each other, each xGMI link carries its
-//     own peer's traffic, and phase-2 chunks never queue behind phase-1 chunks;
+//   * per peer one HIP stream and a point-to-point RCCL communicator
+//     (rccl_p2p.cpp): transfers to different peers never wait for each
+//     other, each xGMI link carries its own peer's traffic;
 //   * every chunk is its own grouped exchange on its pair channel:
 //       P1(r,k): chunk k of my input slice of block p -> p,
 //                chunk k of p's slice of my block -> ring slot     (channel 0)
 //       P2(r,k): my reduced chunk k + its count -> p,
 //                p's reduced chunk k + count -> landing row        (channel 1)
-//     Both sides of a pair issue P1 in (round, chunk) order at scatter time,
-//     and P2 in (round, chunk) order as chunks get reduced, so matching never
-//     depends on timing;
+//     Both sides of a pair issue the same total order -- P1(r, all chunks)
+//     at scatter time, then P2(r, k) in chunk order as chunks get reduced,
+//     then P1(r+1) ... -- so matching never depends on timing (the two phases
+//     also use separate matching channels);
 //   * arrival is an event completing on the pair stream, per chunk: poll()
 //     hands completed arrivals to the unchanged Engine, which applies the
 //     reference's thresholds, reduces chunk k on the compute stream, completes
@@ -128,10 +128,10 @@ class ReactiveLink final : public Link {
   DataPlane* dp_ = nullptr;
   Device* dev_ = nullptr;
   int32_t N_ = 0, me_ = 0, L_ = 0, kme_ = 0, kmax_ = 0, max_slots_ = 16;
-  std::vector<StreamH> s1_, s2_;  // [N] phase-1 / phase-2 pair streams, null for me
+  std::vector<StreamH> s1_, s2_;  // [N] phase-1 / phase-2 pair streams (one stream per peer today), null for me
   std::vector<uint8_t> lost_;     // [N]
   std::map<int32_t, RoundState> rounds_;
-  int32_t p1_round_ = 0;  // next round whose P1 is not issued
+  int32_t p1_round_ = 0;  // next round whose P1 is not issued (== p2_round_ or p2_round_ + 1)
   int32_t p2_round_ = 0;  // round whose P2 chunks are being issued
   bool issuing_ = false;
   std::deque<Pending> pending_;
