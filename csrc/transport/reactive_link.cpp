@@ -2,6 +2,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdlib>
 #include <cstring>
 
 namespace akka {
@@ -9,7 +10,7 @@ namespace akka {
 namespace {
 constexpr int32_t kPhase1 = 0;  // pair channel of phase 1 (scatter)
 constexpr int32_t kPhase2 = 1;  // pair channel of phase 2 (reduced chunks + counts)
-constexpr int32_t kCountBlock = 1024;  // pinned count slots allocated at a time
+constexpr int32_t kCountRows = 64;  // pinned count rows allocated at a time
 }  // namespace
 
 ReactiveLink::ReactiveLink(Engine* engine, P2P* p2p, int32_t max_slots)
@@ -61,6 +62,15 @@ void ReactiveLink::bind(DataPlane* dp) {
   // channels.
   for (int32_t p = 0; p < N_; ++p)
     if (p != me_) s1_[size_t(p)] = s2_[size_t(p)] = dev_->create_stream();
+  // Transfer groups: gm_ consecutive chunks per exchange, so that a group
+  // carries at least AKKA_REACTIVE_GROUP_BYTES (default 16 MiB) -- every chunk
+  // is still received, reduced and delivered to the engine on its own; only
+  // the number of p2p groups (host enqueue + arrival polling per group) drops
+  // for small maxChunkSize.  A function of the geometry: identical on every rank.
+  int64_t min_bytes = int64_t(16) << 20;
+  if (const char* v = std::getenv("AKKA_REACTIVE_GROUP_BYTES")) min_bytes = std::max<int64_t>(0, std::atoll(v));
+  const int64_t cbytes = std::max<int64_t>(1, g.C * int64_t(dp->esize()));
+  gm_ = int32_t(std::clamp<int64_t>((min_bytes + cbytes - 1) / cbytes, 1, std::max(kmax_, 1)));
   recv_dev_ = static_cast<int32_t*>(dev_->alloc(size_t(L_) * N_ * kmax_ * sizeof(int32_t)));
   dp->enable_staging(std::max(max_slots_, L_ + 1), [this](int32_t round) { return reclaim(round); });
 }
@@ -72,6 +82,13 @@ ReactiveLink::RoundState& ReactiveLink::st(int32_t r) {
   s.wire.assign(size_t(std::max(kme_, 1)), 0);
   s.ready.assign(size_t(std::max(kme_, 1)), nullptr);
   return s;
+}
+
+int64_t ReactiveLink::span_len(int32_t block, int32_t k0, int32_t k1) const {
+  // elements of chunks [k0, k1) of `block` (consecutive chunks are contiguous)
+  const Geometry& g = dp_->geometry();
+  if (k1 <= k0) return 0;
+  return g.chunk_start(block, k1 - 1) + g.chunk_len(block, k1 - 1) - g.chunk_start(block, k0);
 }
 
 int32_t ReactiveLink::chunks_with(int32_t p) const {
@@ -91,10 +108,11 @@ EventH ReactiveLink::get_event() {
 void ReactiveLink::put_event(EventH e) { free_events_.push_back(e); }
 
 int32_t* ReactiveLink::get_count_slot() {
+  // a pinned row of gm_ counts (one per chunk of a transfer group)
   if (free_counts_.empty()) {
-    int32_t* b = static_cast<int32_t*>(dev_->alloc_pinned(size_t(kCountBlock) * sizeof(int32_t)));
+    int32_t* b = static_cast<int32_t*>(dev_->alloc_pinned(size_t(kCountRows) * size_t(gm_) * sizeof(int32_t)));
     pinned_blocks_.push_back(b);
-    for (int32_t i = kCountBlock - 1; i >= 0; --i) free_counts_.push_back(b + i);
+    for (int32_t i = kCountRows - 1; i >= 0; --i) free_counts_.push_back(b + size_t(i) * size_t(gm_));
   }
   int32_t* p = free_counts_.back();
   free_counts_.pop_back();
@@ -212,28 +230,33 @@ void ReactiveLink::issue_p1(int32_t r) {
     dev_->wait(ps, rel);
     const int32_t kp = g.num_chunks(p);
     const char* in = static_cast<const char*>(dp_->staged_input(r, p));
-    for (int32_t k = 0; k < chunks_with(p); ++k) {
+    const int32_t kall = chunks_with(p);
+    for (int32_t k0 = 0; k0 < kall; k0 += gm_) {
+      const int32_t k1 = std::min(k0 + gm_, kall);
       ops.clear();
-      if (k < kp) {
-        ops.push_back({true, p, const_cast<char*>(in) + size_t(g.chunk_start(p, k)) * es,
-                       size_t(g.chunk_len(p, k)) * es, kPhase1});
-        stats_.bytes_sent += g.chunk_len(p, k) * int64_t(es);
+      if (k0 < kp) {  // chunks [k0, min(k1, kp)) of block p: contiguous in the staged input
+        const int64_t len = span_len(p, k0, std::min(k1, kp));
+        ops.push_back({true, p, const_cast<char*>(in) + size_t(g.chunk_start(p, k0)) * es, size_t(len) * es, kPhase1});
+        stats_.bytes_sent += len * int64_t(es);
       }
-      if (k < kme_) ops.push_back({false, p, dp_->scatter_slot(r, p, k), size_t(g.chunk_len(me_, k)) * es, kPhase1});
+      if (k0 < kme_)  // p's chunks [k0, min(k1, kme)) of my block: contiguous in its ring slot
+        ops.push_back({false, p, dp_->scatter_slot(r, p, k0), size_t(span_len(me_, k0, std::min(k1, kme_))) * es,
+                       kPhase1});
       p2p_->group(ps, ops);
       ++stats_.groups;
       Pending pd;
       pd.round = r;
       pd.peer = p;
       pd.phase = 1;
-      pd.chunk = k;
+      pd.chunk = k0;
+      pd.chunk_end = k1;
       pd.ev = get_event();
       dev_->record(pd.ev, ps);
-      // one host notification per pair and round (the last chunk): a host
-      // callback blocks its stream until it ran, and hundreds per round
-      // serialise on the runtime's callback thread; earlier chunks are
+      // one host notification per pair and round (the last group): a host
+      // callback blocks its stream until it ran, and many per round
+      // serialise on the runtime's callback thread; earlier groups are
       // picked up by the waiter's periodic poll
-      if (k + 1 == chunks_with(p)) arm(ps);
+      if (k1 == kall) arm(ps);
       pending_.push_back(pd);
       ++s.open;
       ++s.p1_open;
@@ -265,34 +288,46 @@ bool ReactiveLink::issue_p2(int32_t r) {
   }
   std::vector<P2POp> ops;
   while (s.p2_next < kmax_) {
-    const int32_t k = s.p2_next;
-    if (k < kme_) {
-      if (s.wire[size_t(k)] == 0) {
-        if (!s.completed) break;  // not reduced yet: later chunks wait too (per-pair order)
-        // round completed before this chunk reached its threshold: count 0
-        dev_->fill_i32(cs, dp_->wire_dev(r) + k, 0, 1);
-        s.ready[size_t(k)] = get_event();
-        dev_->record(s.ready[size_t(k)], cs);
-        ++stats_.unreduced_chunks;
-      }
+    const int32_t k0 = s.p2_next;
+    const int32_t k1 = std::min(k0 + gm_, kmax_);
+    // the group goes out once every chunk of mine in it is reduced (or the
+    // round completed: the rest then carry count 0) -- fixed group bounds,
+    // so both sides of a pair build the same groups
+    const int32_t m1 = std::min(k1, kme_);
+    bool ready = true;
+    for (int32_t k = k0; k < m1 && ready; ++k) ready = s.wire[size_t(k)] != 0 || s.completed;
+    if (!ready) break;
+    EventH rdy = nullptr;
+    if (k0 < kme_) {
+      for (int32_t k = k0; k < m1; ++k)
+        if (s.wire[size_t(k)] == 0) {  // round completed before this chunk reached its threshold
+          dev_->fill_i32(cs, dp_->wire_dev(r) + k, 0, 1);
+          ++stats_.unreduced_chunks;
+        }
+      // everything the group's sends read (reduces, count fills) is on the
+      // compute stream before this point
+      rdy = get_event();
+      dev_->record(rdy, cs);
     }
     bool issued = false;
     for (int32_t i = 1; i < N_; ++i) {
       const int32_t p = (me_ + i) % N_;
-      if (!exchanges_with(p) || k >= chunks_with(p)) continue;
+      if (!exchanges_with(p) || k0 >= chunks_with(p)) continue;
       StreamH ps = s2_[size_t(p)];
       const int32_t kp = g.num_chunks(p);
       int32_t* rdev = recv_dev_ + (row * size_t(N_) + size_t(p)) * size_t(kmax_);
       ops.clear();
-      if (k < kme_) {
-        dev_->wait(ps, s.ready[size_t(k)]);
-        ops.push_back({true, p, dp_->mine_at(r, k), size_t(g.chunk_len(me_, k)) * es, kPhase2});
-        ops.push_back({true, p, dp_->wire_dev(r) + k, sizeof(int32_t), kPhase2});
-        stats_.bytes_sent += g.chunk_len(me_, k) * int64_t(es) + int64_t(sizeof(int32_t));
+      if (k0 < kme_) {
+        dev_->wait(ps, rdy);
+        const int64_t len = span_len(me_, k0, m1);
+        ops.push_back({true, p, dp_->mine_at(r, k0), size_t(len) * es, kPhase2});
+        ops.push_back({true, p, dp_->wire_dev(r) + k0, size_t(m1 - k0) * sizeof(int32_t), kPhase2});
+        stats_.bytes_sent += len * int64_t(es) + int64_t(m1 - k0) * int64_t(sizeof(int32_t));
       }
-      if (k < kp) {
-        ops.push_back({false, p, dp_->landing_at(r, p, k), size_t(g.chunk_len(p, k)) * es, kPhase2});
-        ops.push_back({false, p, rdev + k, sizeof(int32_t), kPhase2});
+      const int32_t p1 = std::min(k1, kp);
+      if (k0 < kp) {
+        ops.push_back({false, p, dp_->landing_at(r, p, k0), size_t(span_len(p, k0, p1)) * es, kPhase2});
+        ops.push_back({false, p, rdev + k0, size_t(p1 - k0) * sizeof(int32_t), kPhase2});
       }
       p2p_->group(ps, ops);
       ++stats_.groups;
@@ -300,24 +335,27 @@ bool ReactiveLink::issue_p2(int32_t r) {
       pd.round = r;
       pd.peer = p;
       pd.phase = 2;
-      pd.chunk = k;
-      if (k < kp) {
+      pd.chunk = k0;
+      pd.chunk_end = k1;
+      if (k0 < kp) {
         pd.count = get_count_slot();
-        dev_->copy(ps, pd.count, rdev + k, sizeof(int32_t), CopyKind::DeviceToHost);
+        dev_->copy(ps, pd.count, rdev + k0, size_t(p1 - k0) * sizeof(int32_t), CopyKind::DeviceToHost);
       }
       pd.ev = get_event();
       dev_->record(pd.ev, ps);
-      if (k + 1 == chunks_with(p)) arm(ps);  // see issue_p1
+      if (k1 >= chunks_with(p)) arm(ps);  // see issue_p1
       pending_.push_back(pd);
       ++s.open;
       issued = true;
     }
     if (issued && s.p1_open > 0) ++stats_.p2_overlapped;
-    if (k < kme_) {
-      put_event(s.ready[size_t(k)]);  // the waits above captured its record
-      s.ready[size_t(k)] = nullptr;
-    }
-    ++s.p2_next;
+    if (rdy) put_event(rdy);  // the waits above captured its record
+    for (int32_t k = k0; k < m1; ++k)
+      if (s.ready[size_t(k)]) {
+        put_event(s.ready[size_t(k)]);
+        s.ready[size_t(k)] = nullptr;
+      }
+    s.p2_next = k1;
   }
   if (s.p2_next < kmax_) return false;
   s.p2_done = true;
@@ -394,30 +432,32 @@ bool ReactiveLink::poll() {
       }
     }
     if (pd.phase == 1) {
-      if (pd.chunk < kme_) {
+      for (int32_t k = pd.chunk; k < std::min(pd.chunk_end, kme_); ++k) {
         ++stats_.p1_arrivals;
         Payload p;
         p.kind = PayloadKind::Landed;
-        p.len = g.chunk_len(me_, pd.chunk);
+        p.len = g.chunk_len(me_, k);
         p.on_host = dev_->is_host();
-        engine_->on_scatter(pd.peer, me_, pd.chunk, pd.round, p);
+        engine_->on_scatter(pd.peer, me_, k, pd.round, p);
       }
     } else if (pd.count) {
-      ++stats_.p2_arrivals;
-      const int32_t w = *pd.count;
+      const int32_t kp = g.num_chunks(pd.peer);
+      std::vector<int32_t> w(pd.count, pd.count + (std::min(pd.chunk_end, kp) - pd.chunk));
       free_counts_.push_back(pd.count);
-      if (w > 0) {  // 0: the owner never reduced this chunk
+      for (int32_t k = pd.chunk; k < std::min(pd.chunk_end, kp); ++k) {
+        ++stats_.p2_arrivals;
+        const int32_t wk = w[size_t(k - pd.chunk)];
+        if (wk <= 0) continue;  // 0: the owner never reduced this chunk
         Payload p;
         p.kind = PayloadKind::Landed;
-        p.len = g.chunk_len(pd.peer, pd.chunk);
+        p.len = g.chunk_len(pd.peer, k);
         p.on_host = dev_->is_host();
-        if (w == 1 && pd.round >= engine_->round()) {
+        if (wk == 1 && pd.round >= engine_->round()) {
           // Reduced from zero contributions: reads as zeros (a forced reduce of
           // a round whose landing row may already have been reused).
-          dev_->zero(dev_->compute_stream(), dp_->landing_at(pd.round, pd.peer, pd.chunk),
-                     size_t(p.len) * dp_->esize());
+          dev_->zero(dev_->compute_stream(), dp_->landing_at(pd.round, pd.peer, k), size_t(p.len) * dp_->esize());
         }
-        engine_->on_reduce(pd.peer, me_, pd.chunk, pd.round, w - 1, p);
+        engine_->on_reduce(pd.peer, me_, k, pd.round, wk - 1, p);
       }
     }
     if (pd.round < p2_round_) retire(pd.round);

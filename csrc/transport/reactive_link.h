@@ -15,11 +15,14 @@
 //   * per peer one HIP stream and a point-to-point RCCL communicator
 //     (rccl_p2p.cpp): transfers to different peers never wait for each
 //     other, each xGMI link carries its own peer's traffic;
-//   * every chunk is its own grouped exchange on its pair channel:
-//       P1(r,k): chunk k of my input slice of block p -> p,
-//                chunk k of p's slice of my block -> ring slot     (channel 0)
-//       P2(r,k): my reduced chunk k + its count -> p,
-//                p's reduced chunk k + count -> landing row        (channel 1)
+//   * chunks move in transfer groups of gm consecutive chunks (gm = 1 when a
+//     chunk is >= 16 MiB; small maxChunkSize is batched so a group carries
+//     >= 16 MiB -- fixed bounds, the same on every rank):
+//       P1(r,g): chunks of group g of my input slice of block p -> p,
+//                those of p's slice of my block -> ring slot       (channel 0)
+//       P2(r,g): my reduced chunks of group g + their counts -> p,
+//                p's reduced chunks + counts -> landing row        (channel 1)
+//     and every chunk is still delivered, reduced and counted on its own;
 //     Both sides of a pair issue the same total order -- P1(r, all chunks)
 //     at scatter time, then P2(r, k) in chunk order as chunks get reduced,
 //     then P1(r+1) ... -- so matching never depends on timing (the two phases
@@ -28,9 +31,9 @@
 //     hands completed arrivals to the unchanged Engine, which applies the
 //     reference's thresholds, reduces chunk k on the compute stream, completes
 //     rounds and runs catch-up -- without waiting for stragglers;
-//   * P2(r,k) is issued as soon as my chunk k is reduced (its count rides in
-//     the same launch: a 4-byte fill merged into the reduce), or once the
-//     round completed (then unreduced chunks go out with count 0);
+//   * P2(r,g) is issued as soon as my chunks of group g are reduced (each
+//     count rides in its reduce launch: a 4-byte fill merged into it), or once
+//     the round completed (then unreduced chunks go out with count 0);
 //   * the data plane runs in staged mode (per-round send slots + a landing
 //     row), so transfers still in flight after a round completed never touch
 //     memory the caller owns.  A frozen peer pins one send slot per round; the
@@ -102,9 +105,10 @@ class ReactiveLink final : public Link {
     int32_t round = 0;
     int32_t peer = 0;
     int32_t phase = 0;
-    int32_t chunk = 0;
+    int32_t chunk = 0;      // first chunk of the group
+    int32_t chunk_end = 0;  // one past its last chunk
     EventH ev = nullptr;
-    int32_t* count = nullptr;  // pinned, phase 2
+    int32_t* count = nullptr;  // pinned row, phase 2
   };
 
   RoundState& st(int32_t r);
@@ -121,7 +125,9 @@ class ReactiveLink final : public Link {
   EventH get_event();
   void put_event(EventH e);
   int32_t* get_count_slot();
-  int32_t chunks_with(int32_t p) const;  // P1/P2 chunk groups per round with peer p
+  int32_t chunks_with(int32_t p) const;  // chunk indices exchanged per round with peer p
+  int64_t span_len(int32_t block, int32_t k0, int32_t k1) const;
+  int32_t gm_ = 1;  // chunks per transfer group
 
   Engine* engine_;
   P2P* p2p_;

@@ -418,12 +418,13 @@ def test_partial_membership_islands_reactive():
         assert st["p1_arrivals"] == k * (1 + 3) and st["p2_arrivals"] == k * (1 + 3), st
 
 
-def test_chunk_granular_phase2_overlaps_phase1():
+def test_chunk_granular_phase2_overlaps_phase1(monkeypatch):
     """maxChunkSize is the transfer unit (W:218-232): every chunk is its own
     P1 / P2 exchange, and a chunk is broadcast the moment it is reduced
     (W:177-181) -- chunk 0's phase-2 groups go out while later phase-1 chunks
     of the same round are still in flight (phase 2 has its own pair channel,
     so it never queues behind them)."""
+    monkeypatch.setenv("AKKA_REACTIVE_GROUP_BYTES", "0")  # one chunk per transfer group
     n, S, C = 3, 3 * 8 * 16, 16  # 8 chunks per block
     cl = ReactiveSimCluster(n, S, C, max_lag=1)
     xs = [torch.randint(-8, 9, (S,), generator=torch.Generator().manual_seed(i)).float() for i in range(n)]
@@ -437,4 +438,25 @@ def test_chunk_granular_phase2_overlaps_phase1():
         st = cl.workers[i].state()["link"]
         assert st["p2_overlapped"] > 0, st
         assert st["p1_arrivals"] == (n - 1) * 8 and st["p2_arrivals"] == (n - 1) * 8
+    cl.drain()
+
+
+@pytest.mark.parametrize("group_bytes", ["0", "128", "1000000"])
+@pytest.mark.parametrize("th", [1.0, 0.67])
+def test_transfer_groups_any_size(group_bytes, th, monkeypatch):
+    """Transfer groups of 1, 2 and all chunks (fixed bounds from the
+    geometry): same sums / contributor counts, every chunk delivered once."""
+    monkeypatch.setenv("AKKA_REACTIVE_GROUP_BYTES", group_bytes)
+    n, S, C = 3, 3 * 7 * 16 + 5, 16  # 7-8 chunks per block, short last chunk
+    cl = ReactiveSimCluster(n, S, C, th_reduce=th, th_complete=th, max_lag=1)
+    for r in range(3):
+        for i in range(n):
+            cl.start(i, _x(i, S))
+        cl.run(lambda: all(cl.done(i, r) for i in range(n)))
+    cl.settle()
+    for i in range(n):
+        for r in range(3):
+            mask = _check_masks(cl.outputs[i][r], S, n)
+            if th == 1.0:
+                assert bool((mask == (1 << n) - 1).all())
     cl.drain()
