@@ -74,6 +74,7 @@ def test_full_pacing_waits_for_every_rank():
     rounds, nap = 4, 0.3
     res = _run(1.0, rounds, nap)
     for rank, elapsed, waits, _ in res[:3]:
-        # round r+1 starts only after the sleeper completed round r
-        assert elapsed > nap * (rounds - 1), (rank, elapsed)
+        # round r+1 starts only after the sleeper completed round r (the
+        # ranks' clocks start a little apart: 20% slack)
+        assert elapsed > 0.8 * nap * (rounds - 1), (rank, elapsed)
         assert waits >= rounds - 2
