@@ -195,6 +195,10 @@ class AllreduceWorker:
         if rccl and self.transport_spec is None:
             self.transport_spec = ("rccl", tinfo["uid"], int(m.destId), int(m.workerNum),
                                    list(tinfo.get("members") or []))
+        elif tinfo and tinfo.get("kind") in ("loopback", "loopback_pair", "sim") and self.transport_spec is None:
+            # in-process data planes handed out by the control plane (tests /
+            # single-process clusters): the hub is shared by every worker
+            self.transport_spec = (tinfo["kind"], tinfo["hub"], int(m.destId))
         first = self._core.init(int(m.destId), int(m.workerNum), float(m.thReduce), float(m.thComplete),
                                 int(m.maxLag), int(m.dataSize), int(m.maxChunkSize), peers)
         self.peers = dict(m.workers)
