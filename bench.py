@@ -271,8 +271,12 @@ def main() -> int:
     elif int(os.environ.get("WORLD_SIZE", "1")) > 1:
         # comm + compute + caller (+ RCCL's own) streams each on their own
         # hardware queue, so chunk reduces never serialise behind transfers;
-        # config 4 (reactive transport) needs one more per peer: N + 4
-        need = min(32, max(8, int(os.environ["WORLD_SIZE"]) + 4))
+        # config 4 (reactive transport, run first among the extras) adds one
+        # stream per peer + comm + compute on top of the headline worker's two,
+        # torch's default stream and the comparator's RCCL stream: N + 8 keeps
+        # every stream on its own hardware queue (a stream parked on the
+        # straggler must not hold up a reduce that shares its queue)
+        need = min(32, max(8, int(os.environ["WORLD_SIZE"]) + 8))
         if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < need:
             os.environ["GPU_MAX_HW_QUEUES"] = str(need)
     rank = int(os.environ.get("RANK", "0"))
