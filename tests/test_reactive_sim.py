@@ -260,13 +260,15 @@ def test_threshold_allreduce_reactive_guards():
     assert torch.equal(o.data, torch.arange(16.0))
 
 
-@pytest.mark.parametrize("seed", range(12))
+@pytest.mark.parametrize("seed", range(24))
 def test_fuzz_small_pool_freezes_and_thresholds(seed, monkeypatch):
     """Random freezes with a tiny send-slot pool (reclaim by stream wait),
     random thresholds/lag/geometry: every round of every rank completes, the
     contributor-mask/count invariant holds, nothing stays in flight."""
     rng = random.Random(1000 + seed)
     monkeypatch.setenv("AKKA_REACTIVE_SLOTS", str(rng.choice([2, 3, 4])))
+    # transfer groups of 1 chunk, a few chunks, or whole blocks
+    monkeypatch.setenv("AKKA_REACTIVE_GROUP_BYTES", str(rng.choice([0, 24, 100, 1 << 24])))
     n = rng.choice([2, 3, 4])
     S = rng.choice([9, 64, 130])
     C = rng.choice([1, 5, 16, 200])
