@@ -406,6 +406,22 @@ void DataPlane::upload_counts(int32_t round, const std::vector<int32_t>& blocks,
   const Binding& b = binding(round);
   if (!b.counts) return;
   bool copied = false;
+  if (int32_t(blocks.size()) == g_.N && g_.N > 1) {
+    // every block, one value everywhere (exact rounds: all N): ONE 32-bit
+    // fill of the whole [N][kmax] table instead of a fill per block (each a
+    // separate ~5 us launch on the compute stream, seen in the N=8 trace);
+    // entries past a block's last chunk are never read
+    const int32_t* row = staging_ + size_t(round % L_) * g_.N * kmax_;
+    const int32_t v = row[0];
+    bool same = true;
+    for (int32_t j = 0; j < g_.N && same; ++j)
+      for (int32_t k = 0; k < g_.num_chunks(j) && same; ++k) same = row[size_t(j) * kmax_ + k] == v;
+    if (same) {
+      dev_->fill_i32(s, b.counts, v, size_t(g_.N) * kmax_);
+      if (s == dev_->comm_stream()) binding_mut(round).comm_used = true;
+      return;
+    }
+  }
   for (int32_t blk : blocks) {
     const int32_t* src = staging_ + (size_t(round % L_) * g_.N + size_t(blk)) * kmax_;
     const int32_t kb = std::max(1, g_.num_chunks(blk));
