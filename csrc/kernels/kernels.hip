@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include <cstdlib>
 #include <cstring>
@@ -346,14 +347,28 @@ __global__ __launch_bounds__(kBlock) void count_mean_kernel(T* dst, const T* src
   }
 }
 
-template <typename T, int NSRC, int POL>
-void launch_vec_pol(hipStream_t s, const SrcTable& t, v4u* dst, int64_t nvec, int blocks_per_cu) {
-  constexpr int U0 = NSRC <= 4 ? 4 : (NSRC <= 8 ? 2 : 1);
-  constexpr int UNROLL = POL == kBoth ? (U0 < 2 ? U0 : 2) : U0;
+template <typename T, int NSRC, int POL, int UNROLL>
+void launch_vec_u(hipStream_t s, const SrcTable& t, v4u* dst, int64_t nvec, int blocks_per_cu) {
   const int64_t cap = int64_t(kCUs) * blocks_per_cu;
   int64_t want = (nvec + int64_t(kBlock) * UNROLL - 1) / (int64_t(kBlock) * UNROLL);
   int grid = int(want < cap ? (want < 1 ? 1 : want) : cap);
   hipLaunchKernelGGL((reduce_vec_kernel<T, NSRC, UNROLL, POL>), dim3(grid), dim3(kBlock), 0, s, t, dst, nvec);
+}
+
+template <typename T, int NSRC, int POL>
+void launch_vec_pol(hipStream_t s, const SrcTable& t, v4u* dst, int64_t nvec, int blocks_per_cu) {
+  constexpr int U0 = NSRC <= 4 ? 4 : (NSRC <= 8 ? 2 : 1);
+  constexpr int UNROLL = POL == kBoth ? (U0 < 2 ? U0 : 2) : U0;
+  if constexpr (NSRC == 8 && POL == kNts && std::is_same<T, float>::value) {
+    // experiments (bench/reduce_kernel_bw.py sweeps): loads in flight per lane
+    static const int u = [] {
+      const char* v = std::getenv("AKKA_VEC_UNROLL");
+      return v ? std::atoi(v) : 0;
+    }();
+    if (u == 1) return launch_vec_u<T, NSRC, POL, 1>(s, t, dst, nvec, blocks_per_cu);
+    if (u == 4) return launch_vec_u<T, NSRC, POL, 4>(s, t, dst, nvec, blocks_per_cu);
+  }
+  launch_vec_u<T, NSRC, POL, UNROLL>(s, t, dst, nvec, blocks_per_cu);
 }
 
 template <typename T, int NSRC>
