@@ -307,6 +307,7 @@ class WorkerCore final : public EngineHost {
       ls["bulk_rounds"] = stream_link_->stats().bulk_rounds;
       ls["collective_rounds"] = stream_link_->stats().collective_rounds;
       ls["exact_step_rounds"] = stream_link_->stats().exact_step_rounds;
+      ls["exact_unit_chunks"] = stream_link_->exact_unit_chunks();
       ls["graph_captures"] = stream_link_->stats().graph_captures;
       ls["graph_replays"] = stream_link_->stats().graph_replays;
       ls["graphs"] = stream_link_->graphs();

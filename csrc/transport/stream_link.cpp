@@ -1,6 +1,7 @@
 #include "stream_link.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace akka {
 
@@ -279,10 +280,22 @@ void StreamLink::build_exact_template() {
   // The exact round's step schedule depends only on the geometry and the lag:
   // built once, then every round only adds three base pointers.  Same groups
   // and per-pair order as schedule() minus the counts exchange (all N).
-  const Geometry& g = dp_->geometry();
+  const Geometry& g0 = dp_->geometry();
   const int32_t me = dp_->me();
-  const int32_t N = g.N;
+  const int32_t N = g0.N;
   const size_t es = dp_->esize();
+  // Transfer unit: m consecutive chunks moved as one (>= 16 MiB per unit, or
+  // AKKA_EXACT_UNIT_BYTES).  The outcome of an exact round does not depend on
+  // how its bytes are cut, and every p2p op costs the host 4-7 us inside
+  // ncclGroupEnd (profiles/r02/host): fewer, larger steps.  A function of the
+  // geometry only, so every rank builds the same groups.
+  int64_t min_bytes = int64_t(16) << 20;
+  if (const char* v = std::getenv("AKKA_EXACT_UNIT_BYTES")) min_bytes = std::max<int64_t>(0, std::atoll(v));
+  const int64_t cbytes = std::max<int64_t>(1, g0.C * int64_t(es));
+  unit_chunks_ = int32_t(std::clamp<int64_t>((min_bytes + cbytes - 1) / cbytes, 1,
+                                             std::max(1, g0.max_block_len_chunks())));
+  gx_ = Geometry(g0.S, N, g0.C * unit_chunks_);
+  const Geometry& g = gx_;
   const int32_t kme = g.num_chunks(me);
   const int32_t steps = g.max_block_len_chunks() + lag_;
   const char* ring0 = static_cast<const char*>(dp_->scatter_slot(0, 0, 0));
@@ -295,8 +308,8 @@ void StreamLink::build_exact_template() {
       const int32_t peer = (me + i) % N;
       const int32_t kp = g.num_chunks(peer);
       if (s < kp) v.push_back({true, peer, 0, g.chunk_offset(peer, s) * int64_t(es), size_t(g.chunk_len(peer, s)) * es});
-      if (s < kme)
-        v.push_back({false, peer, 1, static_cast<const char*>(dp_->scatter_slot(0, peer, s)) - ring0,
+      if (s < kme)  // unit s starts at chunk s*m of the slot
+        v.push_back({false, peer, 1, static_cast<const char*>(dp_->scatter_slot(0, peer, s * unit_chunks_)) - ring0,
                      size_t(g.chunk_len(me, s)) * es});
       if (bcast) v.push_back({true, peer, 2, g.chunk_offset(me, kb) * int64_t(es), size_t(g.chunk_len(me, kb)) * es});
       if (kb >= 0 && kb < kp)
@@ -381,7 +394,7 @@ void StreamLink::exact_steps(int32_t r) {
 }
 
 void StreamLink::exact_body(int32_t r, char* const base[3], bool captured) {
-  const Geometry& g = dp_->geometry();
+  const Geometry& g = gx_;  // transfer units (build_exact_template)
   const int32_t me = dp_->me();
   const int32_t N = g.N;
   const size_t es = dp_->esize();
@@ -402,12 +415,12 @@ void StreamLink::exact_body(int32_t r, char* const base[3], bool captured) {
     for (const OpT& t : exact_[s]) ops.push_back({t.send, t.peer, base[t.base] + t.off, t.bytes});
     if (!ops.empty()) p2p_->group(comm, ops);
     if (int32_t(s) < kme) {
-      // chunk s of my block landed from every peer: reduce it (compute stream)
+      // unit s of my block landed from every peer: reduce it (compute stream)
       dp_->compute_wait(dp_->record_comm());
       const int32_t k = int32_t(s);
       for (int32_t src = 0; src < N; ++src)  // ascending source id, like the message flow
         srcs[size_t(src)] = src == me ? static_cast<const void*>(base[0] + g.chunk_offset(me, k) * int64_t(es))
-                                      : dp_->scatter_slot(r, src, k);
+                                      : dp_->scatter_slot(r, src, k * unit_chunks_);
       auto specs = split_reduce(base[2] + g.chunk_offset(me, k) * int64_t(es), srcs, g.chunk_len(me, k));
       dev->reduce(cs, specs.data(), int32_t(specs.size()), dp_->dtype());
       reduced_ev_[size_t(k)] = dp_->record_compute();

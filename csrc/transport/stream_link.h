@@ -75,6 +75,7 @@ class StreamLink final : public Link {
   void set_graphs(bool on);
   bool graphs() const { return graphs_; }
   const std::string& graph_error() const { return graph_error_; }
+  int32_t exact_unit_chunks() const { return unit_chunks_; }
   Lane lane() const { return lane_; }
   const StreamLinkStats& stats() const { return stats_; }
   int32_t lag() const { return lag_; }
@@ -112,6 +113,8 @@ class StreamLink final : public Link {
   std::string graph_error_;
   void collective_round(int32_t round, bool native);
   std::vector<std::vector<OpT>> exact_;  // [step] -> ops
+  Geometry gx_;                          // exact rounds' transfer units (unit_chunks_ chunks each)
+  int32_t unit_chunks_ = 1;
   std::vector<P2POp> scratch_;
   std::vector<EventH> reduced_ev_;
   struct RoundQ {

@@ -37,7 +37,8 @@ def test_exact_sum_all_ranks(n, S, C):
 
 
 @pytest.mark.parametrize("lag", [1, 2, 3])
-def test_broadcast_lag_variants(lag):
+def test_broadcast_lag_variants(lag, monkeypatch):
+    monkeypatch.setenv("AKKA_EXACT_UNIT_BYTES", "0")  # one chunk per step
     n, S, C = 4, 4096, 100
     cl = SimCluster(n, S, C, broadcast_lag=lag)
     xs = _inputs(n, S, 0)
@@ -105,9 +106,10 @@ def test_threshold_reduce_subset_is_deterministic():
         assert bool((o.count == m).all())
 
 
-def test_mismatched_schedule_is_detected():
+def test_mismatched_schedule_is_detected(monkeypatch):
     # uneven chunks (8,8,8,6 per block): a rank with a different broadcast lag
     # issues its per-pair ops in a different order -> a size mismatch, not silent corruption
+    monkeypatch.setenv("AKKA_EXACT_UNIT_BYTES", "0")
     n, S, C = 2, 60, 8
     cl = SimCluster(n, S, C, broadcast_lag=[1, 2])
     xs = _inputs(n, S, 0)
@@ -173,7 +175,8 @@ def test_collective_lane_only_for_exact_rounds():
     assert all(w.state()["link"]["exact_step_rounds"] == 0 for w in cl.workers)
 
 
-def test_auto_lane_without_native_collectives_keeps_chunk_schedule():
+def test_auto_lane_without_native_collectives_keeps_chunk_schedule(monkeypatch):
+    monkeypatch.setenv("AKKA_EXACT_UNIT_BYTES", "0")
     n, S, C = 4, 4096, 100
     cl = SimCluster(n, S, C)
     cl.allreduce(_inputs(n, S, 0))
@@ -280,3 +283,27 @@ def test_lone_member_completes_from_itself():
         assert torch.equal(o.data[:S // 2], x[:S // 2]) and bool((o.count[:S // 2] == 1).all())
         assert int(o.count[S // 2:].abs().sum()) == 0
     assert w.state()["link"]["unreduced_chunks"] == 0
+
+
+@pytest.mark.parametrize("unit_bytes", ["0", "800", "1200", str(16 << 20)])
+@pytest.mark.parametrize("n,S,C", [(4, 4096, 100), (3, 1000, 7), (8, 8192 + 5, 64)])
+def test_exact_transfer_units(unit_bytes, n, S, C, monkeypatch):
+    """Exact p2p rounds move m consecutive chunks per step (>= the unit
+    bytes, fixed by the geometry): same sums and traffic, fewer groups."""
+    monkeypatch.setenv("AKKA_EXACT_UNIT_BYTES", unit_bytes)
+    cl = SimCluster(n, S, C, max_lag=1, lane="p2p")
+    before = 0
+    for r in range(3):
+        xs = _inputs(n, S, r)
+        outs = cl.allreduce(xs)
+        want = torch.stack(xs).sum(0)
+        assert all(torch.equal(o.data, want) and bool((o.count == n).all()) for o in outs)
+        assert cl.bytes_moved() - before == 2 * (n - 1) * S * 4
+        before = cl.bytes_moved()
+    g = Geometry(S, n, C)
+    m = max(1, min(-(-int(unit_bytes) // (C * 4)), g.kmax)) if int(unit_bytes) else 1
+    st = cl.workers[0].state()["link"]
+    assert st["exact_unit_chunks"] == m
+    kx, lag = Geometry(S, n, C * m).kmax, 2
+    busy = len({s for s in range(kx)} | {s for s in range(lag, kx + lag)})  # steps with any op
+    assert st["groups"] == 3 * busy
