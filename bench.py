@@ -69,6 +69,9 @@ def parse():
     p.add_argument("--lane", choices=["auto", "p2p", "collective"], default="auto",
                    help="exact-round lane of the stream transport (stream_link.h): auto = RCCL reduce-scatter + "
                         "all-gather when the buffer splits evenly, else the chunk-pipelined p2p schedule")
+    p.add_argument("--lane-select", choices=["on", "off"], default="on",
+                   help="with --lane auto at N>1 (stream transport): before the warmup, run one exact round and a "
+                        "few timed rounds on each lane and keep the faster exact one (every rank agrees)")
     p.add_argument("--async-op", choices=["auto", "on", "off"], default="auto",
                    help="async rounds (event hand-off) -- auto: on for N>1 (saves a stream hop per round), off for "
                         "N=1 (local rounds run on the caller's stream, nothing to hop)")
@@ -410,6 +413,51 @@ def main() -> int:
     if ar.transport == "reactive":
         args.async_op = False  # reactive rounds return once complete (progress is host-polled)
 
+    def lane_rate(k: int) -> float:
+        """Seconds per round of the current lane over k rounds (max over ranks)."""
+        o = ar(x, async_op=args.async_op, out=out_buf)
+        o.wait()
+        _sync()
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(k):
+            o = ar(x, async_op=args.async_op, out=out_buf)
+        o.wait()
+        _sync()
+        barrier()
+        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item()) / k
+
+    # Lane selection (untimed, before the warmup): both exact-round lanes of
+    # the stream transport compute the same exact sum -- RCCL reduce-scatter +
+    # all-gather, or the chunk-pipelined direct p2p schedule with our reduce
+    # kernel.  Which one is faster depends on N, the xGMI topology and the
+    # buffer, so each is checked for exactness and timed briefly here; every
+    # rank sees the same max-over-ranks numbers and keeps the same lane.
+    chosen_lane = args.lane
+
+    def lane_select():
+        env_phase_stall(rank, "lane_select")
+        res = {}
+        for ln in ("collective", "p2p"):
+            ar.set_lane(ln)
+            exact = exact_round(f"lane_{ln}")
+            res[ln] = {"exact": exact, "ms": round(lane_rate(3) * 1e3, 4) if exact else None}
+        good = [ln for ln in res if res[ln]["exact"]]
+        if not good:
+            raise RuntimeError(f"no exact lane: {res}")
+        pick = min(good, key=lambda ln: res[ln]["ms"])
+        ar.set_lane(pick)
+        res["chosen"] = pick
+        return res
+
+    lane_sel = None
+    if world > 1 and ar.transport == "stream" and args.lane == "auto" and args.lane_select == "on":
+        lane_sel = guard.run("lane_select", dl, lane_select)
+        chosen_lane = lane_sel["chosen"]
+
     def warmup():
         env_phase_stall(rank, "warmup")
         out = None
@@ -422,6 +470,8 @@ def main() -> int:
         _sync()
 
     guard.run("warmup", dl, warmup)
+
+    link0 = dict(ar.state().get("link", {}))  # counters before the timed rounds
 
     def timed_region():
         env_phase_stall(rank, "timed")
@@ -485,8 +535,13 @@ def main() -> int:
     # and the chunk-pipelined p2p schedule.
     def other_lane():
         st0 = ar.state().get("link", {})
-        used = "collective" if st0.get("bulk_rounds", 0) > st0.get("exact_step_rounds", 0) else "p2p"
-        if world == 1 or ar.transport != "stream":
+        # lane of the timed rounds: collective rounds vs exact p2p-step rounds since link0
+        coll = st0.get("collective_rounds", 0) - link0.get("collective_rounds", 0)
+        steps_p2p = st0.get("exact_step_rounds", 0) - link0.get("exact_step_rounds", 0)
+        used = "collective" if coll > steps_p2p else "p2p"
+        if world == 1:
+            return "local", None
+        if ar.transport != "stream":
             return used, None
         other = "p2p" if used == "collective" else "collective"
         try:
@@ -508,13 +563,14 @@ def main() -> int:
             return used, {"lane": other, "algbw_GBps": round(nbytes / (float(t.item()) / k) / 1e9, 3),
                           "steps": k}
         finally:
-            ar.set_lane(args.lane)
+            ar.set_lane(chosen_lane)
 
     st = ar.state()  # headline rounds only (before the other lane runs)
     lane_used, lane_other = guard.run("other_lane", dl, other_lane)
 
     link = st.get("link", {})
-    rounds_done = max(1, link.get("rounds", st["stats"]["rounds_completed"]) or 1)
+    # per-round link counters of the timed rounds only (plus the check round)
+    rounds_done = max(1, link.get("rounds", 0) - link0.get("rounds", 0))
     line = dict(base)
     line.update({
         "value": round(algbw, 3),
@@ -522,7 +578,7 @@ def main() -> int:
         "busbw_GBps": round(busbw, 3) if busbw is not None else None,
         "exact": ok,
         "preflight": "passed" if "preflight" in guard.history else "skipped",
-        "groups_per_round": round(link.get("groups", 0) / rounds_done, 3),
+        "groups_per_round": round((link.get("groups", 0) - link0.get("groups", 0)) / rounds_done, 3),
         "host_us_per_round": round(host_s / args.steps * 1e6, 2),
         "p2p_kind": p2p0.get("kind"),
         "p2p_nranks": p2p0.get("nranks"),
@@ -531,6 +587,7 @@ def main() -> int:
         "rank_devices": ranks,
         "lane": lane_used,
         "other_lane": lane_other,
+        "lane_select": lane_sel,
         "rccl_allreduce_algbw_GBps": round(rccl, 3) if rccl else None,
     })
     line["config"] = dict(base["config"])

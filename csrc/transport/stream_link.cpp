@@ -234,6 +234,7 @@ void StreamLink::collective_round(int32_t r, bool native) {
     ++stats_.collective_rounds;
     return;
   }
+  ++stats_.collective_rounds;
   // Whole-block direct exchange: the reference's scatter / reduce / broadcast
   // (W:212-268) with one message per peer and phase.
   std::vector<P2POp>& ops = scratch_;

@@ -36,6 +36,8 @@ namespace akka {
 
 struct StreamLinkStats {
   int64_t groups = 0, ops = 0, bytes_sent = 0, rounds = 0, unreduced_chunks = 0;
+  // bulk rounds by lane: collective = RCCL reduce-scatter + all-gather or the
+  // whole-block exchange; exact_step_rounds = the exact p2p step template
   int64_t bulk_rounds = 0, collective_rounds = 0, exact_step_rounds = 0, graph_captures = 0, graph_replays = 0;
 };
 

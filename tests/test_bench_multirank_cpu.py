@@ -40,7 +40,7 @@ def _run(n, *extra, env=None, expect_rc=0):
 
 @pytest.mark.parametrize("n,transport", [(2, "stream"), (3, "stream"), (2, "reactive")])
 def test_bench_multirank_line(n, transport):
-    d = _run(n, "--transport", transport)
+    d = _run(n, "--transport", transport, "--lane-select", "off")
     assert d["n_gpus"] == n and d["steps"] == 3 and d["warmup"] == 1
     assert d["exact"] is True and d["value"] > 0
     assert d["config"]["parallelism"] == f"dp{n}" and d["config"]["transport"] == "gloo-p2p"
@@ -63,6 +63,19 @@ def test_bench_collective_lane_line():
     d = _run(3, "--lane", "collective")
     assert d["exact"] is True and d["lane"] == "collective" and d["other_lane"]["lane"] == "p2p"
     assert d["groups_per_round"] == 2.0
+
+
+def test_bench_lane_select():
+    """--lane auto at N>1: each lane is checked exact and timed before the
+    warmup, and the timed rounds run on the faster one (every rank agrees)."""
+    d = _run(3)
+    sel = d["lane_select"]
+    assert sel["collective"]["exact"] is True and sel["p2p"]["exact"] is True
+    assert sel["collective"]["ms"] > 0 and sel["p2p"]["ms"] > 0
+    faster = min(("collective", "p2p"), key=lambda ln: sel[ln]["ms"])
+    assert sel["chosen"] == faster and d["lane"] == faster
+    assert d["other_lane"]["lane"] != faster
+    assert d["exact"] is True and d["groups_per_round"] > 0
 
 
 def test_bench_multirank_extras_deadline():
