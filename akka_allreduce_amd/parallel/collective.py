@@ -239,6 +239,12 @@ class ThresholdAllreduce:
             raise ValueError("lanes belong to the scheduled (stream) transport")
         self.worker.set_lane(lane)
 
+    def set_exact_unit_bytes(self, nbytes: int = -1) -> None:
+        """Transfer-unit size of exact p2p-lane rounds (AllreduceWorker.set_exact_unit_bytes)."""
+        if self.transport != "stream":
+            raise ValueError("transfer units belong to the scheduled (stream) transport")
+        self.worker.set_exact_unit_bytes(nbytes)
+
     def set_graphs(self, on: bool = True) -> None:
         """HIP-graph replay of exact p2p-lane rounds (see AllreduceWorker.set_graphs)."""
         if self.transport != "stream":

@@ -334,6 +334,13 @@ class AllreduceWorker:
         the p2p schedule."""
         self._core.set_lane(lane)
 
+    def set_exact_unit_bytes(self, nbytes: int = -1) -> None:
+        """Minimum bytes per transfer unit of exact p2p-lane rounds (whole
+        chunks; a unit larger than a block means one message per peer and
+        phase).  -1 restores the default (AKKA_EXACT_UNIT_BYTES or 16 MiB).
+        Every rank must switch at the same round."""
+        self._core.set_exact_unit_bytes(int(nbytes))
+
     def set_graphs(self, on: bool = True) -> None:
         """Replay exact p2p-lane rounds from captured HIP graphs: a round whose
         buffers (input, ring row, output) were seen before is captured once,

@@ -436,20 +436,30 @@ def main() -> int:
     # kernel.  Which one is faster depends on N, the xGMI topology and the
     # buffer, so each is checked for exactness and timed briefly here; every
     # rank sees the same max-over-ranks numbers and keeps the same lane.
-    chosen_lane = args.lane
+    # candidate -> (lane, minimum exact transfer-unit bytes; -1 = default 16 MiB)
+    lanes = {"collective": ("collective", -1), "p2p": ("p2p", -1), "p2p_block": ("p2p", 1 << 40)}
+    fixed = dict(lanes, auto=("auto", -1))
+
+    def apply_lane(name: str) -> None:
+        ln, unit = fixed[name]
+        ar.set_lane(ln)
+        if ar.transport == "stream" and world > 1:
+            ar.set_exact_unit_bytes(unit)
+
+    chosen_lane = args.lane if args.lane != "auto" else None
 
     def lane_select():
         env_phase_stall(rank, "lane_select")
         res = {}
-        for ln in ("collective", "p2p"):
-            ar.set_lane(ln)
-            exact = exact_round(f"lane_{ln}")
-            res[ln] = {"exact": exact, "ms": round(lane_rate(3) * 1e3, 4) if exact else None}
-        good = [ln for ln in res if res[ln]["exact"]]
+        for name in lanes:
+            apply_lane(name)
+            exact = exact_round(f"lane_{name}")
+            res[name] = {"exact": exact, "ms": round(lane_rate(3) * 1e3, 4) if exact else None}
+        good = [n for n in lanes if res[n]["exact"]]
         if not good:
             raise RuntimeError(f"no exact lane: {res}")
-        pick = min(good, key=lambda ln: res[ln]["ms"])
-        ar.set_lane(pick)
+        pick = min(good, key=lambda n: res[n]["ms"])
+        apply_lane(pick)
         res["chosen"] = pick
         return res
 
@@ -538,14 +548,14 @@ def main() -> int:
         # lane of the timed rounds: collective rounds vs exact p2p-step rounds since link0
         coll = st0.get("collective_rounds", 0) - link0.get("collective_rounds", 0)
         steps_p2p = st0.get("exact_step_rounds", 0) - link0.get("exact_step_rounds", 0)
-        used = "collective" if coll > steps_p2p else "p2p"
+        used = chosen_lane or ("collective" if coll > steps_p2p else "p2p")
         if world == 1:
             return "local", None
         if ar.transport != "stream":
             return used, None
         other = "p2p" if used == "collective" else "collective"
         try:
-            ar.set_lane(other)
+            apply_lane(other)
             for _ in range(2):
                 o = ar(x, async_op=args.async_op, out=out_buf)
             o.wait()
@@ -563,7 +573,7 @@ def main() -> int:
             return used, {"lane": other, "algbw_GBps": round(nbytes / (float(t.item()) / k) / 1e9, 3),
                           "steps": k}
         finally:
-            ar.set_lane(chosen_lane)
+            apply_lane(chosen_lane or args.lane)
 
     st = ar.state()  # headline rounds only (before the other lane runs)
     lane_used, lane_other = guard.run("other_lane", dl, other_lane)

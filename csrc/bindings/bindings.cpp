@@ -357,6 +357,10 @@ class WorkerCore final : public EngineHost {
     else if (lane == "collective") stream_link_->set_lane(Lane::Collective);
     else throw AkkaError("akka: lane must be 'auto', 'p2p' or 'collective'");
   }
+  void set_exact_unit_bytes(int64_t bytes) {
+    AKKA_CHECK(stream_link_, "set_exact_unit_bytes: scheduled (stream) transport only");
+    stream_link_->set_exact_unit_bytes(bytes);
+  }
   void set_graphs(bool on) {
     AKKA_CHECK(stream_link_, "set_graphs: scheduled (stream) transport only");
     stream_link_->set_graphs(on);
@@ -547,6 +551,7 @@ PYBIND11_MODULE(_native, m) {
       .def("p2p_check", &WorkerCore::p2p_check)
       .def("set_lane", &WorkerCore::set_lane)
       .def("set_graphs", &WorkerCore::set_graphs)
+      .def("set_exact_unit_bytes", &WorkerCore::set_exact_unit_bytes)
       .def("scatter_count", &WorkerCore::scatter_count)
       .def("reduced_arrivals", &WorkerCore::reduced_arrivals);
 

@@ -21,12 +21,22 @@ StreamLink::~StreamLink() {
 
 void StreamLink::set_graphs(bool on) {
   graphs_ = on && dp_ && !dp_->device()->is_host();
-  if (!graphs_ && !graphs_map_.empty()) {
-    Device* dev = dp_->device();
-    dev->sync_stream(dev->comm_stream());
-    for (auto& kv : graphs_map_) dev->destroy_graph(kv.second.exec);
-    graphs_map_.clear();
-  }
+  if (!graphs_) drop_graphs();
+}
+
+void StreamLink::drop_graphs() {
+  if (graphs_map_.empty()) return;
+  Device* dev = dp_->device();
+  dev->sync_stream(dev->comm_stream());
+  for (auto& kv : graphs_map_) dev->destroy_graph(kv.second.exec);
+  graphs_map_.clear();
+}
+
+void StreamLink::set_exact_unit_bytes(int64_t bytes) {
+  if (bytes == unit_bytes_) return;
+  unit_bytes_ = bytes;
+  exact_.clear();  // rebuilt by the next exact round
+  drop_graphs();   // captured with the old template
 }
 
 void StreamLink::send_scatter(int32_t dest, int32_t chunk, int32_t round, const Payload& p) {
@@ -291,7 +301,9 @@ void StreamLink::build_exact_template() {
   // ncclGroupEnd (profiles/r02/host): fewer, larger steps.  A function of the
   // geometry only, so every rank builds the same groups.
   int64_t min_bytes = int64_t(16) << 20;
-  if (const char* v = std::getenv("AKKA_EXACT_UNIT_BYTES")) min_bytes = std::max<int64_t>(0, std::atoll(v));
+  if (unit_bytes_ >= 0) min_bytes = unit_bytes_;
+  else if (const char* v = std::getenv("AKKA_EXACT_UNIT_BYTES")) min_bytes = std::max<int64_t>(0, std::atoll(v));
+  min_bytes = std::min<int64_t>(min_bytes, int64_t(1) << 50);
   const int64_t cbytes = std::max<int64_t>(1, g0.C * int64_t(es));
   unit_chunks_ = int32_t(std::clamp<int64_t>((min_bytes + cbytes - 1) / cbytes, 1,
                                              std::max(1, g0.max_block_len_chunks())));

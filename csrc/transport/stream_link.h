@@ -78,6 +78,10 @@ class StreamLink final : public Link {
   bool graphs() const { return graphs_; }
   const std::string& graph_error() const { return graph_error_; }
   int32_t exact_unit_chunks() const { return unit_chunks_; }
+  // Minimum bytes of an exact-round transfer unit (< 0: AKKA_EXACT_UNIT_BYTES
+  // or 16 MiB).  Rebuilds the template at the next exact round; like set_lane,
+  // every rank must switch at the same round.
+  void set_exact_unit_bytes(int64_t bytes);
   Lane lane() const { return lane_; }
   const StreamLinkStats& stats() const { return stats_; }
   int32_t lag() const { return lag_; }
@@ -117,6 +121,8 @@ class StreamLink final : public Link {
   std::vector<std::vector<OpT>> exact_;  // [step] -> ops
   Geometry gx_;                          // exact rounds' transfer units (unit_chunks_ chunks each)
   int32_t unit_chunks_ = 1;
+  int64_t unit_bytes_ = -1;
+  void drop_graphs();
   std::vector<P2POp> scratch_;
   std::vector<EventH> reduced_ev_;
   struct RoundQ {

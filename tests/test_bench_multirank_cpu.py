@@ -70,11 +70,11 @@ def test_bench_lane_select():
     warmup, and the timed rounds run on the faster one (every rank agrees)."""
     d = _run(3)
     sel = d["lane_select"]
-    assert sel["collective"]["exact"] is True and sel["p2p"]["exact"] is True
-    assert sel["collective"]["ms"] > 0 and sel["p2p"]["ms"] > 0
-    faster = min(("collective", "p2p"), key=lambda ln: sel[ln]["ms"])
+    cands = ("collective", "p2p", "p2p_block")
+    assert all(sel[c]["exact"] is True and sel[c]["ms"] > 0 for c in cands)
+    faster = min(cands, key=lambda ln: sel[ln]["ms"])
     assert sel["chosen"] == faster and d["lane"] == faster
-    assert d["other_lane"]["lane"] != faster
+    assert d["other_lane"]["lane"] == ("p2p" if faster == "collective" else "collective")
     assert d["exact"] is True and d["groups_per_round"] > 0
 
 

@@ -307,3 +307,22 @@ def test_exact_transfer_units(unit_bytes, n, S, C, monkeypatch):
     kx, lag = Geometry(S, n, C * m).kmax, 2
     busy = len({s for s in range(kx)} | {s for s in range(lag, kx + lag)})  # steps with any op
     assert st["groups"] == 3 * busy
+
+
+def test_exact_unit_switch_between_rounds():
+    """set_exact_unit_bytes rebuilds the exact template at the next round
+    (what bench.py's lane selection does between its candidates): sums stay
+    exact and the unit follows the setting, per chunk / whole block / default."""
+    n, S, C = 3, 3000, 50
+    cl = SimCluster(n, S, C, max_lag=1, lane="p2p")
+    g = Geometry(S, n, C)
+    for r, (unit, m) in enumerate([(0, 1), (1 << 40, g.kmax), (C * 4 * 3, 3), (0, 1), (-1, None)]):
+        for w in cl.workers:
+            w.set_exact_unit_bytes(unit)
+        xs = _inputs(n, S, r)
+        outs = cl.allreduce(xs)
+        want = torch.stack(xs).sum(0)
+        assert all(torch.equal(o.data, want) and bool((o.count == n).all()) for o in outs), (r, unit)
+        got = cl.workers[0].state()["link"]["exact_unit_chunks"]
+        if m is not None:
+            assert got == m, (unit, got)
