@@ -31,11 +31,12 @@ HOST_SOURCES = [
     "transport/stream_link.cpp",
     "transport/reactive_link.cpp",
     "transport/rccl_p2p.cpp",
+    "transport/ipc_lane.cpp",
     "kernels/hip_device.cpp",
     "runtime/watchdog.cpp",
     "bindings/bindings.cpp",
 ]
-HIP_SOURCES = ["kernels/kernels.hip"]
+HIP_SOURCES = ["kernels/kernels.hip", "kernels/ipc.hip"]
 
 
 def ext_path() -> str:

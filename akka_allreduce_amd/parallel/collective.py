@@ -148,9 +148,14 @@ class ThresholdAllreduce:
         transport: str = "stream",
         lane: str = "auto",
         th_allreduce: Optional[float] = None,
+        data_plane: str = "rccl",
     ):
         if transport not in ("stream", "reactive"):
             raise ValueError("transport must be 'stream' or 'reactive'")
+        if data_plane not in ("rccl", "ipc"):
+            raise ValueError("data_plane must be 'rccl' or 'ipc'")
+        if data_plane == "ipc" and (transport != "stream" or th_reduce < 1.0 or th_complete < 1.0):
+            raise ValueError("the ipc-only data plane runs exact rounds (thresholds 1) on the stream transport")
         r, w, local = env_rank_world()
         import torch.distributed as dist
 
@@ -164,13 +169,18 @@ class ThresholdAllreduce:
             device = torch.device("cuda", local % max(1, torch.cuda.device_count())) if torch.cuda.is_available() \
                 else torch.device("cpu")
         self.device = torch.device(device)
+        if data_plane == "ipc" and self.device.type != "cuda":
+            raise ValueError("the ipc-only data plane maps peer GPU memory: it needs a cuda device")
         if transport == "reactive" and self.world_size > 1 and self.device.type == "cuda":
             need = min(32, self.world_size + 4)
             have = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
             if have < need:
                 raise RuntimeError(f"reactive transport at N={self.world_size} needs GPU_MAX_HW_QUEUES >= {need} "
                                    f"(have {have}); export it (<= 32) before the first HIP call")
-        if self.device.type == "cuda":
+        if self.device.type == "cuda" and data_plane == "ipc" and self.world_size > 1:
+            torch.cuda.set_device(self.device)
+            spec = ("none", self.rank, self.world_size)
+        elif self.device.type == "cuda":
             torch.cuda.set_device(self.device)
             uid = share_unique_id(self.rank, self.world_size, store)
             spec = ("rccl", uid, self.rank, self.world_size) if self.world_size > 1 else ("local",)
@@ -193,6 +203,12 @@ class ThresholdAllreduce:
         self.worker.tell(InitWorkers(peers, self.world_size, None, self.rank, th_reduce, th_complete, max_lag,
                                      int(data_size), int(max_chunk_size)))
         self.data_size = int(data_size)
+        self.store = store
+        self._iid = ThresholdAllreduce._instances
+        self._ipc_epoch = 0
+        if data_plane == "ipc" and self.world_size > 1:
+            self.enable_ipc()
+            lane = "ipc"
         if self.transport == "stream":
             self.worker.set_lane(lane)
         from ..utils.faults import env_straggler_delay
@@ -238,6 +254,33 @@ class ThresholdAllreduce:
         if self.transport != "stream":
             raise ValueError("lanes belong to the scheduled (stream) transport")
         self.worker.set_lane(lane)
+
+    def enable_ipc(self) -> None:
+        """Open the one-sided xGMI lane (csrc/transport/ipc_lane.h): every
+        rank creates its window, the handles go to every rank (the TCPStore
+        given at construction, else torch.distributed), every rank maps the
+        others'.  Collective; afterwards ``set_lane("ipc")`` runs exact rounds
+        as push / reduce / pull kernels over mapped peer memory."""
+        if self.transport != "stream" or self.device.type != "cuda" or self.world_size < 2:
+            raise ValueError("the ipc lane needs the stream transport on GPUs with N > 1")
+        mine = self.worker.ipc_handle()
+        if self.store is not None:
+            self._ipc_epoch += 1
+            key = f"akka/ipc/{self._iid}/{self._ipc_epoch}"
+            self.store.set(f"{key}/{self.rank}", mine)
+            handles = [bytes(self.store.get(f"{key}/{i}")) for i in range(self.world_size)]
+        else:
+            import torch.distributed as dist
+
+            if not dist.is_initialized():
+                raise RuntimeError("enable_ipc: initialise torch.distributed (gloo is enough) or pass a store")
+            handles = [None] * self.world_size
+            dist.all_gather_object(handles, mine)
+        self.worker.ipc_open(handles)
+
+    def ipc_error(self) -> int:
+        """Non-zero once a wait of the ipc lane timed out (synchronises)."""
+        return self.worker.ipc_error()
 
     def set_exact_unit_bytes(self, nbytes: int = -1) -> None:
         """Transfer-unit size of exact p2p-lane rounds (AllreduceWorker.set_exact_unit_bytes)."""

@@ -257,6 +257,9 @@ class AllreduceWorker:
         elif kind == "callback":
             _, fn, rank, nranks = spec
             self._core.connect_callback(fn, int(rank), int(nranks))
+        elif kind == "none":  # ipc-only data plane: exact rounds on the one-sided lane
+            _, rank, nranks = spec
+            self._core.connect_none(int(rank), int(nranks))
         else:
             raise ValueError(f"unknown transport spec {spec!r}")
 
@@ -340,6 +343,25 @@ class AllreduceWorker:
         phase).  -1 restores the default (AKKA_EXACT_UNIT_BYTES or 16 MiB).
         Every rank must switch at the same round."""
         self._core.set_exact_unit_bytes(int(nbytes))
+
+    # ---- one-sided xGMI lane (csrc/transport/ipc_lane.h) ----
+    def ipc_handle(self) -> bytes:
+        """Create this rank's window (once) and return its handle, to be
+        exchanged with every rank of the job (ipc_open)."""
+        return bytes(self._core.ipc_handle())
+
+    def ipc_open(self, handles: list) -> None:
+        """Map every other rank's window; ``handles[i]`` is rank i's
+        ipc_handle().  Afterwards ``set_lane("ipc")`` is allowed."""
+        self._core.ipc_open([bytes(h) for h in handles])
+
+    def ipc_error(self) -> int:
+        """Non-zero once a wait of the ipc lane timed out on this rank
+        (synchronises the device)."""
+        return int(self._core.ipc_error())
+
+    def ipc_close(self) -> None:
+        self._core.ipc_close()
 
     def set_graphs(self, on: bool = True) -> None:
         """Replay exact p2p-lane rounds from captured HIP graphs: a round whose

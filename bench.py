@@ -72,6 +72,8 @@ def parse():
     p.add_argument("--lane-select", choices=["on", "off"], default="on",
                    help="with --lane auto at N>1 (stream transport): before the warmup, run one exact round and a "
                         "few timed rounds on each lane and keep the faster exact one (every rank agrees)")
+    p.add_argument("--ipc", choices=["on", "off"], default="on",
+                   help="lane selection also tries the one-sided xGMI lane (mapped peer windows, ipc_lane.h)")
     p.add_argument("--async-op", choices=["auto", "on", "off"], default="auto",
                    help="async rounds (event hand-off) -- auto: on for N>1 (saves a stream hop per round), off for "
                         "N=1 (local rounds run on the caller's stream, nothing to hop)")
@@ -375,11 +377,11 @@ def main() -> int:
         if world > 1:
             dist.barrier()
 
-    def exact_round(tag: str) -> bool:
-        # every rank contributes rank+1 -> sum = N(N+1)/2 exactly, count N
-        y = torch.full((S,), float(rank + 1), device=dev, dtype=dtype)
+    def exact_round(tag: str, salt: int = 0) -> bool:
+        # every rank contributes (rank+1)(salt+1) -> sum = (salt+1) N(N+1)/2 exactly, count N
+        y = torch.full((S,), float((rank + 1) * (salt + 1)), device=dev, dtype=dtype)
         o = ar(y)
-        want = float(world * (world + 1) // 2)
+        want = float((salt + 1) * world * (world + 1) // 2)
         ok = bool(torch.all(o.data == want).item()) and bool(torch.all(o.count == world).item())
         if world > 1:
             f = torch.tensor([1 if ok else 0])
@@ -438,7 +440,7 @@ def main() -> int:
     # rank sees the same max-over-ranks numbers and keeps the same lane.
     # candidate -> (lane, minimum exact transfer-unit bytes; -1 = default 16 MiB)
     lanes = {"collective": ("collective", -1), "p2p": ("p2p", -1), "p2p_block": ("p2p", 1 << 40)}
-    fixed = dict(lanes, auto=("auto", -1))
+    fixed = dict(lanes, auto=("auto", -1), ipc=("ipc", -1))
 
     def apply_lane(name: str) -> None:
         ln, unit = fixed[name]
@@ -451,10 +453,27 @@ def main() -> int:
     def lane_select():
         env_phase_stall(rank, "lane_select")
         res = {}
+        if dev.type == "cuda" and args.ipc == "on":
+            # the one-sided xGMI lane (ipc_lane.h) joins the candidates when every
+            # rank could map every other rank's window
+            err = None
+            try:
+                ar.enable_ipc()
+            except Exception as e:  # noqa: BLE001 - reported, the lane is just skipped
+                err = f"{type(e).__name__}: {e}"[:200]
+            flag = torch.tensor([0 if err else 1])
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+            if flag.item():
+                lanes["ipc"] = ("ipc", -1)
+            else:
+                res["ipc"] = {"exact": None, "ms": None, "error": err or "another rank could not open its windows"}
         for name in lanes:
             apply_lane(name)
-            exact = exact_round(f"lane_{name}")
-            res[name] = {"exact": exact, "ms": round(lane_rate(3) * 1e3, 4) if exact else None}
+            exact = exact_round(f"lane_{name}", salt=1) and exact_round(f"lane_{name}", salt=2)
+            ms = round(lane_rate(3) * 1e3, 4) if exact else None
+            if exact:  # and again after rounds of other data (stale reads would show here)
+                exact = exact_round(f"lane_{name}", salt=3)
+            res[name] = {"exact": exact, "ms": ms if exact else None}
         good = [n for n in lanes if res[n]["exact"]]
         if not good:
             raise RuntimeError(f"no exact lane: {res}")

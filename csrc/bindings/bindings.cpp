@@ -179,6 +179,37 @@ class WorkerCore final : public EngineHost {
     self_drive_ = true;
     make_reactive_link();
   }
+  // ipc-only data plane: no two-sided transport; exact rounds on the ipc lane.
+  void connect_none(int32_t rank, int32_t nranks) {
+    AKKA_CHECK(dev_ && !dev_->is_host(), "the ipc-only data plane needs a HIP device");
+    AKKA_CHECK(link_kind_ == "stream", "the ipc lane belongs to the scheduled (stream) transport");
+    p2p_ = std::make_unique<NullP2P>(rank, nranks);
+    make_stream_link();
+  }
+  // ---- one-sided xGMI lane (ipc_lane.h) ----
+  py::bytes ipc_handle() {
+    AKKA_CHECK(stream_link_ && dp_, "ipc_handle: scheduled (stream) transport, after init");
+    if (!ipc_pending_)
+      ipc_pending_ = std::make_unique<IpcLane>(dev_.get(), dp_->geometry(), dp_->me(), dt_);
+    return py::bytes(ipc_pending_->handle());
+  }
+  void ipc_open(std::vector<std::string> handles) {
+    AKKA_CHECK(ipc_pending_, "ipc_open: call ipc_handle first");
+    {
+      py::gil_scoped_release nogil;
+      ipc_pending_->open(handles);
+    }
+    stream_link_->set_ipc(std::move(ipc_pending_));
+  }
+  uint32_t ipc_error() {
+    AKKA_CHECK(stream_link_ && stream_link_->ipc(), "ipc_error: the ipc lane is not open");
+    py::gil_scoped_release nogil;
+    return stream_link_->ipc()->error();
+  }
+  void ipc_close() {
+    ipc_pending_.reset();
+    if (stream_link_) stream_link_->set_ipc(nullptr);
+  }
   void connect_local() {  // N == 1: stream link without peers
     AKKA_CHECK(engine_->geometry().N == 1, "connect_local is for single-worker jobs");
     make_stream_link(/*any_kind=*/true);
@@ -313,7 +344,18 @@ class WorkerCore final : public EngineHost {
       ls["graphs"] = stream_link_->graphs();
       if (!stream_link_->graph_error().empty()) ls["graph_error"] = stream_link_->graph_error();
       const Lane ln = stream_link_->lane();
-      ls["lane"] = ln == Lane::Auto ? "auto" : ln == Lane::P2P ? "p2p" : "collective";
+      ls["lane"] = ln == Lane::Auto ? "auto" : ln == Lane::P2P ? "p2p" : ln == Lane::Ipc ? "ipc" : "collective";
+      ls["ipc_rounds"] = stream_link_->stats().ipc_rounds;
+      if (IpcLane* ipc = stream_link_->ipc()) {
+        py::dict is;
+        is["portions"] = ipc->nportions();
+        is["portion_bytes"] = ipc->portion_elems() * int64_t(dtype_size(dt_));
+        is["window_bytes"] = int64_t(ipc->window_bytes());
+        is["rounds"] = ipc->stats().rounds;
+        is["bytes_pushed"] = ipc->stats().bytes_pushed;
+        is["bytes_pulled"] = ipc->stats().bytes_pulled;
+        ls["ipc"] = is;
+      }
       d["link"] = ls;
     }
     if (reactive_link_) {
@@ -355,7 +397,11 @@ class WorkerCore final : public EngineHost {
     if (lane == "auto") stream_link_->set_lane(Lane::Auto);
     else if (lane == "p2p") stream_link_->set_lane(Lane::P2P);
     else if (lane == "collective") stream_link_->set_lane(Lane::Collective);
-    else throw AkkaError("akka: lane must be 'auto', 'p2p' or 'collective'");
+    else if (lane == "ipc") {
+      AKKA_CHECK(stream_link_->ipc() && stream_link_->ipc()->ready(), "set_lane('ipc'): open the ipc windows first");
+      stream_link_->set_lane(Lane::Ipc);
+    }
+    else throw AkkaError("akka: lane must be 'auto', 'p2p', 'collective' or 'ipc'");
   }
   void set_exact_unit_bytes(int64_t bytes) {
     AKKA_CHECK(stream_link_, "set_exact_unit_bytes: scheduled (stream) transport only");
@@ -454,6 +500,7 @@ class WorkerCore final : public EngineHost {
     bool stream_wait;
   };
   std::unordered_map<int32_t, Prebound> pre_;
+  std::unique_ptr<IpcLane> ipc_pending_;  // created by ipc_handle, moved into the link by ipc_open
   std::vector<int32_t> fast_delivered_;
 
   py::object host_;
@@ -552,6 +599,11 @@ PYBIND11_MODULE(_native, m) {
       .def("set_lane", &WorkerCore::set_lane)
       .def("set_graphs", &WorkerCore::set_graphs)
       .def("set_exact_unit_bytes", &WorkerCore::set_exact_unit_bytes)
+      .def("connect_none", &WorkerCore::connect_none)
+      .def("ipc_handle", &WorkerCore::ipc_handle)
+      .def("ipc_open", &WorkerCore::ipc_open)
+      .def("ipc_error", &WorkerCore::ipc_error)
+      .def("ipc_close", &WorkerCore::ipc_close)
       .def("scatter_count", &WorkerCore::scatter_count)
       .def("reduced_arrivals", &WorkerCore::reduced_arrivals);
 

@@ -1,0 +1,270 @@
+// gfx950 kernels of the one-sided xGMI exact round (ipc_kernels.h).
+//
+// Memory-model protocol (HIP / LLVM AMDGPU, system scope because producer and
+// consumer sit on different devices and the bytes cross xGMI):
+//   producer: its stores -> s_waitcnt vmcnt(0) in every wave -> workgroup
+//             barrier -> lane 0: release fence (system) -> s_waitcnt vmcnt(0)
+//             -> relaxed system-scope store (or add) of the flag word;
+//   consumer: lane 0 polls the flag with relaxed system-scope loads (with
+//             s_sleep) -> acquire fence (system) -> s_waitcnt vmcnt(0) ->
+//             workgroup barrier -> plain loads of the payload.
+// The explicit s_waitcnt after the release fence is there on purpose: the
+// compiler may drop its own when it proves the scoreboard empty, letting the
+// flag overtake the write-back (MI355X_MICROARCH.md, compiler hazard).
+// Every wait is bounded (wall clock, `timeout` ticks): on expiry the waiting
+// workgroup sets the window's error word, skips its data work and still
+// signals, so every grid drains and no GPU is ever left spinning; the round is
+// then reported as failed (IpcLane::error) and must not be trusted.
+#include <hip/hip_runtime.h>
+
+#include "ipc_kernels.h"
+
+namespace akka {
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kUnroll = 4;       // 16-B vectors per thread per source in flight
+constexpr int kReduceSplit = 4;  // workgroups per portion in the reduce kernel
+
+__device__ inline bool reached(uint32_t v, uint32_t want) { return int32_t(v - want) >= 0; }
+
+__device__ inline uint32_t sys_load(uint32_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Lane 0 only.  true once *f reached `want`; false on timeout or when another
+// workgroup already reported one (err != 0).
+__device__ bool wait_flag(uint32_t* f, uint32_t want, uint32_t* err, uint64_t deadline) {
+  uint32_t spins = 0;
+  while (true) {
+    if (reached(sys_load(f), want)) return true;
+    if ((++spins & 63) == 0) {
+      if (sys_load(err) != 0) return false;
+      if (wall_clock64() > deadline) {
+        __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return false;
+      }
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+
+// Whole workgroup: publish this workgroup's stores, then set (add) the flag.
+__device__ inline void publish(uint32_t* f, uint32_t v, bool add) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (add) __hip_atomic_fetch_add(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    else __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// Whole workgroup: acquire after lane 0's successful waits.  Returns the
+// shared verdict.
+__device__ inline bool acquire_all(bool ok_lane0) {
+  __shared__ int ok;
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    ok = ok_lane0 ? 1 : 0;
+  }
+  __syncthreads();
+  return ok != 0;
+}
+
+__device__ void copy_bytes(char* __restrict__ dst, const char* __restrict__ src, int64_t bytes) {
+  if (((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src) | uintptr_t(bytes)) & 15) == 0) {
+    const uint4* s = reinterpret_cast<const uint4*>(src);
+    uint4* d = reinterpret_cast<uint4*>(dst);
+    const int64_t n = bytes >> 4;
+    int64_t i = threadIdx.x;
+    for (; i + (kUnroll - 1) * kThreads < n; i += kUnroll * kThreads) {
+      uint4 v[kUnroll];
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) v[u] = s[i + u * kThreads];
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) d[i + u * kThreads] = v[u];
+    }
+    for (; i < n; i += kThreads) d[i] = s[i];
+  } else {
+    for (int64_t i = threadIdx.x; i < bytes; i += kThreads) dst[i] = src[i];
+  }
+}
+
+__device__ inline float bf16_to_f32(uint16_t h) { return __uint_as_float(uint32_t(h) << 16); }
+__device__ inline uint16_t f32_to_bf16(float f) {
+  const uint32_t u = __float_as_uint(f);
+  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x007fffffu)) return uint16_t((u >> 16) | 0x40);  // quiet NaN
+  return uint16_t((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+
+template <typename T>
+struct Elt;
+template <>
+struct Elt<float> {
+  static constexpr int kPerVec = 4;
+  __device__ static void add(float* acc, const uint4& v) {
+    acc[0] += __uint_as_float(v.x);
+    acc[1] += __uint_as_float(v.y);
+    acc[2] += __uint_as_float(v.z);
+    acc[3] += __uint_as_float(v.w);
+  }
+  __device__ static uint4 pack(const float* acc) {
+    return make_uint4(__float_as_uint(acc[0]), __float_as_uint(acc[1]), __float_as_uint(acc[2]),
+                      __float_as_uint(acc[3]));
+  }
+  __device__ static float load1(const char* p) { return *reinterpret_cast<const float*>(p); }
+  __device__ static void store1(char* p, float v) { *reinterpret_cast<float*>(p) = v; }
+};
+template <>
+struct Elt<uint16_t> {
+  static constexpr int kPerVec = 8;
+  __device__ static void add(float* acc, const uint4& v) {
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      acc[2 * i] += __uint_as_float(w[i] << 16);
+      acc[2 * i + 1] += __uint_as_float(w[i] & 0xffff0000u);
+    }
+  }
+  __device__ static uint4 pack(const float* acc) {
+    uint32_t w[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) w[i] = uint32_t(f32_to_bf16(acc[2 * i])) | (uint32_t(f32_to_bf16(acc[2 * i + 1])) << 16);
+    return make_uint4(w[0], w[1], w[2], w[3]);
+  }
+  __device__ static float load1(const char* p) { return bf16_to_f32(*reinterpret_cast<const uint16_t*>(p)); }
+  __device__ static void store1(char* p, float v) { *reinterpret_cast<uint16_t*>(p) = f32_to_bf16(v); }
+};
+
+// Sum of the N sources of `n` elements, ascending source rank (source `me`
+// is the round input, the others are window slots), to `o` and `r`.
+template <typename T>
+__device__ void reduce_span(const IpcArgs& a, const char* mine, const char* slots, int64_t slot_bytes, char* o,
+                            char* r, int64_t n) {
+  constexpr int ES = sizeof(T);
+  constexpr int PV = Elt<T>::kPerVec;
+  const int N = a.N, me = a.me;
+  bool vec = ((uintptr_t(mine) | uintptr_t(slots) | uintptr_t(slot_bytes) | uintptr_t(o) | uintptr_t(r) |
+               uintptr_t(n * ES)) & 15) == 0;
+  if (vec) {
+    const int64_t nv = n / PV;
+    for (int64_t i0 = threadIdx.x; i0 < nv; i0 += kUnroll * kThreads) {
+      float acc[kUnroll][PV];
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u)
+#pragma unroll
+        for (int e = 0; e < PV; ++e) acc[u][e] = 0.f;
+      for (int s = 0; s < N; ++s) {
+        const uint4* src = reinterpret_cast<const uint4*>(s == me ? mine : slots + int64_t(s) * slot_bytes);
+        uint4 v[kUnroll];
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) {
+          const int64_t i = i0 + int64_t(u) * kThreads;
+          v[u] = i < nv ? src[i] : make_uint4(0, 0, 0, 0);
+        }
+#pragma unroll
+        for (int u = 0; u < kUnroll; ++u) Elt<T>::add(acc[u], v[u]);
+      }
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) {
+        const int64_t i = i0 + int64_t(u) * kThreads;
+        if (i < nv) {
+          const uint4 w = Elt<T>::pack(acc[u]);
+          reinterpret_cast<uint4*>(o)[i] = w;
+          reinterpret_cast<uint4*>(r)[i] = w;
+        }
+      }
+    }
+  } else {
+    for (int64_t i = threadIdx.x; i < n; i += kThreads) {
+      float acc = 0.f;
+      for (int s = 0; s < N; ++s) acc += Elt<T>::load1((s == me ? mine : slots + int64_t(s) * slot_bytes) + i * ES);
+      Elt<T>::store1(o + i * ES, acc);
+      Elt<T>::store1(r + i * ES, acc);
+    }
+  }
+}
+
+// grid (nportions, N-1): portion j of my input's block p -> rank p's slot [me].
+template <int ES>
+__global__ __launch_bounds__(kThreads) void ipc_push_kernel(IpcArgs a) {
+  const int32_t j = blockIdx.x;
+  const int32_t p = (a.me + 1 + int32_t(blockIdx.y)) % a.N;
+  const int64_t e0 = int64_t(j) * a.portion;
+  const int64_t n = max(int64_t(0), min(a.portion, a.blen[p] - e0));
+  if (n > 0)
+    copy_bytes(a.data[p] + (int64_t(a.me) * a.slot + e0) * ES, a.in + (a.bstart[p] + e0) * ES, n * ES);
+  publish(a.flags[p] + ipc_flag_push(a.me, j, a.nportions), a.round, false);
+}
+
+// grid (nportions * kReduceSplit): wait for portion j of every peer's push,
+// sum, write my output block and my `reduced` row, add 1 to reduced[j].
+template <typename T>
+__global__ __launch_bounds__(kThreads) void ipc_reduce_kernel(IpcArgs a) {
+  constexpr int ES = sizeof(T);
+  const int32_t j = blockIdx.x / kReduceSplit;
+  const int32_t part = blockIdx.x % kReduceSplit;
+  const int32_t me = a.me;
+  uint32_t* fl = a.flags[me];
+  uint32_t* err = fl + ipc_flag_error(a.N, a.nportions);
+  bool ok = true;
+  if (threadIdx.x == 0) {
+    const uint64_t deadline = wall_clock64() + a.timeout;
+    for (int32_t s = 0; s < a.N && ok; ++s)
+      if (s != me) ok = wait_flag(fl + ipc_flag_push(s, j, a.nportions), a.round, err, deadline);
+  }
+  ok = acquire_all(ok);
+  const int64_t e0 = int64_t(j) * a.portion;
+  const int64_t n = max(int64_t(0), min(a.portion, a.blen[me] - e0));
+  // this workgroup's part of the portion (a multiple of 64 elements)
+  const int64_t per = ((a.portion / kReduceSplit) + 63) / 64 * 64;
+  const int64_t p0 = min(n, part * per), p1 = min(n, p0 + per);
+  if (ok && p1 > p0) {
+    const int64_t e = e0 + p0;
+    reduce_span<T>(a, a.in + (a.bstart[me] + e) * ES, a.data[me] + e * ES, a.slot * ES,
+                   a.out + (a.bstart[me] + e) * ES, a.data[me] + (int64_t(a.N) * a.slot + e) * ES, p1 - p0);
+  }
+  publish(fl + ipc_flag_reduced(j, a.N, a.nportions), 1u, true);
+}
+
+// grid (nportions, N-1): wait for rank p's reduced portion j, copy it into my
+// output's block p.
+template <int ES>
+__global__ __launch_bounds__(kThreads) void ipc_pull_kernel(IpcArgs a) {
+  const int32_t j = blockIdx.x;
+  const int32_t p = (a.me + 1 + int32_t(blockIdx.y)) % a.N;
+  uint32_t* err = a.flags[a.me] + ipc_flag_error(a.N, a.nportions);
+  bool ok = true;
+  if (threadIdx.x == 0) {
+    const uint64_t deadline = wall_clock64() + a.timeout;
+    ok = wait_flag(a.flags[p] + ipc_flag_reduced(j, a.N, a.nportions), a.round * uint32_t(kReduceSplit), err,
+                   deadline);
+  }
+  ok = acquire_all(ok);
+  const int64_t e0 = int64_t(j) * a.portion;
+  const int64_t n = max(int64_t(0), min(a.portion, a.blen[p] - e0));
+  if (ok && n > 0)
+    copy_bytes(a.out + (a.bstart[p] + e0) * ES, a.data[p] + (int64_t(a.N) * a.slot + e0) * ES, n * ES);
+}
+
+template <typename T>
+void launch_round(hipStream_t s, const IpcArgs& a) {
+  constexpr int ES = sizeof(T);
+  const dim3 peers(unsigned(a.nportions), unsigned(a.N - 1));
+  hipLaunchKernelGGL(ipc_push_kernel<ES>, peers, dim3(kThreads), 0, s, a);
+  hipLaunchKernelGGL(ipc_reduce_kernel<T>, dim3(unsigned(a.nportions * kReduceSplit)), dim3(kThreads), 0, s, a);
+  hipLaunchKernelGGL(ipc_pull_kernel<ES>, peers, dim3(kThreads), 0, s, a);
+}
+
+}  // namespace
+
+void launch_ipc_round(hipStream_t s, const IpcArgs& a, DType dt) {
+  if (a.N < 2) return;
+  if (dt == DType::F32) launch_round<float>(s, a);
+  else launch_round<uint16_t>(s, a);
+}
+
+}  // namespace akka

@@ -1,0 +1,158 @@
+// IpcLane host side: windows, handle exchange, round launch (ipc_lane.h).
+#include "ipc_lane.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+
+#include "../kernels/ipc_kernels.h"
+
+namespace akka {
+
+#define AKKA_IPC_HIP(call)                                                                   \
+  do {                                                                                       \
+    hipError_t e_ = (call);                                                                  \
+    if (e_ != hipSuccess)                                                                    \
+      throw AkkaError(std::string("akka ipc: ") + #call + " failed: " + hipGetErrorString(e_)); \
+  } while (0)
+
+namespace {
+
+constexpr char kMagic[8] = {'A', 'K', 'I', 'P', 'C', '0', '1', 0};
+
+struct HandleBlob {  // what handle() serialises
+  char magic[8];
+  int32_t rank, nranks, esize, pad;
+  int64_t S, slot, portion;
+  hipIpcMemHandle_t data, flags;
+};
+
+int64_t env_i64(const char* name, int64_t dflt) {
+  const char* v = std::getenv(name);
+  return v && *v ? std::atoll(v) : dflt;
+}
+
+}  // namespace
+
+IpcLane::IpcLane(Device* dev, const Geometry& g, int32_t me, DType dt)
+    : dev_(dev), g_(g), me_(me), dt_(dt), es_(dtype_size(dt)) {
+  AKKA_CHECK(dev_ && !dev_->is_host(), "ipc lane needs a HIP device");
+  AKKA_CHECK(g_.N >= 2 && g_.N <= kIpcMaxRanks, "ipc lane: 2..16 ranks");
+  AKKA_CHECK(me_ >= 0 && me_ < g_.N, "ipc lane: rank out of range");
+  AKKA_IPC_HIP(hipSetDevice(dev_->device_index()));
+  int64_t maxb = 0;
+  for (int32_t p = 0; p < g_.N; ++p) maxb = std::max(maxb, g_.block_len(p));
+  slot_ = std::max<int64_t>(64, (maxb + 63) / 64 * 64);
+  // Portion: the unit one producer workgroup hands to one consumer workgroup
+  // (AKKA_IPC_PORTION_BYTES, default 128 KiB; whole 1024-element multiples).
+  const int64_t pbytes = std::max<int64_t>(4096, env_i64("AKKA_IPC_PORTION_BYTES", int64_t(128) << 10));
+  portion_ = std::max<int64_t>(1024, (pbytes / int64_t(es_)) / 1024 * 1024);
+  nportions_ = int32_t(std::max<int64_t>(1, (maxb + portion_ - 1) / portion_));
+  data_bytes_ = size_t(g_.N + 1) * size_t(slot_) * es_;
+  flag_bytes_ = ipc_flag_bytes(g_.N, nportions_);
+  AKKA_IPC_HIP(hipMalloc(reinterpret_cast<void**>(&data_), data_bytes_));
+  // Flags uncached: every poll and every signal goes to memory.
+  if (hipExtMallocWithFlags(reinterpret_cast<void**>(&flags_), flag_bytes_, hipDeviceMallocUncached) != hipSuccess) {
+    (void)hipGetLastError();
+    AKKA_IPC_HIP(hipMalloc(reinterpret_cast<void**>(&flags_), flag_bytes_));
+  }
+  AKKA_IPC_HIP(hipMemset(flags_, 0, flag_bytes_));
+  AKKA_IPC_HIP(hipDeviceSynchronize());
+  int khz = 0;
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev_->device_index()) != hipSuccess || khz <= 0)
+    khz = 100000;  // 100 MHz
+  timeout_ticks_ = uint64_t(std::max<int64_t>(1, env_i64("AKKA_IPC_TIMEOUT_MS", 10000))) * uint64_t(khz);
+  peer_data_.assign(size_t(g_.N), nullptr);
+  peer_flags_.assign(size_t(g_.N), nullptr);
+  peer_data_[size_t(me_)] = data_;
+  peer_flags_[size_t(me_)] = flags_;
+}
+
+IpcLane::~IpcLane() {
+  hipSetDevice(dev_->device_index());
+  hipDeviceSynchronize();  // no kernel of ours may still touch a window
+  for (int32_t p = 0; p < g_.N; ++p) {
+    if (p == me_) continue;
+    if (peer_data_[size_t(p)]) hipIpcCloseMemHandle(peer_data_[size_t(p)]);
+    if (peer_flags_[size_t(p)]) hipIpcCloseMemHandle(peer_flags_[size_t(p)]);
+  }
+  if (data_) hipFree(data_);
+  if (flags_) hipFree(flags_);
+}
+
+std::string IpcLane::handle() const {
+  HandleBlob b;
+  std::memset(&b, 0, sizeof(b));
+  std::memcpy(b.magic, kMagic, sizeof(kMagic));
+  b.rank = me_;
+  b.nranks = g_.N;
+  b.esize = int32_t(es_);
+  b.S = g_.S;
+  b.slot = slot_;
+  b.portion = portion_;
+  AKKA_IPC_HIP(hipIpcGetMemHandle(&b.data, data_));
+  AKKA_IPC_HIP(hipIpcGetMemHandle(&b.flags, flags_));
+  return std::string(reinterpret_cast<const char*>(&b), sizeof(b));
+}
+
+void IpcLane::open(const std::vector<std::string>& handles) {
+  AKKA_CHECK(!ready_, "ipc lane: windows already open");
+  AKKA_CHECK(int32_t(handles.size()) == g_.N, "ipc lane: need one handle per rank");
+  AKKA_IPC_HIP(hipSetDevice(dev_->device_index()));
+  for (int32_t p = 0; p < g_.N; ++p) {
+    const std::string& h = handles[size_t(p)];
+    AKKA_CHECK(h.size() == sizeof(HandleBlob), "ipc lane: malformed handle");
+    HandleBlob b;
+    std::memcpy(&b, h.data(), sizeof(b));
+    AKKA_CHECK(std::memcmp(b.magic, kMagic, sizeof(kMagic)) == 0, "ipc lane: not an ipc window handle");
+    AKKA_CHECK(b.rank == p && b.nranks == g_.N && b.esize == int32_t(es_) && b.S == g_.S && b.slot == slot_ &&
+                   b.portion == portion_,
+               "ipc lane: rank " + std::to_string(p) + "'s window was built for another geometry");
+    if (p == me_) continue;
+    void* d = nullptr;
+    void* f = nullptr;
+    AKKA_IPC_HIP(hipIpcOpenMemHandle(&d, b.data, hipIpcMemLazyEnablePeerAccess));
+    AKKA_IPC_HIP(hipIpcOpenMemHandle(&f, b.flags, hipIpcMemLazyEnablePeerAccess));
+    peer_data_[size_t(p)] = static_cast<char*>(d);
+    peer_flags_[size_t(p)] = static_cast<uint32_t*>(f);
+  }
+  ready_ = true;
+}
+
+void IpcLane::round(StreamH s, const void* in, void* out) {
+  AKKA_CHECK(ready_, "ipc lane: open() the peer windows first");
+  IpcArgs a;
+  std::memset(&a, 0, sizeof(a));
+  for (int32_t p = 0; p < g_.N; ++p) {
+    a.data[p] = peer_data_[size_t(p)];
+    a.flags[p] = peer_flags_[size_t(p)];
+    a.bstart[p] = g_.block_start(p);
+    a.blen[p] = g_.block_len(p);
+  }
+  a.slot = slot_;
+  a.portion = portion_;
+  a.nportions = nportions_;
+  a.N = g_.N;
+  a.me = me_;
+  a.round = ++round_;
+  a.timeout = timeout_ticks_;
+  a.in = static_cast<const char*>(in);
+  a.out = static_cast<char*>(out);
+  launch_ipc_round(static_cast<hipStream_t>(s), a, dt_);
+  AKKA_IPC_HIP(hipGetLastError());
+  ++stats_.rounds;
+  stats_.bytes_pushed += (g_.S - g_.block_len(me_)) * int64_t(es_);
+  stats_.bytes_pulled += (g_.S - g_.block_len(me_)) * int64_t(es_);
+}
+
+uint32_t IpcLane::error() {
+  uint32_t v = 0;
+  AKKA_IPC_HIP(hipSetDevice(dev_->device_index()));
+  AKKA_IPC_HIP(hipDeviceSynchronize());  // the rounds enqueued so far have drained
+  AKKA_IPC_HIP(hipMemcpy(&v, flags_ + ipc_flag_error(g_.N, nportions_), sizeof(v), hipMemcpyDeviceToHost));
+  return v;
+}
+
+}  // namespace akka

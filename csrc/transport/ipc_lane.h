@@ -1,0 +1,77 @@
+// IpcLane: exact rounds as one-sided xGMI loads/stores between the GPUs of a
+// node (kernels: csrc/kernels/ipc.hip, protocol in ipc_kernels.h).
+//
+// Why a lane of its own: on one node every MI355X maps every other one's HBM
+// over xGMI, so an exact round (thresholds 1, every chunk from every peer)
+// needs no message matching at all.  Each rank owns a window
+//   [slot 0 | slot 1 | ... | slot N-1 | reduced]      (each slot >= one block)
+// plus a small flag area (uncached).  Rank q pushes block p of its input into
+// slot q of rank p's window, rank p sums its N slots into its output block and
+// `reduced` row, and every rank pulls the reduced rows of the others -- all
+// seven links of a rank busy in both phases, driven by the CUs, with round-id
+// flags per portion instead of RCCL groups: three kernel launches per round
+// and no host work beyond them.  The reference's scatter / reduce / broadcast
+// (W:212-268) for the exact case; thresholds < 1 keep the p2p schedule.
+//
+// Setup is collective: every rank creates its window (handle()), the handles
+// are exchanged out of band (torch.distributed, any backend) and every rank
+// opens the others' (open()).  Rounds are numbered 1, 2, ... per lane: every
+// rank must run the same exact rounds on this lane, in the same order (the
+// same contract as the other lanes).  Waits inside the kernels are bounded:
+// a missing peer turns into error() != 0, never a hung GPU.
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../engine/device.h"
+#include "../engine/geometry.h"
+
+namespace akka {
+
+struct IpcLaneStats {
+  int64_t rounds = 0, bytes_pushed = 0, bytes_pulled = 0;
+};
+
+class IpcLane {
+ public:
+  IpcLane(Device* dev, const Geometry& g, int32_t me, DType dt);
+  ~IpcLane();
+  IpcLane(const IpcLane&) = delete;
+  IpcLane& operator=(const IpcLane&) = delete;
+
+  // This rank's window handle (data + flags), with the geometry it was built for.
+  std::string handle() const;
+  // Open every other rank's window; handles[i] is rank i's handle().
+  void open(const std::vector<std::string>& handles);
+  bool ready() const { return ready_; }
+  // Enqueue one exact round on `s`: in[S] from every rank summed into out[S].
+  void round(StreamH s, const void* in, void* out);
+  // Synchronous read of the window's error word (a wait timed out).
+  uint32_t error();
+  int32_t nportions() const { return nportions_; }
+  int64_t portion_elems() const { return portion_; }
+  size_t window_bytes() const { return data_bytes_; }
+  const IpcLaneStats& stats() const { return stats_; }
+
+ private:
+  Device* dev_;
+  Geometry g_;
+  int32_t me_;
+  DType dt_;
+  size_t es_;
+  int64_t slot_ = 0, portion_ = 0;
+  int32_t nportions_ = 0;
+  size_t data_bytes_ = 0, flag_bytes_ = 0;
+  char* data_ = nullptr;
+  uint32_t* flags_ = nullptr;
+  std::vector<char*> peer_data_;      // [N] mapped windows (own = data_)
+  std::vector<uint32_t*> peer_flags_; // [N]
+  uint32_t round_ = 0;
+  uint64_t timeout_ticks_ = 0;
+  bool ready_ = false;
+  IpcLaneStats stats_;
+};
+
+}  // namespace akka

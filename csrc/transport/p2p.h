@@ -81,6 +81,22 @@ class P2P {
   }
 };
 
+// No two-sided transport: a job whose exact rounds all run on the one-sided
+// ipc lane (ipc_lane.h).  Any message-driven schedule fails loudly.
+class NullP2P final : public P2P {
+ public:
+  NullP2P(int32_t rank, int32_t nranks) : rank_(rank), nranks_(nranks) {}
+  int32_t rank() const override { return rank_; }
+  int32_t nranks() const override { return nranks_; }
+  void group(StreamH, const std::vector<P2POp>&) override {
+    throw AkkaError("akka: this job has no p2p transport (ipc-only data plane): only exact rounds on the ipc lane");
+  }
+  const char* name() const override { return "none"; }
+
+ private:
+  int32_t rank_, nranks_;
+};
+
 // ---- CPU simulator ------------------------------------------------------------
 class SimHub;
 std::shared_ptr<SimHub> make_sim_hub(int32_t nranks);

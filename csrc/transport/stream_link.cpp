@@ -210,13 +210,33 @@ bool StreamLink::bulk_round(int32_t r) {
   if (N < 2) return false;  // a local round is already one pass
   AKKA_CHECK(p2p_->nranks() == N && p2p_->rank() == dp_->me(), "p2p communicator does not match the worker geometry");
   const bool native = p2p_->has_collectives() && g.S == int64_t(N) * g.step;
-  if (lane_ == Lane::Collective || (lane_ == Lane::Auto && native)) collective_round(r, native);
+  if (lane_ == Lane::Ipc) ipc_round(r);
+  else if (lane_ == Lane::Collective || (lane_ == Lane::Auto && native)) collective_round(r, native);
   else exact_steps(r);
   p2p_->check();
   stats_.rounds++;
   stats_.bulk_rounds++;
   mark_scheduled(r);
   return true;
+}
+
+void StreamLink::set_ipc(std::unique_ptr<IpcLane> ipc) {
+  if (ipc_ && dp_) dp_->device()->sync_stream(dp_->device()->comm_stream());
+  ipc_ = std::move(ipc);
+}
+
+void StreamLink::ipc_round(int32_t r) {
+  AKKA_CHECK(ipc_ && ipc_->ready(), "ipc lane selected but its windows are not open (ipc_open)");
+  Device* dev = dp_->device();
+  engine_->ensure_output(r);
+  StreamH comm = dev->comm_stream();
+  dp_->comm_wait(dp_->row_release_event(r));
+  dp_->wait_input(r, comm);
+  dp_->mark_comm_used(r);
+  ipc_->round(comm, dp_->input_chunk(r, 0, 0).ptr, dp_->output_at(r, 0, 0));
+  const Geometry& g = dp_->geometry();
+  stats_.bytes_sent += int64_t(2) * (g.S - g.block_len(dp_->me())) * int64_t(dp_->esize());
+  ++stats_.ipc_rounds;
 }
 
 void StreamLink::collective_round(int32_t r, bool native) {

@@ -30,6 +30,7 @@
 #include <tuple>
 
 #include "../engine/engine.h"
+#include "ipc_lane.h"
 #include "p2p.h"
 
 namespace akka {
@@ -39,6 +40,7 @@ struct StreamLinkStats {
   // bulk rounds by lane: collective = RCCL reduce-scatter + all-gather or the
   // whole-block exchange; exact_step_rounds = the exact p2p step template
   int64_t bulk_rounds = 0, collective_rounds = 0, exact_step_rounds = 0, graph_captures = 0, graph_replays = 0;
+  int64_t ipc_rounds = 0;
 };
 
 // Which schedule runs an exact-threshold round (thReduce = thComplete = 1):
@@ -48,7 +50,9 @@ struct StreamLinkStats {
 //             whole-block direct exchange (one grouped p2p per phase around
 //             one N-way reduce);
 //  Auto       Collective when the transport has native collectives and the
-//             geometry is even, else P2P.
+//             geometry is even, else P2P;
+//  Ipc        one-sided xGMI loads/stores between mapped windows (ipc_lane.h),
+//             once set_ipc() handed the link an opened IpcLane.
 // Exact rounds never go through the engine's per-chunk message flow: their
 // outcome is fixed (every chunk = sum of all N, count N), so the link runs
 // them from a per-geometry op template with no engine callbacks, no op maps
@@ -56,7 +60,7 @@ struct StreamLinkStats {
 // message-driven step schedule (schedule()).  Which path a round takes is a
 // function of the round's parameters only, identical on every rank (the
 // schedules must match pairwise).
-enum class Lane : int32_t { Auto = 0, P2P = 1, Collective = 2 };
+enum class Lane : int32_t { Auto = 0, P2P = 1, Collective = 2, Ipc = 3 };
 
 class StreamLink final : public Link {
  public:
@@ -73,6 +77,9 @@ class StreamLink final : public Link {
   bool takes_exact_rounds() const override { return dp_ && dp_->geometry().N > 1; }
 
   void set_lane(Lane l) { lane_ = l; }
+  // The one-sided lane's windows (created + opened by the caller); nullptr drops it.
+  void set_ipc(std::unique_ptr<IpcLane> ipc);
+  IpcLane* ipc() const { return ipc_.get(); }
   // Replay exact p2p-lane rounds from captured HIP graphs (off by default).
   void set_graphs(bool on);
   bool graphs() const { return graphs_; }
@@ -118,6 +125,8 @@ class StreamLink final : public Link {
   int64_t exact_groups_ = 0, exact_ops_ = 0, exact_bytes_ = 0;
   std::string graph_error_;
   void collective_round(int32_t round, bool native);
+  void ipc_round(int32_t round);
+  std::unique_ptr<IpcLane> ipc_;
   std::vector<std::vector<OpT>> exact_;  // [step] -> ops
   Geometry gx_;                          // exact rounds' transfer units (unit_chunks_ chunks each)
   int32_t unit_chunks_ = 1;

@@ -1,0 +1,81 @@
+"""Rank program for tests/test_ipc_gpu.py (run under torch.distributed.run):
+every rank of the job drives the SAME GPU (a 1-GPU box), with the ipc-only data
+plane -- windows in one process's HBM mapped into the others through IPC
+handles, so the push / reduce / pull kernels, their round-id flags and the
+cross-process hand-offs run for real (cross-XCD, not cross-xGMI).  Prints one
+JSON line per rank."""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+
+def expected(S, world, r, dtype, g_seed):
+    acc = None
+    for src in range(world):
+        x = torch.randn(S, generator=torch.Generator().manual_seed(g_seed * 1000 + src * 7 + r), dtype=torch.float32)
+        x = x.to(dtype).float()
+        acc = x if acc is None else acc + x  # ascending source rank, fp32 (the kernel's order)
+    return acc.to(dtype)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--size", type=int, default=1 << 20)
+    ap.add_argument("--rounds", type=int, default=4)
+    ap.add_argument("--dtype", default="float32")
+    ap.add_argument("--skip-rank", type=int, default=-1, help="this rank runs only round 0 (a missing peer)")
+    ap.add_argument("--time", action="store_true")
+    a = ap.parse_args()
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    dist.init_process_group("gloo")
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dtype = torch.float32 if a.dtype == "float32" else torch.bfloat16
+    from akka_allreduce_amd.parallel import ThresholdAllreduce
+
+    ar = ThresholdAllreduce(a.size, max_chunk_size=max(1, a.size // 16), dtype=dtype, device=dev, data_plane="ipc")
+    res = {"rank": rank, "exact": [], "lane": ar.state()["link"]["lane"]}
+    for r in range(a.rounds):
+        if r > 0 and rank == a.skip_rank:
+            break
+        x = torch.randn(a.size, generator=torch.Generator().manual_seed(5 * 1000 + rank * 7 + r),
+                        dtype=torch.float32).to(dtype).to(dev)
+        o = ar(x)
+        torch.cuda.synchronize()
+        want = expected(a.size, world, r, dtype, 5)
+        res["exact"].append(bool(torch.equal(o.data.cpu(), want)) and bool((o.count.cpu() == world).all()))
+    res["ipc_error"] = ar.ipc_error()
+    st = ar.state()["link"]
+    res["ipc_rounds"] = st["ipc_rounds"]
+    res["ipc"] = st.get("ipc")
+    if a.time and a.skip_rank < 0:
+        x = torch.randn(a.size, device=dev).to(dtype)
+        out = torch.empty_like(x)
+        for _ in range(3):
+            ar(x, out=out)
+        torch.cuda.synchronize()
+        dist.barrier()
+        import time
+
+        t0 = time.perf_counter()
+        k = 10
+        for _ in range(k):
+            ar(x, out=out)
+        torch.cuda.synchronize()
+        dist.barrier()
+        res["ms_per_round"] = (time.perf_counter() - t0) / k * 1e3
+    print(json.dumps(res), flush=True)
+    # every rank's kernels have drained (ipc_error synchronised) before any
+    # window is released
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,62 @@
+"""The one-sided xGMI lane (csrc/transport/ipc_lane.h, csrc/kernels/ipc.hip)
+with real processes: 2-3 ranks share the one GPU of the box, each maps the
+others' windows through IPC handles, and every round is checked bitwise
+against the fp32 sum in ascending source order (the kernel's order) on the
+CPU.  Covers even/uneven geometries (vector and scalar paths), bf16, empty
+blocks, and a missing peer: the bounded waits turn it into ipc_error != 0 on
+the others instead of a hung GPU."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.gpu
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run(n, *extra, env=None, timeout=180):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "tests", "ipc_ranks.py"), *extra]
+    e = dict(os.environ)
+    e.update(env or {})
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=ROOT, env=e)
+    rows = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")]
+    return r, sorted(rows, key=lambda d: d["rank"])
+
+
+@pytest.mark.parametrize("n,size,dtype", [
+    (2, 1 << 20, "float32"),      # even blocks: 16-B vector paths
+    (3, 1 << 20, "float32"),      # 3 blocks of 349526/349525/349525: scalar paths
+    (2, 3 * (1 << 18) + 8, "bfloat16"),
+    (3, 2, "float32"),            # S < N: an empty block
+    (2, 5 << 20, "float32"),      # several portions per block
+])
+def test_ipc_lane_exact(n, size, dtype):
+    r, rows = _run(n, "--size", str(size), "--dtype", dtype, "--rounds", "4")
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert len(rows) == n
+    for d in rows:
+        assert d["lane"] == "ipc" and d["ipc_error"] == 0, d
+        assert d["exact"] == [True] * 4, d
+        assert d["ipc_rounds"] == 4 and d["ipc"]["rounds"] == 4
+
+
+def test_ipc_lane_missing_peer_times_out_cleanly():
+    """Rank 1 leaves after round 0: rank 0's round 1 waits (bounded, 0.5 s)
+    for rank 1's flags, reports ipc_error and the job still ends."""
+    r, rows = _run(2, "--size", str(1 << 16), "--rounds", "2", "--skip-rank", "1",
+                   env={"AKKA_IPC_TIMEOUT_MS": "500"})
+    assert r.returncode == 0, r.stderr[-3000:]
+    d0 = rows[0]
+    assert d0["exact"][0] is True and d0["ipc_error"] != 0, d0
+    assert rows[1]["exact"] == [True]

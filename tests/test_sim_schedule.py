@@ -326,3 +326,22 @@ def test_exact_unit_switch_between_rounds():
         got = cl.workers[0].state()["link"]["exact_unit_chunks"]
         if m is not None:
             assert got == m, (unit, got)
+
+
+def test_ipc_lane_needs_open_windows():
+    """set_lane('ipc') before the windows are mapped fails loudly (the ipc
+    lane itself runs on GPUs only: tests/test_ipc_gpu.py)."""
+    cl = SimCluster(2, 100, 10)
+    with pytest.raises(Exception, match="ipc"):
+        cl.workers[0].set_lane("ipc")
+    with pytest.raises(Exception, match="ipc"):
+        cl.workers[0].ipc_handle()  # host device: no HIP windows
+
+
+def test_ipc_data_plane_validation():
+    from akka_allreduce_amd.parallel import ThresholdAllreduce
+
+    with pytest.raises(ValueError, match="cuda"):
+        ThresholdAllreduce(16, rank=0, world_size=1, device=torch.device("cpu"), data_plane="ipc")
+    with pytest.raises(ValueError, match="exact"):
+        ThresholdAllreduce(16, rank=0, world_size=1, device=torch.device("cpu"), data_plane="ipc", th_reduce=0.5)
