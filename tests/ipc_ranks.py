@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--dtype", default="float32")
     ap.add_argument("--skip-rank", type=int, default=-1, help="this rank runs only round 0 (a missing peer)")
     ap.add_argument("--time", action="store_true")
+    ap.add_argument("--out-dir", default="", help="write rank<i>.json there (stdout lines of ranks interleave)")
     a = ap.parse_args()
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     dist.init_process_group("gloo")
@@ -70,7 +71,11 @@ def main():
         torch.cuda.synchronize()
         dist.barrier()
         res["ms_per_round"] = (time.perf_counter() - t0) / k * 1e3
-    print(json.dumps(res), flush=True)
+    if a.out_dir:
+        with open(os.path.join(a.out_dir, f"rank{rank}.json"), "w") as f:
+            json.dump(res, f)
+    else:
+        print(json.dumps(res), flush=True)
     # every rank's kernels have drained (ipc_error synchronised) before any
     # window is released
     dist.barrier()

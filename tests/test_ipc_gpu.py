@@ -10,6 +10,7 @@ import os
 import socket
 import subprocess
 import sys
+import tempfile
 
 import pytest
 
@@ -24,14 +25,20 @@ def _free_port() -> int:
 
 
 def _run(n, *extra, env=None, timeout=180):
-    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
-           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
-           os.path.join(ROOT, "tests", "ipc_ranks.py"), *extra]
-    e = dict(os.environ)
-    e.update(env or {})
-    r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=ROOT, env=e)
-    rows = [json.loads(ln) for ln in r.stdout.splitlines() if ln.startswith("{")]
-    return r, sorted(rows, key=lambda d: d["rank"])
+    with tempfile.TemporaryDirectory() as out:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+               os.path.join(ROOT, "tests", "ipc_ranks.py"), "--out-dir", out, *extra]
+        e = dict(os.environ)
+        e.update(env or {})
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=ROOT, env=e)
+        rows = []
+        for i in range(n):
+            path = os.path.join(out, f"rank{i}.json")
+            if os.path.exists(path):
+                with open(path) as f:
+                    rows.append(json.load(f))
+    return r, rows
 
 
 @pytest.mark.parametrize("n,size,dtype", [
