@@ -351,6 +351,8 @@ class WorkerCore final : public EngineHost {
         is["portions"] = ipc->nportions();
         is["portion_bytes"] = ipc->portion_elems() * int64_t(dtype_size(dt_));
         is["window_bytes"] = int64_t(ipc->window_bytes());
+        is["max_wgs"] = ipc->max_wgs();
+        is["ranks_on_this_gpu"] = ipc->ranks_on_this_gpu();
         is["rounds"] = ipc->stats().rounds;
         is["bytes_pushed"] = ipc->stats().bytes_pushed;
         is["bytes_pulled"] = ipc->stats().bytes_pulled;

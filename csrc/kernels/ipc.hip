@@ -17,6 +17,8 @@
 // then reported as failed (IpcLane::error) and must not be trusted.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "ipc_kernels.h"
 
 namespace akka {
@@ -200,54 +202,65 @@ __global__ __launch_bounds__(kThreads) void ipc_push_kernel(IpcArgs a) {
   publish(a.flags[p] + ipc_flag_push(a.me, j, a.nportions), a.round, false);
 }
 
-// grid (nportions * kReduceSplit): wait for portion j of every peer's push,
-// sum, write my output block and my `reduced` row, add 1 to reduced[j].
+// grid <= max_wgs, looping over (portion j, part) items: wait for portion j of
+// every peer's push, sum, write my output block and my `reduced` row, add 1 to
+// reduced[j].  The grid is capped so that workgroups parked on flags never
+// fill the machine (ranks sharing a card in tests need room for each other's
+// push kernels).
 template <typename T>
 __global__ __launch_bounds__(kThreads) void ipc_reduce_kernel(IpcArgs a) {
   constexpr int ES = sizeof(T);
-  const int32_t j = blockIdx.x / kReduceSplit;
-  const int32_t part = blockIdx.x % kReduceSplit;
   const int32_t me = a.me;
   uint32_t* fl = a.flags[me];
   uint32_t* err = fl + ipc_flag_error(a.N, a.nportions);
-  bool ok = true;
-  if (threadIdx.x == 0) {
-    const uint64_t deadline = wall_clock64() + a.timeout;
-    for (int32_t s = 0; s < a.N && ok; ++s)
-      if (s != me) ok = wait_flag(fl + ipc_flag_push(s, j, a.nportions), a.round, err, deadline);
-  }
-  ok = acquire_all(ok);
-  const int64_t e0 = int64_t(j) * a.portion;
-  const int64_t n = max(int64_t(0), min(a.portion, a.blen[me] - e0));
-  // this workgroup's part of the portion (a multiple of 64 elements)
+  const int32_t items = a.nportions * kReduceSplit;
+  // each item's part of its portion (a multiple of 64 elements)
   const int64_t per = ((a.portion / kReduceSplit) + 63) / 64 * 64;
-  const int64_t p0 = min(n, part * per), p1 = min(n, p0 + per);
-  if (ok && p1 > p0) {
-    const int64_t e = e0 + p0;
-    reduce_span<T>(a, a.in + (a.bstart[me] + e) * ES, a.data[me] + e * ES, a.slot * ES,
-                   a.out + (a.bstart[me] + e) * ES, a.data[me] + (int64_t(a.N) * a.slot + e) * ES, p1 - p0);
+  for (int32_t w = blockIdx.x; w < items; w += gridDim.x) {
+    const int32_t j = w / kReduceSplit;
+    const int32_t part = w % kReduceSplit;
+    bool ok = true;
+    if (threadIdx.x == 0) {
+      const uint64_t deadline = wall_clock64() + a.timeout;
+      for (int32_t s = 0; s < a.N && ok; ++s)
+        if (s != me) ok = wait_flag(fl + ipc_flag_push(s, j, a.nportions), a.round, err, deadline);
+    }
+    ok = acquire_all(ok);
+    const int64_t e0 = int64_t(j) * a.portion;
+    const int64_t n = max(int64_t(0), min(a.portion, a.blen[me] - e0));
+    const int64_t p0 = min(n, part * per), p1 = min(n, p0 + per);
+    if (ok && p1 > p0) {
+      const int64_t e = e0 + p0;
+      reduce_span<T>(a, a.in + (a.bstart[me] + e) * ES, a.data[me] + e * ES, a.slot * ES,
+                     a.out + (a.bstart[me] + e) * ES, a.data[me] + (int64_t(a.N) * a.slot + e) * ES, p1 - p0);
+    }
+    publish(fl + ipc_flag_reduced(j, a.N, a.nportions), 1u, true);  // ends with a workgroup barrier
   }
-  publish(fl + ipc_flag_reduced(j, a.N, a.nportions), 1u, true);
 }
 
-// grid (nportions, N-1): wait for rank p's reduced portion j, copy it into my
-// output's block p.
+// grid <= max_wgs, looping over (portion j, peer) items, peers interleaved so
+// every link is busy at once: wait for rank p's reduced portion j, copy it into
+// my output's block p.
 template <int ES>
 __global__ __launch_bounds__(kThreads) void ipc_pull_kernel(IpcArgs a) {
-  const int32_t j = blockIdx.x;
-  const int32_t p = (a.me + 1 + int32_t(blockIdx.y)) % a.N;
   uint32_t* err = a.flags[a.me] + ipc_flag_error(a.N, a.nportions);
-  bool ok = true;
-  if (threadIdx.x == 0) {
-    const uint64_t deadline = wall_clock64() + a.timeout;
-    ok = wait_flag(a.flags[p] + ipc_flag_reduced(j, a.N, a.nportions), a.round * uint32_t(kReduceSplit), err,
-                   deadline);
+  const int32_t items = a.nportions * (a.N - 1);
+  for (int32_t w = blockIdx.x; w < items; w += gridDim.x) {
+    const int32_t j = w / (a.N - 1);
+    const int32_t p = (a.me + 1 + w % (a.N - 1)) % a.N;
+    bool ok = true;
+    if (threadIdx.x == 0) {
+      const uint64_t deadline = wall_clock64() + a.timeout;
+      ok = wait_flag(a.flags[p] + ipc_flag_reduced(j, a.N, a.nportions), a.round * uint32_t(kReduceSplit), err,
+                     deadline);
+    }
+    ok = acquire_all(ok);
+    const int64_t e0 = int64_t(j) * a.portion;
+    const int64_t n = max(int64_t(0), min(a.portion, a.blen[p] - e0));
+    if (ok && n > 0)
+      copy_bytes(a.out + (a.bstart[p] + e0) * ES, a.data[p] + (int64_t(a.N) * a.slot + e0) * ES, n * ES);
+    __syncthreads();  // `ok` is rewritten by the next item
   }
-  ok = acquire_all(ok);
-  const int64_t e0 = int64_t(j) * a.portion;
-  const int64_t n = max(int64_t(0), min(a.portion, a.blen[p] - e0));
-  if (ok && n > 0)
-    copy_bytes(a.out + (a.bstart[p] + e0) * ES, a.data[p] + (int64_t(a.N) * a.slot + e0) * ES, n * ES);
 }
 
 template <typename T>
@@ -255,8 +268,11 @@ void launch_round(hipStream_t s, const IpcArgs& a) {
   constexpr int ES = sizeof(T);
   const dim3 peers(unsigned(a.nportions), unsigned(a.N - 1));
   hipLaunchKernelGGL(ipc_push_kernel<ES>, peers, dim3(kThreads), 0, s, a);
-  hipLaunchKernelGGL(ipc_reduce_kernel<T>, dim3(unsigned(a.nportions * kReduceSplit)), dim3(kThreads), 0, s, a);
-  hipLaunchKernelGGL(ipc_pull_kernel<ES>, peers, dim3(kThreads), 0, s, a);
+  const int32_t cap = a.max_wgs > 0 ? a.max_wgs : 1024;
+  hipLaunchKernelGGL(ipc_reduce_kernel<T>, dim3(unsigned(std::min(a.nportions * kReduceSplit, cap))), dim3(kThreads), 0,
+                     s, a);
+  hipLaunchKernelGGL(ipc_pull_kernel<ES>, dim3(unsigned(std::min(a.nportions * (a.N - 1), cap))), dim3(kThreads), 0, s,
+                     a);
 }
 
 }  // namespace

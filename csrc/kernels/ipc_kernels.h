@@ -31,6 +31,7 @@ struct IpcArgs {
   int64_t slot;       // elements per window slot (>= every block, 64-element multiple)
   int64_t portion;    // elements per portion (a multiple of 1024)
   int32_t nportions;  // portions per slot
+  int32_t max_wgs;    // grid cap of the kernels that wait (reduce, pull)
   int32_t N = 0, me = 0;
   uint32_t round = 0;       // this round's id (1, 2, ... identical on every rank)
   uint64_t timeout = 0;     // per wait, in wall-clock ticks (100 MHz)

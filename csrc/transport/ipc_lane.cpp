@@ -26,6 +26,7 @@ struct HandleBlob {  // what handle() serialises
   char magic[8];
   int32_t rank, nranks, esize, pad;
   int64_t S, slot, portion;
+  char bus[32];  // PCI bus id of the rank's GPU: ranks sharing a card (tests) share its CUs
   hipIpcMemHandle_t data, flags;
 };
 
@@ -92,6 +93,7 @@ std::string IpcLane::handle() const {
   b.S = g_.S;
   b.slot = slot_;
   b.portion = portion_;
+  AKKA_IPC_HIP(hipDeviceGetPCIBusId(b.bus, int(sizeof(b.bus)) - 1, dev_->device_index()));
   AKKA_IPC_HIP(hipIpcGetMemHandle(&b.data, data_));
   AKKA_IPC_HIP(hipIpcGetMemHandle(&b.flags, flags_));
   return std::string(reinterpret_cast<const char*>(&b), sizeof(b));
@@ -101,6 +103,9 @@ void IpcLane::open(const std::vector<std::string>& handles) {
   AKKA_CHECK(!ready_, "ipc lane: windows already open");
   AKKA_CHECK(int32_t(handles.size()) == g_.N, "ipc lane: need one handle per rank");
   AKKA_IPC_HIP(hipSetDevice(dev_->device_index()));
+  char mybus[32] = {};
+  AKKA_IPC_HIP(hipDeviceGetPCIBusId(mybus, int(sizeof(mybus)) - 1, dev_->device_index()));
+  int32_t sharers = 0;
   for (int32_t p = 0; p < g_.N; ++p) {
     const std::string& h = handles[size_t(p)];
     AKKA_CHECK(h.size() == sizeof(HandleBlob), "ipc lane: malformed handle");
@@ -110,6 +115,7 @@ void IpcLane::open(const std::vector<std::string>& handles) {
     AKKA_CHECK(b.rank == p && b.nranks == g_.N && b.esize == int32_t(es_) && b.S == g_.S && b.slot == slot_ &&
                    b.portion == portion_,
                "ipc lane: rank " + std::to_string(p) + "'s window was built for another geometry");
+    if (std::strncmp(b.bus, mybus, sizeof(mybus)) == 0) ++sharers;
     if (p == me_) continue;
     void* d = nullptr;
     void* f = nullptr;
@@ -118,6 +124,10 @@ void IpcLane::open(const std::vector<std::string>& handles) {
     peer_data_[size_t(p)] = static_cast<char*>(d);
     peer_flags_[size_t(p)] = static_cast<uint32_t*>(f);
   }
+  // Grid cap of the waiting kernels: their parked workgroups must leave room
+  // for the other ranks' push kernels when several ranks share one card.
+  max_wgs_ = int32_t(std::max<int64_t>(64, env_i64("AKKA_IPC_MAX_WGS", 1024) / std::max(1, sharers)));
+  sharers_ = sharers;
   ready_ = true;
 }
 
@@ -134,6 +144,7 @@ void IpcLane::round(StreamH s, const void* in, void* out) {
   a.slot = slot_;
   a.portion = portion_;
   a.nportions = nportions_;
+  a.max_wgs = max_wgs_;
   a.N = g_.N;
   a.me = me_;
   a.round = ++round_;

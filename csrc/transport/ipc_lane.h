@@ -53,6 +53,8 @@ class IpcLane {
   int32_t nportions() const { return nportions_; }
   int64_t portion_elems() const { return portion_; }
   size_t window_bytes() const { return data_bytes_; }
+  int32_t max_wgs() const { return max_wgs_; }
+  int32_t ranks_on_this_gpu() const { return sharers_; }
   const IpcLaneStats& stats() const { return stats_; }
 
  private:
@@ -69,6 +71,7 @@ class IpcLane {
   std::vector<char*> peer_data_;      // [N] mapped windows (own = data_)
   std::vector<uint32_t*> peer_flags_; // [N]
   uint32_t round_ = 0;
+  int32_t max_wgs_ = 1024, sharers_ = 1;
   uint64_t timeout_ticks_ = 0;
   bool ready_ = false;
   IpcLaneStats stats_;

@@ -47,6 +47,7 @@ def _run(n, *extra, env=None, timeout=180):
     (2, 3 * (1 << 18) + 8, "bfloat16"),
     (3, 2, "float32"),            # S < N: an empty block
     (2, 5 << 20, "float32"),      # several portions per block
+    (4, 1 << 24, "float32"),      # 64 MiB: more waiting workgroups than the grid cap (ranks share the card)
 ])
 def test_ipc_lane_exact(n, size, dtype):
     r, rows = _run(n, "--size", str(size), "--dtype", dtype, "--rounds", "4")
@@ -56,6 +57,7 @@ def test_ipc_lane_exact(n, size, dtype):
         assert d["lane"] == "ipc" and d["ipc_error"] == 0, d
         assert d["exact"] == [True] * 4, d
         assert d["ipc_rounds"] == 4 and d["ipc"]["rounds"] == 4
+        assert d["ipc"]["ranks_on_this_gpu"] == n and d["ipc"]["max_wgs"] == max(64, 1024 // n)
 
 
 def test_ipc_lane_missing_peer_times_out_cleanly():
