@@ -72,6 +72,9 @@ def parse():
     p.add_argument("--lane-select", choices=["on", "off"], default="on",
                    help="with --lane auto at N>1 (stream transport): before the warmup, run one exact round and a "
                         "few timed rounds on each lane and keep the faster exact one (every rank agrees)")
+    p.add_argument("--data-plane", choices=["rccl", "ipc"], default="rccl",
+                   help="ipc: no RCCL communicator, every exact round on the one-sided xGMI lane (with "
+                        "AKKA_SHARE_GPU=1 this rehearses the N-rank flow with N processes on one card)")
     p.add_argument("--ipc", choices=["on", "off"], default="on",
                    help="lane selection also tries the one-sided xGMI lane (mapped peer windows, ipc_lane.h)")
     p.add_argument("--async-op", choices=["auto", "on", "off"], default="auto",
@@ -353,7 +356,8 @@ def main() -> int:
         env_phase_stall(rank, "rccl_init")
         return ThresholdAllreduce(S, max_chunk_size=C, dtype=dtype, th_reduce=args.th_reduce,
                                   th_complete=args.th_complete, max_lag=args.max_lag, broadcast_lag=args.bcast_lag,
-                                  device=dev, transport=args.transport, lane=args.lane)
+                                  device=dev, transport=args.transport, lane=args.lane,
+                                  data_plane=args.data_plane)
 
     ar = guard.run("rccl_init", dl, rccl_init)
 
@@ -483,7 +487,8 @@ def main() -> int:
         return res
 
     lane_sel = None
-    if world > 1 and ar.transport == "stream" and args.lane == "auto" and args.lane_select == "on":
+    if world > 1 and ar.transport == "stream" and args.lane == "auto" and args.lane_select == "on" \
+            and args.data_plane == "rccl":
         lane_sel = guard.run("lane_select", dl, lane_select)
         chosen_lane = lane_sel["chosen"]
 
@@ -570,6 +575,8 @@ def main() -> int:
         used = chosen_lane or ("collective" if coll > steps_p2p else "p2p")
         if world == 1:
             return "local", None
+        if args.data_plane == "ipc":
+            return "ipc", None
         if ar.transport != "stream":
             return used, None
         other = "p2p" if used == "collective" else "collective"
@@ -621,13 +628,17 @@ def main() -> int:
     })
     line["config"] = dict(base["config"])
     line["config"].update({
-        "transport": ("rccl-pair-reactive" if ar.transport == "reactive" else "rccl-p2p-xgmi")
+        "transport": ("xgmi-ipc" if lane_used == "ipc" else
+                      "rccl-pair-reactive" if ar.transport == "reactive" else "rccl-p2p-xgmi")
         if world > 1 and dev.type == "cuda" else ("gloo-p2p" if world > 1 else "local"),
+        "data_plane": args.data_plane,
         "async_op": args.async_op,
         "output": "fresh tensor per round" if args.fresh_out else "preallocated, reused",
     })
     if rccl_err:
         line["rccl_compare_error"] = rccl_err
+    if os.environ.get("AKKA_SHARE_GPU") == "1" and world > 1:
+        line["data"] += "; N ranks sharing ONE GPU (rehearsal of the N-rank flow, not the metric)"
     if world == 1:
         line["note"] = ("N=1 has no peer: the round is one local reduce pass (input -> output), HBM-bound; "
                         "N>1 is xGMI-bound, compare it with rccl_allreduce_algbw_GBps")

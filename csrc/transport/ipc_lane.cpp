@@ -47,8 +47,8 @@ IpcLane::IpcLane(Device* dev, const Geometry& g, int32_t me, DType dt)
   for (int32_t p = 0; p < g_.N; ++p) maxb = std::max(maxb, g_.block_len(p));
   slot_ = std::max<int64_t>(64, (maxb + 63) / 64 * 64);
   // Portion: the unit one producer workgroup hands to one consumer workgroup
-  // (AKKA_IPC_PORTION_BYTES, default 128 KiB; whole 1024-element multiples).
-  const int64_t pbytes = std::max<int64_t>(4096, env_i64("AKKA_IPC_PORTION_BYTES", int64_t(128) << 10));
+  // (AKKA_IPC_PORTION_BYTES, default 512 KiB; whole 1024-element multiples).
+  const int64_t pbytes = std::max<int64_t>(4096, env_i64("AKKA_IPC_PORTION_BYTES", int64_t(512) << 10));
   portion_ = std::max<int64_t>(1024, (pbytes / int64_t(es_)) / 1024 * 1024);
   nportions_ = int32_t(std::max<int64_t>(1, (maxb + portion_ - 1) / portion_));
   data_bytes_ = size_t(g_.N + 1) * size_t(slot_) * es_;
