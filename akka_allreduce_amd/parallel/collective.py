@@ -278,6 +278,10 @@ class ThresholdAllreduce:
             dist.all_gather_object(handles, mine)
         self.worker.ipc_open(handles)
 
+    def set_ipc_mode(self, mode: str) -> None:
+        """Phase 2 of the ipc lane: ``"pull"`` or ``"bcast"`` (AllreduceWorker.ipc_set_mode)."""
+        self.worker.ipc_set_mode(mode)
+
     def ipc_error(self) -> int:
         """Non-zero once a wait of the ipc lane timed out (synchronises)."""
         return self.worker.ipc_error()

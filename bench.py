@@ -444,12 +444,14 @@ def main() -> int:
     # rank sees the same max-over-ranks numbers and keeps the same lane.
     # candidate -> (lane, minimum exact transfer-unit bytes; -1 = default 16 MiB)
     lanes = {"collective": ("collective", -1), "p2p": ("p2p", -1), "p2p_block": ("p2p", 1 << 40)}
-    fixed = dict(lanes, auto=("auto", -1), ipc=("ipc", -1))
+    fixed = dict(lanes, auto=("auto", -1), ipc=("ipc", -1), ipc_bcast=("ipc", -1))
 
     def apply_lane(name: str) -> None:
         ln, unit = fixed[name]
         ar.set_lane(ln)
-        if ar.transport == "stream" and world > 1:
+        if ln == "ipc":
+            ar.set_ipc_mode("bcast" if name == "ipc_bcast" else "pull")
+        elif ar.transport == "stream" and world > 1 and args.data_plane == "rccl":
             ar.set_exact_unit_bytes(unit)
 
     chosen_lane = args.lane if args.lane != "auto" else None
@@ -457,7 +459,10 @@ def main() -> int:
     def lane_select():
         env_phase_stall(rank, "lane_select")
         res = {}
-        if dev.type == "cuda" and args.ipc == "on":
+        if args.data_plane == "ipc":  # windows opened at construction; only the ipc lanes exist
+            lanes.clear()
+            lanes.update(ipc=("ipc", -1), ipc_bcast=("ipc", -1))
+        elif dev.type == "cuda" and args.ipc == "on":
             # the one-sided xGMI lane (ipc_lane.h) joins the candidates when every
             # rank could map every other rank's window
             err = None
@@ -469,6 +474,7 @@ def main() -> int:
             dist.all_reduce(flag, op=dist.ReduceOp.MIN)
             if flag.item():
                 lanes["ipc"] = ("ipc", -1)
+                lanes["ipc_bcast"] = ("ipc", -1)
             else:
                 res["ipc"] = {"exact": None, "ms": None, "error": err or "another rank could not open its windows"}
         for name in lanes:
@@ -487,8 +493,7 @@ def main() -> int:
         return res
 
     lane_sel = None
-    if world > 1 and ar.transport == "stream" and args.lane == "auto" and args.lane_select == "on" \
-            and args.data_plane == "rccl":
+    if world > 1 and ar.transport == "stream" and args.lane == "auto" and args.lane_select == "on":
         lane_sel = guard.run("lane_select", dl, lane_select)
         chosen_lane = lane_sel["chosen"]
 
@@ -572,11 +577,11 @@ def main() -> int:
         # lane of the timed rounds: collective rounds vs exact p2p-step rounds since link0
         coll = st0.get("collective_rounds", 0) - link0.get("collective_rounds", 0)
         steps_p2p = st0.get("exact_step_rounds", 0) - link0.get("exact_step_rounds", 0)
-        used = chosen_lane or ("collective" if coll > steps_p2p else "p2p")
+        used = chosen_lane or ("ipc" if args.data_plane == "ipc" else "collective" if coll > steps_p2p else "p2p")
         if world == 1:
             return "local", None
         if args.data_plane == "ipc":
-            return "ipc", None
+            return used, None
         if ar.transport != "stream":
             return used, None
         other = "p2p" if used == "collective" else "collective"
@@ -628,7 +633,7 @@ def main() -> int:
     })
     line["config"] = dict(base["config"])
     line["config"].update({
-        "transport": ("xgmi-ipc" if lane_used == "ipc" else
+        "transport": ("xgmi-ipc" if str(lane_used).startswith("ipc") else
                       "rccl-pair-reactive" if ar.transport == "reactive" else "rccl-p2p-xgmi")
         if world > 1 and dev.type == "cuda" else ("gloo-p2p" if world > 1 else "local"),
         "data_plane": args.data_plane,

@@ -206,6 +206,11 @@ class WorkerCore final : public EngineHost {
     py::gil_scoped_release nogil;
     return stream_link_->ipc()->error();
   }
+  void ipc_set_mode(const std::string& mode) {
+    AKKA_CHECK(stream_link_ && stream_link_->ipc(), "ipc_set_mode: the ipc lane is not open");
+    AKKA_CHECK(mode == "pull" || mode == "bcast", "ipc mode must be 'pull' or 'bcast'");
+    stream_link_->ipc()->set_bcast(mode == "bcast");
+  }
   void ipc_close() {
     ipc_pending_.reset();
     if (stream_link_) stream_link_->set_ipc(nullptr);
@@ -354,6 +359,8 @@ class WorkerCore final : public EngineHost {
         is["max_wgs"] = ipc->max_wgs();
         is["ranks_on_this_gpu"] = ipc->ranks_on_this_gpu();
         is["rounds"] = ipc->stats().rounds;
+        is["bcast_rounds"] = ipc->stats().bcast_rounds;
+        is["mode"] = ipc->bcast() ? "bcast" : "pull";
         is["bytes_pushed"] = ipc->stats().bytes_pushed;
         is["bytes_pulled"] = ipc->stats().bytes_pulled;
         ls["ipc"] = is;
@@ -606,6 +613,7 @@ PYBIND11_MODULE(_native, m) {
       .def("ipc_open", &WorkerCore::ipc_open)
       .def("ipc_error", &WorkerCore::ipc_error)
       .def("ipc_close", &WorkerCore::ipc_close)
+      .def("ipc_set_mode", &WorkerCore::ipc_set_mode)
       .def("scatter_count", &WorkerCore::scatter_count)
       .def("reduced_arrivals", &WorkerCore::reduced_arrivals);
 

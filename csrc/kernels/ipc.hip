@@ -26,7 +26,7 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int kUnroll = 4;       // 16-B vectors per thread per source in flight
-constexpr int kReduceSplit = 4;  // workgroups per portion in the reduce kernel
+constexpr int kReduceSplit = kIpcReduceSplit;
 
 __device__ inline bool reached(uint32_t v, uint32_t want) { return int32_t(v - want) >= 0; }
 
@@ -51,16 +51,18 @@ __device__ bool wait_flag(uint32_t* f, uint32_t want, uint32_t* err, uint64_t de
   }
 }
 
-// Whole workgroup: publish this workgroup's stores, then set (add) the flag.
-__device__ inline void publish(uint32_t* f, uint32_t v, bool add) {
+// Whole workgroup: make this workgroup's stores visible at system scope.
+// Lane 0 may then signal (flag stores).
+__device__ inline void release_wg() {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    if (add) __hip_atomic_fetch_add(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    else __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
+}
+__device__ inline void signal(uint32_t* f, uint32_t v) {  // lane 0, after release_wg
+  __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // Whole workgroup: acquire after lane 0's successful waits.  Returns the
@@ -142,15 +144,18 @@ struct Elt<uint16_t> {
 };
 
 // Sum of the N sources of `n` elements, ascending source rank (source `me`
-// is the round input, the others are window slots), to `o` and `r`.
+// is the round input, the others are window slots), to `o`, to `r` (pull
+// mode) or, with gather_off >= 0 (bcast mode), to every peer's window at
+// byte offset gather_off.
 template <typename T>
 __device__ void reduce_span(const IpcArgs& a, const char* mine, const char* slots, int64_t slot_bytes, char* o,
-                            char* r, int64_t n) {
+                            char* r, int64_t gather_off, int64_t n) {
   constexpr int ES = sizeof(T);
   constexpr int PV = Elt<T>::kPerVec;
   const int N = a.N, me = a.me;
+  const bool bc = gather_off >= 0;
   bool vec = ((uintptr_t(mine) | uintptr_t(slots) | uintptr_t(slot_bytes) | uintptr_t(o) | uintptr_t(r) |
-               uintptr_t(n * ES)) & 15) == 0;
+               uintptr_t(bc ? gather_off : 0) | uintptr_t(n * ES)) & 15) == 0;
   if (vec) {
     const int64_t nv = n / PV;
     for (int64_t i0 = threadIdx.x; i0 < nv; i0 += kUnroll * kThreads) {
@@ -176,7 +181,12 @@ __device__ void reduce_span(const IpcArgs& a, const char* mine, const char* slot
         if (i < nv) {
           const uint4 w = Elt<T>::pack(acc[u]);
           reinterpret_cast<uint4*>(o)[i] = w;
-          reinterpret_cast<uint4*>(r)[i] = w;
+          if (bc) {
+            for (int p = 0; p < N; ++p)
+              if (p != me) reinterpret_cast<uint4*>(a.data[p] + gather_off)[i] = w;
+          } else {
+            reinterpret_cast<uint4*>(r)[i] = w;
+          }
         }
       }
     }
@@ -185,7 +195,12 @@ __device__ void reduce_span(const IpcArgs& a, const char* mine, const char* slot
       float acc = 0.f;
       for (int s = 0; s < N; ++s) acc += Elt<T>::load1((s == me ? mine : slots + int64_t(s) * slot_bytes) + i * ES);
       Elt<T>::store1(o + i * ES, acc);
-      Elt<T>::store1(r + i * ES, acc);
+      if (bc) {
+        for (int p = 0; p < N; ++p)
+          if (p != me) Elt<T>::store1(a.data[p] + gather_off + i * ES, acc);
+      } else {
+        Elt<T>::store1(r + i * ES, acc);
+      }
     }
   }
 }
@@ -199,21 +214,22 @@ __global__ __launch_bounds__(kThreads) void ipc_push_kernel(IpcArgs a) {
   const int64_t n = max(int64_t(0), min(a.portion, a.blen[p] - e0));
   if (n > 0)
     copy_bytes(a.data[p] + (int64_t(a.me) * a.slot + e0) * ES, a.in + (a.bstart[p] + e0) * ES, n * ES);
-  publish(a.flags[p] + ipc_flag_push(a.me, j, a.nportions), a.round, false);
+  release_wg();
+  if (threadIdx.x == 0) signal(a.flags[p] + ipc_flag_push(a.me, j, a.nportions), a.round);
 }
 
 // grid <= max_wgs, looping over (portion j, part) items: wait for portion j of
-// every peer's push, sum, write my output block and my `reduced` row, add 1 to
-// reduced[j].  The grid is capped so that workgroups parked on flags never
-// fill the machine (ranks sharing a card in tests need room for each other's
-// push kernels).
+// every peer's push, sum, write my output block and my `reduced` row (pull
+// mode) or every peer's gather slot [me] (bcast mode), then signal.  The grid
+// is capped so that workgroups parked on flags never fill the machine (ranks
+// sharing a card in tests need room for each other's push kernels).
 template <typename T>
 __global__ __launch_bounds__(kThreads) void ipc_reduce_kernel(IpcArgs a) {
   constexpr int ES = sizeof(T);
-  const int32_t me = a.me;
+  const int32_t me = a.me, N = a.N, np = a.nportions;
   uint32_t* fl = a.flags[me];
-  uint32_t* err = fl + ipc_flag_error(a.N, a.nportions);
-  const int32_t items = a.nportions * kReduceSplit;
+  uint32_t* err = fl + ipc_flag_error(N, np);
+  const int32_t items = np * kReduceSplit;
   // each item's part of its portion (a multiple of 64 elements)
   const int64_t per = ((a.portion / kReduceSplit) + 63) / 64 * 64;
   for (int32_t w = blockIdx.x; w < items; w += gridDim.x) {
@@ -222,8 +238,8 @@ __global__ __launch_bounds__(kThreads) void ipc_reduce_kernel(IpcArgs a) {
     bool ok = true;
     if (threadIdx.x == 0) {
       const uint64_t deadline = wall_clock64() + a.timeout;
-      for (int32_t s = 0; s < a.N && ok; ++s)
-        if (s != me) ok = wait_flag(fl + ipc_flag_push(s, j, a.nportions), a.round, err, deadline);
+      for (int32_t s = 0; s < N && ok; ++s)
+        if (s != me) ok = wait_flag(fl + ipc_flag_push(s, j, np), a.round, err, deadline);
     }
     ok = acquire_all(ok);
     const int64_t e0 = int64_t(j) * a.portion;
@@ -232,33 +248,49 @@ __global__ __launch_bounds__(kThreads) void ipc_reduce_kernel(IpcArgs a) {
     if (ok && p1 > p0) {
       const int64_t e = e0 + p0;
       reduce_span<T>(a, a.in + (a.bstart[me] + e) * ES, a.data[me] + e * ES, a.slot * ES,
-                     a.out + (a.bstart[me] + e) * ES, a.data[me] + (int64_t(a.N) * a.slot + e) * ES, p1 - p0);
+                     a.out + (a.bstart[me] + e) * ES, a.data[me] + (int64_t(N) * a.slot + e) * ES,
+                     a.bcast ? (int64_t(N + 1 + me) * a.slot + e) * ES : int64_t(-1), p1 - p0);
     }
-    publish(fl + ipc_flag_reduced(j, a.N, a.nportions), 1u, true);  // ends with a workgroup barrier
+    release_wg();
+    if (threadIdx.x == 0) {
+      if (a.bcast) {
+        for (int32_t p = 0; p < N; ++p)
+          if (p != me) signal(a.flags[p] + ipc_flag_gather(me, j, part, N, np), a.round);
+      } else {
+        signal(fl + ipc_flag_reduced(j, part, N, np), a.round);
+      }
+    }
+    __syncthreads();  // `ok` is rewritten by the next item
   }
 }
 
 // grid <= max_wgs, looping over (portion j, peer) items, peers interleaved so
-// every link is busy at once: wait for rank p's reduced portion j, copy it into
-// my output's block p.
+// every link is busy at once: wait for rank p's reduced portion j (all its
+// parts), copy it into my output's block p.  Pull mode: the rows are read
+// from rank p's window over xGMI; bcast mode: rank p already wrote them into
+// my gather slot [p], the copy is local.
 template <int ES>
-__global__ __launch_bounds__(kThreads) void ipc_pull_kernel(IpcArgs a) {
-  uint32_t* err = a.flags[a.me] + ipc_flag_error(a.N, a.nportions);
-  const int32_t items = a.nportions * (a.N - 1);
+__global__ __launch_bounds__(kThreads) void ipc_phase2_kernel(IpcArgs a) {
+  const int32_t me = a.me, N = a.N, np = a.nportions;
+  uint32_t* err = a.flags[me] + ipc_flag_error(N, np);
+  const int32_t items = np * (N - 1);
   for (int32_t w = blockIdx.x; w < items; w += gridDim.x) {
-    const int32_t j = w / (a.N - 1);
-    const int32_t p = (a.me + 1 + w % (a.N - 1)) % a.N;
+    const int32_t j = w / (N - 1);
+    const int32_t p = (me + 1 + w % (N - 1)) % N;
     bool ok = true;
     if (threadIdx.x == 0) {
       const uint64_t deadline = wall_clock64() + a.timeout;
-      ok = wait_flag(a.flags[p] + ipc_flag_reduced(j, a.N, a.nportions), a.round * uint32_t(kReduceSplit), err,
-                     deadline);
+      for (int32_t part = 0; part < kReduceSplit && ok; ++part)
+        ok = wait_flag(a.bcast ? a.flags[me] + ipc_flag_gather(p, j, part, N, np)
+                               : a.flags[p] + ipc_flag_reduced(j, part, N, np),
+                       a.round, err, deadline);
     }
     ok = acquire_all(ok);
     const int64_t e0 = int64_t(j) * a.portion;
     const int64_t n = max(int64_t(0), min(a.portion, a.blen[p] - e0));
-    if (ok && n > 0)
-      copy_bytes(a.out + (a.bstart[p] + e0) * ES, a.data[p] + (int64_t(a.N) * a.slot + e0) * ES, n * ES);
+    const char* src = a.bcast ? a.data[me] + (int64_t(N + 1 + p) * a.slot + e0) * ES
+                              : a.data[p] + (int64_t(N) * a.slot + e0) * ES;
+    if (ok && n > 0) copy_bytes(a.out + (a.bstart[p] + e0) * ES, src, n * ES);
     __syncthreads();  // `ok` is rewritten by the next item
   }
 }
@@ -271,8 +303,8 @@ void launch_round(hipStream_t s, const IpcArgs& a) {
   const int32_t cap = a.max_wgs > 0 ? a.max_wgs : 1024;
   hipLaunchKernelGGL(ipc_reduce_kernel<T>, dim3(unsigned(std::min(a.nportions * kReduceSplit, cap))), dim3(kThreads), 0,
                      s, a);
-  hipLaunchKernelGGL(ipc_pull_kernel<ES>, dim3(unsigned(std::min(a.nportions * (a.N - 1), cap))), dim3(kThreads), 0, s,
-                     a);
+  hipLaunchKernelGGL(ipc_phase2_kernel<ES>, dim3(unsigned(std::min(a.nportions * (a.N - 1), cap))), dim3(kThreads), 0,
+                     s, a);
 }
 
 }  // namespace

@@ -51,7 +51,7 @@ IpcLane::IpcLane(Device* dev, const Geometry& g, int32_t me, DType dt)
   const int64_t pbytes = std::max<int64_t>(4096, env_i64("AKKA_IPC_PORTION_BYTES", int64_t(512) << 10));
   portion_ = std::max<int64_t>(1024, (pbytes / int64_t(es_)) / 1024 * 1024);
   nportions_ = int32_t(std::max<int64_t>(1, (maxb + portion_ - 1) / portion_));
-  data_bytes_ = size_t(g_.N + 1) * size_t(slot_) * es_;
+  data_bytes_ = size_t(ipc_window_slots(g_.N)) * size_t(slot_) * es_;
   flag_bytes_ = ipc_flag_bytes(g_.N, nportions_);
   AKKA_IPC_HIP(hipMalloc(reinterpret_cast<void**>(&data_), data_bytes_));
   // Flags uncached: every poll and every signal goes to memory.
@@ -145,6 +145,7 @@ void IpcLane::round(StreamH s, const void* in, void* out) {
   a.portion = portion_;
   a.nportions = nportions_;
   a.max_wgs = max_wgs_;
+  a.bcast = bcast_ ? 1 : 0;
   a.N = g_.N;
   a.me = me_;
   a.round = ++round_;
@@ -154,6 +155,7 @@ void IpcLane::round(StreamH s, const void* in, void* out) {
   launch_ipc_round(static_cast<hipStream_t>(s), a, dt_);
   AKKA_IPC_HIP(hipGetLastError());
   ++stats_.rounds;
+  if (bcast_) ++stats_.bcast_rounds;
   stats_.bytes_pushed += (g_.S - g_.block_len(me_)) * int64_t(es_);
   stats_.bytes_pulled += (g_.S - g_.block_len(me_)) * int64_t(es_);
 }

@@ -4,10 +4,12 @@
 // Why a lane of its own: on one node every MI355X maps every other one's HBM
 // over xGMI, so an exact round (thresholds 1, every chunk from every peer)
 // needs no message matching at all.  Each rank owns a window
-//   [slot 0 | slot 1 | ... | slot N-1 | reduced]      (each slot >= one block)
+//   [slot 0 | ... | slot N-1 | reduced | gather 0 | ... | gather N-1]
+// (each slot >= one block; ipc_kernels.h)
 // plus a small flag area (uncached).  Rank q pushes block p of its input into
 // slot q of rank p's window, rank p sums its N slots into its output block and
-// `reduced` row, and every rank pulls the reduced rows of the others -- all
+// `reduced` row, and every rank pulls the reduced rows of the others (or, in
+// bcast mode, rank p stores them into everyone's gather slot [p]) -- all
 // seven links of a rank busy in both phases, driven by the CUs, with round-id
 // flags per portion instead of RCCL groups: three kernel launches per round
 // and no host work beyond them.  The reference's scatter / reduce / broadcast
@@ -31,7 +33,7 @@
 namespace akka {
 
 struct IpcLaneStats {
-  int64_t rounds = 0, bytes_pushed = 0, bytes_pulled = 0;
+  int64_t rounds = 0, bcast_rounds = 0, bytes_pushed = 0, bytes_pulled = 0;
 };
 
 class IpcLane {
@@ -46,6 +48,11 @@ class IpcLane {
   // Open every other rank's window; handles[i] is rank i's handle().
   void open(const std::vector<std::string>& handles);
   bool ready() const { return ready_; }
+  // Phase 2 by remote writes (the reducer stores its rows into every peer's
+  // gather slot) instead of remote reads.  Every rank must use the same mode
+  // in a round; modes may change between rounds.
+  void set_bcast(bool on) { bcast_ = on; }
+  bool bcast() const { return bcast_; }
   // Enqueue one exact round on `s`: in[S] from every rank summed into out[S].
   void round(StreamH s, const void* in, void* out);
   // Synchronous read of the window's error word (a wait timed out).
@@ -74,6 +81,7 @@ class IpcLane {
   int32_t max_wgs_ = 1024, sharers_ = 1;
   uint64_t timeout_ticks_ = 0;
   bool ready_ = false;
+  bool bcast_ = false;
   IpcLaneStats stats_;
 };
 

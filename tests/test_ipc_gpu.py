@@ -60,6 +60,23 @@ def test_ipc_lane_exact(n, size, dtype):
         assert d["ipc"]["ranks_on_this_gpu"] == n and d["ipc"]["max_wgs"] == max(64, 1024 // n)
 
 
+@pytest.mark.parametrize("n,size,mode", [
+    (2, 1 << 20, "bcast"),
+    (3, 1 << 20, "bcast"),        # scalar paths
+    (3, 5 << 20, "alternate"),    # pull / bcast every other round: round-id flags serve both
+    (4, 1 << 24, "bcast"),
+])
+def test_ipc_lane_bcast_mode(n, size, mode):
+    """Phase 2 as remote writes: each reducer stores its rows into every
+    peer's gather slot, and a local copy moves them into the output."""
+    r, rows = _run(n, "--size", str(size), "--rounds", "4", "--mode", mode)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert len(rows) == n
+    for d in rows:
+        assert d["ipc_error"] == 0 and d["exact"] == [True] * 4, d
+        assert d["ipc"]["bcast_rounds"] == (4 if mode == "bcast" else 2)
+
+
 def test_ipc_lane_missing_peer_times_out_cleanly():
     """Rank 1 leaves after round 0: rank 0's round 1 waits (bounded, 0.5 s)
     for rank 1's flags, reports ipc_error and the job still ends."""
