@@ -183,8 +183,23 @@ def run_cfg4(world: int, rank: int, dev, barrier, size_mb: float, delay_ms: floa
     return res
 
 
+def apply_lane_choice(ar, name) -> None:
+    """Put a fresh ThresholdAllreduce on the lane the headline's lane selection
+    chose (collective / p2p / p2p_block / ipc / ipc_bcast); None: leave auto."""
+    if not name or ar.world_size < 2 or ar.transport != "stream":
+        return
+    if name.startswith("ipc"):
+        ar.enable_ipc()
+        ar.set_lane("ipc")
+        ar.set_ipc_mode("bcast" if name == "ipc_bcast" else "pull")
+    else:
+        ar.set_lane("p2p" if name.startswith("p2p") else name)
+        ar.set_exact_unit_bytes(1 << 40 if name == "p2p_block" else -1)
+
+
 def run_extras(world: int, dev, barrier, which=("cfg3", "cfg4", "cfg5"), rank: int = 0,
-               cfg4_size_mb: float = 64.0, cfg4_delay_ms: float = 50.0, cfg4_rounds: int = 10) -> dict:
+               cfg4_size_mb: float = 64.0, cfg4_delay_ms: float = 50.0, cfg4_rounds: int = 10,
+               lane: str | None = None) -> dict:
     """BASELINE config 3 (8-rank bf16, 1 GB buffer, link-sized chunks),
     config 4 (threshold 0.75/0.75 + straggler, N>1 only) and config 5 (2-layer
     MLP DP-SGD step/s) at this N, on synthetic data."""
@@ -207,6 +222,7 @@ def run_extras(world: int, dev, barrier, which=("cfg3", "cfg4", "cfg5"), rank: i
         S = nbytes // 2
         ar = ThresholdAllreduce(S, max_chunk_size=(8 << 20) // 2, dtype=torch.bfloat16, device=dev)
         keep.append(ar)
+        apply_lane_choice(ar, lane)
         x = torch.randn(S, device=dev, dtype=torch.bfloat16)
         out = torch.empty_like(x)
         steps = 10
@@ -230,6 +246,7 @@ def run_extras(world: int, dev, barrier, which=("cfg3", "cfg4", "cfg5"), rank: i
         bucket = GradientBucket(list(model.parameters()), flatten_params=True)
         ar = ThresholdAllreduce(bucket.numel, max_chunk_size=(4 << 20) // 4, device=dev)
         keep.append(ar)
+        apply_lane_choice(ar, lane)
         gen = torch.Generator(device=dev).manual_seed(1000 + (ar.rank or 0))
         xb, yb = synthetic_batch(batch, d_in, classes, device=dev, generator=gen)
         steps = 20
@@ -663,7 +680,9 @@ def main() -> int:
         guard.arm(args.extras_deadline_s, late, exit_code=0 if ok in (None, True) else 1)
         which = tuple(args.extras_only.split(",")) if args.extras_only else ("cfg3", "cfg4", "cfg5")
         line["extra_configs"] = run_extras(world, dev, barrier, which, rank, args.cfg4_size_mb,
-                                           args.cfg4_delay_ms, args.cfg4_rounds)
+                                           args.cfg4_delay_ms, args.cfg4_rounds, lane=chosen_lane)
+        if chosen_lane and world > 1:
+            line["extra_configs"]["lane"] = chosen_lane
         guard.disarm()
 
     if rank == 0:
