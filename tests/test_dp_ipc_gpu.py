@@ -1,0 +1,60 @@
+"""Multi-process data-parallel training on the GPU: N ranks
+(sharing the box's one GPU) run dp_sgd_step on their own batches, the
+gradient buckets meet in the ipc-lane allreduce, and after a few steps
+  * every rank holds bit-identical parameters, and
+  * they match one process applying the mean of the N ranks' gradients
+    (plain autograd + SGD, fp32), to fp32 reduction-order tolerance."""
+import os
+import socket
+import subprocess
+import sys
+import tempfile
+
+import pytest
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.gpu
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _reference(n, steps, dev):
+    from akka_allreduce_amd.models.mlp import MLP, synthetic_batch
+
+    torch.manual_seed(0)
+    model = MLP(256, 512, 10).to(dev)
+    for s in range(steps):
+        grads = None
+        for r in range(n):
+            g = torch.Generator(device=dev).manual_seed(100 * s + r)
+            x, y = synthetic_batch(64, 256, 10, device=dev, generator=g)
+            model.zero_grad(set_to_none=True)
+            torch.nn.functional.cross_entropy(model(x), y).backward()
+            gr = [p.grad.detach().clone() for p in model.parameters()]
+            grads = gr if grads is None else [a + b for a, b in zip(grads, gr)]
+        with torch.no_grad():
+            for p, g_ in zip(model.parameters(), grads):
+                p -= 0.1 * g_ / n
+    return torch.cat([p.detach().reshape(-1).float().cpu() for p in model.parameters()])
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_dp_sgd_multiprocess_ipc(n):
+    steps = 3
+    with tempfile.TemporaryDirectory() as out:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+               os.path.join(ROOT, "tests", "dp_ranks.py"), "--out-dir", out, "--steps", str(steps)]
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT)
+        assert r.returncode == 0, r.stderr[-3000:]
+        res = [torch.load(os.path.join(out, f"rank{i}.pt"), weights_only=True) for i in range(n)]
+    for d in res:
+        assert d["ipc_error"] == 0 and d["ipc_rounds"] == steps
+        assert torch.equal(d["flat"], res[0]["flat"])  # every rank applied the same averaged gradient
+    want = _reference(n, steps, torch.device("cuda", 0))
+    torch.testing.assert_close(res[0]["flat"], want, rtol=1e-4, atol=1e-5)
