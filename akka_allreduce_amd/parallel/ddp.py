@@ -27,13 +27,15 @@ class ThresholdHookState:
     all queued in stream order (DDP waits on the future's CUDA event, not on
     the host), so bucket communication overlaps the rest of the backward pass
     like DDP's own allreduce hook.  ``th_allreduce``: master-style round
-    pacing across ranks (see ThresholdAllreduce)."""
+    pacing across ranks (see ThresholdAllreduce).  ``data_plane="ipc"``: exact
+    rounds on the one-sided xGMI lane, no RCCL communicator (ThresholdAllreduce)."""
 
     def __init__(self, *, th_reduce: float = 1.0, th_complete: float = 1.0, max_lag: int = 2,
                  max_chunk_size: int = 1 << 20, transport: str = "stream", broadcast_lag: int = 2,
-                 async_op: bool = True, th_allreduce=None):
+                 async_op: bool = True, th_allreduce=None, data_plane: str = "rccl"):
         self.kw = dict(th_reduce=th_reduce, th_complete=th_complete, max_lag=max_lag, max_chunk_size=max_chunk_size,
-                       transport=transport, broadcast_lag=broadcast_lag, th_allreduce=th_allreduce)
+                       transport=transport, broadcast_lag=broadcast_lag, th_allreduce=th_allreduce,
+                       data_plane=data_plane)
         self.engines: Dict[Tuple[int, torch.dtype, torch.device], ThresholdAllreduce] = {}
         self.rounds = 0
         self.async_op = async_op

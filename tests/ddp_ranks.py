@@ -1,0 +1,49 @@
+"""Rank program for tests/test_dp_ipc_gpu.py::test_torch_ddp_hook_multiprocess:
+torch DistributedDataParallel (gloo process group, every rank on the box's one
+GPU) with the threshold-allreduce comm hook on the ipc-only data plane.
+Saves the final flat parameters to <out>/rank<i>.pt."""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out-dir", required=True)
+    ap.add_argument("--steps", type=int, default=3)
+    a = ap.parse_args()
+    rank = int(os.environ["RANK"])
+    dist.init_process_group("gloo")
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    from akka_allreduce_amd.models.mlp import MLP, synthetic_batch
+    from akka_allreduce_amd.parallel.ddp import ThresholdHookState, threshold_allreduce_hook
+
+    torch.manual_seed(0)
+    model = torch.nn.parallel.DistributedDataParallel(MLP(256, 512, 10).to(dev), device_ids=[0],
+                                                      bucket_cap_mb=0.25)
+    state = ThresholdHookState(data_plane="ipc", max_chunk_size=1 << 14)
+    model.register_comm_hook(state, threshold_allreduce_hook)
+    opt = torch.optim.SGD(model.parameters(), lr=0.1)
+    for s in range(a.steps):
+        g = torch.Generator(device=dev).manual_seed(100 * s + rank)
+        x, y = synthetic_batch(64, 256, 10, device=dev, generator=g)
+        opt.zero_grad(set_to_none=True)
+        torch.nn.functional.cross_entropy(model(x), y).backward()
+        opt.step()
+    torch.cuda.synchronize()
+    flat = torch.cat([p.detach().reshape(-1).float().cpu() for p in model.parameters()])
+    errs = [ar.ipc_error() for ar in state.engines.values()]
+    torch.save({"flat": flat, "buckets": len(state.engines), "rounds": state.rounds, "ipc_errors": errs},
+               os.path.join(a.out_dir, f"rank{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

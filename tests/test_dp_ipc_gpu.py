@@ -58,3 +58,24 @@ def test_dp_sgd_multiprocess_ipc(n):
         assert torch.equal(d["flat"], res[0]["flat"])  # every rank applied the same averaged gradient
     want = _reference(n, steps, torch.device("cuda", 0))
     torch.testing.assert_close(res[0]["flat"], want, rtol=1e-4, atol=1e-5)
+
+
+def test_torch_ddp_hook_multiprocess():
+    """torch DDP with the comm hook on the ipc data plane, 2 processes: the
+    hook's rounds average every bucket across the processes (same result as
+    the mean-gradient reference), several buckets -> several allreduce
+    engines, all created collectively inside backward."""
+    n, steps = 2, 3
+    with tempfile.TemporaryDirectory() as out:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+               os.path.join(ROOT, "tests", "ddp_ranks.py"), "--out-dir", out, "--steps", str(steps)]
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT)
+        assert r.returncode == 0, r.stderr[-3000:]
+        res = [torch.load(os.path.join(out, f"rank{i}.pt"), weights_only=True) for i in range(n)]
+    for d in res:
+        assert d["ipc_errors"] and all(e == 0 for e in d["ipc_errors"])
+        assert d["buckets"] >= 1 and d["rounds"] >= steps
+        assert torch.equal(d["flat"], res[0]["flat"])
+    want = _reference(n, steps, torch.device("cuda", 0))
+    torch.testing.assert_close(res[0]["flat"], want, rtol=1e-4, atol=1e-5)
