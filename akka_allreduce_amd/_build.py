@@ -32,6 +32,7 @@ HOST_SOURCES = [
     "transport/reactive_link.cpp",
     "transport/rccl_p2p.cpp",
     "transport/ipc_lane.cpp",
+    "transport/ipc_p2p.cpp",
     "kernels/hip_device.cpp",
     "runtime/watchdog.cpp",
     "bindings/bindings.cpp",

@@ -80,6 +80,24 @@ def share_unique_id(rank: int, world: int, store: Any = None) -> bytes:
     return obj[0]
 
 
+def _handle_exchange(rank: int, world: int, store: Any, key: str):
+    """A function mine -> [every rank's bytes] over the store or torch.distributed."""
+
+    def exchange(mine: bytes) -> list:
+        if store is not None:
+            store.set(f"{key}/{rank}", mine)
+            return [bytes(store.get(f"{key}/{i}")) for i in range(world)]
+        import torch.distributed as dist
+
+        if not dist.is_initialized():
+            raise RuntimeError("exchanging window handles needs torch.distributed (gloo is enough) or a store")
+        out = [None] * world
+        dist.all_gather_object(out, mine)
+        return out
+
+    return exchange
+
+
 class RoundPacer:
     """The master's round pacing (M:54-63) without a master process: round r
     may start on a rank once at least ``thAllreduce * N`` ranks (float32
@@ -152,8 +170,8 @@ class ThresholdAllreduce:
     ):
         if transport not in ("stream", "reactive"):
             raise ValueError("transport must be 'stream' or 'reactive'")
-        if data_plane not in ("rccl", "ipc"):
-            raise ValueError("data_plane must be 'rccl' or 'ipc'")
+        if data_plane not in ("rccl", "ipc", "ipc_p2p"):
+            raise ValueError("data_plane must be 'rccl', 'ipc' or 'ipc_p2p'")
         if data_plane == "ipc" and (transport != "stream" or th_reduce < 1.0 or th_complete < 1.0):
             raise ValueError("the ipc-only data plane runs exact rounds (thresholds 1) on the stream transport")
         r, w, local = env_rank_world()
@@ -169,7 +187,7 @@ class ThresholdAllreduce:
             device = torch.device("cuda", local % max(1, torch.cuda.device_count())) if torch.cuda.is_available() \
                 else torch.device("cpu")
         self.device = torch.device(device)
-        if data_plane == "ipc" and self.device.type != "cuda":
+        if data_plane != "rccl" and self.device.type != "cuda":
             raise ValueError("the ipc-only data plane maps peer GPU memory: it needs a cuda device")
         if transport == "reactive" and self.world_size > 1 and self.device.type == "cuda":
             need = min(32, self.world_size + 4)
@@ -180,6 +198,12 @@ class ThresholdAllreduce:
         if self.device.type == "cuda" and data_plane == "ipc" and self.world_size > 1:
             torch.cuda.set_device(self.device)
             spec = ("none", self.rank, self.world_size)
+        elif self.device.type == "cuda" and data_plane == "ipc_p2p" and self.world_size > 1:
+            # every schedule (thresholds, reactive) over mailboxes in mapped peer
+            # memory instead of RCCL (csrc/transport/ipc_p2p.cpp)
+            torch.cuda.set_device(self.device)
+            spec = ("ipc_p2p", self.rank, self.world_size,
+                    _handle_exchange(self.rank, self.world_size, store, f"akka/p2p/{ThresholdAllreduce._instances}"))
         elif self.device.type == "cuda":
             torch.cuda.set_device(self.device)
             uid = share_unique_id(self.rank, self.world_size, store)

@@ -257,6 +257,10 @@ class AllreduceWorker:
         elif kind == "callback":
             _, fn, rank, nranks = spec
             self._core.connect_callback(fn, int(rank), int(nranks))
+        elif kind == "ipc_p2p":  # grouped send/recv over mapped peer memory, handles exchanged by `exchange`
+            _, rank, nranks, exchange = spec
+            self._core.connect_ipc_p2p(int(rank), int(nranks))
+            self._core.p2p_open([bytes(h) for h in exchange(bytes(self._core.p2p_handle()))])
         elif kind == "none":  # ipc-only data plane: exact rounds on the one-sided lane
             _, rank, nranks = spec
             self._core.connect_none(int(rank), int(nranks))

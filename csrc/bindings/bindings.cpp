@@ -179,6 +179,23 @@ class WorkerCore final : public EngineHost {
     self_drive_ = true;
     make_reactive_link();
   }
+  // Grouped send/recv over mapped peer memory instead of RCCL (ipc_p2p.cpp);
+  // then p2p_handle() to every rank and p2p_open(all handles).
+  void connect_ipc_p2p(int32_t rank, int32_t nranks) {
+    AKKA_CHECK(dev_ && !dev_->is_host(), "ipc p2p needs a HIP device");
+    p2p_ = make_ipc_p2p(rank, nranks, device_idx_);
+    if (link_kind_ == "reactive") make_reactive_link();
+    else make_stream_link();
+  }
+  py::bytes p2p_handle() {
+    AKKA_CHECK(p2p_, "p2p_handle: no transport");
+    return py::bytes(p2p_->handle());
+  }
+  void p2p_open(std::vector<std::string> handles) {
+    AKKA_CHECK(p2p_, "p2p_open: no transport");
+    py::gil_scoped_release nogil;
+    p2p_->open(handles);
+  }
   // ipc-only data plane: no two-sided transport; exact rounds on the ipc lane.
   void connect_none(int32_t rank, int32_t nranks) {
     AKKA_CHECK(dev_ && !dev_->is_host(), "the ipc-only data plane needs a HIP device");
@@ -609,6 +626,9 @@ PYBIND11_MODULE(_native, m) {
       .def("set_graphs", &WorkerCore::set_graphs)
       .def("set_exact_unit_bytes", &WorkerCore::set_exact_unit_bytes)
       .def("connect_none", &WorkerCore::connect_none)
+      .def("connect_ipc_p2p", &WorkerCore::connect_ipc_p2p)
+      .def("p2p_handle", &WorkerCore::p2p_handle)
+      .def("p2p_open", &WorkerCore::p2p_open)
       .def("ipc_handle", &WorkerCore::ipc_handle)
       .def("ipc_open", &WorkerCore::ipc_open)
       .def("ipc_error", &WorkerCore::ipc_error)

@@ -92,6 +92,10 @@ __device__ void copy_bytes(char* __restrict__ dst, const char* __restrict__ src,
       for (int u = 0; u < kUnroll; ++u) d[i + u * kThreads] = v[u];
     }
     for (; i < n; i += kThreads) d[i] = s[i];
+  } else if (((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src) | uintptr_t(bytes)) & 3) == 0) {
+    const uint32_t* s = reinterpret_cast<const uint32_t*>(src);
+    uint32_t* d = reinterpret_cast<uint32_t*>(dst);
+    for (int64_t i = threadIdx.x; i < (bytes >> 2); i += kThreads) d[i] = s[i];
   } else {
     for (int64_t i = threadIdx.x; i < bytes; i += kThreads) dst[i] = src[i];
   }
@@ -307,7 +311,80 @@ void launch_round(hipStream_t s, const IpcArgs& a) {
                      s, a);
 }
 
+// Like wait_flag, but also gives up when the host marked `peer` dead.
+__device__ bool wait_flag_p2p(uint32_t* f, uint32_t want, uint32_t* err, const uint32_t* dead, int32_t peer,
+                              uint64_t deadline) {
+  uint32_t spins = 0;
+  while (true) {
+    if (reached(sys_load(f), want)) return true;
+    if ((++spins & 63) == 0) {
+      if (__hip_atomic_load(dead + peer, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0) return false;
+      if (sys_load(err) != 0) return false;
+      if (wall_clock64() > deadline) {
+        __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        return false;
+      }
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+
+// grid = nqueues * wpp.  Workgroup (queue, w) moves part w of every piece of
+// every op of its queue, in order.
+__global__ __launch_bounds__(kThreads) void ipc_p2p_kernel(IpcP2PArgs a) {
+  const int32_t qi = int32_t(blockIdx.x) / a.wpp;
+  const int32_t w = int32_t(blockIdx.x) % a.wpp;
+  const int32_t me = a.me;
+  for (int32_t oi = a.qstart[qi]; oi < a.qstart[qi + 1]; ++oi) {
+    const IpcP2POp op = a.ops[oi];
+    const int32_t peer = op.peer, ch = op.ch;
+    const int64_t npieces = (op.bytes + a.piece - 1) / a.piece;
+    for (int64_t k = 0; k < npieces; ++k) {
+      const uint32_t seq = op.seq + uint32_t(k);
+      const int32_t slot = int32_t(seq % uint32_t(a.nslots));
+      const int64_t pb0 = k * a.piece;
+      const int64_t pbytes = min(a.piece, op.bytes - pb0);
+      const int64_t part = ((pbytes + a.wpp - 1) / a.wpp + 15) / 16 * 16;
+      const int64_t b0 = min(pbytes, int64_t(w) * part), b1 = min(pbytes, b0 + part);
+      bool ok = true;
+      if (op.send) {
+        if (threadIdx.x == 0 && seq >= uint32_t(a.nslots)) {
+          const uint64_t deadline = wall_clock64() + a.timeout;
+          ok = wait_flag_p2p(a.flags[me] + ipc_p2p_flag_consumed(peer, ch, slot, w, a.N, a.nch, a.nslots, a.wpp),
+                             seq - uint32_t(a.nslots) + 1u, a.err, a.dead, peer, deadline);
+        }
+        ok = acquire_all(ok);
+        if (ok && b1 > b0)
+          copy_bytes(a.mbox[peer] + ipc_p2p_box(me, ch, slot, a.nch, a.nslots) * a.piece + b0, op.buf + pb0 + b0,
+                     b1 - b0);
+        release_wg();
+        if (threadIdx.x == 0)
+          signal(a.flags[peer] + ipc_p2p_flag_written(me, ch, slot, w, a.nch, a.nslots, a.wpp), seq + 1u);
+      } else {
+        if (threadIdx.x == 0) {
+          const uint64_t deadline = wall_clock64() + a.timeout;
+          ok = wait_flag_p2p(a.flags[me] + ipc_p2p_flag_written(peer, ch, slot, w, a.nch, a.nslots, a.wpp),
+                             seq + 1u, a.err, a.dead, peer, deadline);
+        }
+        ok = acquire_all(ok);
+        if (ok && b1 > b0)
+          copy_bytes(op.buf + pb0 + b0, a.mbox[me] + ipc_p2p_box(peer, ch, slot, a.nch, a.nslots) * a.piece + b0,
+                     b1 - b0);
+        release_wg();
+        if (threadIdx.x == 0)
+          signal(a.flags[peer] + ipc_p2p_flag_consumed(me, ch, slot, w, a.N, a.nch, a.nslots, a.wpp), seq + 1u);
+      }
+      __syncthreads();  // `ok` is rewritten by the next piece
+    }
+  }
+}
+
 }  // namespace
+
+void launch_ipc_p2p_group(hipStream_t s, const IpcP2PArgs& a) {
+  if (a.nqueues <= 0) return;
+  hipLaunchKernelGGL(ipc_p2p_kernel, dim3(unsigned(a.nqueues * a.wpp)), dim3(kThreads), 0, s, a);
+}
 
 void launch_ipc_round(hipStream_t s, const IpcArgs& a, DType dt) {
   if (a.N < 2) return;

@@ -69,6 +69,57 @@ __host__ __device__ inline size_t ipc_flag_bytes(int32_t N, int32_t np) {
 }
 __host__ __device__ inline int64_t ipc_window_slots(int32_t N) { return 2 * int64_t(N) + 1; }
 
+// ---- two-sided p2p over mapped mailboxes (csrc/transport/ipc_p2p.cpp) ----
+// Every rank's window holds, per (source rank, channel), `nslots` mailbox
+// slots of `piece` bytes.  An op of B bytes moves as ceil(B / piece) pieces
+// with consecutive sequence numbers per (pair, channel, direction); piece q
+// uses slot q % nslots.  Each piece is split over `wpp` workgroups, and every
+// (slot, workgroup) pair has its own round-id style flags:
+//   written [src][ch][slot][w]  in the receiver's area, set by the sender;
+//   consumed[dst][ch][slot][w]  in the sender's area, set by the receiver.
+// A sender waits for `consumed` of piece q - nslots before reusing the slot.
+constexpr int kIpcP2PMaxOps = 80;
+
+struct IpcP2POp {
+  char* buf;       // local source (send) or destination (recv)
+  int64_t bytes;   // > 0
+  uint32_t seq;    // first piece's sequence number
+  int8_t send, peer, ch, pad;
+  int64_t pad2;
+};
+
+struct IpcP2PArgs {
+  char* mbox[kIpcMaxRanks];       // mailbox region of every rank, mapped here (own = local)
+  uint32_t* flags[kIpcMaxRanks];  // flag area of every rank, mapped here
+  uint32_t* err;                  // host-pinned: set on a timed-out wait or a dead peer
+  const uint32_t* dead;           // host-pinned [N]: peers aborted by the host
+  int64_t piece;
+  int32_t nslots, wpp, nch, N, me, nops, nqueues, pad;
+  uint64_t timeout;
+  int16_t qstart[kIpcP2PMaxOps + 1];  // ops of queue i: [qstart[i], qstart[i+1]), in issue order
+  IpcP2POp ops[kIpcP2PMaxOps];
+};
+
+__host__ __device__ inline int64_t ipc_p2p_box(int32_t rank, int32_t ch, int32_t slot, int32_t nch, int32_t nslots) {
+  return (int64_t(rank) * nch + ch) * nslots + slot;
+}
+__host__ __device__ inline int64_t ipc_p2p_flag_written(int32_t src, int32_t ch, int32_t slot, int32_t w, int32_t nch,
+                                                        int32_t nslots, int32_t wpp) {
+  return (ipc_p2p_box(src, ch, slot, nch, nslots) * wpp + w) * kIpcFlagStride;
+}
+__host__ __device__ inline int64_t ipc_p2p_flag_consumed(int32_t dst, int32_t ch, int32_t slot, int32_t w,
+                                                         int32_t N, int32_t nch, int32_t nslots, int32_t wpp) {
+  return (int64_t(N) * nch * nslots * wpp + ipc_p2p_box(dst, ch, slot, nch, nslots) * wpp + w) * kIpcFlagStride;
+}
+__host__ __device__ inline size_t ipc_p2p_flag_bytes(int32_t N, int32_t nch, int32_t nslots, int32_t wpp) {
+  return size_t(2) * N * nch * nslots * wpp * kIpcFlagStride * sizeof(uint32_t);
+}
+
+// One group: every queue (ops sharing direction, peer and channel) gets `wpp`
+// workgroups that walk its ops in order; all queues run concurrently (the
+// group semantics of a grouped send/recv).
+void launch_ipc_p2p_group(hipStream_t s, const IpcP2PArgs& a);
+
 // Enqueue one round on `s`: push, reduce, then pull (bcast = 0) or, with
 // bcast = 1, the reducer writes its rows into every peer's gather slot and a
 // local gather copies them out.

@@ -72,6 +72,12 @@ class P2P {
     return false;
   }
 
+  // Transports over mapped peer memory (ipc_p2p.cpp): this rank's handle,
+  // to be exchanged with every rank, then open() with all of them.
+  virtual std::string handle() const { throw AkkaError(std::string("akka: ") + name() + " p2p has no handle"); }
+  virtual void open(const std::vector<std::string>&) {
+    throw AkkaError(std::string("akka: ") + name() + " p2p has nothing to open");
+  }
   virtual bool has_collectives() const { return false; }
   virtual void reduce_scatter(StreamH, const void*, void*, size_t, DType) {
     throw AkkaError(std::string("akka: ") + name() + " p2p has no reduce_scatter");
@@ -134,6 +140,11 @@ inline int32_t tournament_rounds(int32_t n) { return ((n % 2) ? n + 1 : n) - 1; 
 std::unique_ptr<P2P> make_rccl_pair_p2p(const std::vector<uint8_t>& uid, int32_t rank, int32_t nranks,
                                         int32_t device);
 const char* rccl_version_string();
+// ---- mapped peer memory (xGMI) ---------------------------------------------------
+// Grouped send/recv through mailboxes in every rank's window (ipc_p2p.cpp);
+// handle() / open() exchange the windows before the first group.
+std::unique_ptr<P2P> make_ipc_p2p(int32_t rank, int32_t nranks, int32_t device);
+
 // One-GPU shape rehearsal (1-rank comm posing as rank/nranks, ops to self).
 std::unique_ptr<P2P> make_rccl_shape_p2p(int32_t rank, int32_t nranks, int32_t device);
 

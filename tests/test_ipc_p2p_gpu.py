@@ -1,0 +1,93 @@
+"""Grouped send/recv over mapped peer memory (csrc/transport/ipc_p2p.cpp)
+driving the real schedules across processes that share the box's one GPU
+(RCCL refuses two ranks on one device, so these schedules had only run in
+one process before).  Rank r contributes 2**r, so every output value names
+the exact set of ranks summed into it and must agree with its count.
+
+* scheduled transport, exact rounds, each lane: chunk-pipelined p2p template
+  (per chunk and whole-block units) and the whole-block exchange;
+* scheduled transport at thresholds 0.75: the message-driven schedule;
+* straggler-tolerant (reactive) transport, thresholds 0.75, one rank sleeping
+  before every round: the others complete rounds without it (BASELINE
+  config 4 on real GPU processes)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+import tempfile
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+pytestmark = pytest.mark.gpu
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _run(n, *extra, env=None, timeout=240):
+    with tempfile.TemporaryDirectory() as out:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+               os.path.join(ROOT, "tests", "p2p_ranks.py"), "--out-dir", out, *extra]
+        e = dict(os.environ)
+        e.update(env or {})
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=ROOT, env=e)
+        rows = []
+        for i in range(n):
+            path = os.path.join(out, f"rank{i}.json")
+            if os.path.exists(path):
+                with open(path) as f:
+                    rows.append(json.load(f))
+    return r, rows
+
+
+@pytest.mark.parametrize("n,lane,unit", [
+    (2, "p2p", 0),              # one transfer per chunk
+    (3, "p2p", -1),             # 16 MiB units (whole blocks here)
+    (3, "collective", -1),      # no native collectives: whole-block exchange
+    (4, "p2p", 0),
+])
+def test_ipc_p2p_exact_lanes(n, lane, unit):
+    r, rows = _run(n, "--lane", lane, "--unit-bytes", str(unit), "--size", str((1 << 20) + 7), "--chunk",
+                   str(1 << 15))
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert len(rows) == n
+    for d in rows:
+        for rd in d["rounds"]:
+            assert rd["all"] and rd["min_count"] == n and rd["max_count"] == n, d
+
+
+def test_ipc_p2p_threshold_schedule():
+    """thReduce = thComplete = 0.75 at N=4 on the scheduled transport: the
+    engine's message flow; every chunk holds at least 3 contributions and its
+    value is exactly the sum of the ranks its count says."""
+    n = 4
+    r, rows = _run(n, "--th", "0.75", "--size", str(1 << 18), "--chunk", str(1 << 12), "--rounds", "5",
+                   "--max-lag", "2")
+    assert r.returncode == 0, r.stderr[-3000:]
+    for d in rows:
+        for rd in d["rounds"]:
+            assert rd["count_matches_members"] and rd["min_count"] >= 3, d
+
+
+def test_ipc_p2p_reactive_straggler():
+    """BASELINE config 4 shape on GPU processes: reactive transport, 0.75 /
+    0.75, rank 3 sleeps 300 ms before each round.  Ranks 0-2 must not wait for
+    it: their rounds complete in far less than the sleep, with counts >= 3 and
+    values that match the counts."""
+    n, delay = 4, 300.0
+    r, rows = _run(n, "--transport", "reactive", "--th", "0.75", "--size", str(1 << 20), "--chunk", str(1 << 16),
+                   "--rounds", "6", "--straggler-ms", str(delay), env={"GPU_MAX_HW_QUEUES": "8"})
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert len(rows) == n
+    for d in rows:
+        for rd in d["rounds"]:
+            assert rd["count_matches_members"] and rd["min_count"] >= 3, d
+    for d in rows[:3]:
+        later = d["ms_per_round"][2:]  # after the first rounds' warm-up
+        assert max(later) < delay / 2, d["ms_per_round"]
