@@ -61,6 +61,8 @@ def main():
             "all": bool((v == 2 ** world - 1).all()),
             "count_matches_members": bool((pop == cnt).all() & (data == v.float()).all()),
             "min_count": int(cnt.min()), "max_count": int(cnt.max()),
+            "min_nonzero_count": int(cnt[cnt > 0].min()) if bool((cnt > 0).any()) else 0,
+            "frac_present": float((cnt > 0).float().mean()),
             "has_self": bool(((v >> rank) & 1).all()) if a.th >= 1 else None,
         })
     res["ms_per_round"] = [round(t * 1e3, 3) for t in t_fast]
