@@ -72,9 +72,10 @@ def parse():
     p.add_argument("--lane-select", choices=["on", "off"], default="on",
                    help="with --lane auto at N>1 (stream transport): before the warmup, run one exact round and a "
                         "few timed rounds on each lane and keep the faster exact one (every rank agrees)")
-    p.add_argument("--data-plane", choices=["rccl", "ipc"], default="rccl",
-                   help="ipc: no RCCL communicator, every exact round on the one-sided xGMI lane (with "
-                        "AKKA_SHARE_GPU=1 this rehearses the N-rank flow with N processes on one card)")
+    p.add_argument("--data-plane", choices=["rccl", "ipc", "ipc_p2p"], default="rccl",
+                   help="ipc: no RCCL communicator, every exact round on the one-sided xGMI lane; ipc_p2p: the "
+                        "p2p schedules over mailboxes in mapped peer memory (with AKKA_SHARE_GPU=1 either rehearses "
+                        "the N-rank flow with N processes on one card)")
     p.add_argument("--ipc", choices=["on", "off"], default="on",
                    help="lane selection also tries the one-sided xGMI lane (mapped peer windows, ipc_lane.h)")
     p.add_argument("--async-op", choices=["auto", "on", "off"], default="auto",
@@ -124,7 +125,8 @@ class _Skip(Exception):
     pass
 
 
-def run_cfg4(world: int, rank: int, dev, barrier, size_mb: float, delay_ms: float, rounds: int) -> dict:
+def run_cfg4(world: int, rank: int, dev, barrier, size_mb: float, delay_ms: float, rounds: int,
+             data_plane: str = "rccl") -> dict:
     """BASELINE config 4: threshold allreduce at thReduce = thComplete = 0.75,
     maxLag 1, with rank N-1 an induced straggler (sleeps ``delay_ms`` before
     each round), on the straggler-tolerant reactive transport (one pair
@@ -143,7 +145,7 @@ def run_cfg4(world: int, rank: int, dev, barrier, size_mb: float, delay_ms: floa
     S = int(size_mb * (1 << 20)) // esize
     C = max(1, min(S, (4 << 20) // esize))
     ar = ThresholdAllreduce(S, max_chunk_size=C, th_reduce=0.75, th_complete=0.75, max_lag=1, device=dev,
-                            transport="reactive")
+                            transport="reactive", data_plane=data_plane)
     run_cfg4.keep = ar  # type: ignore[attr-defined]
     straggler = world - 1
     g = torch.Generator(device=dev).manual_seed(77 + rank)
@@ -189,7 +191,8 @@ def apply_lane_choice(ar, name) -> None:
     if not name or ar.world_size < 2 or ar.transport != "stream":
         return
     if name.startswith("ipc"):
-        ar.enable_ipc()
+        if not ar.state().get("link", {}).get("ipc"):
+            ar.enable_ipc()
         ar.set_lane("ipc")
         ar.set_ipc_mode("bcast" if name == "ipc_bcast" else "pull")
     else:
@@ -199,7 +202,7 @@ def apply_lane_choice(ar, name) -> None:
 
 def run_extras(world: int, dev, barrier, which=("cfg3", "cfg4", "cfg5"), rank: int = 0,
                cfg4_size_mb: float = 64.0, cfg4_delay_ms: float = 50.0, cfg4_rounds: int = 10,
-               lane: str | None = None) -> dict:
+               lane: str | None = None, data_plane: str = "rccl") -> dict:
     """BASELINE config 3 (8-rank bf16, 1 GB buffer, link-sized chunks),
     config 4 (threshold 0.75/0.75 + straggler, N>1 only) and config 5 (2-layer
     MLP DP-SGD step/s) at this N, on synthetic data."""
@@ -211,8 +214,11 @@ def run_extras(world: int, dev, barrier, which=("cfg3", "cfg4", "cfg5"), rank: i
     keep = []  # communicators stay alive until exit (no per-rank teardown ordering)
     if "cfg4" in which and world > 1:
         try:
+            # thresholds < 1 need a two-sided transport: RCCL pair communicators, or
+            # the mailbox p2p over mapped memory when the job runs without RCCL
             res["cfg4_threshold_straggler"] = run_cfg4(world, rank, dev, barrier, cfg4_size_mb, cfg4_delay_ms,
-                                                       cfg4_rounds)
+                                                       cfg4_rounds,
+                                                       data_plane="rccl" if data_plane == "rccl" else "ipc_p2p")
         except Exception as e:
             res["cfg4_error"] = f"{type(e).__name__}: {e}"[:300]
     try:
@@ -220,7 +226,8 @@ def run_extras(world: int, dev, barrier, which=("cfg3", "cfg4", "cfg5"), rank: i
             raise _Skip()
         nbytes = 1 << 30
         S = nbytes // 2
-        ar = ThresholdAllreduce(S, max_chunk_size=(8 << 20) // 2, dtype=torch.bfloat16, device=dev)
+        ar = ThresholdAllreduce(S, max_chunk_size=(8 << 20) // 2, dtype=torch.bfloat16, device=dev,
+                                data_plane=data_plane)
         keep.append(ar)
         apply_lane_choice(ar, lane)
         x = torch.randn(S, device=dev, dtype=torch.bfloat16)
@@ -244,7 +251,7 @@ def run_extras(world: int, dev, barrier, which=("cfg3", "cfg4", "cfg5"), rank: i
         d_in, hidden, classes, batch = 4096, 8192, 1000, 256
         model = MLP(d_in, hidden, classes).to(dev)
         bucket = GradientBucket(list(model.parameters()), flatten_params=True)
-        ar = ThresholdAllreduce(bucket.numel, max_chunk_size=(4 << 20) // 4, device=dev)
+        ar = ThresholdAllreduce(bucket.numel, max_chunk_size=(4 << 20) // 4, device=dev, data_plane=data_plane)
         keep.append(ar)
         apply_lane_choice(ar, lane)
         gen = torch.Generator(device=dev).manual_seed(1000 + (ar.rank or 0))
@@ -302,7 +309,8 @@ def main() -> int:
         # every stream on its own hardware queue (a stream parked on the
         # straggler must not hold up a reduce that shares its queue)
         need = min(32, max(8, int(os.environ["WORLD_SIZE"]) + 8))
-        if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < need:
+        # ranks sharing one card (rehearsal) split its hardware queues: keep the caller's setting
+        if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < need and os.environ.get("AKKA_SHARE_GPU") != "1":
             os.environ["GPU_MAX_HW_QUEUES"] = str(need)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -468,7 +476,7 @@ def main() -> int:
         ar.set_lane(ln)
         if ln == "ipc":
             ar.set_ipc_mode("bcast" if name == "ipc_bcast" else "pull")
-        elif ar.transport == "stream" and world > 1 and args.data_plane == "rccl":
+        elif ar.transport == "stream" and world > 1 and args.data_plane != "ipc":
             ar.set_exact_unit_bytes(unit)
 
     chosen_lane = args.lane if args.lane != "auto" else None
@@ -651,6 +659,7 @@ def main() -> int:
     line["config"] = dict(base["config"])
     line["config"].update({
         "transport": ("xgmi-ipc" if str(lane_used).startswith("ipc") else
+                      "xgmi-mailbox-p2p" if args.data_plane == "ipc_p2p" else
                       "rccl-pair-reactive" if ar.transport == "reactive" else "rccl-p2p-xgmi")
         if world > 1 and dev.type == "cuda" else ("gloo-p2p" if world > 1 else "local"),
         "data_plane": args.data_plane,
@@ -680,7 +689,8 @@ def main() -> int:
         guard.arm(args.extras_deadline_s, late, exit_code=0 if ok in (None, True) else 1)
         which = tuple(args.extras_only.split(",")) if args.extras_only else ("cfg3", "cfg4", "cfg5")
         line["extra_configs"] = run_extras(world, dev, barrier, which, rank, args.cfg4_size_mb,
-                                           args.cfg4_delay_ms, args.cfg4_rounds, lane=chosen_lane)
+                                           args.cfg4_delay_ms, args.cfg4_rounds, lane=chosen_lane,
+                                           data_plane=args.data_plane)
         if chosen_lane and world > 1:
             line["extra_configs"]["lane"] = chosen_lane
         guard.disarm()
