@@ -287,7 +287,14 @@ class ThresholdAllreduce:
         as push / reduce / pull kernels over mapped peer memory."""
         if self.transport != "stream" or self.device.type != "cuda" or self.world_size < 2:
             raise ValueError("the ipc lane needs the stream transport on GPUs with N > 1")
-        mine = self.worker.ipc_handle()
+        # every rank takes part in the exchange even if its own window failed
+        # (an empty handle), so a local failure can never leave the others
+        # blocked in the collective
+        err = None
+        try:
+            mine = self.worker.ipc_handle()
+        except Exception as e:  # noqa: BLE001 - re-raised below, after the exchange
+            mine, err = b"", e
         if self.store is not None:
             self._ipc_epoch += 1
             key = f"akka/ipc/{self._iid}/{self._ipc_epoch}"
@@ -300,6 +307,11 @@ class ThresholdAllreduce:
                 raise RuntimeError("enable_ipc: initialise torch.distributed (gloo is enough) or pass a store")
             handles = [None] * self.world_size
             dist.all_gather_object(handles, mine)
+        if err is not None:
+            raise err
+        missing = [i for i, h in enumerate(handles) if not h]
+        if missing:
+            raise RuntimeError(f"enable_ipc: ranks {missing} could not create their ipc windows")
         self.worker.ipc_open(handles)
 
     def set_ipc_mode(self, mode: str) -> None:
