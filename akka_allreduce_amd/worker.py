@@ -259,8 +259,18 @@ class AllreduceWorker:
             self._core.connect_callback(fn, int(rank), int(nranks))
         elif kind == "ipc_p2p":  # grouped send/recv over mapped peer memory, handles exchanged by `exchange`
             _, rank, nranks, exchange = spec
-            self._core.connect_ipc_p2p(int(rank), int(nranks))
-            self._core.p2p_open([bytes(h) for h in exchange(bytes(self._core.p2p_handle()))])
+            err = None
+            try:
+                self._core.connect_ipc_p2p(int(rank), int(nranks))
+                mine = bytes(self._core.p2p_handle())
+            except Exception as e:  # noqa: BLE001 - join the exchange anyway, then re-raise
+                mine, err = b"", e
+            handles = exchange(mine)
+            if err is not None:
+                raise err
+            if not all(handles):
+                raise RuntimeError("ipc p2p: some ranks could not create their mailboxes")
+            self._core.p2p_open([bytes(h) for h in handles])
         elif kind == "none":  # ipc-only data plane: exact rounds on the one-sided lane
             _, rank, nranks = spec
             self._core.connect_none(int(rank), int(nranks))
