@@ -21,6 +21,7 @@
 #include "../engine/engine.h"
 #include "../kernels/kernels.h"
 #include "../runtime/watchdog.h"
+#include "../transport/ipc_p2p.h"
 #include "../transport/p2p.h"
 #include "../transport/reactive_link.h"
 #include "harness_p2p.h"
@@ -805,5 +806,50 @@ PYBIND11_MODULE(_native, m) {
     return d;
   });
   m.def("float_threshold", &float_threshold);
+  // CPU checks of the ipc transports' host logic (tests/test_ipc_layout.py)
+  m.def("ipc_p2p_plan", [](std::vector<std::tuple<bool, int32_t, int64_t, int32_t>> ops, int32_t nranks,
+                           int64_t piece, std::vector<uint32_t> dead, std::vector<uint32_t> send_seq,
+                           std::vector<uint32_t> recv_seq) {
+    std::vector<P2POp> v;
+    for (auto& t : ops) v.push_back({std::get<0>(t), std::get<1>(t), nullptr, size_t(std::get<2>(t)), std::get<3>(t)});
+    dead.resize(size_t(nranks), 0);
+    IpcP2PPlan plan = plan_ipc_p2p_group(v, nranks, piece, 2, dead.data(), send_seq, recv_seq);
+    py::list queues;
+    for (size_t q = 0; q + 1 < plan.qstart.size(); ++q) {
+      py::list ql;
+      for (int32_t i = plan.qstart[q]; i < plan.qstart[q + 1]; ++i) {
+        const IpcP2POp& o = plan.ops[size_t(i)];
+        ql.append(py::make_tuple(bool(o.send), int(o.peer), int(o.ch), o.bytes, o.seq));
+      }
+      queues.append(ql);
+    }
+    return py::make_tuple(queues, send_seq, recv_seq, plan.bytes_sent);
+  });
+  m.def("ipc_layout", [](int32_t N, int32_t np, int32_t nslots, int32_t wpp) {
+    py::dict d;
+    std::vector<int64_t> lane, p2p;
+    for (int32_t src = 0; src < N; ++src)
+      for (int32_t j = 0; j < np; ++j) lane.push_back(ipc_flag_push(src, j, np));
+    for (int32_t j = 0; j < np; ++j)
+      for (int32_t part = 0; part < kIpcReduceSplit; ++part) lane.push_back(ipc_flag_reduced(j, part, N, np));
+    for (int32_t src = 0; src < N; ++src)
+      for (int32_t j = 0; j < np; ++j)
+        for (int32_t part = 0; part < kIpcReduceSplit; ++part) lane.push_back(ipc_flag_gather(src, j, part, N, np));
+    lane.push_back(ipc_flag_error(N, np));
+    for (int32_t r = 0; r < N; ++r)
+      for (int32_t ch = 0; ch < 2; ++ch)
+        for (int32_t sl = 0; sl < nslots; ++sl)
+          for (int32_t w = 0; w < wpp; ++w) {
+            p2p.push_back(ipc_p2p_flag_written(r, ch, sl, w, 2, nslots, wpp));
+            p2p.push_back(ipc_p2p_flag_consumed(r, ch, sl, w, N, 2, nslots, wpp));
+          }
+    d["lane_flags"] = lane;
+    d["lane_flag_bytes"] = int64_t(ipc_flag_bytes(N, np));
+    d["p2p_flags"] = p2p;
+    d["p2p_flag_bytes"] = int64_t(ipc_p2p_flag_bytes(N, 2, nslots, wpp));
+    d["stride"] = kIpcFlagStride;
+    d["window_slots"] = ipc_window_slots(N);
+    return d;
+  });
   m.attr("build_arch") = "gfx950";
 }

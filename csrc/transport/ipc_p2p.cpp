@@ -28,6 +28,7 @@
 #include <tuple>
 
 #include "../kernels/ipc_kernels.h"
+#include "ipc_p2p.h"
 #include "p2p.h"
 
 namespace akka {
@@ -145,28 +146,10 @@ class IpcP2P final : public P2P {
 
   void group(StreamH stream, const std::vector<P2POp>& ops) override {
     AKKA_CHECK(ready_, "ipc p2p: open() the peer mailboxes first");
-    // queues in order of first appearance; ops keep their issue order inside
-    std::map<std::tuple<int, int, int>, int> qindex;
-    std::vector<std::vector<const P2POp*>> queues;
-    for (const P2POp& op : ops) {
-      if (op.bytes == 0) continue;
-      AKKA_CHECK(op.peer >= 0 && op.peer < n_, "ipc p2p: peer out of range");
-      if (host_[1 + op.peer]) continue;  // aborted peer: its transfers are dropped
-      const int ch = std::min<int>(op.channel, kChannels - 1);
-      auto key = std::make_tuple(op.send ? 1 : 0, op.peer, ch);
-      auto it = qindex.find(key);
-      if (it == qindex.end()) {
-        it = qindex.emplace(key, int(queues.size())).first;
-        queues.emplace_back();
-      }
-      queues[size_t(it->second)].push_back(&op);
-    }
-    if (queues.empty()) return;
+    IpcP2PPlan plan = plan_ipc_p2p_group(ops, n_, piece_, kChannels, host_ + 1, send_seq_, recv_seq_);
+    if (plan.ops.empty()) return;
     IpcP2PArgs a;
     std::memset(&a, 0, sizeof(a));
-    int32_t nops = 0;
-    for (const auto& q : queues) nops += int32_t(q.size());
-    AKKA_CHECK(nops <= kIpcP2PMaxOps, "ipc p2p: more than " + std::to_string(kIpcP2PMaxOps) + " ops in one group");
     for (int32_t p = 0; p < n_; ++p) {
       a.mbox[p] = peer_mbox_[size_t(p)];
       a.flags[p] = peer_flags_[size_t(p)];
@@ -180,29 +163,14 @@ class IpcP2P final : public P2P {
     a.N = n_;
     a.me = rank_;
     a.timeout = timeout_;
-    int32_t k = 0;
-    for (size_t qi = 0; qi < queues.size(); ++qi) {
-      a.qstart[qi] = int16_t(k);
-      for (const P2POp* op : queues[qi]) {
-        const int ch = std::min<int>(op->channel, kChannels - 1);
-        uint32_t& seq = (op->send ? send_seq_ : recv_seq_)[size_t(op->peer) * kChannels + size_t(ch)];
-        IpcP2POp& o = a.ops[k++];
-        o.buf = static_cast<char*>(op->buf);
-        o.bytes = int64_t(op->bytes);
-        o.seq = seq;
-        o.send = op->send ? 1 : 0;
-        o.peer = int8_t(op->peer);
-        o.ch = int8_t(ch);
-        seq += uint32_t((int64_t(op->bytes) + piece_ - 1) / piece_);
-        bytes_ += op->send ? int64_t(op->bytes) : 0;
-      }
-    }
-    a.qstart[queues.size()] = int16_t(k);
-    a.nops = k;
-    a.nqueues = int32_t(queues.size());
+    a.nops = int32_t(plan.ops.size());
+    a.nqueues = int32_t(plan.qstart.size()) - 1;
+    std::copy(plan.ops.begin(), plan.ops.end(), a.ops);
+    for (size_t i = 0; i < plan.qstart.size(); ++i) a.qstart[i] = int16_t(plan.qstart[i]);
     launch_ipc_p2p_group(static_cast<hipStream_t>(stream), a);
     AKKA_P2P_HIP(hipGetLastError());
     ++groups_;
+    bytes_ += plan.bytes_sent;
   }
 
   void check() override {
@@ -233,6 +201,53 @@ class IpcP2P final : public P2P {
 };
 
 }  // namespace
+
+IpcP2PPlan plan_ipc_p2p_group(const std::vector<P2POp>& ops, int32_t nranks, int64_t piece, int32_t nch,
+                              const uint32_t* dead, std::vector<uint32_t>& send_seq, std::vector<uint32_t>& recv_seq) {
+  AKKA_CHECK(piece > 0 && nch > 0, "ipc p2p plan: bad piece / channel count");
+  AKKA_CHECK(send_seq.size() == size_t(nranks) * size_t(nch) && recv_seq.size() == send_seq.size(),
+             "ipc p2p plan: sequence tables do not match nranks x channels");
+  // queues in order of first appearance; ops keep their issue order inside
+  std::map<std::tuple<int, int, int>, size_t> qindex;
+  std::vector<std::vector<const P2POp*>> queues;
+  for (const P2POp& op : ops) {
+    if (op.bytes == 0) continue;
+    AKKA_CHECK(op.peer >= 0 && op.peer < nranks, "ipc p2p: peer out of range");
+    if (dead && dead[op.peer]) continue;  // aborted peer: its transfers are dropped
+    const int ch = std::min<int>(op.channel, nch - 1);
+    auto key = std::make_tuple(op.send ? 1 : 0, op.peer, ch);
+    auto it = qindex.find(key);
+    if (it == qindex.end()) {
+      it = qindex.emplace(key, queues.size()).first;
+      queues.emplace_back();
+    }
+    queues[it->second].push_back(&op);
+  }
+  IpcP2PPlan plan;
+  size_t nops = 0;
+  for (const auto& q : queues) nops += q.size();
+  AKKA_CHECK(nops <= size_t(kIpcP2PMaxOps), "ipc p2p: more than " + std::to_string(kIpcP2PMaxOps) + " ops in one group");
+  for (const auto& q : queues) {
+    plan.qstart.push_back(int32_t(plan.ops.size()));
+    for (const P2POp* op : q) {
+      const int ch = std::min<int>(op->channel, nch - 1);
+      uint32_t& seq = (op->send ? send_seq : recv_seq)[size_t(op->peer) * size_t(nch) + size_t(ch)];
+      IpcP2POp o;
+      std::memset(&o, 0, sizeof(o));
+      o.buf = static_cast<char*>(op->buf);
+      o.bytes = int64_t(op->bytes);
+      o.seq = seq;
+      o.send = op->send ? 1 : 0;
+      o.peer = int8_t(op->peer);
+      o.ch = int8_t(ch);
+      plan.ops.push_back(o);
+      seq += uint32_t((int64_t(op->bytes) + piece - 1) / piece);
+      if (op->send) plan.bytes_sent += int64_t(op->bytes);
+    }
+  }
+  if (!plan.ops.empty()) plan.qstart.push_back(int32_t(plan.ops.size()));
+  return plan;
+}
 
 std::unique_ptr<P2P> make_ipc_p2p(int32_t rank, int32_t nranks, int32_t device) {
   return std::make_unique<IpcP2P>(rank, nranks, device);
