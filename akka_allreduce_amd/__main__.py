@@ -52,8 +52,9 @@ def _master(a: argparse.Namespace) -> int:
 def _worker(a: argparse.Namespace) -> int:
     import os
 
-    if a.transport == "reactive":
-        # one stream per peer: they must not share hardware queues (read at HIP init)
+    if a.transport == "reactive" and os.environ.get("AKKA_SHARE_GPU") != "1":
+        # one stream per peer: they must not share hardware queues (read at HIP
+        # init); workers sharing one card split its queues: keep their setting
         os.environ["GPU_MAX_HW_QUEUES"] = "32"
     import torch
 
@@ -130,7 +131,9 @@ def main(argv=None) -> int:
     m.add_argument("--th-allreduce", type=float)
     m.add_argument("--th-reduce", type=float)
     m.add_argument("--th-complete", type=float)
-    m.add_argument("--transport", choices=["auto", "rccl", "tcp"])
+    m.add_argument("--transport", choices=["auto", "rccl", "tcp", "ipc_p2p"],
+                   help="GPU data plane the master hands out: RCCL (auto/rccl), or ipc_p2p = mailboxes in mapped "
+                        "peer memory (no RCCL; several workers may share one GPU)")
     m.set_defaults(fn=_master)
 
     w = sub.add_parser("worker", help="run one AllreduceWorker (one per GPU)")

@@ -95,6 +95,13 @@ class MasterProcess:
                  unreachable_after_s: float = 10.0, transport: str = "auto"):
         self.node = Node(host, port, name="master")
         self.transport = transport
+        self._store = None
+        if transport == "ipc_p2p":
+            # the workers' rendezvous for their mailbox window handles: a
+            # key-value store hosted by the master (no RCCL id to mint)
+            from torch.distributed import TCPStore
+
+            self._store = TCPStore(host, 0, is_master=True, wait_for_workers=False)
         self._gpu_workers: Dict[str, bool] = {}  # worker address -> has a GPU
         self.master = AllreduceMaster.from_configs(thresholds, data, workers, on_finished=self._finished,
                                                    transport_info=self._transport_info)
@@ -117,6 +124,12 @@ class MasterProcess:
         return self.node.address
 
     def _transport_info(self) -> Optional[Dict[str, Any]]:
+        if self._store is not None:
+            # fixed membership per window set: a death is handled by aborting
+            # the dead peer (ReactiveLink / IpcP2P.abort_peer), not a new epoch
+            if getattr(self, "_ipc_key", None) is None:
+                self._ipc_key = f"akka/cluster/{int(time.time() * 1e6)}"
+            return {"kind": "ipc_p2p", "store": [self.node.host, int(self._store.port)], "key": self._ipc_key}
         refs = list(self.master.workers.values())
         all_gpu = bool(refs) and all(self._gpu_workers.get(getattr(r, "address", ""), False) for r in refs)
         want_rccl = self.transport == "rccl" or (self.transport == "auto" and all_gpu)

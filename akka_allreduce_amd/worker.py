@@ -195,6 +195,18 @@ class AllreduceWorker:
         if rccl and self.transport_spec is None:
             self.transport_spec = ("rccl", tinfo["uid"], int(m.destId), int(m.workerNum),
                                    list(tinfo.get("members") or []))
+        elif tinfo and tinfo.get("kind") == "ipc_p2p" and self.transport_spec is None \
+                and self.transport in ("stream", "reactive"):
+            # mailboxes in mapped peer memory; handles meet in the master's store
+            from torch.distributed import TCPStore
+
+            from .parallel.collective import _handle_exchange
+
+            host, port = tinfo["store"]
+            store = TCPStore(host, int(port), is_master=False)
+            self._ipc_store = store  # keep the connection for the job's lifetime
+            self.transport_spec = ("ipc_p2p", int(m.destId), int(m.workerNum),
+                                   _handle_exchange(int(m.destId), int(m.workerNum), store, tinfo["key"]))
         elif tinfo and tinfo.get("kind") in ("loopback", "loopback_pair", "sim") and self.transport_spec is None:
             # in-process data planes handed out by the control plane (tests /
             # single-process clusters): the hub is shared by every worker
