@@ -314,9 +314,10 @@ class ThresholdAllreduce:
             raise RuntimeError(f"enable_ipc: ranks {missing} could not create their ipc windows")
         self.worker.ipc_open(handles)
 
-    def set_ipc_mode(self, mode: str) -> None:
-        """Phase 2 of the ipc lane: ``"pull"`` or ``"bcast"`` (AllreduceWorker.ipc_set_mode)."""
-        self.worker.ipc_set_mode(mode)
+    def set_ipc_mode(self, mode: str, fused: bool = False) -> None:
+        """Phase 2 of the ipc lane: ``"pull"`` or ``"bcast"``, optionally ``fused``
+        into one launch (AllreduceWorker.ipc_set_mode)."""
+        self.worker.ipc_set_mode(mode, fused)
 
     def ipc_error(self) -> int:
         """Non-zero once a wait of the ipc lane timed out (synchronises)."""

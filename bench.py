@@ -194,7 +194,7 @@ def apply_lane_choice(ar, name) -> None:
         if not ar.state().get("link", {}).get("ipc"):
             ar.enable_ipc()
         ar.set_lane("ipc")
-        ar.set_ipc_mode("bcast" if name == "ipc_bcast" else "pull")
+        ar.set_ipc_mode("bcast" if name.endswith("bcast") else "pull", fused="fused" in name)
     else:
         ar.set_lane("p2p" if name.startswith("p2p") else name)
         ar.set_exact_unit_bytes(1 << 40 if name == "p2p_block" else -1)
@@ -469,13 +469,15 @@ def main() -> int:
     # rank sees the same max-over-ranks numbers and keeps the same lane.
     # candidate -> (lane, minimum exact transfer-unit bytes; -1 = default 16 MiB)
     lanes = {"collective": ("collective", -1), "p2p": ("p2p", -1), "p2p_block": ("p2p", 1 << 40)}
-    fixed = dict(lanes, auto=("auto", -1), ipc=("ipc", -1), ipc_bcast=("ipc", -1))
+    ipc_lanes = {"ipc": ("ipc", -1), "ipc_bcast": ("ipc", -1), "ipc_fused": ("ipc", -1),
+                 "ipc_fused_bcast": ("ipc", -1)}
+    fixed = dict(lanes, auto=("auto", -1), **ipc_lanes)
 
     def apply_lane(name: str) -> None:
         ln, unit = fixed[name]
         ar.set_lane(ln)
         if ln == "ipc":
-            ar.set_ipc_mode("bcast" if name == "ipc_bcast" else "pull")
+            ar.set_ipc_mode("bcast" if name.endswith("bcast") else "pull", fused="fused" in name)
         elif ar.transport == "stream" and world > 1 and args.data_plane != "ipc":
             ar.set_exact_unit_bytes(unit)
 
@@ -486,7 +488,7 @@ def main() -> int:
         res = {}
         if args.data_plane == "ipc":  # windows opened at construction; only the ipc lanes exist
             lanes.clear()
-            lanes.update(ipc=("ipc", -1), ipc_bcast=("ipc", -1))
+            lanes.update(ipc_lanes)
         elif dev.type == "cuda" and args.ipc == "on":
             # the one-sided xGMI lane (ipc_lane.h) joins the candidates when every
             # rank could map every other rank's window
@@ -498,8 +500,7 @@ def main() -> int:
             flag = torch.tensor([0 if err else 1])
             dist.all_reduce(flag, op=dist.ReduceOp.MIN)
             if flag.item():
-                lanes["ipc"] = ("ipc", -1)
-                lanes["ipc_bcast"] = ("ipc", -1)
+                lanes.update(ipc_lanes)
             else:
                 res["ipc"] = {"exact": None, "ms": None, "error": err or "another rank could not open its windows"}
         for name in lanes:

@@ -224,10 +224,11 @@ class WorkerCore final : public EngineHost {
     py::gil_scoped_release nogil;
     return stream_link_->ipc()->error();
   }
-  void ipc_set_mode(const std::string& mode) {
+  void ipc_set_mode(const std::string& mode, bool fused) {
     AKKA_CHECK(stream_link_ && stream_link_->ipc(), "ipc_set_mode: the ipc lane is not open");
     AKKA_CHECK(mode == "pull" || mode == "bcast", "ipc mode must be 'pull' or 'bcast'");
     stream_link_->ipc()->set_bcast(mode == "bcast");
+    stream_link_->ipc()->set_fused(fused);
   }
   void ipc_close() {
     ipc_pending_.reset();
@@ -379,6 +380,7 @@ class WorkerCore final : public EngineHost {
         is["rounds"] = ipc->stats().rounds;
         is["bcast_rounds"] = ipc->stats().bcast_rounds;
         is["mode"] = ipc->bcast() ? "bcast" : "pull";
+        is["fused"] = ipc->fused();
         is["bytes_pushed"] = ipc->stats().bytes_pushed;
         is["bytes_pulled"] = ipc->stats().bytes_pulled;
         ls["ipc"] = is;
@@ -634,7 +636,7 @@ PYBIND11_MODULE(_native, m) {
       .def("ipc_open", &WorkerCore::ipc_open)
       .def("ipc_error", &WorkerCore::ipc_error)
       .def("ipc_close", &WorkerCore::ipc_close)
-      .def("ipc_set_mode", &WorkerCore::ipc_set_mode)
+      .def("ipc_set_mode", &WorkerCore::ipc_set_mode, py::arg("mode"), py::arg("fused") = false)
       .def("scatter_count", &WorkerCore::scatter_count)
       .def("reduced_arrivals", &WorkerCore::reduced_arrivals);
 

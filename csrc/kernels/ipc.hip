@@ -209,106 +209,153 @@ __device__ void reduce_span(const IpcArgs& a, const char* mine, const char* slot
   }
 }
 
-// grid (nportions, N-1): portion j of my input's block p -> rank p's slot [me].
+// ---- the three phases of a round, one work item each ----------------------
+
+// Portion j of my input's block p -> rank p's slot [me], then its push flag.
 template <int ES>
-__global__ __launch_bounds__(kThreads) void ipc_push_kernel(IpcArgs a) {
-  const int32_t j = blockIdx.x;
-  const int32_t p = (a.me + 1 + int32_t(blockIdx.y)) % a.N;
+__device__ void push_item(const IpcArgs& a, int32_t j, int32_t p) {
   const int64_t e0 = int64_t(j) * a.portion;
   const int64_t n = max(int64_t(0), min(a.portion, a.blen[p] - e0));
   if (n > 0)
     copy_bytes(a.data[p] + (int64_t(a.me) * a.slot + e0) * ES, a.in + (a.bstart[p] + e0) * ES, n * ES);
   release_wg();
   if (threadIdx.x == 0) signal(a.flags[p] + ipc_flag_push(a.me, j, a.nportions), a.round);
+  __syncthreads();
 }
 
-// grid <= max_wgs, looping over (portion j, part) items: wait for portion j of
-// every peer's push, sum, write my output block and my `reduced` row (pull
-// mode) or every peer's gather slot [me] (bcast mode), then signal.  The grid
-// is capped so that workgroups parked on flags never fill the machine (ranks
-// sharing a card in tests need room for each other's push kernels).
+// Part `part` of portion j of my block: wait for every peer's push of it, sum,
+// write my output block and my `reduced` row (pull mode) or every peer's
+// gather slot [me] (bcast mode), then signal.
 template <typename T>
-__global__ __launch_bounds__(kThreads) void ipc_reduce_kernel(IpcArgs a) {
+__device__ void reduce_item(const IpcArgs& a, int32_t j, int32_t part) {
   constexpr int ES = sizeof(T);
   const int32_t me = a.me, N = a.N, np = a.nportions;
   uint32_t* fl = a.flags[me];
   uint32_t* err = fl + ipc_flag_error(N, np);
-  const int32_t items = np * kReduceSplit;
   // each item's part of its portion (a multiple of 64 elements)
   const int64_t per = ((a.portion / kReduceSplit) + 63) / 64 * 64;
-  for (int32_t w = blockIdx.x; w < items; w += gridDim.x) {
-    const int32_t j = w / kReduceSplit;
-    const int32_t part = w % kReduceSplit;
-    bool ok = true;
-    if (threadIdx.x == 0) {
-      const uint64_t deadline = wall_clock64() + a.timeout;
-      for (int32_t s = 0; s < N && ok; ++s)
-        if (s != me) ok = wait_flag(fl + ipc_flag_push(s, j, np), a.round, err, deadline);
-    }
-    ok = acquire_all(ok);
-    const int64_t e0 = int64_t(j) * a.portion;
-    const int64_t n = max(int64_t(0), min(a.portion, a.blen[me] - e0));
-    const int64_t p0 = min(n, part * per), p1 = min(n, p0 + per);
-    if (ok && p1 > p0) {
-      const int64_t e = e0 + p0;
-      reduce_span<T>(a, a.in + (a.bstart[me] + e) * ES, a.data[me] + e * ES, a.slot * ES,
-                     a.out + (a.bstart[me] + e) * ES, a.data[me] + (int64_t(N) * a.slot + e) * ES,
-                     a.bcast ? (int64_t(N + 1 + me) * a.slot + e) * ES : int64_t(-1), p1 - p0);
-    }
-    release_wg();
-    if (threadIdx.x == 0) {
-      if (a.bcast) {
-        for (int32_t p = 0; p < N; ++p)
-          if (p != me) signal(a.flags[p] + ipc_flag_gather(me, j, part, N, np), a.round);
-      } else {
-        signal(fl + ipc_flag_reduced(j, part, N, np), a.round);
-      }
-    }
-    __syncthreads();  // `ok` is rewritten by the next item
+  bool ok = true;
+  if (threadIdx.x == 0) {
+    const uint64_t deadline = wall_clock64() + a.timeout;
+    for (int32_t s = 0; s < N && ok; ++s)
+      if (s != me) ok = wait_flag(fl + ipc_flag_push(s, j, np), a.round, err, deadline);
   }
+  ok = acquire_all(ok);
+  const int64_t e0 = int64_t(j) * a.portion;
+  const int64_t n = max(int64_t(0), min(a.portion, a.blen[me] - e0));
+  const int64_t p0 = min(n, part * per), p1 = min(n, p0 + per);
+  if (ok && p1 > p0) {
+    const int64_t e = e0 + p0;
+    reduce_span<T>(a, a.in + (a.bstart[me] + e) * ES, a.data[me] + e * ES, a.slot * ES,
+                   a.out + (a.bstart[me] + e) * ES, a.data[me] + (int64_t(N) * a.slot + e) * ES,
+                   a.bcast ? (int64_t(N + 1 + me) * a.slot + e) * ES : int64_t(-1), p1 - p0);
+  }
+  release_wg();
+  if (threadIdx.x == 0) {
+    if (a.bcast) {
+      for (int32_t p = 0; p < N; ++p)
+        if (p != me) signal(a.flags[p] + ipc_flag_gather(me, j, part, N, np), a.round);
+    } else {
+      signal(fl + ipc_flag_reduced(j, part, N, np), a.round);
+    }
+  }
+  __syncthreads();  // `ok` is rewritten by the next item
 }
 
-// grid <= max_wgs, looping over (portion j, peer) items, peers interleaved so
-// every link is busy at once: wait for rank p's reduced portion j (all its
-// parts), copy it into my output's block p.  Pull mode: the rows are read
-// from rank p's window over xGMI; bcast mode: rank p already wrote them into
-// my gather slot [p], the copy is local.
+// Rank p's reduced portion j (all its parts) -> my output's block p.  Pull
+// mode reads it from rank p's window over xGMI; bcast mode finds it in my
+// gather slot [p] (rank p wrote it there), the copy is local.
 template <int ES>
-__global__ __launch_bounds__(kThreads) void ipc_phase2_kernel(IpcArgs a) {
+__device__ void phase2_item(const IpcArgs& a, int32_t j, int32_t p) {
   const int32_t me = a.me, N = a.N, np = a.nportions;
   uint32_t* err = a.flags[me] + ipc_flag_error(N, np);
-  const int32_t items = np * (N - 1);
-  for (int32_t w = blockIdx.x; w < items; w += gridDim.x) {
-    const int32_t j = w / (N - 1);
-    const int32_t p = (me + 1 + w % (N - 1)) % N;
-    bool ok = true;
-    if (threadIdx.x == 0) {
-      const uint64_t deadline = wall_clock64() + a.timeout;
-      for (int32_t part = 0; part < kReduceSplit && ok; ++part)
-        ok = wait_flag(a.bcast ? a.flags[me] + ipc_flag_gather(p, j, part, N, np)
-                               : a.flags[p] + ipc_flag_reduced(j, part, N, np),
-                       a.round, err, deadline);
-    }
-    ok = acquire_all(ok);
-    const int64_t e0 = int64_t(j) * a.portion;
-    const int64_t n = max(int64_t(0), min(a.portion, a.blen[p] - e0));
-    const char* src = a.bcast ? a.data[me] + (int64_t(N + 1 + p) * a.slot + e0) * ES
-                              : a.data[p] + (int64_t(N) * a.slot + e0) * ES;
-    if (ok && n > 0) copy_bytes(a.out + (a.bstart[p] + e0) * ES, src, n * ES);
-    __syncthreads();  // `ok` is rewritten by the next item
+  bool ok = true;
+  if (threadIdx.x == 0) {
+    const uint64_t deadline = wall_clock64() + a.timeout;
+    for (int32_t part = 0; part < kReduceSplit && ok; ++part)
+      ok = wait_flag(a.bcast ? a.flags[me] + ipc_flag_gather(p, j, part, N, np)
+                             : a.flags[p] + ipc_flag_reduced(j, part, N, np),
+                     a.round, err, deadline);
+  }
+  ok = acquire_all(ok);
+  const int64_t e0 = int64_t(j) * a.portion;
+  const int64_t n = max(int64_t(0), min(a.portion, a.blen[p] - e0));
+  const char* src = a.bcast ? a.data[me] + (int64_t(N + 1 + p) * a.slot + e0) * ES
+                            : a.data[p] + (int64_t(N) * a.slot + e0) * ES;
+  if (ok && n > 0) copy_bytes(a.out + (a.bstart[p] + e0) * ES, src, n * ES);
+  __syncthreads();  // `ok` is rewritten by the next item
+}
+
+// Items in portion-major order (all peers of portion 0, then portion 1, ...),
+// peers rotated from me + 1 so every link is busy at once.
+__device__ inline int32_t item_peer(const IpcArgs& a, int32_t w) { return (a.me + 1 + w % (a.N - 1)) % a.N; }
+
+// ---- three kernels on one stream -----------------------------------------
+// push never waits; reduce and phase 2 loop over their items under a grid cap
+// so that workgroups parked on flags never fill the machine (ranks sharing a
+// card in tests need room for each other's push kernels).
+
+template <int ES>
+__global__ __launch_bounds__(kThreads) void ipc_push_kernel(IpcArgs a) {
+  const int32_t items = a.nportions * (a.N - 1);
+  for (int32_t w = blockIdx.x; w < items; w += gridDim.x) push_item<ES>(a, w / (a.N - 1), item_peer(a, w));
+}
+
+template <typename T>
+__global__ __launch_bounds__(kThreads) void ipc_reduce_kernel(IpcArgs a) {
+  const int32_t items = a.nportions * kReduceSplit;
+  for (int32_t w = blockIdx.x; w < items; w += gridDim.x) reduce_item<T>(a, w / kReduceSplit, w % kReduceSplit);
+}
+
+template <int ES>
+__global__ __launch_bounds__(kThreads) void ipc_phase2_kernel(IpcArgs a) {
+  const int32_t items = a.nportions * (a.N - 1);
+  for (int32_t w = blockIdx.x; w < items; w += gridDim.x) phase2_item<ES>(a, w / (a.N - 1), item_peer(a, w));
+}
+
+// ---- one fused launch -----------------------------------------------------
+// Roles by workgroup id: [0, gp) push, [gp, gp + gr) reduce, the rest phase 2.
+// A reducer starts on portion j as soon as its pushes landed and phase 2 moves
+// portion j while later portions are still being pushed, so the links stay
+// busy across the reduce.  Deadlock-free without co-residency: workgroups are
+// dispatched in id order (per XCD), pushers never wait, reducers wait only on
+// (remote) pushers and phase-2 workgroups only on (remote) reducers -- every
+// role depends on roles with lower ids only.
+template <typename T>
+__global__ __launch_bounds__(kThreads) void ipc_fused_kernel(IpcArgs a, int32_t gp, int32_t gr) {
+  constexpr int ES = sizeof(T);
+  const int32_t b = blockIdx.x;
+  if (b < gp) {
+    const int32_t items = a.nportions * (a.N - 1);
+    for (int32_t w = b; w < items; w += gp) push_item<ES>(a, w / (a.N - 1), item_peer(a, w));
+  } else if (b < gp + gr) {
+    const int32_t items = a.nportions * kReduceSplit;
+    for (int32_t w = b - gp; w < items; w += gr) reduce_item<T>(a, w / kReduceSplit, w % kReduceSplit);
+  } else {
+    const int32_t gq = int32_t(gridDim.x) - gp - gr;
+    const int32_t items = a.nportions * (a.N - 1);
+    for (int32_t w = b - gp - gr; w < items; w += gq) phase2_item<ES>(a, w / (a.N - 1), item_peer(a, w));
   }
 }
 
 template <typename T>
 void launch_round(hipStream_t s, const IpcArgs& a) {
   constexpr int ES = sizeof(T);
-  const dim3 peers(unsigned(a.nportions), unsigned(a.N - 1));
-  hipLaunchKernelGGL(ipc_push_kernel<ES>, peers, dim3(kThreads), 0, s, a);
   const int32_t cap = a.max_wgs > 0 ? a.max_wgs : 1024;
-  hipLaunchKernelGGL(ipc_reduce_kernel<T>, dim3(unsigned(std::min(a.nportions * kReduceSplit, cap))), dim3(kThreads), 0,
-                     s, a);
-  hipLaunchKernelGGL(ipc_phase2_kernel<ES>, dim3(unsigned(std::min(a.nportions * (a.N - 1), cap))), dim3(kThreads), 0,
-                     s, a);
+  const int32_t push_items = a.nportions * (a.N - 1), red_items = a.nportions * kReduceSplit;
+  if (a.fused) {
+    // one grid of <= cap workgroups split over the roles by their work
+    const int32_t total = push_items + red_items + push_items;
+    const int32_t budget = std::min(cap, total);
+    const int32_t gp = std::max(1, int32_t(int64_t(budget) * push_items / total));
+    const int32_t gr = std::max(1, int32_t(int64_t(budget) * red_items / total));
+    const int32_t gq = std::max(1, budget - gp - gr);
+    hipLaunchKernelGGL(ipc_fused_kernel<T>, dim3(unsigned(gp + gr + gq)), dim3(kThreads), 0, s, a, gp, gr);
+    return;
+  }
+  hipLaunchKernelGGL(ipc_push_kernel<ES>, dim3(unsigned(push_items)), dim3(kThreads), 0, s, a);
+  hipLaunchKernelGGL(ipc_reduce_kernel<T>, dim3(unsigned(std::min(red_items, cap))), dim3(kThreads), 0, s, a);
+  hipLaunchKernelGGL(ipc_phase2_kernel<ES>, dim3(unsigned(std::min(push_items, cap))), dim3(kThreads), 0, s, a);
 }
 
 // Like wait_flag, but also gives up when the host marked `peer` dead.

@@ -146,6 +146,7 @@ void IpcLane::round(StreamH s, const void* in, void* out) {
   a.nportions = nportions_;
   a.max_wgs = max_wgs_;
   a.bcast = bcast_ ? 1 : 0;
+  a.fused = fused_ ? 1 : 0;
   a.N = g_.N;
   a.me = me_;
   a.round = ++round_;

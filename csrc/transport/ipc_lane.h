@@ -53,6 +53,10 @@ class IpcLane {
   // in a round; modes may change between rounds.
   void set_bcast(bool on) { bcast_ = on; }
   bool bcast() const { return bcast_; }
+  // One launch per round with push / reduce / phase-2 roles (pipelined by
+  // portion) instead of three kernels.
+  void set_fused(bool on) { fused_ = on; }
+  bool fused() const { return fused_; }
   // Enqueue one exact round on `s`: in[S] from every rank summed into out[S].
   void round(StreamH s, const void* in, void* out);
   // Synchronous read of the window's error word (a wait timed out).
@@ -81,7 +85,7 @@ class IpcLane {
   int32_t max_wgs_ = 1024, sharers_ = 1;
   uint64_t timeout_ticks_ = 0;
   bool ready_ = false;
-  bool bcast_ = false;
+  bool bcast_ = false, fused_ = false;
   IpcLaneStats stats_;
 };
 

@@ -31,7 +31,7 @@ def main():
     ap.add_argument("--dtype", default="float32")
     ap.add_argument("--skip-rank", type=int, default=-1, help="this rank runs only round 0 (a missing peer)")
     ap.add_argument("--time", action="store_true")
-    ap.add_argument("--mode", default="pull", choices=["pull", "bcast", "alternate"])
+    ap.add_argument("--mode", default="pull", choices=["pull", "bcast", "alternate", "fused", "fused_bcast", "rotate"])
     ap.add_argument("--out-dir", default="", help="write rank<i>.json there (stdout lines of ranks interleave)")
     a = ap.parse_args()
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
@@ -47,7 +47,10 @@ def main():
         if r > 0 and rank == a.skip_rank:
             break
         if a.mode != "pull":
-            ar.set_ipc_mode("bcast" if a.mode == "bcast" or r % 2 else "pull")
+            variants = [("pull", False), ("bcast", False), ("pull", True), ("bcast", True)]
+            mode, fused = {"bcast": ("bcast", False), "fused": ("pull", True), "fused_bcast": ("bcast", True),
+                           "alternate": variants[r % 2], "rotate": variants[r % 4]}[a.mode]
+            ar.set_ipc_mode(mode, fused)
         x = torch.randn(a.size, generator=torch.Generator().manual_seed(5 * 1000 + rank * 7 + r),
                         dtype=torch.float32).to(dtype).to(dev)
         o = ar(x)

@@ -65,16 +65,21 @@ def test_ipc_lane_exact(n, size, dtype):
     (3, 1 << 20, "bcast"),        # scalar paths
     (3, 5 << 20, "alternate"),    # pull / bcast every other round: round-id flags serve both
     (4, 1 << 24, "bcast"),
+    (3, 5 << 20, "fused"),        # one launch per round, roles pipelined by portion
+    (4, 1 << 24, "fused_bcast"),
+    (2, 786440, "rotate"),        # pull / bcast / fused pull / fused bcast, round by round (scalar paths)
 ])
 def test_ipc_lane_bcast_mode(n, size, mode):
-    """Phase 2 as remote writes: each reducer stores its rows into every
-    peer's gather slot, and a local copy moves them into the output."""
+    """Phase 2 as remote writes (each reducer stores its rows into every
+    peer's gather slot, a local copy moves them into the output), and the
+    fused single-launch round, in either phase-2 mode."""
     r, rows = _run(n, "--size", str(size), "--rounds", "4", "--mode", mode)
     assert r.returncode == 0, r.stderr[-3000:]
     assert len(rows) == n
     for d in rows:
         assert d["ipc_error"] == 0 and d["exact"] == [True] * 4, d
-        assert d["ipc"]["bcast_rounds"] == (4 if mode == "bcast" else 2)
+        want_bcast = {"bcast": 4, "fused_bcast": 4, "fused": 0, "alternate": 2, "rotate": 2}[mode]
+        assert d["ipc"]["bcast_rounds"] == want_bcast
 
 
 def test_ipc_lane_missing_peer_times_out_cleanly():
