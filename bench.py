@@ -159,7 +159,12 @@ def run_cfg4(world: int, rank: int, dev, barrier, size_mb: float, delay_ms: floa
         t0 = time.perf_counter()
         for _ in range(rounds):
             outs.append(ar(x))
-        _sync()
+        # every round's output is ready on the caller's stream (the round's done
+        # point is waited for there); a device-wide synchronize would also wait
+        # for the transfers still parked on the straggler's pair stream -- the
+        # very wait this config shows the fast ranks do not need
+        if dev.type == "cuda":
+            torch.cuda.current_stream(dev).synchronize()
         dt = time.perf_counter() - t0
         cnt = [float(o.count.float().mean()) for o in outs]
         ar.fault_delay_s = 0.0
@@ -221,6 +226,16 @@ def run_extras(world: int, dev, barrier, which=("cfg3", "cfg4", "cfg5"), rank: i
                                                        data_plane="rccl" if data_plane == "rccl" else "ipc_p2p")
         except Exception as e:
             res["cfg4_error"] = f"{type(e).__name__}: {e}"[:300]
+            if data_plane == "rccl" and dev.type == "cuda":
+                # the pair communicators failed: the same schedule over the
+                # mailbox p2p in mapped peer memory (no RCCL)
+                try:
+                    r4 = run_cfg4(world, rank, dev, barrier, cfg4_size_mb, cfg4_delay_ms, cfg4_rounds,
+                                  data_plane="ipc_p2p")
+                    r4["data_plane"] = "ipc_p2p (after the RCCL attempt failed)"
+                    res["cfg4_threshold_straggler"] = r4
+                except Exception as e2:
+                    res["cfg4_error_ipc_p2p"] = f"{type(e2).__name__}: {e2}"[:300]
     try:
         if "cfg3" not in which:
             raise _Skip()
