@@ -45,3 +45,42 @@ def test_bench_extras_deadline_keeps_headline():
     d = json.loads(lines[0])
     assert d["exact"] is True and d["value"] > 0
     assert "extras_error" in d and "extra_configs" not in d
+
+
+@pytest.mark.parametrize("plane", ["ipc", "ipc_p2p"])
+def test_bench_multirank_on_one_card(plane):
+    """The driver's N>1 invocation (torch.distributed.run, one process per
+    rank) on the box's one GPU: ranks share the card (AKKA_SHARE_GPU=1) with a
+    data plane that needs no RCCL communicator.  One line, every phase passed,
+    every lane candidate exact, the chosen lane timed, cfg4 from the fast ranks'
+    side.  (Numbers are HBM-local, not the metric.)"""
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    n = 4 if plane == "ipc_p2p" else 2
+    extra = ["--extras", "on", "--extras-only", "cfg4", "--cfg4-size-mb", "4", "--cfg4-delay-ms", "40",
+             "--cfg4-rounds", "4"] if plane == "ipc_p2p" else ["--extras", "off"]
+    env = dict(os.environ, AKKA_SHARE_GPU="1", GPU_MAX_HW_QUEUES="8")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+                        "--gpus", str(n), "--steps", "4", "--warmup", "2", "--size-mb", "16", "--data-plane", plane,
+                        "--compare-rccl", "off", *extra],
+                       capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip().startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == n and d["exact"] is True and d["preflight"] == "passed" and d["value"] > 0
+    assert d["config"]["data_plane"] == plane and d["p2p_nranks"] == n
+    sel = d["lane_select"]
+    cands = [k for k in sel if k != "chosen"]
+    assert all(sel[k]["exact"] is True for k in cands), sel
+    assert d["lane"] == sel["chosen"]
+    if plane == "ipc_p2p":
+        assert {"collective", "p2p", "p2p_block", "ipc", "ipc_bcast", "ipc_fused", "ipc_fused_bcast"} <= set(cands)
+        c4 = d["extra_configs"]["cfg4_threshold_straggler"]
+        assert c4["fast_rank_ms_per_round_with_straggler"] < c4["straggler_ms_per_round_with_straggler"], c4
+    else:
+        assert set(cands) == {"ipc", "ipc_bcast", "ipc_fused", "ipc_fused_bcast"}
