@@ -381,6 +381,7 @@ class WorkerCore final : public EngineHost {
         is["bcast_rounds"] = ipc->stats().bcast_rounds;
         is["mode"] = ipc->bcast() ? "bcast" : "pull";
         is["fused"] = ipc->fused();
+        is["memory"] = ipc->memory_kind();
         is["bytes_pushed"] = ipc->stats().bytes_pushed;
         is["bytes_pulled"] = ipc->stats().bytes_pulled;
         ls["ipc"] = is;

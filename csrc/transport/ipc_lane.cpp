@@ -37,6 +37,23 @@ int64_t env_i64(const char* name, int64_t dflt) {
 
 }  // namespace
 
+void* ipc_alloc_window(size_t bytes, std::string* kind) {
+  const char* want = std::getenv("AKKA_IPC_MEM");
+  const std::string w = want && *want ? want : "fine";
+  void* p = nullptr;
+  if (w == "fine" || w == "uncached") {
+    const unsigned flags = w == "fine" ? hipDeviceMallocFinegrained : hipDeviceMallocUncached;
+    if (hipExtMallocWithFlags(&p, bytes, flags) == hipSuccess) {
+      if (kind) *kind = w;
+      return p;
+    }
+    (void)hipGetLastError();
+  }
+  AKKA_IPC_HIP(hipMalloc(&p, bytes));
+  if (kind) *kind = "coarse";
+  return p;
+}
+
 IpcLane::IpcLane(Device* dev, const Geometry& g, int32_t me, DType dt)
     : dev_(dev), g_(g), me_(me), dt_(dt), es_(dtype_size(dt)) {
   AKKA_CHECK(dev_ && !dev_->is_host(), "ipc lane needs a HIP device");
@@ -53,7 +70,7 @@ IpcLane::IpcLane(Device* dev, const Geometry& g, int32_t me, DType dt)
   nportions_ = int32_t(std::max<int64_t>(1, (maxb + portion_ - 1) / portion_));
   data_bytes_ = size_t(ipc_window_slots(g_.N)) * size_t(slot_) * es_;
   flag_bytes_ = ipc_flag_bytes(g_.N, nportions_);
-  AKKA_IPC_HIP(hipMalloc(reinterpret_cast<void**>(&data_), data_bytes_));
+  data_ = static_cast<char*>(ipc_alloc_window(data_bytes_, &mem_kind_));
   // Flags uncached: every poll and every signal goes to memory.
   if (hipExtMallocWithFlags(reinterpret_cast<void**>(&flags_), flag_bytes_, hipDeviceMallocUncached) != hipSuccess) {
     (void)hipGetLastError();

@@ -32,6 +32,14 @@
 
 namespace akka {
 
+// Device memory another GPU writes into and this one reads (or the reverse)
+// over xGMI.  Coarse-grained memory (plain hipMalloc) is only coherent at
+// kernel boundaries of ONE device: a line of it cached in this GPU's L2 is not
+// invalidated when a peer overwrites the memory behind it.  The windows are
+// therefore fine-grained by default (AKKA_IPC_MEM = fine | uncached | coarse);
+// `kind` reports what was allocated.
+void* ipc_alloc_window(size_t bytes, std::string* kind);
+
 struct IpcLaneStats {
   int64_t rounds = 0, bcast_rounds = 0, bytes_pushed = 0, bytes_pulled = 0;
 };
@@ -64,6 +72,7 @@ class IpcLane {
   int32_t nportions() const { return nportions_; }
   int64_t portion_elems() const { return portion_; }
   size_t window_bytes() const { return data_bytes_; }
+  const std::string& memory_kind() const { return mem_kind_; }
   int32_t max_wgs() const { return max_wgs_; }
   int32_t ranks_on_this_gpu() const { return sharers_; }
   const IpcLaneStats& stats() const { return stats_; }
@@ -86,6 +95,7 @@ class IpcLane {
   uint64_t timeout_ticks_ = 0;
   bool ready_ = false;
   bool bcast_ = false, fused_ = false;
+  std::string mem_kind_;
   IpcLaneStats stats_;
 };
 

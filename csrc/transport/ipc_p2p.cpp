@@ -28,6 +28,7 @@
 #include <tuple>
 
 #include "../kernels/ipc_kernels.h"
+#include "ipc_lane.h"
 #include "ipc_p2p.h"
 #include "p2p.h"
 
@@ -67,7 +68,7 @@ class IpcP2P final : public P2P {
     wpp_ = int32_t(std::clamp<int64_t>(env_i64("AKKA_IPC_P2P_WGS", 8), 1, 64));
     mbox_bytes_ = size_t(n_) * kChannels * size_t(nslots_) * size_t(piece_);
     flag_bytes_ = ipc_p2p_flag_bytes(n_, kChannels, nslots_, wpp_);
-    AKKA_P2P_HIP(hipMalloc(reinterpret_cast<void**>(&mbox_), mbox_bytes_));
+    mbox_ = static_cast<char*>(ipc_alloc_window(mbox_bytes_, &mem_kind_));  // fine-grained (ipc_lane.h)
     if (hipExtMallocWithFlags(reinterpret_cast<void**>(&flags_), flag_bytes_, hipDeviceMallocUncached) != hipSuccess) {
       (void)hipGetLastError();
       AKKA_P2P_HIP(hipMalloc(reinterpret_cast<void**>(&flags_), flag_bytes_));
@@ -106,6 +107,7 @@ class IpcP2P final : public P2P {
   int32_t nranks() const override { return n_; }
   const char* name() const override { return "ipc"; }
   P2PInfo info() const override { return P2PInfo{"ipc", n_, rank_, device_, 0}; }
+  const std::string& memory_kind() const { return mem_kind_; }
 
   std::string handle() const override {
     Blob b;
@@ -189,6 +191,7 @@ class IpcP2P final : public P2P {
   int32_t nslots_ = 4, wpp_ = 8;
   size_t mbox_bytes_ = 0, flag_bytes_ = 0;
   char* mbox_ = nullptr;
+  std::string mem_kind_;
   uint32_t* flags_ = nullptr;
   uint32_t* host_ = nullptr;      // [0] error, [1 + p] peer p aborted
   uint32_t* host_dev_ = nullptr;  // the same, as the device sees it
