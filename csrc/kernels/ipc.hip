@@ -101,6 +101,49 @@ __device__ void copy_bytes(char* __restrict__ dst, const char* __restrict__ src,
   }
 }
 
+// ---- reads of window memory another rank wrote ------------------------------
+// Every byte a peer stored into a window (slots, reduced rows, gather rows,
+// mailboxes) is read with system-coherent buffer loads (sc0 sc1: L1 and L2
+// bypassed), so no line cached from an earlier round can be returned -- the
+// consumer side of the hand-off is correct whatever caching policy the
+// window's memory has on this or the peer GPU.  Buffer loads also bound every
+// read by the span's size (out-of-range reads return 0).
+constexpr int kSysAux = 17;  // sc0 | sc1
+
+__device__ inline __amdgpu_buffer_rsrc_t sys_rsrc(const void* base, int64_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, int(min(bytes, int64_t(0x7fffffff))),
+                                           0x00020000);
+}
+__device__ inline uint4 load_sys16(__amdgpu_buffer_rsrc_t r, int64_t off) {
+  const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, int(off), 0, kSysAux);
+  return make_uint4(v[0], v[1], v[2], v[3]);
+}
+
+// dst (local, plain stores) <- src (window memory written by a peer).
+__device__ void copy_in(char* __restrict__ dst, const char* __restrict__ src, int64_t bytes) {
+  const auto r = sys_rsrc(src, bytes);
+  if (((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src) | uintptr_t(bytes)) & 15) == 0) {
+    uint4* d = reinterpret_cast<uint4*>(dst);
+    const int64_t n = bytes >> 4;
+    int64_t i = threadIdx.x;
+    for (; i + (kUnroll - 1) * kThreads < n; i += kUnroll * kThreads) {
+      uint4 v[kUnroll];
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) v[u] = load_sys16(r, (i + u * kThreads) * 16);
+#pragma unroll
+      for (int u = 0; u < kUnroll; ++u) d[i + u * kThreads] = v[u];
+    }
+    for (; i < n; i += kThreads) d[i] = load_sys16(r, i * 16);
+  } else if (((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src) | uintptr_t(bytes)) & 3) == 0) {
+    uint32_t* d = reinterpret_cast<uint32_t*>(dst);
+    for (int64_t i = threadIdx.x; i < (bytes >> 2); i += kThreads)
+      d[i] = __builtin_amdgcn_raw_buffer_load_b32(r, int(i * 4), 0, kSysAux);
+  } else {
+    for (int64_t i = threadIdx.x; i < bytes; i += kThreads)
+      dst[i] = char(__builtin_amdgcn_raw_buffer_load_b8(r, int(i), 0, kSysAux));
+  }
+}
+
 __device__ inline float bf16_to_f32(uint16_t h) { return __uint_as_float(uint32_t(h) << 16); }
 __device__ inline uint16_t f32_to_bf16(float f) {
   const uint32_t u = __float_as_uint(f);
@@ -124,6 +167,9 @@ struct Elt<float> {
                       __float_as_uint(acc[3]));
   }
   __device__ static float load1(const char* p) { return *reinterpret_cast<const float*>(p); }
+  __device__ static float load1_sys(__amdgpu_buffer_rsrc_t r, int64_t off) {
+    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, int(off), 0, kSysAux));
+  }
   __device__ static void store1(char* p, float v) { *reinterpret_cast<float*>(p) = v; }
 };
 template <>
@@ -144,6 +190,9 @@ struct Elt<uint16_t> {
     return make_uint4(w[0], w[1], w[2], w[3]);
   }
   __device__ static float load1(const char* p) { return bf16_to_f32(*reinterpret_cast<const uint16_t*>(p)); }
+  __device__ static float load1_sys(__amdgpu_buffer_rsrc_t r, int64_t off) {
+    return bf16_to_f32(uint16_t(__builtin_amdgcn_raw_buffer_load_b16(r, int(off), 0, kSysAux)));
+  }
   __device__ static void store1(char* p, float v) { *reinterpret_cast<uint16_t*>(p) = f32_to_bf16(v); }
 };
 
@@ -169,12 +218,18 @@ __device__ void reduce_span(const IpcArgs& a, const char* mine, const char* slot
 #pragma unroll
         for (int e = 0; e < PV; ++e) acc[u][e] = 0.f;
       for (int s = 0; s < N; ++s) {
-        const uint4* src = reinterpret_cast<const uint4*>(s == me ? mine : slots + int64_t(s) * slot_bytes);
         uint4 v[kUnroll];
+        if (s == me) {  // my own input: ordinary memory of this rank
+          const uint4* src = reinterpret_cast<const uint4*>(mine);
 #pragma unroll
-        for (int u = 0; u < kUnroll; ++u) {
-          const int64_t i = i0 + int64_t(u) * kThreads;
-          v[u] = i < nv ? src[i] : make_uint4(0, 0, 0, 0);
+          for (int u = 0; u < kUnroll; ++u) {
+            const int64_t i = i0 + int64_t(u) * kThreads;
+            v[u] = i < nv ? src[i] : make_uint4(0, 0, 0, 0);
+          }
+        } else {  // slot s: written by rank s
+          const auto r = sys_rsrc(slots + int64_t(s) * slot_bytes, n * ES);
+#pragma unroll
+          for (int u = 0; u < kUnroll; ++u) v[u] = load_sys16(r, (i0 + int64_t(u) * kThreads) * 16);  // 0 past the end
         }
 #pragma unroll
         for (int u = 0; u < kUnroll; ++u) Elt<T>::add(acc[u], v[u]);
@@ -197,7 +252,9 @@ __device__ void reduce_span(const IpcArgs& a, const char* mine, const char* slot
   } else {
     for (int64_t i = threadIdx.x; i < n; i += kThreads) {
       float acc = 0.f;
-      for (int s = 0; s < N; ++s) acc += Elt<T>::load1((s == me ? mine : slots + int64_t(s) * slot_bytes) + i * ES);
+      for (int s = 0; s < N; ++s)
+        acc += s == me ? Elt<T>::load1(mine + i * ES)
+                       : Elt<T>::load1_sys(sys_rsrc(slots + int64_t(s) * slot_bytes, n * ES), i * ES);
       Elt<T>::store1(o + i * ES, acc);
       if (bc) {
         for (int p = 0; p < N; ++p)
@@ -282,7 +339,7 @@ __device__ void phase2_item(const IpcArgs& a, int32_t j, int32_t p) {
   const int64_t n = max(int64_t(0), min(a.portion, a.blen[p] - e0));
   const char* src = a.bcast ? a.data[me] + (int64_t(N + 1 + p) * a.slot + e0) * ES
                             : a.data[p] + (int64_t(N) * a.slot + e0) * ES;
-  if (ok && n > 0) copy_bytes(a.out + (a.bstart[p] + e0) * ES, src, n * ES);
+  if (ok && n > 0) copy_in(a.out + (a.bstart[p] + e0) * ES, src, n * ES);
   __syncthreads();  // `ok` is rewritten by the next item
 }
 
@@ -415,8 +472,8 @@ __global__ __launch_bounds__(kThreads) void ipc_p2p_kernel(IpcP2PArgs a) {
         }
         ok = acquire_all(ok);
         if (ok && b1 > b0)
-          copy_bytes(op.buf + pb0 + b0, a.mbox[me] + ipc_p2p_box(peer, ch, slot, a.nch, a.nslots) * a.piece + b0,
-                     b1 - b0);
+          copy_in(op.buf + pb0 + b0, a.mbox[me] + ipc_p2p_box(peer, ch, slot, a.nch, a.nslots) * a.piece + b0,
+                  b1 - b0);
         release_wg();
         if (threadIdx.x == 0)
           signal(a.flags[peer] + ipc_p2p_flag_consumed(me, ch, slot, w, a.N, a.nch, a.nslots, a.wpp), seq + 1u);
