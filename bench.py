@@ -54,7 +54,7 @@ def parse():
     p.add_argument("--preflight", choices=["auto", "on"], default="auto",
                    help="auto: preflight round only at N>1")
     p.add_argument("--pg-timeout-s", type=float, default=300.0, help="host (gloo) process group timeout")
-    p.add_argument("--extras-only", default="", help="comma list of extra configs to run (cfg3,cfg4,cfg5)")
+    p.add_argument("--extras-only", default="", help="comma list of extra configs to run (cfg1,cfg3,cfg4,cfg5)")
     p.add_argument("--cfg4-size-mb", type=float, default=64.0, help="config 4 buffer (MiB)")
     p.add_argument("--cfg4-delay-ms", type=float, default=50.0, help="config 4 straggler delay per round")
     p.add_argument("--cfg4-rounds", type=int, default=10)
@@ -190,6 +190,69 @@ def run_cfg4(world: int, rank: int, dev, barrier, size_mb: float, delay_ms: floa
     return res
 
 
+def run_cfg1(rounds: int = 300) -> dict:
+    """BASELINE config 1, the reference's README demo: a master and 2 worker
+    PROCESSES (the CLI, as `sbt runMain ...` in the reference) over loopback
+    TCP, dataSize 10, maxChunkSize 2, maxLag 1, CPU data plane.  Run twice:
+    the demo's thresholds (1 / 1 / 0.8, M:98-107) and exact thresholds with
+    the sink's assertMultiple check (W:337-340).  Reports rounds per second
+    and the sink's own MB/s figure (W:329-342) over the last checkpoint
+    interval of each worker."""
+    import re
+    import socket
+    import subprocess
+    import tempfile
+
+    base = [sys.executable, "-m", "akka_allreduce_amd", "--log-level", "WARNING"]
+    cp = max(1, rounds // 3)
+    res = {"workers": 2, "data_size": 10, "max_chunk_size": 2, "max_lag": 1, "rounds": rounds,
+           "transport": "tcp, one process per worker (cpu)"}
+    for tag, thc, mult in (("demo_thresholds", 0.8, 0), ("exact_assert", 1.0, 2)):
+        with socket.socket() as sk:
+            sk.bind(("127.0.0.1", 0))
+            port = sk.getsockname()[1]
+        with tempfile.TemporaryDirectory() as td:
+            logs = [open(os.path.join(td, f"p{i}.log"), "w+") for i in range(3)]
+            procs = [subprocess.Popen(base + ["master", "--port", str(port), "--workers", "2", "--data-size", "10",
+                                              "--max-chunk-size", "2", "--max-round", str(rounds), "--max-lag", "1",
+                                              "--th-reduce", "1.0", "--th-complete", str(thc), "--transport", "tcp"],
+                                      stdout=logs[0], stderr=subprocess.STDOUT, cwd=os.path.dirname(__file__) or ".")]
+            t_end = time.time() + 20
+            while time.time() < t_end:  # master listening?
+                try:
+                    socket.create_connection(("127.0.0.1", port), timeout=0.5).close()
+                    break
+                except OSError:
+                    time.sleep(0.1)
+            procs += [subprocess.Popen(base + ["worker", "--master", f"127.0.0.1:{port}", "--data-size", "10",
+                                               "--checkpoint", str(cp), "--assert-multiple", str(mult), "--device",
+                                               "cpu"], stdout=logs[i], stderr=subprocess.STDOUT,
+                                       cwd=os.path.dirname(__file__) or ".") for i in (1, 2)]
+            rcs = []
+            try:
+                for p in procs:
+                    rcs.append(p.wait(timeout=90))
+            finally:
+                for p in procs:
+                    if p.poll() is None:
+                        p.kill()
+                        p.wait()
+            entry = {"rcs": rcs, "rounds_per_s": [], "sink_MBps": [], "failures": []}
+            for f in logs[1:]:
+                f.seek(0)
+                txt = f.read()
+                el = [float(x) for x in re.findall(r"Mbytes in ([0-9.]+) seconds", txt)]
+                mb = [float(x) for x in re.findall(r"at ([0-9.]+) MBytes/sec", txt)]
+                fl = re.findall(r"failures=(\d+)", txt)
+                entry["rounds_per_s"].append(round(cp / el[-1], 1) if el else None)
+                entry["sink_MBps"].append(mb[-1] if mb else None)
+                entry["failures"].append(int(fl[-1]) if fl else None)
+            for f in logs:
+                f.close()
+            res[tag] = entry
+    return res
+
+
 def apply_lane_choice(ar, name) -> None:
     """Put a fresh ThresholdAllreduce on the lane the headline's lane selection
     chose (collective / p2p / p2p_block / ipc / ipc_bcast); None: leave auto."""
@@ -205,7 +268,7 @@ def apply_lane_choice(ar, name) -> None:
         ar.set_exact_unit_bytes(1 << 40 if name == "p2p_block" else -1)
 
 
-def run_extras(world: int, dev, barrier, which=("cfg3", "cfg4", "cfg5"), rank: int = 0,
+def run_extras(world: int, dev, barrier, which=("cfg1", "cfg3", "cfg4", "cfg5"), rank: int = 0,
                cfg4_size_mb: float = 64.0, cfg4_delay_ms: float = 50.0, cfg4_rounds: int = 10,
                lane: str | None = None, data_plane: str = "rccl") -> dict:
     """BASELINE config 3 (8-rank bf16, 1 GB buffer, link-sized chunks),
@@ -217,6 +280,11 @@ def run_extras(world: int, dev, barrier, which=("cfg3", "cfg4", "cfg5"), rank: i
 
     res: dict = {}
     keep = []  # communicators stay alive until exit (no per-rank teardown ordering)
+    if "cfg1" in which and rank == 0:
+        try:
+            res["cfg1_readme_demo_cluster"] = run_cfg1()
+        except Exception as e:
+            res["cfg1_error"] = f"{type(e).__name__}: {e}"[:200]
     if "cfg4" in which and world > 1:
         try:
             # thresholds < 1 need a two-sided transport: RCCL pair communicators, or
@@ -703,7 +771,7 @@ def main() -> int:
         late = dict(line)
         late["extras_error"] = f"extras not done after {args.extras_deadline_s:g} s; skipped"
         guard.arm(args.extras_deadline_s, late, exit_code=0 if ok in (None, True) else 1)
-        which = tuple(args.extras_only.split(",")) if args.extras_only else ("cfg3", "cfg4", "cfg5")
+        which = tuple(args.extras_only.split(",")) if args.extras_only else ("cfg1", "cfg3", "cfg4", "cfg5")
         line["extra_configs"] = run_extras(world, dev, barrier, which, rank, args.cfg4_size_mb,
                                            args.cfg4_delay_ms, args.cfg4_rounds, lane=chosen_lane,
                                            data_plane=args.data_plane)
