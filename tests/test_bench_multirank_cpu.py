@@ -124,3 +124,15 @@ def test_bench_cfg4_threshold_straggler():
     assert c["straggler_ms_per_round_with_straggler"] >= delay
     assert c["fast_rank_ms_per_round_with_straggler"] < delay / 3, c
     assert 0 < c["fast_rank_mean_count_with_straggler"] <= 3
+
+
+def test_bench_cfg1_readme_demo():
+    """BASELINE config 1 in the bench extras: the reference's README demo as
+    a master and 2 worker processes over TCP, with the demo's thresholds and
+    with exact thresholds + the sink's assertMultiple check."""
+    d = _run(2, "--extras", "on", "--extras-only", "cfg1")
+    c = d["extra_configs"]["cfg1_readme_demo_cluster"]
+    for tag in ("demo_thresholds", "exact_assert"):
+        assert c[tag]["rcs"] == [0, 0, 0], c
+        assert all(r and r > 0 for r in c[tag]["rounds_per_s"]), c
+    assert c["exact_assert"]["failures"] == [0, 0]
