@@ -429,7 +429,19 @@ def main() -> int:
             "thresholds": [1.0, args.th_reduce, args.th_complete],
         },
     }
-    guard = PhaseGuard(base, rank, world, debug_path)
+    # stdout carries exactly ONE line, this rank-0 JSON line: everything else
+    # that writes to fd 1 (gloo's connection banners, RCCL's version banner,
+    # stray prints of any rank) goes to stderr from here on.  The real stdout
+    # stays reachable through a private descriptor, for the result line and
+    # for the native watchdog's failure line.
+    sys.stdout.flush()
+    out_fd = os.dup(1)
+    os.dup2(2, 1)
+    json_out = os.fdopen(out_fd, "w", buffering=1)
+    from akka_allreduce_amd._native_loader import load as _load_native
+
+    _load_native().watchdog_set_out_fd(out_fd)
+    guard = PhaseGuard(base, rank, world, debug_path, stream=json_out)
     dl = args.phase_deadline_s
 
     def init():
@@ -780,7 +792,7 @@ def main() -> int:
         guard.disarm()
 
     if rank == 0:
-        print(json.dumps(line), flush=True)
+        print(json.dumps(line), file=json_out, flush=True)
     if world > 1 and dist.is_initialized():
         guard.run("teardown", dl, lambda: (dist.barrier(), dist.destroy_process_group()), agree=False)
     return 0 if ok in (None, True) else 1

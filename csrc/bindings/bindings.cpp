@@ -662,6 +662,7 @@ PYBIND11_MODULE(_native, m) {
         py::arg("beacon_path") = "",
         "Native phase watchdog (runtime/watchdog.h): on expiry write `line` and _exit(exit_code)");
   m.def("watchdog_disarm", &watchdog_disarm);
+  m.def("watchdog_set_out_fd", &watchdog_set_out_fd);
   m.def("watchdog_install_sigterm", &watchdog_install_sigterm);
   m.def("json_escape", &json_escape);
   m.def("hw_queue_probe", [](int32_t kmax, int32_t wait_ms) {

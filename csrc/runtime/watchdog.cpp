@@ -1,3 +1,4 @@
+#include <atomic>
 #include "watchdog.h"
 
 #include <fcntl.h>
@@ -22,6 +23,7 @@ struct State {
   double seconds = 0;
   std::string line;
   bool to_stdout = false;
+  std::atomic<int> out_fd{1};  // "stdout" for failure lines (watchdog_set_out_fd)
   std::string debug_path;
   std::string beacon_path;
   int exit_code = 3;
@@ -82,7 +84,7 @@ void replace_token(std::string& s, const std::string& token, const std::string& 
   replace_token(line, "\"__AKKA_REASON__\"", "\"" + json_escape(reason) + "\"");
   replace_token(line, "\"__AKKA_TAIL__\"", "\"" + json_escape(tail) + "\"");
   if (!line.empty() && line.back() != '\n') line.push_back('\n');
-  write_all(to_stdout ? 1 : 2, line);
+  write_all(to_stdout ? st().out_fd.load() : 2, line);
   write_all(2, "akka watchdog: " + reason + "; exiting " + std::to_string(code) + "\n");
   if (!tail.empty()) write_all(2, "---- tail of " + path + " ----\n" + tail + "\n");
   ::fsync(1);
@@ -200,6 +202,8 @@ std::string json_escape(const std::string& s) {
   }
   return o;
 }
+
+void watchdog_set_out_fd(int fd) { st().out_fd.store(fd < 0 ? 1 : fd); }
 
 void watchdog_arm(double seconds, const std::string& line, bool to_stdout, const std::string& debug_path,
                   int exit_code, int tail_bytes, const std::string& beacon_path) {

@@ -25,6 +25,9 @@ namespace akka {
 // armed, the watchdog checks for it every 200 ms and fires at once ("failure
 // reported by a rank: <file contents>"), so one rank's error ends every rank promptly
 // even when the others are blocked in a collective that will never match.
+// The descriptor failure lines go to when `to_stdout` (default 1): a program
+// that moves fd 1 elsewhere keeps a private copy of its real stdout here.
+void watchdog_set_out_fd(int fd);
 void watchdog_arm(double seconds, const std::string& line, bool to_stdout, const std::string& debug_path,
                   int exit_code, int tail_bytes, const std::string& beacon_path = "");
 void watchdog_disarm();

@@ -33,8 +33,10 @@ def _run(n, *extra, env=None, expect_rc=0):
         assert r.returncode == 0, r.stderr[-3000:]
     else:
         assert r.returncode != 0, r.stdout[-3000:]
-    lines = [ln for ln in r.stdout.splitlines() if ln.strip().startswith("{")]
-    assert len(lines) == 1, (r.stdout, r.stderr[-3000:])
+    # stdout carries exactly the one JSON line (banners of gloo / RCCL and any
+    # rank's prints are moved to stderr)
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1 and lines[0].startswith("{"), (r.stdout, r.stderr[-3000:])
     return json.loads(lines[0])
 
 
