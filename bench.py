@@ -539,23 +539,6 @@ def main() -> int:
     if ar.transport == "reactive":
         args.async_op = False  # reactive rounds return once complete (progress is host-polled)
 
-    def lane_rate(k: int) -> float:
-        """Seconds per round of the current lane over k rounds (max over ranks)."""
-        o = ar(x, async_op=args.async_op, out=out_buf)
-        o.wait()
-        _sync()
-        barrier()
-        t0 = time.perf_counter()
-        for _ in range(k):
-            o = ar(x, async_op=args.async_op, out=out_buf)
-        o.wait()
-        _sync()
-        barrier()
-        t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
-        if world > 1:
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        return float(t.item()) / k
-
     # Lane selection (untimed, before the warmup): both exact-round lanes of
     # the stream transport compute the same exact sum -- RCCL reduce-scatter +
     # all-gather, or the chunk-pipelined direct p2p schedule with our reduce
@@ -578,6 +561,44 @@ def main() -> int:
 
     chosen_lane = args.lane if args.lane != "auto" else None
 
+    def local_exact(salt: int) -> bool:
+        y = torch.full((S,), float((rank + 1) * (salt + 1)), device=dev, dtype=dtype)
+        o = ar(y)
+        want = float((salt + 1) * world * (world + 1) // 2)
+        return bool(torch.all(o.data == want).item()) and bool(torch.all(o.count == world).item())
+
+    def eval_lane(name: str) -> dict:
+        """One candidate: three exact rounds with different values (the last
+        after timed rounds of other data, so a stale read would show) and 8
+        timed rounds.  Only rounds run inside the try -- no collective of the
+        host group -- so a rank whose rounds raise (an RCCL or ipc error)
+        still meets the others at the single agreement below."""
+        ok, ms, err = False, 0.0, None
+        try:
+            apply_lane(name)
+            ok = local_exact(1) and local_exact(2)
+            if ok:
+                o = ar(x, async_op=args.async_op, out=out_buf)
+                o.wait()
+                _sync()
+                t0 = time.perf_counter()
+                for _ in range(8):  # the ranks are coupled by the rounds themselves
+                    o = ar(x, async_op=args.async_op, out=out_buf)
+                o.wait()
+                _sync()
+                ms = (time.perf_counter() - t0) / 8 * 1e3
+                ok = local_exact(3)
+        except Exception as e:  # noqa: BLE001 - the lane is rejected, the run goes on
+            ok, err = False, f"{type(e).__name__}: {e}"[:160]
+        t = torch.tensor([0.0 if ok else 1.0, ms], dtype=torch.float64)
+        if world > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        good = float(t[0].item()) == 0.0
+        d = {"exact": good, "ms": round(float(t[1].item()), 4) if good else None}
+        if err:
+            d["error"] = err
+        return d
+
     def lane_select():
         env_phase_stall(rank, "lane_select")
         res = {}
@@ -599,14 +620,7 @@ def main() -> int:
             else:
                 res["ipc"] = {"exact": None, "ms": None, "error": err or "another rank could not open its windows"}
         for name in lanes:
-            apply_lane(name)
-            exact = exact_round(f"lane_{name}", salt=1) and exact_round(f"lane_{name}", salt=2)
-            # 8 rounds between barriers: a barrier's own latency stays a small
-            # share of the per-round figure the lanes are compared on
-            ms = round(lane_rate(8) * 1e3, 4) if exact else None
-            if exact:  # and again after rounds of other data (stale reads would show here)
-                exact = exact_round(f"lane_{name}", salt=3)
-            res[name] = {"exact": exact, "ms": ms if exact else None}
+            res[name] = eval_lane(name)
         good = [n for n in lanes if res[n]["exact"]]
         if not good:
             raise RuntimeError(f"no exact lane: {res}")

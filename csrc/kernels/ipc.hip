@@ -288,7 +288,7 @@ __device__ void reduce_item(const IpcArgs& a, int32_t j, int32_t part) {
   constexpr int ES = sizeof(T);
   const int32_t me = a.me, N = a.N, np = a.nportions;
   uint32_t* fl = a.flags[me];
-  uint32_t* err = fl + ipc_flag_error(N, np);
+  uint32_t* err = a.err;
   // each item's part of its portion (a multiple of 64 elements)
   const int64_t per = ((a.portion / kReduceSplit) + 63) / 64 * 64;
   bool ok = true;
@@ -325,7 +325,7 @@ __device__ void reduce_item(const IpcArgs& a, int32_t j, int32_t part) {
 template <int ES>
 __device__ void phase2_item(const IpcArgs& a, int32_t j, int32_t p) {
   const int32_t me = a.me, N = a.N, np = a.nportions;
-  uint32_t* err = a.flags[me] + ipc_flag_error(N, np);
+  uint32_t* err = a.err;
   bool ok = true;
   if (threadIdx.x == 0) {
     const uint64_t deadline = wall_clock64() + a.timeout;

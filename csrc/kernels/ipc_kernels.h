@@ -49,6 +49,7 @@ struct IpcArgs {
   uint64_t timeout = 0;     // per wait, in wall-clock ticks (100 MHz)
   const char* in = nullptr;  // round input [S]
   char* out = nullptr;       // round output [S]
+  uint32_t* err = nullptr;   // host-mapped error word: set on a timed-out wait (read by the host each round)
 };
 
 // Flag words of one rank's flag area (uint32 index).

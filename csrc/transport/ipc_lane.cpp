@@ -77,6 +77,11 @@ IpcLane::IpcLane(Device* dev, const Geometry& g, int32_t me, DType dt)
     AKKA_IPC_HIP(hipMalloc(reinterpret_cast<void**>(&flags_), flag_bytes_));
   }
   AKKA_IPC_HIP(hipMemset(flags_, 0, flag_bytes_));
+  // the error word lives in host memory: the host reads it every round for free
+  AKKA_IPC_HIP(hipHostMalloc(reinterpret_cast<void**>(&err_host_), sizeof(uint32_t),
+                             hipHostMallocMapped | hipHostMallocCoherent));
+  *err_host_ = 0;
+  AKKA_IPC_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&err_dev_), err_host_, 0));
   AKKA_IPC_HIP(hipDeviceSynchronize());
   int khz = 0;
   if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev_->device_index()) != hipSuccess || khz <= 0)
@@ -98,6 +103,7 @@ IpcLane::~IpcLane() {
   }
   if (data_) hipFree(data_);
   if (flags_) hipFree(flags_);
+  if (err_host_) hipHostFree(err_host_);
 }
 
 std::string IpcLane::handle() const {
@@ -170,6 +176,7 @@ void IpcLane::round(StreamH s, const void* in, void* out) {
   a.timeout = timeout_ticks_;
   a.in = static_cast<const char*>(in);
   a.out = static_cast<char*>(out);
+  a.err = err_dev_;
   launch_ipc_round(static_cast<hipStream_t>(s), a, dt_);
   AKKA_IPC_HIP(hipGetLastError());
   ++stats_.rounds;
@@ -179,11 +186,11 @@ void IpcLane::round(StreamH s, const void* in, void* out) {
 }
 
 uint32_t IpcLane::error() {
-  uint32_t v = 0;
   AKKA_IPC_HIP(hipSetDevice(dev_->device_index()));
   AKKA_IPC_HIP(hipDeviceSynchronize());  // the rounds enqueued so far have drained
-  AKKA_IPC_HIP(hipMemcpy(&v, flags_ + ipc_flag_error(g_.N, nportions_), sizeof(v), hipMemcpyDeviceToHost));
-  return v;
+  return error_now();
 }
+
+uint32_t IpcLane::error_now() const { return __atomic_load_n(err_host_, __ATOMIC_ACQUIRE); }
 
 }  // namespace akka

@@ -67,8 +67,10 @@ class IpcLane {
   bool fused() const { return fused_; }
   // Enqueue one exact round on `s`: in[S] from every rank summed into out[S].
   void round(StreamH s, const void* in, void* out);
-  // Synchronous read of the window's error word (a wait timed out).
+  // The error word (a wait timed out): error() after draining the device,
+  // error_now() as far as the kernels got (no synchronisation).
   uint32_t error();
+  uint32_t error_now() const;
   int32_t nportions() const { return nportions_; }
   int64_t portion_elems() const { return portion_; }
   size_t window_bytes() const { return data_bytes_; }
@@ -88,6 +90,8 @@ class IpcLane {
   size_t data_bytes_ = 0, flag_bytes_ = 0;
   char* data_ = nullptr;
   uint32_t* flags_ = nullptr;
+  uint32_t* err_host_ = nullptr;  // host-mapped error word
+  uint32_t* err_dev_ = nullptr;
   std::vector<char*> peer_data_;      // [N] mapped windows (own = data_)
   std::vector<uint32_t*> peer_flags_; // [N]
   uint32_t round_ = 0;

@@ -227,6 +227,10 @@ void StreamLink::set_ipc(std::unique_ptr<IpcLane> ipc) {
 
 void StreamLink::ipc_round(int32_t r) {
   AKKA_CHECK(ipc_ && ipc_->ready(), "ipc lane selected but its windows are not open (ipc_open)");
+  // a wait of an earlier round timed out (a peer missing or too late): like
+  // an RCCL async error, it ends the lane's rounds with an exception
+  AKKA_CHECK(ipc_->error_now() == 0,
+             "ipc lane: a wait of an earlier round timed out (peer missing?); its rounds are not trustworthy");
   Device* dev = dp_->device();
   engine_->ensure_output(r);
   StreamH comm = dev->comm_stream();

@@ -58,6 +58,13 @@ def main():
         want = expected(a.size, world, r, dtype, 5)
         res["exact"].append(bool(torch.equal(o.data.cpu(), want)) and bool((o.count.cpu() == world).all()))
     res["ipc_error"] = ar.ipc_error()
+    if a.skip_rank >= 0 and rank != a.skip_rank and res["ipc_error"]:
+        # the next round on this lane refuses to run (like an RCCL async error)
+        try:
+            ar(torch.zeros(a.size, device=dev, dtype=dtype))
+            res["next_round_raised"] = False
+        except Exception as e:  # noqa: BLE001
+            res["next_round_raised"] = "timed out" in str(e)
     st = ar.state()["link"]
     res["ipc_rounds"] = st["ipc_rounds"]
     res["ipc"] = st.get("ipc")

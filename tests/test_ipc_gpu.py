@@ -84,10 +84,12 @@ def test_ipc_lane_bcast_mode(n, size, mode):
 
 def test_ipc_lane_missing_peer_times_out_cleanly():
     """Rank 1 leaves after round 0: rank 0's round 1 waits (bounded, 0.5 s)
-    for rank 1's flags, reports ipc_error and the job still ends."""
+    for rank 1's flags, reports ipc_error, its next round raises, and the job
+    still ends."""
     r, rows = _run(2, "--size", str(1 << 16), "--rounds", "2", "--skip-rank", "1",
                    env={"AKKA_IPC_TIMEOUT_MS": "500"})
     assert r.returncode == 0, r.stderr[-3000:]
     d0 = rows[0]
     assert d0["exact"][0] is True and d0["ipc_error"] != 0, d0
+    assert d0["next_round_raised"] is True, d0  # the error surfaces as an exception at the next round
     assert rows[1]["exact"] == [True]
