@@ -335,6 +335,114 @@ class ThresholdAllreduce:
             raise ValueError("graphs belong to the scheduled (stream) transport")
         self.worker.set_graphs(on)
 
+    # ---- lane tuning -------------------------------------------------------
+    LANES = {  # candidate -> (lane, exact transfer-unit bytes or -1, ipc mode, ipc fused)
+        "collective": ("collective", -1, None, False),
+        "p2p": ("p2p", -1, None, False),
+        "p2p_block": ("p2p", 1 << 40, None, False),
+        "ipc": ("ipc", -1, "pull", False),
+        "ipc_bcast": ("ipc", -1, "bcast", False),
+        "ipc_fused": ("ipc", -1, "pull", True),
+        "ipc_fused_bcast": ("ipc", -1, "bcast", True),
+    }
+
+    def use_lane(self, name: str) -> None:
+        """Switch to a named lane candidate (see LANES); every rank must do the
+        same at the same round."""
+        ln, unit, mode, fused = self.LANES[name]
+        self.set_lane(ln)
+        if ln == "ipc":
+            self.set_ipc_mode(mode, fused)
+        elif self.world_size > 1:
+            self.set_exact_unit_bytes(unit)
+
+    def tune(self, candidates=None, rounds: int = 8, try_ipc: bool = True) -> dict:
+        """Pick the fastest exact lane for this buffer on this job (collective).
+
+        Every candidate runs three exact rounds with different integer data (the
+        last after `rounds` timed rounds of other data, so a stale read shows)
+        and the timed rounds.  Only rounds run inside a try -- no host-group
+        collective -- so a rank whose rounds raise still meets the others at the
+        one agreement per candidate (max over ranks of time and failure).  The
+        one-sided lanes join when every rank could map every other rank's
+        window.  Leaves the object on the winner; returns every candidate's
+        result and the choice.  Needs thresholds 1 (exact rounds)."""
+        import time
+
+        import torch.distributed as dist
+
+        if self.transport != "stream" or self.world_size < 2:
+            raise ValueError("lane tuning needs the stream transport and N > 1")
+        res: dict = {}
+        ipc_open = bool(self.state().get("link", {}).get("ipc"))
+        cands = list(candidates) if candidates is not None else None
+        if cands is None:
+            spec = self.worker.transport_spec or ("",)
+            cands = [] if spec[0] == "none" else ["collective", "p2p", "p2p_block"]  # "none": ipc-only job
+            if self.device.type == "cuda" and try_ipc:
+                if not ipc_open:
+                    err = None
+                    try:
+                        self.enable_ipc()
+                    except Exception as e:  # noqa: BLE001 - the ipc lanes are skipped
+                        err = f"{type(e).__name__}: {e}"[:200]
+                    flag = torch.tensor([0 if err else 1])
+                    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+                    ipc_open = bool(flag.item())
+                    if not ipc_open:
+                        res["ipc"] = {"exact": None, "ms": None,
+                                      "error": err or "another rank could not open its windows"}
+                if ipc_open:
+                    cands += ["ipc", "ipc_bcast", "ipc_fused", "ipc_fused_bcast"]
+        S, N, r = self.data_size, self.world_size, self.rank
+        dtype = self.worker.dtype
+        x = torch.randn(S, device=self.device).to(dtype)
+        buf = torch.empty(S, device=self.device, dtype=dtype)
+        cuda = self.device.type == "cuda"
+
+        def sync():
+            if cuda:
+                torch.cuda.synchronize(self.device)
+
+        def exact(salt: int) -> bool:
+            y = torch.full((S,), float((r + 1) * (salt + 1)), device=self.device, dtype=dtype)
+            o = self(y)
+            want = float((salt + 1) * N * (N + 1) // 2)
+            return bool(torch.all(o.data == want).item()) and bool(torch.all(o.count == N).item())
+
+        for name in cands:
+            ok, ms, err = False, 0.0, None
+            try:
+                self.use_lane(name)
+                ok = exact(1) and exact(2)
+                if ok:
+                    o = self(x, async_op=cuda, out=buf)
+                    o.wait()
+                    sync()
+                    t0 = time.perf_counter()
+                    for _ in range(rounds):  # the ranks are coupled by the rounds themselves
+                        o = self(x, async_op=cuda, out=buf)
+                    o.wait()
+                    sync()
+                    ms = (time.perf_counter() - t0) / rounds * 1e3
+                    ok = exact(3)
+            except Exception as e:  # noqa: BLE001 - the candidate is rejected
+                ok, err = False, f"{type(e).__name__}: {e}"[:160]
+            t = torch.tensor([0.0 if ok else 1.0, ms], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            good = float(t[0].item()) == 0.0
+            res[name] = {"exact": good, "ms": round(float(t[1].item()), 4) if good else None}
+            if err:
+                res[name]["error"] = err
+        good = [n for n in cands if res[n]["exact"]]
+        if not good:
+            raise RuntimeError(f"no exact lane: {res}")
+        pick = min(good, key=lambda n: res[n]["ms"])
+        self.use_lane(pick)
+        res["chosen"] = pick
+        self.tuned = res
+        return res
+
     def state(self) -> dict:
         return self.worker.state()
 

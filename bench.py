@@ -255,17 +255,12 @@ def run_cfg1(rounds: int = 300) -> dict:
 
 def apply_lane_choice(ar, name) -> None:
     """Put a fresh ThresholdAllreduce on the lane the headline's lane selection
-    chose (collective / p2p / p2p_block / ipc / ipc_bcast); None: leave auto."""
+    chose (ThresholdAllreduce.LANES); None: leave auto."""
     if not name or ar.world_size < 2 or ar.transport != "stream":
         return
-    if name.startswith("ipc"):
-        if not ar.state().get("link", {}).get("ipc"):
-            ar.enable_ipc()
-        ar.set_lane("ipc")
-        ar.set_ipc_mode("bcast" if name.endswith("bcast") else "pull", fused="fused" in name)
-    else:
-        ar.set_lane("p2p" if name.startswith("p2p") else name)
-        ar.set_exact_unit_bytes(1 << 40 if name == "p2p_block" else -1)
+    if name.startswith("ipc") and not ar.state().get("link", {}).get("ipc"):
+        ar.enable_ipc()
+    ar.use_lane(name)
 
 
 def run_extras(world: int, dev, barrier, which=("cfg1", "cfg3", "cfg4", "cfg5"), rank: int = 0,
@@ -539,95 +534,18 @@ def main() -> int:
     if ar.transport == "reactive":
         args.async_op = False  # reactive rounds return once complete (progress is host-polled)
 
-    # Lane selection (untimed, before the warmup): both exact-round lanes of
-    # the stream transport compute the same exact sum -- RCCL reduce-scatter +
-    # all-gather, or the chunk-pipelined direct p2p schedule with our reduce
-    # kernel.  Which one is faster depends on N, the xGMI topology and the
-    # buffer, so each is checked for exactness and timed briefly here; every
-    # rank sees the same max-over-ranks numbers and keeps the same lane.
-    # candidate -> (lane, minimum exact transfer-unit bytes; -1 = default 16 MiB)
-    lanes = {"collective": ("collective", -1), "p2p": ("p2p", -1), "p2p_block": ("p2p", 1 << 40)}
-    ipc_lanes = {"ipc": ("ipc", -1), "ipc_bcast": ("ipc", -1), "ipc_fused": ("ipc", -1),
-                 "ipc_fused_bcast": ("ipc", -1)}
-    fixed = dict(lanes, auto=("auto", -1), **ipc_lanes)
-
-    def apply_lane(name: str) -> None:
-        ln, unit = fixed[name]
-        ar.set_lane(ln)
-        if ln == "ipc":
-            ar.set_ipc_mode("bcast" if name.endswith("bcast") else "pull", fused="fused" in name)
-        elif ar.transport == "stream" and world > 1 and args.data_plane != "ipc":
-            ar.set_exact_unit_bytes(unit)
-
+    # Lane selection (untimed, before the warmup): every exact-round lane of
+    # the stream transport computes the same exact sum -- RCCL reduce-scatter +
+    # all-gather, the chunk-pipelined direct p2p schedule with our reduce
+    # kernel (16 MiB or whole-block units), or the one-sided ipc kernels over
+    # mapped peer windows (four variants).  Which is fastest depends on N, the
+    # xGMI topology and the buffer, so ThresholdAllreduce.tune checks each for
+    # exactness and times it on this job; every rank agrees on the result.
     chosen_lane = args.lane if args.lane != "auto" else None
-
-    def local_exact(salt: int) -> bool:
-        y = torch.full((S,), float((rank + 1) * (salt + 1)), device=dev, dtype=dtype)
-        o = ar(y)
-        want = float((salt + 1) * world * (world + 1) // 2)
-        return bool(torch.all(o.data == want).item()) and bool(torch.all(o.count == world).item())
-
-    def eval_lane(name: str) -> dict:
-        """One candidate: three exact rounds with different values (the last
-        after timed rounds of other data, so a stale read would show) and 8
-        timed rounds.  Only rounds run inside the try -- no collective of the
-        host group -- so a rank whose rounds raise (an RCCL or ipc error)
-        still meets the others at the single agreement below."""
-        ok, ms, err = False, 0.0, None
-        try:
-            apply_lane(name)
-            ok = local_exact(1) and local_exact(2)
-            if ok:
-                o = ar(x, async_op=args.async_op, out=out_buf)
-                o.wait()
-                _sync()
-                t0 = time.perf_counter()
-                for _ in range(8):  # the ranks are coupled by the rounds themselves
-                    o = ar(x, async_op=args.async_op, out=out_buf)
-                o.wait()
-                _sync()
-                ms = (time.perf_counter() - t0) / 8 * 1e3
-                ok = local_exact(3)
-        except Exception as e:  # noqa: BLE001 - the lane is rejected, the run goes on
-            ok, err = False, f"{type(e).__name__}: {e}"[:160]
-        t = torch.tensor([0.0 if ok else 1.0, ms], dtype=torch.float64)
-        if world > 1:
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        good = float(t[0].item()) == 0.0
-        d = {"exact": good, "ms": round(float(t[1].item()), 4) if good else None}
-        if err:
-            d["error"] = err
-        return d
 
     def lane_select():
         env_phase_stall(rank, "lane_select")
-        res = {}
-        if args.data_plane == "ipc":  # windows opened at construction; only the ipc lanes exist
-            lanes.clear()
-            lanes.update(ipc_lanes)
-        elif dev.type == "cuda" and args.ipc == "on":
-            # the one-sided xGMI lane (ipc_lane.h) joins the candidates when every
-            # rank could map every other rank's window
-            err = None
-            try:
-                ar.enable_ipc()
-            except Exception as e:  # noqa: BLE001 - reported, the lane is just skipped
-                err = f"{type(e).__name__}: {e}"[:200]
-            flag = torch.tensor([0 if err else 1])
-            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-            if flag.item():
-                lanes.update(ipc_lanes)
-            else:
-                res["ipc"] = {"exact": None, "ms": None, "error": err or "another rank could not open its windows"}
-        for name in lanes:
-            res[name] = eval_lane(name)
-        good = [n for n in lanes if res[n]["exact"]]
-        if not good:
-            raise RuntimeError(f"no exact lane: {res}")
-        pick = min(good, key=lambda n: res[n]["ms"])
-        apply_lane(pick)
-        res["chosen"] = pick
-        return res
+        return ar.tune(try_ipc=args.ipc == "on")
 
     lane_sel = None
     if world > 1 and ar.transport == "stream" and args.lane == "auto" and args.lane_select == "on":
@@ -723,7 +641,7 @@ def main() -> int:
             return used, None
         other = "p2p" if used == "collective" else "collective"
         try:
-            apply_lane(other)
+            ar.use_lane(other)
             for _ in range(2):
                 o = ar(x, async_op=args.async_op, out=out_buf)
             o.wait()
@@ -741,7 +659,10 @@ def main() -> int:
             return used, {"lane": other, "algbw_GBps": round(nbytes / (float(t.item()) / k) / 1e9, 3),
                           "steps": k}
         finally:
-            apply_lane(chosen_lane or args.lane)
+            if chosen_lane or args.lane != "auto":
+                ar.use_lane(chosen_lane or args.lane)
+            else:
+                ar.set_lane("auto")
 
     st = ar.state()  # headline rounds only (before the other lane runs)
     lane_used, lane_other = guard.run("other_lane", dl, other_lane)
