@@ -28,11 +28,13 @@ class ThresholdHookState:
     the host), so bucket communication overlaps the rest of the backward pass
     like DDP's own allreduce hook.  ``th_allreduce``: master-style round
     pacing across ranks (see ThresholdAllreduce).  ``data_plane="ipc"``: exact
-    rounds on the one-sided xGMI lane, no RCCL communicator (ThresholdAllreduce)."""
+    rounds on the one-sided xGMI lane, no RCCL communicator (ThresholdAllreduce).
+    ``tune`` (exact thresholds): each bucket size's engine measures every exact
+    lane once when it is created and keeps the fastest (ThresholdAllreduce.tune)."""
 
     def __init__(self, *, th_reduce: float = 1.0, th_complete: float = 1.0, max_lag: int = 2,
                  max_chunk_size: int = 1 << 20, transport: str = "stream", broadcast_lag: int = 2,
-                 async_op: bool = True, th_allreduce=None, data_plane: str = "rccl"):
+                 async_op: bool = True, th_allreduce=None, data_plane: str = "rccl", tune: bool = False):
         self.kw = dict(th_reduce=th_reduce, th_complete=th_complete, max_lag=max_lag, max_chunk_size=max_chunk_size,
                        transport=transport, broadcast_lag=broadcast_lag, th_allreduce=th_allreduce,
                        data_plane=data_plane)
@@ -40,12 +42,15 @@ class ThresholdHookState:
         self.rounds = 0
         self.async_op = async_op
         self.async_rounds = 0
+        self.tune = tune and th_reduce >= 1.0 and th_complete >= 1.0
 
     def engine(self, t: torch.Tensor) -> ThresholdAllreduce:
         key = (t.numel(), t.dtype, t.device)
         ar = self.engines.get(key)
         if ar is None:
             ar = ThresholdAllreduce(t.numel(), dtype=t.dtype, device=t.device, **self.kw)
+            if self.tune and ar.world_size > 1 and ar.transport == "stream":
+                ar.tune()  # collective: every rank creates this engine at the same bucket
             self.engines[key] = ar
         return ar
 

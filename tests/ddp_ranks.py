@@ -16,6 +16,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out-dir", required=True)
     ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--tune", action="store_true")
     a = ap.parse_args()
     rank = int(os.environ["RANK"])
     dist.init_process_group("gloo")
@@ -27,7 +28,7 @@ def main():
     torch.manual_seed(0)
     model = torch.nn.parallel.DistributedDataParallel(MLP(256, 512, 10).to(dev), device_ids=[0],
                                                       bucket_cap_mb=0.25)
-    state = ThresholdHookState(data_plane="ipc", max_chunk_size=1 << 14)
+    state = ThresholdHookState(data_plane="ipc", max_chunk_size=1 << 14, tune=a.tune)
     model.register_comm_hook(state, threshold_allreduce_hook)
     opt = torch.optim.SGD(model.parameters(), lr=0.1)
     for s in range(a.steps):
@@ -39,7 +40,9 @@ def main():
     torch.cuda.synchronize()
     flat = torch.cat([p.detach().reshape(-1).float().cpu() for p in model.parameters()])
     errs = [ar.ipc_error() for ar in state.engines.values()]
-    torch.save({"flat": flat, "buckets": len(state.engines), "rounds": state.rounds, "ipc_errors": errs},
+    chosen = [getattr(ar, "tuned", {}).get("chosen") for ar in state.engines.values()]
+    torch.save({"flat": flat, "buckets": len(state.engines), "rounds": state.rounds, "ipc_errors": errs,
+                "chosen": chosen},
                os.path.join(a.out_dir, f"rank{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()

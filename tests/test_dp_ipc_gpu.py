@@ -60,7 +60,8 @@ def test_dp_sgd_multiprocess_ipc(n):
     torch.testing.assert_close(res[0]["flat"], want, rtol=1e-4, atol=1e-5)
 
 
-def test_torch_ddp_hook_multiprocess():
+@pytest.mark.parametrize("tune", [False, True])
+def test_torch_ddp_hook_multiprocess(tune):
     """torch DDP with the comm hook on the ipc data plane, 2 processes: the
     hook's rounds average every bucket across the processes (same result as
     the mean-gradient reference), several buckets -> several allreduce
@@ -70,11 +71,15 @@ def test_torch_ddp_hook_multiprocess():
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
                "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
                os.path.join(ROOT, "tests", "ddp_ranks.py"), "--out-dir", out, "--steps", str(steps)]
+        if tune:
+            cmd.append("--tune")
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT)
         assert r.returncode == 0, r.stderr[-3000:]
         res = [torch.load(os.path.join(out, f"rank{i}.pt"), weights_only=True) for i in range(n)]
     for d in res:
         assert d["ipc_errors"] and all(e == 0 for e in d["ipc_errors"])
+        if tune:  # every bucket engine tuned, the same choice on every rank
+            assert all(c and c.startswith("ipc") for c in d["chosen"]) and d["chosen"] == res[0]["chosen"]
         assert d["buckets"] >= 1 and d["rounds"] >= steps
         assert torch.equal(d["flat"], res[0]["flat"])
     want = _reference(n, steps, torch.device("cuda", 0))
