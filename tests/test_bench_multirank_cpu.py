@@ -80,6 +80,19 @@ def test_bench_lane_select():
     assert d["exact"] is True and d["groups_per_round"] > 0
 
 
+def test_bench_n8_full_flow():
+    """The driver's largest N: 8 ranks through preflight, lane selection,
+    timed rounds, check, comparator and the other lane (uneven blocks: 0.3 MiB
+    of fp32 = 78643 elements over 8 ranks, 16 KiB chunks)."""
+    d = _run(8, "--size-mb", "0.3", "--chunk-mb", "0.015625")
+    assert d["n_gpus"] == 8 and d["config"]["parallelism"] == "dp8" and d["exact"] is True
+    assert d["p2p_nranks"] == 8 and [r["rank"] for r in d["rank_devices"]] == list(range(8))
+    sel = d["lane_select"]
+    assert all(sel[c]["exact"] is True for c in ("collective", "p2p", "p2p_block"))
+    assert d["lane"] == sel["chosen"] and d["xgmi_bound_algbw_GBps"] == pytest.approx(612.0, abs=1.0)
+    assert abs(d["busbw_GBps"] - d["value"] * 2 * 7 / 8) < 1e-2
+
+
 def test_bench_multirank_extras_deadline():
     d = _run(2, "--extras", "on", "--extras-deadline-s", "0.05")
     assert d["exact"] is True and "extras_error" in d and "extra_configs" not in d
