@@ -32,15 +32,24 @@ def main():
     bucket = GradientBucket(list(model.parameters()), flatten_params=True)
     ar = ThresholdAllreduce(bucket.numel, max_chunk_size=1 << 14, device=dev, data_plane="ipc")
     losses = []
+    rec = []  # every round's input and output, for the test's diagnosis on a mismatch
+
+    def recording_ar(t):
+        xin = t.detach().clone()
+        o = ar(t)
+        rec.append((xin, o.data.detach().clone()))  # (not o.count: it would bypass the fused update)
+        return o
+
     for s in range(a.steps):
         g = torch.Generator(device=dev).manual_seed(100 * s + rank)
         x, y = synthetic_batch(64, 256, 10, device=dev, generator=g)
-        loss = dp_sgd_step(model, x, y, 0.1, ar, bucket, compute_dtype=torch.bfloat16 if a.bf16 else None)
+        loss = dp_sgd_step(model, x, y, 0.1, recording_ar, bucket, compute_dtype=torch.bfloat16 if a.bf16 else None)
         losses.append(float(loss))
     torch.cuda.synchronize()
     flat = torch.cat([p.detach().reshape(-1).float().cpu() for p in model.parameters()])
     torch.save({"flat": flat, "losses": losses, "ipc_error": ar.ipc_error(),
-                "ipc_rounds": ar.state()["link"]["ipc_rounds"]}, os.path.join(a.out_dir, f"rank{rank}.pt"))
+                "ipc_rounds": ar.state()["link"]["ipc_rounds"],
+                "rounds_in": [r[0].cpu() for r in rec], "rounds_out": [r[1].cpu() for r in rec]}, os.path.join(a.out_dir, f"rank{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()
 

@@ -53,11 +53,28 @@ def test_dp_sgd_multiprocess_ipc(n):
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT)
         assert r.returncode == 0, r.stderr[-3000:]
         res = [torch.load(os.path.join(out, f"rank{i}.pt"), weights_only=True) for i in range(n)]
+    diag = _round_diagnosis(res, n, steps)
     for d in res:
         assert d["ipc_error"] == 0 and d["ipc_rounds"] == steps
-        assert torch.equal(d["flat"], res[0]["flat"])  # every rank applied the same averaged gradient
+        assert torch.equal(d["flat"], res[0]["flat"]), diag  # every rank applied the same averaged gradient
     want = _reference(n, steps, torch.device("cuda", 0))
-    torch.testing.assert_close(res[0]["flat"], want, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(res[0]["flat"], want, rtol=1e-4, atol=1e-5, msg=lambda m: f"{m}\n{diag}")
+
+
+def _round_diagnosis(res, n, steps) -> str:
+    """Per round and rank: does the allreduce output equal the sum of the
+    ranks' inputs (which blocks do not)?  Tells a wrong round from a wrong
+    update when the final parameters disagree."""
+    lines = []
+    S = res[0]["rounds_in"][0].numel()
+    step = -(-S // n)
+    for s in range(steps):
+        want = sum(res[i]["rounds_in"][s].double() for i in range(n)).float()
+        for i in range(n):
+            bad = ((res[i]["rounds_out"][s] - want).abs() > 1e-6 * (1 + want.abs()))
+            blocks = [int(bad[b * step:(b + 1) * step].sum()) for b in range(n)]
+            lines.append(f"round {s} rank {i}: wrong elements per block {blocks}")
+    return "\n".join(lines)
 
 
 @pytest.mark.parametrize("tune", [False, True])
