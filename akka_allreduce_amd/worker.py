@@ -550,7 +550,11 @@ class AllreduceWorker:
         rec["output"], rec["counts"] = out, counts
         if self._async:
             self._keep_alive_on_internal_streams(out, counts)
-        self._core.bind_output(round_, out.data_ptr(), counts.data_ptr())
+        # the caller's stream allocated them: engine streams that write them
+        # wait for this point (memory the allocator recycled may still be in
+        # use by earlier work on that stream)
+        cuda = self.device.type == "cuda"
+        self._core.bind_output(round_, out.data_ptr(), counts.data_ptr(), self._stream_ptr() if cuda else 0, cuda)
 
     def _deliver(self, round_: int) -> None:
         rec = self._rounds[round_]

@@ -283,8 +283,9 @@ class WorkerCore final : public EngineHost {
   void bind_input(int32_t round, uintptr_t ptr, uintptr_t stream, bool has_stream) {
     dp_->bind_input(round, reinterpret_cast<const void*>(ptr), reinterpret_cast<StreamH>(stream), has_stream);
   }
-  void bind_output(int32_t round, uintptr_t out, uintptr_t counts) {
-    dp_->bind_output(round, reinterpret_cast<void*>(out), reinterpret_cast<int32_t*>(counts));
+  void bind_output(int32_t round, uintptr_t out, uintptr_t counts, uintptr_t stream, bool has_stream) {
+    dp_->bind_output(round, reinterpret_cast<void*>(out), reinterpret_cast<int32_t*>(counts),
+                     reinterpret_cast<StreamH>(stream), has_stream);
   }
   void unbind(int32_t round) { dp_->unbind(round); }
   void stream_wait_done(int32_t round, uintptr_t stream) {
@@ -613,7 +614,8 @@ PYBIND11_MODULE(_native, m) {
       .def("peer_terminated", &WorkerCore::peer_terminated)
       .def("fast_round", &WorkerCore::fast_round)
       .def("bind_input", &WorkerCore::bind_input)
-      .def("bind_output", &WorkerCore::bind_output)
+      .def("bind_output", &WorkerCore::bind_output, py::arg("round"), py::arg("out"), py::arg("counts"),
+           py::arg("stream") = 0, py::arg("has_stream") = false)
       .def("unbind", &WorkerCore::unbind)
       .def("stream_wait_done", &WorkerCore::stream_wait_done)
       .def("sync_done", &WorkerCore::sync_done)

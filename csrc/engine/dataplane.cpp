@@ -262,10 +262,15 @@ EventH DataPlane::binding_event() {
   return e;
 }
 
-void DataPlane::bind_output(int32_t round, void* output, int32_t* counts) {
+void DataPlane::bind_output(int32_t round, void* output, int32_t* counts, StreamH alloc_stream, bool has_stream) {
   Binding& b = bind_[round];
   b.output = output;
   b.counts = counts;
+  if (has_stream && !dev_->is_host() && g_.N > 1) {  // N == 1: everything runs on the producer stream
+    if (!b.output_ready) b.output_ready = binding_event();
+    dev_->record(b.output_ready, alloc_stream);
+    b.output_waited_compute = b.output_waited_comm = false;
+  }
   if (!b.done) b.done = binding_event();
   b.finalized = false;
 }
@@ -283,6 +288,7 @@ void DataPlane::unbind(int32_t round) {
   auto it = bind_.find(round);
   if (it == bind_.end()) return;
   if (it->second.input_ready) spare_events_.push_back(it->second.input_ready);
+  if (it->second.output_ready) spare_events_.push_back(it->second.output_ready);
   if (it->second.done) spare_events_.push_back(it->second.done);
   bind_.erase(it);
 }
@@ -291,8 +297,16 @@ void DataPlane::wait_input(int32_t round, StreamH s) {
   // Each consumer stream waits for the input's producer once per round, and
   // only if it actually reads the input (N=1 never touches the comm stream).
   Binding& b = binding_mut(round);
+  const bool comm = s == dev_->comm_stream();
+  if (b.output_ready) {
+    bool& od = comm ? b.output_waited_comm : b.output_waited_compute;
+    if (!od) {
+      dev_->wait(s, b.output_ready);
+      od = true;
+    }
+  }
   if (!b.input_ready) return;
-  bool& done = (s == dev_->comm_stream()) ? b.input_waited_comm : b.input_waited_compute;
+  bool& done = comm ? b.input_waited_comm : b.input_waited_compute;
   if (done) return;
   dev_->wait(s, b.input_ready);
   done = true;
@@ -405,6 +419,10 @@ void DataPlane::upload_counts(int32_t round, const std::vector<int32_t>& blocks,
   Row& r = row_for(round);
   const Binding& b = binding(round);
   if (!b.counts) return;
+  // the counts memory is the caller's: write it only after the point where
+  // the caller's stream handed it over (an exact round's compute stream has
+  // not waited for anything of the caller's yet)
+  if (!b.exec_on_producer) wait_input(round, s);
   bool copied = false;
   if (int32_t(blocks.size()) == g_.N && g_.N > 1) {
     // every block, one value everywhere (exact rounds: all N): ONE 32-bit
@@ -444,6 +462,7 @@ void DataPlane::finalize(int32_t round, const std::vector<uint8_t>& landed) {
   Binding& b = binding_mut(round);
   AKKA_CHECK(landed.size() == size_t(g_.N) * kmax_, "landed mask has wrong shape");
   const StreamH cs = exec_stream(round);
+  if (!b.exec_on_producer) wait_input(round, cs);  // cs writes the caller's output/counts below
   // Join: everything the comm stream wrote into this round's output.
   if (b.comm_used) {
     EventH ce = record_comm();

@@ -48,7 +48,13 @@ class DataPlane {
   // `ready_stream` is the stream that produced `input`; it may be the null
   // stream (handle 0), so `has_stream` says whether there is one at all.
   void bind_input(int32_t round, const void* input, StreamH ready_stream, bool has_stream);
-  void bind_output(int32_t round, void* output, int32_t* counts);
+  // `alloc_stream` (optional): the stream in whose order output/counts were
+  // allocated (a caching allocator may hand out memory that earlier work on
+  // that stream still uses).  Every other stream that writes them waits for
+  // that point first (wait_input).  Without one, the input's ready point
+  // stands in (the fast path binds the output just before the input).
+  void bind_output(int32_t round, void* output, int32_t* counts, StreamH alloc_stream = nullptr,
+                   bool has_stream = false);
   bool has_input(int32_t round) const;
   bool has_output(int32_t round) const;
   void unbind(int32_t round);
@@ -92,7 +98,9 @@ class DataPlane {
   // or -- for a purely local round (N == 1) -- the input producer's stream.
   StreamH exec_stream(int32_t round) const;
   bool exec_on_producer(int32_t round) const;
-  // Make `s` wait (once per round) for the stream that produced the input.
+  // Make `s` wait (once per round) for the stream that produced the input and
+  // for the point where the output/counts memory was handed over: every
+  // stream that reads the input or writes the output/counts calls it first.
   void wait_input(int32_t round, StreamH s);
   // The comm stream wrote into this round's output (finalize must join it).
   void mark_comm_used(int32_t round);
@@ -134,6 +142,9 @@ class DataPlane {
     EventH input_ready = nullptr;  // recorded on the producer stream
     bool input_waited_compute = false;
     bool input_waited_comm = false;
+    EventH output_ready = nullptr;  // recorded on the stream that allocated output/counts
+    bool output_waited_compute = false;
+    bool output_waited_comm = false;
     bool comm_used = false;  // the comm stream wrote into this round (join at finalize)
     StreamH exec = nullptr;  // stream running this round's compute when exec_on_producer
     bool exec_on_producer = false;

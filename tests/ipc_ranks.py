@@ -33,6 +33,9 @@ def main():
     ap.add_argument("--time", action="store_true")
     ap.add_argument("--mode", default="pull", choices=["pull", "bcast", "alternate", "fused", "fused_bcast", "rotate"])
     ap.add_argument("--out-dir", default="", help="write rank<i>.json there (stdout lines of ranks interleave)")
+    ap.add_argument("--poison", action="store_true",
+                    help="round 0 runs on a fresh stream whose only free block is still being written by a "
+                         "pending spin + fill: the round's output/counts are carved from it")
     a = ap.parse_args()
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     dist.init_process_group("gloo")
@@ -53,7 +56,21 @@ def main():
             ar.set_ipc_mode(mode, fused)
         x = torch.randn(a.size, generator=torch.Generator().manual_seed(5 * 1000 + rank * 7 + r),
                         dtype=torch.float32).to(dtype).to(dev)
-        o = ar(x)
+        if a.poison and r == 0:
+            torch.cuda.synchronize()
+            side = torch.cuda.Stream()
+            with torch.cuda.stream(side):
+                junk = torch.empty((a.size * x.element_size() + 4096) // 4, dtype=torch.int32, device=dev)
+                torch.cuda._sleep(200_000_000)  # the fill below lands ~0.1 s later in this stream's order
+                junk.fill_(-7)
+                lo, hi = junk.data_ptr(), junk.data_ptr() + junk.numel() * 4
+                del junk  # free at once for this stream's next allocations
+                o = ar(x)
+                res["poison_in_block"] = lo <= o.counts_per_chunk.data_ptr() < hi
+            side.synchronize()
+            res["poison_counts_ok"] = bool((o.counts_per_chunk == world).all())
+        else:
+            o = ar(x)
         torch.cuda.synchronize()
         want = expected(a.size, world, r, dtype, 5)
         res["exact"].append(bool(torch.equal(o.data.cpu(), want)) and bool((o.count.cpu() == world).all()))

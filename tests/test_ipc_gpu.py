@@ -93,3 +93,15 @@ def test_ipc_lane_missing_peer_times_out_cleanly():
     assert d0["exact"][0] is True and d0["ipc_error"] != 0, d0
     assert d0["next_round_raised"] is True, d0  # the error surfaces as an exception at the next round
     assert rows[1]["exact"] == [True]
+
+
+def test_ipc_round_waits_for_callers_pending_work_on_its_buffers():
+    """The round's output and counts are carved from a block that a pending
+    kernel on the caller's stream still writes (the caching allocator reuses
+    freed memory in that stream's order).  The ipc lane's streams must write
+    them only after that point: counts read N, the sum is exact."""
+    r, rows = _run(2, "--size", str(1 << 16), "--rounds", "2", "--poison")
+    assert r.returncode == 0 and len(rows) == 2, r.stderr[-3000:]
+    for d in rows:
+        assert d["poison_in_block"], d  # the hazard was really set up
+        assert d["poison_counts_ok"] and all(d["exact"]) and d["ipc_error"] == 0, d
