@@ -22,6 +22,12 @@ for s in $STEPS; do
     ipc2) run 2 n2 --data-plane ipc --extras off || exit 1 ;;
     ipc4) run 4 n4 --data-plane ipc --extras off || exit 1 ;;
     ipc8) run 8 n8 --data-plane ipc --extras off || exit 1 ;;
+    # 8 processes x 4 hardware queues oversubscribe the card's queue slots
+    # (the scheduler then time-slices queues); fewer queues per process:
+    ipc8q2) GPU_MAX_HW_QUEUES=2 run 8 n8_q2 --data-plane ipc --extras off || exit 1 ;;
+    ipc8q1) GPU_MAX_HW_QUEUES=1 run 8 n8_q1 --data-plane ipc --extras off || exit 1 ;;
+    ipc6) run 6 n6 --data-plane ipc --extras off || exit 1 ;;
+    ipc7) run 7 n7 --data-plane ipc --extras off || exit 1 ;;
     p2p8) GPU_MAX_HW_QUEUES=4 run 8 p2p_n8 --data-plane ipc_p2p --extras on --extras-only cfg4 \
             --cfg4-size-mb 64 --cfg4-delay-ms 50 --cfg4-rounds 6 || exit 1 ;;
     p2p4) GPU_MAX_HW_QUEUES=8 run 4 p2p_n4 --data-plane ipc_p2p --extras on --extras-only cfg4,cfg5 \
