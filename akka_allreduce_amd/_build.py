@@ -25,6 +25,7 @@ ARCH = os.environ.get("AKKA_OFFLOAD_ARCH", "gfx950")
 
 HOST_SOURCES = [
     "engine/host_device.cpp",
+    "engine/racecheck.cpp",
     "engine/dataplane.cpp",
     "engine/engine.cpp",
     "transport/sim_p2p.cpp",

@@ -24,10 +24,15 @@ from .collective import _RemoteRank
 class SimCluster:
     def __init__(self, n: int, data_size: int, max_chunk_size: int, *, dtype: torch.dtype = torch.float32,
                  th_reduce: float = 1.0, th_complete: float = 1.0, max_lag: int = 1, broadcast_lag=2,
-                 lane: str = "auto"):
+                 lane: str = "auto", collectives: bool = False):
+        """``collectives``: the simulated communicator also offers RCCL's
+        reduce-scatter / all-gather (the exact-round collective lane).  With
+        ``AKKA_RACECHECK=1`` in the environment every rank's simulated device
+        checks its stream ordering (csrc/engine/racecheck.h) and each worker
+        gets a modelled caller stream (``host_stream``)."""
         nat = _load()
         self.n = n
-        self.hub = nat.SimHub(n)
+        self.hub = nat.SimHub(n, collectives)
         lags = broadcast_lag if isinstance(broadcast_lag, (list, tuple)) else [broadcast_lag] * n
         self.workers: List[AllreduceWorker] = [
             AllreduceWorker(None, None, device="cpu", dtype=dtype, transport="stream",
@@ -38,6 +43,8 @@ class SimCluster:
             peers = {i: (w if i == r else _RemoteRank(i)) for i in range(n)}
             w.tell(InitWorkers(peers, n, None, r, th_reduce, th_complete, max_lag, data_size, max_chunk_size))
             w.set_lane(lane)
+            if w._core.models_streams():  # (the device exists once the worker is initialised)
+                w.host_stream = w._core.create_stream()
 
     def allreduce(self, inputs: Sequence[torch.Tensor]) -> List[AllReduceOutput]:
         """One round on every rank; returns each rank's output (valid after the simulated run)."""
@@ -51,6 +58,10 @@ class SimCluster:
 
     def bytes_moved(self) -> int:
         return self.hub.bytes_moved()
+
+    def race_reports(self) -> List[str]:
+        """Every rank's stream race reports (AKKA_RACECHECK=1), prefixed by rank."""
+        return [f"rank {r}: {m}" for r, w in enumerate(self.workers) for m in w._core.race_reports()]
 
 
 class ReactiveSimCluster:
@@ -80,6 +91,8 @@ class ReactiveSimCluster:
         for r, w in enumerate(self.workers):
             peers = {i: (w if i == r else _RemoteRank(i)) for i in range(n)}
             w.tell(InitWorkers(peers, n, None, r, th_reduce, th_complete, max_lag, data_size, max_chunk_size))
+            if w._core.models_streams():  # AKKA_RACECHECK=1: modelled caller stream
+                w.host_stream = w._core.create_stream()
         self.outputs: List[dict] = [dict() for _ in range(n)]
 
     def start(self, rank: int, x: torch.Tensor) -> None:
@@ -124,6 +137,9 @@ class ReactiveSimCluster:
                                        + "; ".join(f"rank {r}: in_flight={w._core.in_flight()} round={w.round}"
                                                    for r, w in enumerate(self.workers)))
         raise RuntimeError("reactive sim: step budget exhausted")
+
+    def race_reports(self) -> List[str]:
+        return [f"rank {r}: {m}" for r, w in enumerate(self.workers) for m in w._core.race_reports()]
 
     def done(self, rank: int, round_: int) -> bool:
         return round_ in self.outputs[rank]

@@ -110,6 +110,10 @@ class AllreduceWorker:
         self._next_round = 0
         self._in_call = 0
         self._stream_cache: Optional[int] = None
+        # CPU race checking (AKKA_RACECHECK=1): a stream of the simulated
+        # device standing for the caller's stream (producer of inputs,
+        # allocator of outputs); see csrc/engine/racecheck.h
+        self.host_stream: Optional[int] = None
         self._async = False
         self._ext_streams = None
         self._out_override: Dict[int, torch.Tensor] = {}
@@ -343,7 +347,8 @@ class AllreduceWorker:
                 raise ValueError("out must be a contiguous tensor of dataSize elements, worker dtype and device")
             self._out_override[r] = out
         # one stream lookup per call instead of one per callback
-        self._stream_cache = torch.cuda.current_stream(self.device).cuda_stream if self.device.type == "cuda" else 0
+        self._stream_cache = torch.cuda.current_stream(self.device).cuda_stream if self.device.type == "cuda" \
+            else (self.host_stream or 0)
         self._async = bool(async_op) and self.device.type == "cuda"
         try:
             with _tracing.range_(f"akka.round {r}"):
@@ -516,7 +521,7 @@ class AllreduceWorker:
     # ------------------------------------------------------------------ engine callbacks
     def _stream_ptr(self) -> int:
         if self.device.type != "cuda":
-            return 0
+            return self.host_stream or 0
         if self._stream_cache is not None:
             return self._stream_cache
         return torch.cuda.current_stream(self.device).cuda_stream
@@ -537,15 +542,22 @@ class AllreduceWorker:
         # for the round's done event, which follows every read of the input --
         # including the reactive transport's staging copy -- and the caching
         # allocator only reuses the block in that stream's order.)
-        self._core.bind_input(round_, t.data_ptr(), self._stream_ptr(), self.device.type == "cuda")
+        self._core.bind_input(round_, t.data_ptr(), self._stream_ptr(), self._has_stream())
 
-    def _alloc_output(self, round_: int) -> None:
+    def _has_stream(self) -> bool:
+        return self.device.type == "cuda" or self.host_stream is not None
+
+    def _new_output_buffers(self, round_: int) -> Tuple[torch.Tensor, torch.Tensor]:
         g = self.geometry
         out = self._out_override.pop(round_, None)
         if out is None:
             out = torch.empty(g.dataSize, dtype=self.dtype, device=self.device)
         # every entry the count expansion reads is written (uploaded or received)
         counts = torch.empty(g.workerNum * g.kmax, dtype=torch.int32, device=self.device)
+        return out, counts
+
+    def _alloc_output(self, round_: int) -> None:
+        out, counts = self._new_output_buffers(round_)
         rec = self._rounds.setdefault(round_, {})
         rec["output"], rec["counts"] = out, counts
         if self._async:
@@ -553,8 +565,7 @@ class AllreduceWorker:
         # the caller's stream allocated them: engine streams that write them
         # wait for this point (memory the allocator recycled may still be in
         # use by earlier work on that stream)
-        cuda = self.device.type == "cuda"
-        self._core.bind_output(round_, out.data_ptr(), counts.data_ptr(), self._stream_ptr() if cuda else 0, cuda)
+        self._core.bind_output(round_, out.data_ptr(), counts.data_ptr(), self._stream_ptr(), self._has_stream())
 
     def _deliver(self, round_: int) -> None:
         rec = self._rounds[round_]
@@ -571,6 +582,10 @@ class AllreduceWorker:
                     event.record(self._internal_streams()[1])
             else:
                 self._core.stream_wait_done(round_, self._stream_ptr())
+        elif self.host_stream is not None:
+            # modelled caller stream (CPU race checking): the output is valid
+            # in its order, like the caller's stream on a GPU
+            self._core.stream_wait_done(round_, self.host_stream)
         g = self.geometry
         out = AllReduceOutput(rec["output"], iteration=round_,
                               counts_per_chunk=rec["counts"].view(g.workerNum, g.kmax), geometry=g,

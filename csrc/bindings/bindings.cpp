@@ -17,6 +17,7 @@
 #include <cstring>
 #include <deque>
 #include <mutex>
+#include <set>
 
 #include "../engine/engine.h"
 #include "../kernels/kernels.h"
@@ -288,6 +289,25 @@ class WorkerCore final : public EngineHost {
                      reinterpret_cast<StreamH>(stream), has_stream);
   }
   void unbind(int32_t round) { dp_->unbind(round); }
+
+  // ---- stream race checking (host device, AKKA_RACECHECK=1) --------------------
+  bool models_streams() const { return dev_ && dev_->models_streams(); }
+  uintptr_t create_stream() {
+    AKKA_CHECK(dev_, "no device");
+    return reinterpret_cast<uintptr_t>(dev_->create_stream());
+  }
+  // A caller op on `stream` that reads or writes [ptr, ptr + bytes).
+  void declare_access(uintptr_t stream, uintptr_t ptr, size_t bytes, bool write, const std::string& tag) {
+    AKKA_CHECK(dev_, "no device");
+    const char* t = tags_.insert(tag).first->c_str();
+    dev_->declare_access(reinterpret_cast<StreamH>(stream), {{reinterpret_cast<const void*>(ptr), bytes, write, t}});
+  }
+  std::vector<std::string> race_reports() const { return dev_ ? dev_->race_reports() : std::vector<std::string>{}; }
+  int64_t race_count() const { return dev_ ? dev_->race_count() : 0; }
+  void sync_stream(uintptr_t stream) {
+    AKKA_CHECK(dev_, "no device");
+    dev_->sync_stream(reinterpret_cast<StreamH>(stream));
+  }
   void stream_wait_done(int32_t round, uintptr_t stream) {
     dp_->stream_wait_done(round, reinterpret_cast<StreamH>(stream));
   }
@@ -538,6 +558,7 @@ class WorkerCore final : public EngineHost {
   std::string link_kind_;
   int32_t device_idx_;
   bool deferred_;
+  std::set<std::string> tags_;  // stable storage of declared access tags
   int32_t lag_;
   DType dt_ = DType::F32;
   std::unique_ptr<Device> dev_;
@@ -585,7 +606,8 @@ PYBIND11_MODULE(_native, m) {
       });
 
   py::class_<PySimHub>(m, "SimHub")
-      .def(py::init([](int32_t n) { return PySimHub{make_sim_hub(n)}; }))
+      .def(py::init([](int32_t n, bool collectives) { return PySimHub{make_sim_hub(n, collectives)}; }),
+           py::arg("n"), py::arg("collectives") = false)
       .def("bytes_moved", [](const PySimHub& h) { return sim_bytes_moved(h.hub); });
 
   py::class_<WorkerCore>(m, "WorkerCore")
@@ -617,6 +639,12 @@ PYBIND11_MODULE(_native, m) {
       .def("bind_output", &WorkerCore::bind_output, py::arg("round"), py::arg("out"), py::arg("counts"),
            py::arg("stream") = 0, py::arg("has_stream") = false)
       .def("unbind", &WorkerCore::unbind)
+      .def("models_streams", &WorkerCore::models_streams)
+      .def("create_stream", &WorkerCore::create_stream)
+      .def("declare_access", &WorkerCore::declare_access)
+      .def("race_reports", &WorkerCore::race_reports)
+      .def("race_count", &WorkerCore::race_count)
+      .def("sync_stream", &WorkerCore::sync_stream)
       .def("stream_wait_done", &WorkerCore::stream_wait_done)
       .def("sync_done", &WorkerCore::sync_done)
       .def("exec_on_producer", &WorkerCore::exec_on_producer)

@@ -1,5 +1,7 @@
 #include "dataplane.h"
 
+#include <cstdlib>
+
 #include <algorithm>
 
 namespace akka {
@@ -12,6 +14,7 @@ DataPlane::DataPlane(Device* dev, const Geometry& g, int32_t me, int32_t ring_ro
     : dev_(dev), g_(g), me_(me), L_(ring_rows), dt_(dt) {
   AKKA_CHECK(me >= 0 && me < g.N, "worker id out of range");
   AKKA_CHECK(ring_rows >= 1, "ring must have at least one row");
+  if (const char* f = std::getenv("AKKA_FAULT_SKIP_OUTPUT_WAIT")) fault_skip_output_wait_ = *f && *f != '0';
   kme_ = g_.num_chunks(me_);
   kmax_ = std::max(1, g_.max_block_len_chunks());
   my_len_ = g_.block_len(me_);
@@ -211,7 +214,7 @@ void DataPlane::bind_input(int32_t round, const void* input, StreamH ready_strea
     // Stage the input on the compute stream; afterwards nothing reads the
     // caller's tensor, so every consumer is ordered by the compute stream.
     const StreamH cs = dev_->compute_stream();
-    if (has_stream && !dev_->is_host()) {
+    if (has_stream && (!dev_->is_host() || dev_->models_streams())) {
       if (!b.input_ready) b.input_ready = binding_event();
       dev_->record(b.input_ready, ready_stream);
       dev_->wait(cs, b.input_ready);
@@ -225,7 +228,7 @@ void DataPlane::bind_input(int32_t round, const void* input, StreamH ready_strea
     b.input_waited_compute = b.input_waited_comm = true;
     return;
   }
-  if (has_stream && !dev_->is_host()) {
+  if (has_stream && (!dev_->is_host() || dev_->models_streams())) {
     if (g_.N == 1) {
       // A purely local round (no peers, no comm stream) runs its reduce on the
       // producer's own stream: no cross-stream event hop per round.
@@ -266,7 +269,7 @@ void DataPlane::bind_output(int32_t round, void* output, int32_t* counts, Stream
   Binding& b = bind_[round];
   b.output = output;
   b.counts = counts;
-  if (has_stream && !dev_->is_host() && g_.N > 1) {  // N == 1: everything runs on the producer stream
+  if (has_stream && (!dev_->is_host() || dev_->models_streams()) && g_.N > 1) {  // N == 1: everything runs on the producer stream
     if (!b.output_ready) b.output_ready = binding_event();
     dev_->record(b.output_ready, alloc_stream);
     b.output_waited_compute = b.output_waited_comm = false;
@@ -422,7 +425,7 @@ void DataPlane::upload_counts(int32_t round, const std::vector<int32_t>& blocks,
   // the counts memory is the caller's: write it only after the point where
   // the caller's stream handed it over (an exact round's compute stream has
   // not waited for anything of the caller's yet)
-  if (!b.exec_on_producer) wait_input(round, s);
+  if (!b.exec_on_producer && !fault_skip_output_wait_) wait_input(round, s);
   bool copied = false;
   if (int32_t(blocks.size()) == g_.N && g_.N > 1) {
     // every block, one value everywhere (exact rounds: all N): ONE 32-bit
@@ -462,7 +465,8 @@ void DataPlane::finalize(int32_t round, const std::vector<uint8_t>& landed) {
   Binding& b = binding_mut(round);
   AKKA_CHECK(landed.size() == size_t(g_.N) * kmax_, "landed mask has wrong shape");
   const StreamH cs = exec_stream(round);
-  if (!b.exec_on_producer) wait_input(round, cs);  // cs writes the caller's output/counts below
+  // cs writes the caller's output/counts below
+  if (!b.exec_on_producer && !fault_skip_output_wait_) wait_input(round, cs);
   // Join: everything the comm stream wrote into this round's output.
   if (b.comm_used) {
     EventH ce = record_comm();

@@ -200,6 +200,10 @@ class DataPlane {
   SendSlot& slot(int32_t round);
   SendSlot new_slot();
   bool staging_on_ = false;
+  // Fault injection for the race checker's own test (AKKA_FAULT_SKIP_OUTPUT_WAIT=1):
+  // counts upload / finalize skip the wait for the caller's hand-over point,
+  // i.e. the round-2 counts-fill race comes back.
+  bool fault_skip_output_wait_ = false;
   int32_t max_slots_ = 0;
   std::vector<SendSlot> slots_;
   std::map<int32_t, size_t> slot_of_;

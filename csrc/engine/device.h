@@ -12,6 +12,7 @@
 
 #include <functional>
 #include <memory>
+#include <string>
 #include <vector>
 
 #include "common.h"
@@ -35,6 +36,14 @@ struct ReduceSpec {
   int32_t* fill = nullptr;
   int32_t fill_value = 0;
   int32_t fill_n = 0;
+};
+
+// A byte range an op reads or writes (stream race checking, racecheck.h).
+struct Access {
+  const void* ptr;
+  size_t bytes;
+  bool write;
+  const char* tag;
 };
 
 enum class CopyKind : int32_t { Default = 0, HostToDevice = 1, DeviceToHost = 2, DeviceToDevice = 3, HostToHost = 4 };
@@ -94,6 +103,16 @@ class Device {
   virtual void enqueue_host_op(StreamH, std::function<bool()>) {
     throw AkkaError("enqueue_host_op: not a host device");
   }
+
+  // Stream race checking (host device with AKKA_RACECHECK=1, racecheck.h).
+  // models_streams(): callers may hand the engine streams of this device as
+  // the producer of inputs / the allocator of outputs (their events count).
+  virtual bool models_streams() const { return false; }
+  // An op at this point of `s` that touches these bytes (transports and
+  // callers declare what the device ops cannot see, e.g. p2p buffers).
+  virtual void declare_access(StreamH, const std::vector<Access>&) {}
+  virtual std::vector<std::string> race_reports() const { return {}; }
+  virtual int64_t race_count() const { return 0; }
 };
 
 // Reduce specs with more than kMaxReduceSrc sources: fold into passes where

@@ -11,6 +11,7 @@
 #include <map>
 
 #include "device.h"
+#include "racecheck.h"
 
 namespace akka {
 
@@ -79,6 +80,8 @@ class HostDevice final : public Device {
   explicit HostDevice(bool deferred) : deferred_(deferred) {
     queues_[reinterpret_cast<StreamH>(1)];
     queues_[reinterpret_cast<StreamH>(2)];
+    const char* rc = std::getenv("AKKA_RACECHECK");
+    if (rc && *rc && *rc != '0') rc_ = std::make_unique<RaceChecker>();
   }
   ~HostDevice() override = default;
 
@@ -102,10 +105,17 @@ class HostDevice final : public Device {
   void destroy_stream(StreamH s) override { queues_.erase(s); }
 
   EventH create_event() override { return new HostEvent(); }
-  void destroy_event(EventH e) override { delete static_cast<HostEvent*>(e); }
+  void destroy_event(EventH e) override {
+    if (rc_) rc_->forget_event(e);
+    delete static_cast<HostEvent*>(e);
+  }
   void record(EventH e, StreamH s) override {
     auto* ev = static_cast<HostEvent*>(e);
     const int64_t gen = ++ev->recorded;
+    if (rc_) {
+      rc_->tick(s);
+      rc_->record(e, s);
+    }
     run(s, [ev, gen]() {
       if (ev->completed < gen) ev->completed = gen;
       return true;
@@ -114,29 +124,58 @@ class HostDevice final : public Device {
   void wait(StreamH s, EventH e) override {
     auto* ev = static_cast<HostEvent*>(e);
     const int64_t target = ev->recorded;
+    if (rc_) rc_->wait(s, e);  // ordering holds even when the wait is elided below
     if (ev->completed >= target) return;
     run(s, [ev, target]() { return ev->completed >= target; });
   }
   bool query(EventH e) override {
     auto* ev = static_cast<HostEvent*>(e);
-    return ev->completed >= ev->recorded;
+    const bool done = ev->completed >= ev->recorded;
+    if (done && rc_) rc_->host_join_event(e);  // the host saw it: later ops follow it
+    return done;
   }
   void sync_event(EventH e) override {
-    if (!deferred_) return;
     auto* ev = static_cast<HostEvent*>(e);
-    while (ev->completed < ev->recorded && step()) {
-    }  // best effort: a simulated rank cannot block on its peers
+    if (deferred_) {
+      while (ev->completed < ev->recorded && step()) {
+      }  // best effort: a simulated rank cannot block on its peers
+    }
+    if (rc_ && ev->completed >= ev->recorded) rc_->host_join_event(e);
   }
   void sync_stream(StreamH s) override {
-    if (!deferred_) return;
-    while (!queue_of(s).empty() && step()) {
+    if (deferred_) {
+      while (!queue_of(s).empty() && step()) {
+      }
+      AKKA_CHECK(queue_of(s).empty(),
+                 "host device sync would block: the simulated stream waits on a peer (drive the simulator instead)");
     }
-    AKKA_CHECK(queue_of(s).empty(),
-               "host device sync would block: the simulated stream waits on a peer (drive the simulator instead)");
+    if (rc_) rc_->host_join_stream(s);
   }
+
+  bool models_streams() const override { return rc_ != nullptr; }
+  void declare_access(StreamH s, const std::vector<Access>& acc) override {
+    if (!rc_) return;
+    rc_->tick(s);
+    rc_->access(s, acc);
+  }
+  std::vector<std::string> race_reports() const override {
+    return rc_ ? rc_->reports() : std::vector<std::string>{};
+  }
+  int64_t race_count() const override { return rc_ ? rc_->races() : 0; }
 
   void reduce(StreamH s, const ReduceSpec* specs, int32_t n, DType dt) override {
     std::vector<ReduceSpec> v(specs, specs + n);
+    if (rc_) {
+      const size_t es = dt == DType::F32 ? 4 : 2;
+      std::vector<Access> acc;
+      for (const auto& sp : v) {
+        for (int32_t i = 0; i < sp.nsrc; ++i)
+          if (sp.srcs[i] != sp.dst) acc.push_back({sp.srcs[i], size_t(sp.n) * es, false, "reduce.src"});
+        acc.push_back({sp.dst, size_t(sp.n) * es, true, "reduce.dst"});
+        if (sp.fill) acc.push_back({sp.fill, size_t(sp.fill_n) * 4, true, "reduce.fill"});
+      }
+      declare_access(s, acc);
+    }
     run(s, [v, dt]() {
       for (const auto& sp : v) {
         host_reduce(sp, dt);
@@ -148,6 +187,11 @@ class HostDevice final : public Device {
   }
   void copy(StreamH s, void* dst, const void* src, size_t bytes, CopyKind kind) override {
     if (dst == src || bytes == 0) return;
+    if (rc_) {
+      // a host->device copy reads its (pinned, host-owned) source at issue
+      if (kind == CopyKind::HostToDevice) declare_access(s, {{dst, bytes, true, "copy.dst"}});
+      else declare_access(s, {{src, bytes, false, "copy.src"}, {dst, bytes, true, "copy.dst"}});
+    }
     if (deferred_ && kind == CopyKind::HostToDevice) {
       // Host->device copies read their (pinned / message-owned) source when
       // issued; snapshot it so the deferred queue models that contract.
@@ -165,12 +209,14 @@ class HostDevice final : public Device {
     });
   }
   void zero(StreamH s, void* dst, size_t bytes) override {
+    if (rc_) declare_access(s, {{dst, bytes, true, "zero"}});
     run(s, [=]() {
       std::memset(dst, 0, bytes);
       return true;
     });
   }
   void fill_i32(StreamH s, int32_t* dst, int32_t value, size_t n) override {
+    if (rc_) declare_access(s, {{dst, n * sizeof(int32_t), true, "fill_i32"}});
     run(s, [=]() {
       for (size_t i = 0; i < n; ++i) dst[i] = value;
       return true;
@@ -216,6 +262,7 @@ class HostDevice final : public Device {
   }
 
   bool deferred_;
+  std::unique_ptr<RaceChecker> rc_;  // AKKA_RACECHECK=1
   std::map<StreamH, std::deque<std::function<bool()>>> queues_;
   uintptr_t next_stream_ = 16;
 };

@@ -105,7 +105,7 @@ class NullP2P final : public P2P {
 
 // ---- CPU simulator ------------------------------------------------------------
 class SimHub;
-std::shared_ptr<SimHub> make_sim_hub(int32_t nranks);
+std::shared_ptr<SimHub> make_sim_hub(int32_t nranks, bool collectives = false);
 // Endpoint for `rank`; ops are queued on the rank's deferred host device.
 std::unique_ptr<P2P> make_sim_p2p(std::shared_ptr<SimHub> hub, int32_t rank, Device* dev);
 // Drive all ranks' deferred devices until every queue is empty.  Throws with a
