@@ -10,6 +10,7 @@ counts exchange, stream-ordered arrival -- is validated bit-for-bit here.
 """
 from __future__ import annotations
 
+import weakref
 from typing import List, Sequence
 
 import torch
@@ -19,6 +20,11 @@ from ..data import AllReduceOutput
 from ..messages import InitWorkers
 from ..worker import AllreduceWorker
 from .collective import _RemoteRank
+
+
+# Every live simulated cluster (tests/conftest.py checks their race reports
+# after each test when AKKA_RACECHECK=1).
+LIVE_CLUSTERS: "weakref.WeakSet" = weakref.WeakSet()
 
 
 class SimCluster:
@@ -45,6 +51,7 @@ class SimCluster:
             w.set_lane(lane)
             if w._core.models_streams():  # (the device exists once the worker is initialised)
                 w.host_stream = w._core.create_stream()
+        LIVE_CLUSTERS.add(self)
 
     def allreduce(self, inputs: Sequence[torch.Tensor]) -> List[AllReduceOutput]:
         """One round on every rank; returns each rank's output (valid after the simulated run)."""
@@ -94,6 +101,7 @@ class ReactiveSimCluster:
             if w._core.models_streams():  # AKKA_RACECHECK=1: modelled caller stream
                 w.host_stream = w._core.create_stream()
         self.outputs: List[dict] = [dict() for _ in range(n)]
+        LIVE_CLUSTERS.add(self)
 
     def start(self, rank: int, x: torch.Tensor) -> None:
         """Rank ``rank`` starts its next round with contribution ``x``."""

@@ -42,3 +42,18 @@ def native():
     from akka_allreduce_amd import _native_loader
 
     return _native_loader.load()
+
+
+@pytest.fixture(autouse=True)
+def _stream_race_check():
+    """With AKKA_RACECHECK=1 (CPU), every simulated cluster a test built must
+    end race-free: the engine's own stream/event ordering is checked in every
+    simulator test, not only in tests/test_racecheck.py."""
+    yield
+    if os.environ.get("AKKA_RACECHECK", "0") in ("", "0"):
+        return
+    from akka_allreduce_amd.parallel.sim import LIVE_CLUSTERS
+
+    reports = [m for c in list(LIVE_CLUSTERS) for m in c.race_reports()]
+    LIVE_CLUSTERS.clear()
+    assert not reports, "stream races:\n" + "\n".join(reports[:10])

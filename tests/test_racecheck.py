@@ -176,3 +176,18 @@ def test_reactive_transport_is_race_free(th, slow):
 def test_reactive_offstream_read_is_flagged():
     d = _run_reactive({"n": 3, "S": 600, "C": 64, "th": 1.0, "slow": -1, "rounds": 2, "offstream_read": True})
     assert sum(d["races"]) > 0 and any("caller.read" in m for m in d["reports"]), d
+
+
+def test_simulator_suites_are_race_free():
+    """Every schedule test of the simulator (exact lanes, thresholds, lags,
+    uneven geometries, partial membership, reactive fuzzing with frozen and
+    dead ranks) re-run with the checker on: the conftest fixture fails any
+    test whose clusters report a stream race."""
+    e = dict(os.environ)
+    e["AKKA_RACECHECK"] = "1"
+    r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider",
+                        os.path.join(ROOT, "tests", "test_sim_schedule.py"),
+                        os.path.join(ROOT, "tests", "test_reactive_sim.py")],
+                       capture_output=True, text=True, timeout=900, env=e, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
+    assert " passed" in r.stdout and "failed" not in r.stdout
