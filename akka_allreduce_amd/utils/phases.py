@@ -49,6 +49,15 @@ def enable_rccl_debug_log(rank: int) -> str:
     return os.environ.setdefault("NCCL_DEBUG_FILE", rccl_debug_path(rank))
 
 
+
+def progress(msg: str) -> None:
+    """One timestamped line on stderr (bench.py's stdout is reserved for the
+    JSON result): a long multi-rank run shows where each rank is."""
+    import sys
+    import time
+
+    print(f"[akka {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
 class PhaseGuard:
     def __init__(self, base: Dict[str, Any], rank: int, world: int, debug_path: str = "",
                  exit_code: int = 3, stream=None, beacon_path: Optional[str] = None):
@@ -106,6 +115,7 @@ class PhaseGuard:
         self.enter(phase, seconds)
         err = None
         result = None
+        progress(f"rank {self.rank}: phase {phase} (deadline {seconds:g} s)")
         try:
             result = fn()
         except Exception as e:  # reported through the agreement step (or directly)

@@ -259,7 +259,15 @@ def apply_lane_choice(ar, name) -> None:
     if not name or ar.world_size < 2 or ar.transport != "stream":
         return
     if name.startswith("ipc") and not ar.state().get("link", {}).get("ipc"):
-        ar.enable_ipc()
+        try:
+            ar.enable_ipc()  # collective; fails alike on every rank (e.g. a window too large for one mapping)
+        except Exception as e:  # noqa: BLE001 - keep the job on the two-sided lanes
+            from akka_allreduce_amd.utils.phases import progress
+
+            progress(f"rank {ar.rank}: ipc lane unavailable for this buffer ({type(e).__name__}: {str(e)[:120]}); "
+                     "collective lane instead")
+            ar.use_lane("collective")
+            return
     ar.use_lane(name)
 
 
@@ -272,15 +280,18 @@ def run_extras(world: int, dev, barrier, which=("cfg1", "cfg3", "cfg4", "cfg5"),
     import torch
 
     from akka_allreduce_amd.parallel import ThresholdAllreduce
+    from akka_allreduce_amd.utils.phases import progress
 
     res: dict = {}
     keep = []  # communicators stay alive until exit (no per-rank teardown ordering)
+    progress(f"rank {rank}: extras {','.join(which)}")
     if "cfg1" in which and rank == 0:
         try:
             res["cfg1_readme_demo_cluster"] = run_cfg1()
         except Exception as e:
             res["cfg1_error"] = f"{type(e).__name__}: {e}"[:200]
     if "cfg4" in which and world > 1:
+        progress(f"rank {rank}: extra cfg4")
         try:
             # thresholds < 1 need a two-sided transport: RCCL pair communicators, or
             # the mailbox p2p over mapped memory when the job runs without RCCL
@@ -302,6 +313,7 @@ def run_extras(world: int, dev, barrier, which=("cfg1", "cfg3", "cfg4", "cfg5"),
     try:
         if "cfg3" not in which:
             raise _Skip()
+        progress(f"rank {rank}: extra cfg3")
         nbytes = 1 << 30
         S = nbytes // 2
         ar = ThresholdAllreduce(S, max_chunk_size=(8 << 20) // 2, dtype=torch.bfloat16, device=dev,
@@ -322,6 +334,7 @@ def run_extras(world: int, dev, barrier, which=("cfg1", "cfg3", "cfg4", "cfg5"),
     try:
         if "cfg5" not in which:
             raise _Skip()
+        progress(f"rank {rank}: extra cfg5")
         from akka_allreduce_amd.models.mlp import MLP, dp_sgd_step, synthetic_batch
         from akka_allreduce_amd.parallel.dp import GradientBucket
 

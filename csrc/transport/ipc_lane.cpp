@@ -69,6 +69,14 @@ IpcLane::IpcLane(Device* dev, const Geometry& g, int32_t me, DType dt)
   portion_ = std::max<int64_t>(1024, (pbytes / int64_t(es_)) / 1024 * 1024);
   nportions_ = int32_t(std::max<int64_t>(1, (maxb + portion_ - 1) / portion_));
   data_bytes_ = size_t(ipc_window_slots(g_.N)) * size_t(slot_) * es_;
+  // hipIpcOpenMemHandle of a window of 2.5 GiB hung on the test box (1.9 GiB
+  // opened at once; profiles/r02/ipc/README.md): refuse larger windows up
+  // front, every rank alike (the size is a function of the geometry), so the
+  // job keeps its other exact lanes instead of hanging in open().
+  AKKA_CHECK(data_bytes_ <= kIpcMaxWindowBytes,
+             "ipc lane: window of " + std::to_string(data_bytes_ >> 20) + " MiB exceeds the " +
+                 std::to_string(kIpcMaxWindowBytes >> 20) + " MiB an IPC mapping is known to open (buffer too large "
+                 "for this N; use the collective / p2p lanes)");
   flag_bytes_ = ipc_flag_bytes(g_.N, nportions_);
   data_ = static_cast<char*>(ipc_alloc_window(data_bytes_, &mem_kind_));
   // Flags uncached: every poll and every signal goes to memory.

@@ -40,6 +40,9 @@ namespace akka {
 // `kind` reports what was allocated.
 void* ipc_alloc_window(size_t bytes, std::string* kind);
 
+// Largest window the lane builds (one allocation, exported with an IPC handle).
+constexpr size_t kIpcMaxWindowBytes = size_t(1920) << 20;
+
 struct IpcLaneStats {
   int64_t rounds = 0, bcast_rounds = 0, bytes_pushed = 0, bytes_pulled = 0;
 };

@@ -30,6 +30,8 @@ for s in $STEPS; do
     ipc7) run 7 n7 --data-plane ipc --extras off || exit 1 ;;
     p2p8) GPU_MAX_HW_QUEUES=4 run 8 p2p_n8 --data-plane ipc_p2p --extras on --extras-only cfg4 \
             --cfg4-size-mb 64 --cfg4-delay-ms 50 --cfg4-rounds 6 || exit 1 ;;
+    all4) GPU_MAX_HW_QUEUES=8 run 4 all_n4 --data-plane ipc_p2p --extras on --extras-deadline-s 150 \
+            --cfg4-size-mb 64 --cfg4-delay-ms 50 --cfg4-rounds 10 || exit 1 ;;
     p2p4) GPU_MAX_HW_QUEUES=8 run 4 p2p_n4 --data-plane ipc_p2p --extras on --extras-only cfg4,cfg5 \
             --cfg4-size-mb 64 --cfg4-delay-ms 50 --cfg4-rounds 10 || exit 1 ;;
   esac

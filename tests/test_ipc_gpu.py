@@ -105,3 +105,12 @@ def test_ipc_round_waits_for_callers_pending_work_on_its_buffers():
     for d in rows:
         assert d["poison_in_block"], d  # the hazard was really set up
         assert d["poison_counts_ok"] and all(d["exact"]) and d["ipc_error"] == 0, d
+
+
+def test_ipc_window_too_large_for_one_mapping_fails_fast():
+    """A window beyond what one IPC mapping is known to open (an open of a
+    2.5 GiB window hung on the test box) is refused at construction on every
+    rank, with a message, instead of hanging in hipIpcOpenMemHandle."""
+    r, rows = _run(2, "--size", str(210_000_000), "--rounds", "1", timeout=150)
+    assert r.returncode != 0 and not rows
+    assert "exceeds the 1920 MiB an IPC mapping is known to open" in r.stderr, r.stderr[-2000:]
