@@ -407,6 +407,10 @@ class AllreduceWorker:
         later ones are one graph launch (stream_link.h).  GPU only."""
         self._core.set_graphs(bool(on))
 
+    def _alloc_counts(self) -> torch.Tensor:
+        g = self.geometry
+        return torch.empty(g.workerNum * g.kmax, dtype=torch.int32, device=self.device)
+
     def _fast_ok(self, tensor: torch.Tensor) -> bool:
         """Collective-style call on the scheduled transport, whose rounds
         complete inside the call: buffers can be bound natively."""
@@ -422,7 +426,7 @@ class AllreduceWorker:
         elif out.numel() != g.dataSize or out.dtype != self.dtype or out.device != self.device \
                 or not out.is_contiguous():
             raise ValueError("out must be a contiguous tensor of dataSize elements, worker dtype and device")
-        counts = torch.empty(g.workerNum * g.kmax, dtype=torch.int32, device=self.device)
+        counts = self._alloc_counts()
         r = self._next_round
         self._next_round += 1
         cuda = self.device.type == "cuda"
@@ -437,7 +441,8 @@ class AllreduceWorker:
         try:
             with _tracing.range_(f"akka.round {r}"):
                 done = self._core.fast_round(r, x.data_ptr(), out.data_ptr(), counts.data_ptr(),
-                                             stream.cuda_stream if cuda else 0, cuda and not async_op)
+                                             stream.cuda_stream if cuda else (self.host_stream or 0),
+                                             (cuda and not async_op) or (not cuda and self.host_stream is not None))
         except Exception as e:  # tryCatch semantics as in receive()
             self._fast_pending.pop(r, None)
             self.errors.append(e)

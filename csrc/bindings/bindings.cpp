@@ -160,7 +160,7 @@ class WorkerCore final : public EngineHost {
   }
   void connect_callback(py::function fn, int32_t rank, int32_t nranks) {
     AKKA_CHECK(dev_ && dev_->is_host() && !deferred_, "callback p2p runs on an immediate host device");
-    p2p_ = std::make_unique<PyCallbackP2P>(std::move(fn), rank, nranks);
+    p2p_ = std::make_unique<PyCallbackP2P>(std::move(fn), rank, nranks, dev_.get());
     make_stream_link();
   }
   void connect_loopback(const PyLoopbackHub& hub, int32_t rank) {
@@ -499,8 +499,9 @@ class WorkerCore final : public EngineHost {
       host_.attr("_fetch")(round);
       return;
     }
+    // host devices: a modelled caller stream (stream race checking) counts too
     dp_->bind_input(round, reinterpret_cast<const void*>(it->second.in), reinterpret_cast<StreamH>(it->second.stream),
-                    !dev_->is_host());
+                    !dev_->is_host() || (dev_->models_streams() && it->second.stream != 0));
   }
   void alloc_output(int32_t round) override {
     auto it = pre_.find(round);

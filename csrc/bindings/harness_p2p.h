@@ -32,20 +32,26 @@ namespace py = pybind11;
 // real processes on CPU-only machines.
 class PyCallbackP2P final : public P2P {
  public:
-  PyCallbackP2P(py::function fn, int32_t rank, int32_t n) : fn_(std::move(fn)), rank_(rank), n_(n) {}
+  PyCallbackP2P(py::function fn, int32_t rank, int32_t n, Device* dev = nullptr)
+      : fn_(std::move(fn)), rank_(rank), n_(n), dev_(dev) {}
   int32_t rank() const override { return rank_; }
   int32_t nranks() const override { return n_; }
   const char* name() const override { return "callback"; }
-  void group(StreamH, const std::vector<P2POp>& ops) override {
+  void group(StreamH s, const std::vector<P2POp>& ops) override {
     py::list l;
-    for (const auto& op : ops)
+    std::vector<Access> acc;
+    for (const auto& op : ops) {
       l.append(py::make_tuple(op.send, op.peer, reinterpret_cast<uintptr_t>(op.buf), op.bytes, op.channel));
+      acc.push_back({op.buf, op.bytes, !op.send, op.send ? "p2p.send" : "p2p.recv"});
+    }
+    if (dev_) dev_->declare_access(s, acc);  // stream race checking (no-op unless on)
     fn_(l);
   }
 
  private:
   py::function fn_;
   int32_t rank_, n_;
+  Device* dev_;
 };
 
 // Asynchronous grouped p2p through two Python callables (reactive transport

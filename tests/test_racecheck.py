@@ -191,3 +191,42 @@ def test_simulator_suites_are_race_free():
                        capture_output=True, text=True, timeout=900, env=e, cwd=ROOT)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-2000:]
     assert " passed" in r.stdout and "failed" not in r.stdout
+
+
+def _run_fast(n, lane, mode=""):
+    import json
+    import socket
+    import tempfile
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    e = dict(os.environ)
+    e["AKKA_RACECHECK"] = "1"
+    with tempfile.TemporaryDirectory() as out:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+               "--master-addr", "127.0.0.1", "--master-port", str(port),
+               os.path.join(ROOT, "tests", "race_ranks.py"), "4096", "256", lane, "3", out, mode]
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=e, cwd=ROOT)
+        assert r.returncode == 0, r.stderr[-3000:]
+        rows = []
+        for i in range(n):
+            with open(os.path.join(out, f"rank{i}.json")) as f:
+                rows.append(json.load(f))
+    return rows
+
+
+@pytest.mark.parametrize("lane", ["collective", "p2p"])
+def test_fast_path_across_processes_is_race_free(lane):
+    """ThresholdAllreduce's native fast path (the GPU bench / DP path: caller
+    buffers bound in C++) over gloo processes, checked end to end."""
+    rows = _run_fast(3, lane)
+    for d in rows:
+        assert all(d["exact"]) and d["fast_rounds"] == 3, d
+        assert d["races"] == 0, d["reports"]
+
+
+def test_fast_path_offstream_read_is_flagged():
+    rows = _run_fast(2, "p2p", "offstream")
+    assert all(d["races"] > 0 for d in rows), rows
+    assert any("caller.read" in m for d in rows for m in d["reports"])
