@@ -242,7 +242,7 @@ __device__ void reduce_span(const IpcArgs& a, const char* mine, const char* slot
           reinterpret_cast<uint4*>(o)[i] = w;
           if (bc) {
             for (int p = 0; p < N; ++p)
-              if (p != me) reinterpret_cast<uint4*>(a.data[p] + gather_off)[i] = w;
+              if (p != me) reinterpret_cast<uint4*>(a.gdata[p] + gather_off)[i] = w;
           } else {
             reinterpret_cast<uint4*>(r)[i] = w;
           }
@@ -258,7 +258,7 @@ __device__ void reduce_span(const IpcArgs& a, const char* mine, const char* slot
       Elt<T>::store1(o + i * ES, acc);
       if (bc) {
         for (int p = 0; p < N; ++p)
-          if (p != me) Elt<T>::store1(a.data[p] + gather_off + i * ES, acc);
+          if (p != me) Elt<T>::store1(a.gdata[p] + gather_off + i * ES, acc);
       } else {
         Elt<T>::store1(r + i * ES, acc);
       }
@@ -304,8 +304,8 @@ __device__ void reduce_item(const IpcArgs& a, int32_t j, int32_t part) {
   if (ok && p1 > p0) {
     const int64_t e = e0 + p0;
     reduce_span<T>(a, a.in + (a.bstart[me] + e) * ES, a.data[me] + e * ES, a.slot * ES,
-                   a.out + (a.bstart[me] + e) * ES, a.data[me] + (int64_t(N) * a.slot + e) * ES,
-                   a.bcast ? (int64_t(N + 1 + me) * a.slot + e) * ES : int64_t(-1), p1 - p0);
+                   a.out + (a.bstart[me] + e) * ES, a.gdata[me] + e * ES,
+                   a.bcast ? (int64_t(1 + me) * a.slot + e) * ES : int64_t(-1), p1 - p0);
   }
   release_wg();
   if (threadIdx.x == 0) {
@@ -337,8 +337,8 @@ __device__ void phase2_item(const IpcArgs& a, int32_t j, int32_t p) {
   ok = acquire_all(ok);
   const int64_t e0 = int64_t(j) * a.portion;
   const int64_t n = max(int64_t(0), min(a.portion, a.blen[p] - e0));
-  const char* src = a.bcast ? a.data[me] + (int64_t(N + 1 + p) * a.slot + e0) * ES
-                            : a.data[p] + (int64_t(N) * a.slot + e0) * ES;
+  const char* src = a.bcast ? a.gdata[me] + (int64_t(1 + p) * a.slot + e0) * ES
+                            : a.gdata[p] + e0 * ES;
   if (ok && n > 0) copy_in(a.out + (a.bstart[p] + e0) * ES, src, n * ES);
   __syncthreads();  // `ok` is rewritten by the next item
 }

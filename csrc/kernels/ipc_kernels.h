@@ -27,14 +27,16 @@ constexpr int kIpcMaxRanks = 16;
 constexpr int kIpcFlagStride = 16;  // uint32 words: one 64-B line per flag
 constexpr int kIpcReduceSplit = 4;  // reduce workgroups (parts) per portion
 
-// Window of a rank, in slots of `slot` elements:
-//   [0, N)        slot[src]: src's contribution to my block (pushed by src)
-//   N             reduced: my reduced block (pulled by the others, pull mode)
-//   [N+1, 2N+1)   gather[src]: src's reduced block (pushed by src, bcast mode)
+// Window of a rank, in slots of `slot` elements, as two allocations (each
+// one IPC mapping, so a window may reach twice the largest mapping size):
+//   data:  [0, N)   slot[src]: src's contribution to my block (pushed by src)
+//   gdata: 0        reduced: my reduced block (pulled by the others, pull mode)
+//          [1, N+1) gather[src]: src's reduced block (pushed by src, bcast mode)
 // Flags hold round ids (stores, never counts), so the two phase-2 modes can
 // alternate between rounds.
 struct IpcArgs {
-  char* data[kIpcMaxRanks];       // window base of every rank, mapped in this process (own = local)
+  char* data[kIpcMaxRanks];       // inbound slots of every rank, mapped in this process (own = local)
+  char* gdata[kIpcMaxRanks];      // reduced row + gather slots of every rank, mapped likewise
   uint32_t* flags[kIpcMaxRanks];  // flag area of every rank, mapped in this process
   int64_t bstart[kIpcMaxRanks];   // block start / length (elements)
   int64_t blen[kIpcMaxRanks];

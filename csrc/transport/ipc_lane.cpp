@@ -20,14 +20,14 @@ namespace akka {
 
 namespace {
 
-constexpr char kMagic[8] = {'A', 'K', 'I', 'P', 'C', '0', '1', 0};
+constexpr char kMagic[8] = {'A', 'K', 'I', 'P', 'C', '0', '2', 0};
 
 struct HandleBlob {  // what handle() serialises
   char magic[8];
   int32_t rank, nranks, esize, pad;
   int64_t S, slot, portion;
   char bus[32];  // PCI bus id of the rank's GPU: ranks sharing a card (tests) share its CUs
-  hipIpcMemHandle_t data, flags;
+  hipIpcMemHandle_t data, gdata, flags;
 };
 
 int64_t env_i64(const char* name, int64_t dflt) {
@@ -68,17 +68,22 @@ IpcLane::IpcLane(Device* dev, const Geometry& g, int32_t me, DType dt)
   const int64_t pbytes = std::max<int64_t>(4096, env_i64("AKKA_IPC_PORTION_BYTES", int64_t(512) << 10));
   portion_ = std::max<int64_t>(1024, (pbytes / int64_t(es_)) / 1024 * 1024);
   nportions_ = int32_t(std::max<int64_t>(1, (maxb + portion_ - 1) / portion_));
-  data_bytes_ = size_t(ipc_window_slots(g_.N)) * size_t(slot_) * es_;
-  // hipIpcOpenMemHandle of a window of 2.5 GiB hung on the test box (1.9 GiB
-  // opened at once; profiles/r02/ipc/README.md): refuse larger windows up
-  // front, every rank alike (the size is a function of the geometry), so the
-  // job keeps its other exact lanes instead of hanging in open().
-  AKKA_CHECK(data_bytes_ <= kIpcMaxWindowBytes,
-             "ipc lane: window of " + std::to_string(data_bytes_ >> 20) + " MiB exceeds the " +
-                 std::to_string(kIpcMaxWindowBytes >> 20) + " MiB an IPC mapping is known to open (buffer too large "
-                 "for this N; use the collective / p2p lanes)");
+  // Two allocations (inbound slots | reduced + gather slots), each one IPC
+  // mapping.  hipIpcOpenMemHandle of a 2.5 GiB mapping hung on the test box
+  // (1.9 GiB opened at once; profiles/r02/ipc/README.md): refuse larger ones
+  // up front, every rank alike (the sizes are a function of the geometry),
+  // so the job keeps its other exact lanes instead of hanging in open().
+  in_bytes_ = size_t(g_.N) * size_t(slot_) * es_;
+  out_bytes_ = size_t(g_.N + 1) * size_t(slot_) * es_;
+  data_bytes_ = in_bytes_ + out_bytes_;
+  AKKA_CHECK(std::max(in_bytes_, out_bytes_) <= kIpcMaxWindowBytes,
+             "ipc lane: window part of " + std::to_string(std::max(in_bytes_, out_bytes_) >> 20) +
+                 " MiB exceeds the " + std::to_string(kIpcMaxWindowBytes >> 20) +
+                 " MiB an IPC mapping is known to open (buffer too large for this N; use the collective / p2p "
+                 "lanes)");
   flag_bytes_ = ipc_flag_bytes(g_.N, nportions_);
-  data_ = static_cast<char*>(ipc_alloc_window(data_bytes_, &mem_kind_));
+  data_ = static_cast<char*>(ipc_alloc_window(in_bytes_, &mem_kind_));
+  gdata_ = static_cast<char*>(ipc_alloc_window(out_bytes_, nullptr));
   // Flags uncached: every poll and every signal goes to memory.
   if (hipExtMallocWithFlags(reinterpret_cast<void**>(&flags_), flag_bytes_, hipDeviceMallocUncached) != hipSuccess) {
     (void)hipGetLastError();
@@ -96,8 +101,10 @@ IpcLane::IpcLane(Device* dev, const Geometry& g, int32_t me, DType dt)
     khz = 100000;  // 100 MHz
   timeout_ticks_ = uint64_t(std::max<int64_t>(1, env_i64("AKKA_IPC_TIMEOUT_MS", 10000))) * uint64_t(khz);
   peer_data_.assign(size_t(g_.N), nullptr);
+  peer_gdata_.assign(size_t(g_.N), nullptr);
   peer_flags_.assign(size_t(g_.N), nullptr);
   peer_data_[size_t(me_)] = data_;
+  peer_gdata_[size_t(me_)] = gdata_;
   peer_flags_[size_t(me_)] = flags_;
 }
 
@@ -107,9 +114,11 @@ IpcLane::~IpcLane() {
   for (int32_t p = 0; p < g_.N; ++p) {
     if (p == me_) continue;
     if (peer_data_[size_t(p)]) hipIpcCloseMemHandle(peer_data_[size_t(p)]);
+    if (peer_gdata_[size_t(p)]) hipIpcCloseMemHandle(peer_gdata_[size_t(p)]);
     if (peer_flags_[size_t(p)]) hipIpcCloseMemHandle(peer_flags_[size_t(p)]);
   }
   if (data_) hipFree(data_);
+  if (gdata_) hipFree(gdata_);
   if (flags_) hipFree(flags_);
   if (err_host_) hipHostFree(err_host_);
 }
@@ -126,6 +135,7 @@ std::string IpcLane::handle() const {
   b.portion = portion_;
   AKKA_IPC_HIP(hipDeviceGetPCIBusId(b.bus, int(sizeof(b.bus)) - 1, dev_->device_index()));
   AKKA_IPC_HIP(hipIpcGetMemHandle(&b.data, data_));
+  AKKA_IPC_HIP(hipIpcGetMemHandle(&b.gdata, gdata_));
   AKKA_IPC_HIP(hipIpcGetMemHandle(&b.flags, flags_));
   return std::string(reinterpret_cast<const char*>(&b), sizeof(b));
 }
@@ -149,10 +159,13 @@ void IpcLane::open(const std::vector<std::string>& handles) {
     if (std::strncmp(b.bus, mybus, sizeof(mybus)) == 0) ++sharers;
     if (p == me_) continue;
     void* d = nullptr;
+    void* gd = nullptr;
     void* f = nullptr;
     AKKA_IPC_HIP(hipIpcOpenMemHandle(&d, b.data, hipIpcMemLazyEnablePeerAccess));
+    AKKA_IPC_HIP(hipIpcOpenMemHandle(&gd, b.gdata, hipIpcMemLazyEnablePeerAccess));
     AKKA_IPC_HIP(hipIpcOpenMemHandle(&f, b.flags, hipIpcMemLazyEnablePeerAccess));
     peer_data_[size_t(p)] = static_cast<char*>(d);
+    peer_gdata_[size_t(p)] = static_cast<char*>(gd);
     peer_flags_[size_t(p)] = static_cast<uint32_t*>(f);
   }
   // Grid cap of the waiting kernels: their parked workgroups must leave room
@@ -168,6 +181,7 @@ void IpcLane::round(StreamH s, const void* in, void* out) {
   std::memset(&a, 0, sizeof(a));
   for (int32_t p = 0; p < g_.N; ++p) {
     a.data[p] = peer_data_[size_t(p)];
+    a.gdata[p] = peer_gdata_[size_t(p)];
     a.flags[p] = peer_flags_[size_t(p)];
     a.bstart[p] = g_.block_start(p);
     a.blen[p] = g_.block_len(p);

@@ -4,8 +4,8 @@
 // Why a lane of its own: on one node every MI355X maps every other one's HBM
 // over xGMI, so an exact round (thresholds 1, every chunk from every peer)
 // needs no message matching at all.  Each rank owns a window
-//   [slot 0 | ... | slot N-1 | reduced | gather 0 | ... | gather N-1]
-// (each slot >= one block; ipc_kernels.h)
+//   [slot 0 | ... | slot N-1]  [reduced | gather 0 | ... | gather N-1]
+// (two allocations; each slot >= one block; ipc_kernels.h)
 // plus a small flag area (uncached).  Rank q pushes block p of its input into
 // slot q of rank p's window, rank p sums its N slots into its output block and
 // `reduced` row, and every rank pulls the reduced rows of the others (or, in
@@ -40,7 +40,7 @@ namespace akka {
 // `kind` reports what was allocated.
 void* ipc_alloc_window(size_t bytes, std::string* kind);
 
-// Largest window the lane builds (one allocation, exported with an IPC handle).
+// Largest part of a window the lane builds (one allocation, one IPC handle).
 constexpr size_t kIpcMaxWindowBytes = size_t(1920) << 20;
 
 struct IpcLaneStats {
@@ -90,12 +90,14 @@ class IpcLane {
   size_t es_;
   int64_t slot_ = 0, portion_ = 0;
   int32_t nportions_ = 0;
-  size_t data_bytes_ = 0, flag_bytes_ = 0;
-  char* data_ = nullptr;
+  size_t data_bytes_ = 0, flag_bytes_ = 0, in_bytes_ = 0, out_bytes_ = 0;
+  char* data_ = nullptr;   // inbound slots
+  char* gdata_ = nullptr;  // reduced row + gather slots
   uint32_t* flags_ = nullptr;
   uint32_t* err_host_ = nullptr;  // host-mapped error word
   uint32_t* err_dev_ = nullptr;
   std::vector<char*> peer_data_;      // [N] mapped windows (own = data_)
+  std::vector<char*> peer_gdata_;     // [N] mapped reduced / gather parts (own = gdata_)
   std::vector<uint32_t*> peer_flags_; // [N]
   uint32_t round_ = 0;
   int32_t max_wgs_ = 1024, sharers_ = 1;

@@ -14,6 +14,10 @@ run() {  # run <n> <MiB> <dtype> <mem>
   echo "n=$1 $2MiB $3 $4 rc=$rc"
   return $rc
 }
-for spec in ${SPECS:-"2 384 float32 fine" "2 512 float32 fine" "2 768 float32 fine" "2 1024 float32 fine"}; do
+if [ -n "$SPEC" ]; then  # one case: SPEC="<n> <MiB> <dtype> <mem>"
+  run $SPEC || exit $?
+  exit 0
+fi
+for spec in "2 384 float32 fine" "2 512 float32 fine" "2 768 float32 fine" "2 1024 float32 fine"; do
   run $spec || exit $?
 done

@@ -111,6 +111,7 @@ def test_ipc_window_too_large_for_one_mapping_fails_fast():
     """A window beyond what one IPC mapping is known to open (an open of a
     2.5 GiB window hung on the test box) is refused at construction on every
     rank, with a message, instead of hanging in hipIpcOpenMemHandle."""
-    r, rows = _run(2, "--size", str(210_000_000), "--rounds", "1", timeout=150)
+    # N=2 fp32: slot = S/2 elements; the reduced + gather part is 3 slots
+    r, rows = _run(2, "--size", str(360_000_000), "--rounds", "1", timeout=150)
     assert r.returncode != 0 and not rows
     assert "exceeds the 1920 MiB an IPC mapping is known to open" in r.stderr, r.stderr[-2000:]
