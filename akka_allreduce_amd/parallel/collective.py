@@ -314,10 +314,10 @@ class ThresholdAllreduce:
             raise RuntimeError(f"enable_ipc: ranks {missing} could not create their ipc windows")
         self.worker.ipc_open(handles)
 
-    def set_ipc_mode(self, mode: str, fused: bool = False) -> None:
+    def set_ipc_mode(self, mode: str, fused: bool = False, threads: int = 0) -> None:
         """Phase 2 of the ipc lane: ``"pull"`` or ``"bcast"``, optionally ``fused``
-        into one launch (AllreduceWorker.ipc_set_mode)."""
-        self.worker.ipc_set_mode(mode, fused)
+        into one launch, with ``threads`` per workgroup (AllreduceWorker.ipc_set_mode)."""
+        self.worker.ipc_set_mode(mode, fused, threads)
 
     def ipc_error(self) -> int:
         """Non-zero once a wait of the ipc lane timed out (synchronises)."""
@@ -336,23 +336,27 @@ class ThresholdAllreduce:
         self.worker.set_graphs(on)
 
     # ---- lane tuning -------------------------------------------------------
-    LANES = {  # candidate -> (lane, exact transfer-unit bytes or -1, ipc mode, ipc fused)
-        "collective": ("collective", -1, None, False),
-        "p2p": ("p2p", -1, None, False),
-        "p2p_block": ("p2p", 1 << 40, None, False),
-        "ipc": ("ipc", -1, "pull", False),
-        "ipc_bcast": ("ipc", -1, "bcast", False),
-        "ipc_fused": ("ipc", -1, "pull", True),
-        "ipc_fused_bcast": ("ipc", -1, "bcast", True),
+    LANES = {  # candidate -> (lane, exact transfer-unit bytes or -1, ipc mode, ipc fused, ipc workgroup size)
+        "collective": ("collective", -1, None, False, 0),
+        "p2p": ("p2p", -1, None, False, 0),
+        "p2p_block": ("p2p", 1 << 40, None, False, 0),
+        "ipc": ("ipc", -1, "pull", False, 256),
+        "ipc_bcast": ("ipc", -1, "bcast", False, 256),
+        "ipc_fused": ("ipc", -1, "pull", True, 256),
+        "ipc_fused_bcast": ("ipc", -1, "bcast", True, 256),
+        # 1024-thread workgroups: 4x the loads / stores in flight per CU when a
+        # rank has its GPU to itself (profiles/r02/ipc: -10 % at N=2 on one card)
+        "ipc_wide": ("ipc", -1, "pull", False, 1024),
+        "ipc_bcast_wide": ("ipc", -1, "bcast", False, 1024),
     }
 
     def use_lane(self, name: str) -> None:
         """Switch to a named lane candidate (see LANES); every rank must do the
         same at the same round."""
-        ln, unit, mode, fused = self.LANES[name]
+        ln, unit, mode, fused, threads = self.LANES[name]
         self.set_lane(ln)
         if ln == "ipc":
-            self.set_ipc_mode(mode, fused)
+            self.set_ipc_mode(mode, fused, threads)
         elif self.world_size > 1:
             self.set_exact_unit_bytes(unit)
 
@@ -393,7 +397,7 @@ class ThresholdAllreduce:
                         res["ipc"] = {"exact": None, "ms": None,
                                       "error": err or "another rank could not open its windows"}
                 if ipc_open:
-                    cands += ["ipc", "ipc_bcast", "ipc_fused", "ipc_fused_bcast"]
+                    cands += ["ipc", "ipc_bcast", "ipc_fused", "ipc_fused_bcast", "ipc_wide", "ipc_bcast_wide"]
         S, N, r = self.data_size, self.world_size, self.rank
         dtype = self.worker.dtype
         x = torch.randn(S, device=self.device).to(dtype)

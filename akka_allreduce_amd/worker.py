@@ -391,12 +391,14 @@ class AllreduceWorker:
         (synchronises the device)."""
         return int(self._core.ipc_error())
 
-    def ipc_set_mode(self, mode: str, fused: bool = False) -> None:
+    def ipc_set_mode(self, mode: str, fused: bool = False, threads: int = 0) -> None:
         """Phase 2 of the ipc lane: ``"pull"`` (every rank reads the reduced
         rows over xGMI) or ``"bcast"`` (each reducer writes its rows into every
         peer's window); ``fused``: the three phases as roles of one launch,
-        pipelined by portion.  Every rank must switch at the same round."""
-        self._core.ipc_set_mode(mode, bool(fused))
+        pipelined by portion; ``threads``: workgroup size of the round's
+        kernels (256 / 512 / 1024, 0 keeps it).  Every rank must switch at the
+        same round."""
+        self._core.ipc_set_mode(mode, bool(fused), int(threads))
 
     def ipc_close(self) -> None:
         self._core.ipc_close()

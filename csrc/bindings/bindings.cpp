@@ -225,11 +225,14 @@ class WorkerCore final : public EngineHost {
     py::gil_scoped_release nogil;
     return stream_link_->ipc()->error();
   }
-  void ipc_set_mode(const std::string& mode, bool fused) {
+  void ipc_set_mode(const std::string& mode, bool fused, int32_t threads) {
     AKKA_CHECK(stream_link_ && stream_link_->ipc(), "ipc_set_mode: the ipc lane is not open");
     AKKA_CHECK(mode == "pull" || mode == "bcast", "ipc mode must be 'pull' or 'bcast'");
+    AKKA_CHECK(threads == 0 || threads == 256 || threads == 512 || threads == 1024,
+               "ipc workgroup size must be 256, 512 or 1024 (0: keep)");
     stream_link_->ipc()->set_bcast(mode == "bcast");
     stream_link_->ipc()->set_fused(fused);
+    if (threads) stream_link_->ipc()->set_threads(threads);
   }
   void ipc_close() {
     ipc_pending_.reset();
@@ -668,7 +671,8 @@ PYBIND11_MODULE(_native, m) {
       .def("ipc_open", &WorkerCore::ipc_open)
       .def("ipc_error", &WorkerCore::ipc_error)
       .def("ipc_close", &WorkerCore::ipc_close)
-      .def("ipc_set_mode", &WorkerCore::ipc_set_mode, py::arg("mode"), py::arg("fused") = false)
+      .def("ipc_set_mode", &WorkerCore::ipc_set_mode, py::arg("mode"), py::arg("fused") = false,
+           py::arg("threads") = 0)
       .def("scatter_count", &WorkerCore::scatter_count)
       .def("reduced_arrivals", &WorkerCore::reduced_arrivals);
 

@@ -24,7 +24,8 @@
 namespace akka {
 namespace {
 
-constexpr int kThreads = 256;
+constexpr int kThreads = 256;      // default workgroup size (AKKA_IPC_THREADS: 256 / 512 / 1024)
+constexpr int kMaxThreads = 1024;  // launch bound of the one-sided round kernels
 constexpr int kUnroll = 4;       // 16-B vectors per thread per source in flight
 constexpr int kReduceSplit = kIpcReduceSplit;
 
@@ -84,20 +85,20 @@ __device__ void copy_bytes(char* __restrict__ dst, const char* __restrict__ src,
     uint4* d = reinterpret_cast<uint4*>(dst);
     const int64_t n = bytes >> 4;
     int64_t i = threadIdx.x;
-    for (; i + (kUnroll - 1) * kThreads < n; i += kUnroll * kThreads) {
+    for (; i + (kUnroll - 1) * int(blockDim.x) < n; i += kUnroll * int(blockDim.x)) {
       uint4 v[kUnroll];
 #pragma unroll
-      for (int u = 0; u < kUnroll; ++u) v[u] = s[i + u * kThreads];
+      for (int u = 0; u < kUnroll; ++u) v[u] = s[i + u * int(blockDim.x)];
 #pragma unroll
-      for (int u = 0; u < kUnroll; ++u) d[i + u * kThreads] = v[u];
+      for (int u = 0; u < kUnroll; ++u) d[i + u * int(blockDim.x)] = v[u];
     }
-    for (; i < n; i += kThreads) d[i] = s[i];
+    for (; i < n; i += int(blockDim.x)) d[i] = s[i];
   } else if (((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src) | uintptr_t(bytes)) & 3) == 0) {
     const uint32_t* s = reinterpret_cast<const uint32_t*>(src);
     uint32_t* d = reinterpret_cast<uint32_t*>(dst);
-    for (int64_t i = threadIdx.x; i < (bytes >> 2); i += kThreads) d[i] = s[i];
+    for (int64_t i = threadIdx.x; i < (bytes >> 2); i += int(blockDim.x)) d[i] = s[i];
   } else {
-    for (int64_t i = threadIdx.x; i < bytes; i += kThreads) dst[i] = src[i];
+    for (int64_t i = threadIdx.x; i < bytes; i += int(blockDim.x)) dst[i] = src[i];
   }
 }
 
@@ -126,20 +127,20 @@ __device__ void copy_in(char* __restrict__ dst, const char* __restrict__ src, in
     uint4* d = reinterpret_cast<uint4*>(dst);
     const int64_t n = bytes >> 4;
     int64_t i = threadIdx.x;
-    for (; i + (kUnroll - 1) * kThreads < n; i += kUnroll * kThreads) {
+    for (; i + (kUnroll - 1) * int(blockDim.x) < n; i += kUnroll * int(blockDim.x)) {
       uint4 v[kUnroll];
 #pragma unroll
-      for (int u = 0; u < kUnroll; ++u) v[u] = load_sys16(r, (i + u * kThreads) * 16);
+      for (int u = 0; u < kUnroll; ++u) v[u] = load_sys16(r, (i + u * int(blockDim.x)) * 16);
 #pragma unroll
-      for (int u = 0; u < kUnroll; ++u) d[i + u * kThreads] = v[u];
+      for (int u = 0; u < kUnroll; ++u) d[i + u * int(blockDim.x)] = v[u];
     }
-    for (; i < n; i += kThreads) d[i] = load_sys16(r, i * 16);
+    for (; i < n; i += int(blockDim.x)) d[i] = load_sys16(r, i * 16);
   } else if (((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src) | uintptr_t(bytes)) & 3) == 0) {
     uint32_t* d = reinterpret_cast<uint32_t*>(dst);
-    for (int64_t i = threadIdx.x; i < (bytes >> 2); i += kThreads)
+    for (int64_t i = threadIdx.x; i < (bytes >> 2); i += int(blockDim.x))
       d[i] = __builtin_amdgcn_raw_buffer_load_b32(r, int(i * 4), 0, kSysAux);
   } else {
-    for (int64_t i = threadIdx.x; i < bytes; i += kThreads)
+    for (int64_t i = threadIdx.x; i < bytes; i += int(blockDim.x))
       dst[i] = char(__builtin_amdgcn_raw_buffer_load_b8(r, int(i), 0, kSysAux));
   }
 }
@@ -211,7 +212,7 @@ __device__ void reduce_span(const IpcArgs& a, const char* mine, const char* slot
                uintptr_t(bc ? gather_off : 0) | uintptr_t(n * ES)) & 15) == 0;
   if (vec) {
     const int64_t nv = n / PV;
-    for (int64_t i0 = threadIdx.x; i0 < nv; i0 += kUnroll * kThreads) {
+    for (int64_t i0 = threadIdx.x; i0 < nv; i0 += kUnroll * int(blockDim.x)) {
       float acc[kUnroll][PV];
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u)
@@ -223,20 +224,20 @@ __device__ void reduce_span(const IpcArgs& a, const char* mine, const char* slot
           const uint4* src = reinterpret_cast<const uint4*>(mine);
 #pragma unroll
           for (int u = 0; u < kUnroll; ++u) {
-            const int64_t i = i0 + int64_t(u) * kThreads;
+            const int64_t i = i0 + int64_t(u) * int(blockDim.x);
             v[u] = i < nv ? src[i] : make_uint4(0, 0, 0, 0);
           }
         } else {  // slot s: written by rank s
           const auto r = sys_rsrc(slots + int64_t(s) * slot_bytes, n * ES);
 #pragma unroll
-          for (int u = 0; u < kUnroll; ++u) v[u] = load_sys16(r, (i0 + int64_t(u) * kThreads) * 16);  // 0 past the end
+          for (int u = 0; u < kUnroll; ++u) v[u] = load_sys16(r, (i0 + int64_t(u) * int(blockDim.x)) * 16);  // 0 past the end
         }
 #pragma unroll
         for (int u = 0; u < kUnroll; ++u) Elt<T>::add(acc[u], v[u]);
       }
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) {
-        const int64_t i = i0 + int64_t(u) * kThreads;
+        const int64_t i = i0 + int64_t(u) * int(blockDim.x);
         if (i < nv) {
           const uint4 w = Elt<T>::pack(acc[u]);
           reinterpret_cast<uint4*>(o)[i] = w;
@@ -250,7 +251,7 @@ __device__ void reduce_span(const IpcArgs& a, const char* mine, const char* slot
       }
     }
   } else {
-    for (int64_t i = threadIdx.x; i < n; i += kThreads) {
+    for (int64_t i = threadIdx.x; i < n; i += int(blockDim.x)) {
       float acc = 0.f;
       for (int s = 0; s < N; ++s)
         acc += s == me ? Elt<T>::load1(mine + i * ES)
@@ -353,19 +354,19 @@ __device__ inline int32_t item_peer(const IpcArgs& a, int32_t w) { return (a.me 
 // card in tests need room for each other's push kernels).
 
 template <int ES>
-__global__ __launch_bounds__(kThreads) void ipc_push_kernel(IpcArgs a) {
+__global__ __launch_bounds__(kMaxThreads) void ipc_push_kernel(IpcArgs a) {
   const int32_t items = a.nportions * (a.N - 1);
   for (int32_t w = blockIdx.x; w < items; w += gridDim.x) push_item<ES>(a, w / (a.N - 1), item_peer(a, w));
 }
 
 template <typename T>
-__global__ __launch_bounds__(kThreads) void ipc_reduce_kernel(IpcArgs a) {
+__global__ __launch_bounds__(kMaxThreads) void ipc_reduce_kernel(IpcArgs a) {
   const int32_t items = a.nportions * kReduceSplit;
   for (int32_t w = blockIdx.x; w < items; w += gridDim.x) reduce_item<T>(a, w / kReduceSplit, w % kReduceSplit);
 }
 
 template <int ES>
-__global__ __launch_bounds__(kThreads) void ipc_phase2_kernel(IpcArgs a) {
+__global__ __launch_bounds__(kMaxThreads) void ipc_phase2_kernel(IpcArgs a) {
   const int32_t items = a.nportions * (a.N - 1);
   for (int32_t w = blockIdx.x; w < items; w += gridDim.x) phase2_item<ES>(a, w / (a.N - 1), item_peer(a, w));
 }
@@ -379,7 +380,7 @@ __global__ __launch_bounds__(kThreads) void ipc_phase2_kernel(IpcArgs a) {
 // (remote) pushers and phase-2 workgroups only on (remote) reducers -- every
 // role depends on roles with lower ids only.
 template <typename T>
-__global__ __launch_bounds__(kThreads) void ipc_fused_kernel(IpcArgs a, int32_t gp, int32_t gr) {
+__global__ __launch_bounds__(kMaxThreads) void ipc_fused_kernel(IpcArgs a, int32_t gp, int32_t gr) {
   constexpr int ES = sizeof(T);
   const int32_t b = blockIdx.x;
   if (b < gp) {
@@ -398,7 +399,10 @@ __global__ __launch_bounds__(kThreads) void ipc_fused_kernel(IpcArgs a, int32_t 
 template <typename T>
 void launch_round(hipStream_t s, const IpcArgs& a) {
   constexpr int ES = sizeof(T);
-  const int32_t cap = a.max_wgs > 0 ? a.max_wgs : 1024;
+  // workgroup size and the waiting kernels' grid cap (given in 256-thread
+  // workgroups: the cap bounds parked WAVES, whatever the workgroup size)
+  const int32_t nt = (a.threads == 512 || a.threads == 1024) ? a.threads : kThreads;
+  const int32_t cap = std::max(1, (a.max_wgs > 0 ? a.max_wgs : 1024) * kThreads / nt);
   const int32_t push_items = a.nportions * (a.N - 1), red_items = a.nportions * kReduceSplit;
   if (a.fused) {
     // one grid of <= cap workgroups split over the roles by their work
@@ -407,12 +411,12 @@ void launch_round(hipStream_t s, const IpcArgs& a) {
     const int32_t gp = std::max(1, int32_t(int64_t(budget) * push_items / total));
     const int32_t gr = std::max(1, int32_t(int64_t(budget) * red_items / total));
     const int32_t gq = std::max(1, budget - gp - gr);
-    hipLaunchKernelGGL(ipc_fused_kernel<T>, dim3(unsigned(gp + gr + gq)), dim3(kThreads), 0, s, a, gp, gr);
+    hipLaunchKernelGGL(ipc_fused_kernel<T>, dim3(unsigned(gp + gr + gq)), dim3(unsigned(nt)), 0, s, a, gp, gr);
     return;
   }
-  hipLaunchKernelGGL(ipc_push_kernel<ES>, dim3(unsigned(push_items)), dim3(kThreads), 0, s, a);
-  hipLaunchKernelGGL(ipc_reduce_kernel<T>, dim3(unsigned(std::min(red_items, cap))), dim3(kThreads), 0, s, a);
-  hipLaunchKernelGGL(ipc_phase2_kernel<ES>, dim3(unsigned(std::min(push_items, cap))), dim3(kThreads), 0, s, a);
+  hipLaunchKernelGGL(ipc_push_kernel<ES>, dim3(unsigned(push_items)), dim3(unsigned(nt)), 0, s, a);
+  hipLaunchKernelGGL(ipc_reduce_kernel<T>, dim3(unsigned(std::min(red_items, cap))), dim3(unsigned(nt)), 0, s, a);
+  hipLaunchKernelGGL(ipc_phase2_kernel<ES>, dim3(unsigned(std::min(push_items, cap))), dim3(unsigned(nt)), 0, s, a);
 }
 
 // Like wait_flag, but also gives up when the host marked `peer` dead.

@@ -47,6 +47,7 @@ struct IpcArgs {
   int32_t bcast = 0;  // phase 2: 0 = every rank pulls the reduced rows, 1 = the reducer pushes them
   int32_t fused = 0;  // 1: push, reduce and phase 2 as roles of ONE launch (pipelined by portion)
   int32_t N = 0, me = 0;
+  int32_t threads = 256;    // workgroup size of the round's kernels (256 / 512 / 1024)
   uint32_t round = 0;       // this round's id (1, 2, ... identical on every rank)
   uint64_t timeout = 0;     // per wait, in wall-clock ticks (100 MHz)
   const char* in = nullptr;  // round input [S]

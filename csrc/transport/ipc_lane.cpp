@@ -100,6 +100,8 @@ IpcLane::IpcLane(Device* dev, const Geometry& g, int32_t me, DType dt)
   if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev_->device_index()) != hipSuccess || khz <= 0)
     khz = 100000;  // 100 MHz
   timeout_ticks_ = uint64_t(std::max<int64_t>(1, env_i64("AKKA_IPC_TIMEOUT_MS", 10000))) * uint64_t(khz);
+  threads_ = int32_t(env_i64("AKKA_IPC_THREADS", 256));
+  if (threads_ != 512 && threads_ != 1024) threads_ = 256;
   peer_data_.assign(size_t(g_.N), nullptr);
   peer_gdata_.assign(size_t(g_.N), nullptr);
   peer_flags_.assign(size_t(g_.N), nullptr);
@@ -190,6 +192,7 @@ void IpcLane::round(StreamH s, const void* in, void* out) {
   a.portion = portion_;
   a.nportions = nportions_;
   a.max_wgs = max_wgs_;
+  a.threads = threads_;
   a.bcast = bcast_ ? 1 : 0;
   a.fused = fused_ ? 1 : 0;
   a.N = g_.N;

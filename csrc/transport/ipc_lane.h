@@ -68,6 +68,11 @@ class IpcLane {
   // portion) instead of three kernels.
   void set_fused(bool on) { fused_ = on; }
   bool fused() const { return fused_; }
+  // Workgroup size of the round kernels (256 / 512 / 1024; default
+  // AKKA_IPC_THREADS or 256).  Larger groups keep more loads / stores in
+  // flight per CU when one rank has the GPU to itself.
+  void set_threads(int32_t t) { threads_ = (t == 512 || t == 1024) ? t : 256; }
+  int32_t threads() const { return threads_; }
   // Enqueue one exact round on `s`: in[S] from every rank summed into out[S].
   void round(StreamH s, const void* in, void* out);
   // The error word (a wait timed out): error() after draining the device,
@@ -101,6 +106,7 @@ class IpcLane {
   std::vector<uint32_t*> peer_flags_; // [N]
   uint32_t round_ = 0;
   int32_t max_wgs_ = 1024, sharers_ = 1;
+  int32_t threads_ = 256;  // workgroup size of the round kernels (AKKA_IPC_THREADS)
   uint64_t timeout_ticks_ = 0;
   bool ready_ = false;
   bool bcast_ = false, fused_ = false;

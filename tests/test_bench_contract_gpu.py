@@ -79,8 +79,9 @@ def test_bench_multirank_on_one_card(plane):
     assert all(sel[k]["exact"] is True for k in cands), sel
     assert d["lane"] == sel["chosen"]
     if plane == "ipc_p2p":
-        assert {"collective", "p2p", "p2p_block", "ipc", "ipc_bcast", "ipc_fused", "ipc_fused_bcast"} <= set(cands)
+        assert {"collective", "p2p", "p2p_block", "ipc", "ipc_bcast", "ipc_fused", "ipc_fused_bcast", "ipc_wide",
+                "ipc_bcast_wide"} <= set(cands)
         c4 = d["extra_configs"]["cfg4_threshold_straggler"]
         assert c4["fast_rank_ms_per_round_with_straggler"] < c4["straggler_ms_per_round_with_straggler"], c4
     else:
-        assert set(cands) == {"ipc", "ipc_bcast", "ipc_fused", "ipc_fused_bcast"}
+        assert set(cands) == {"ipc", "ipc_bcast", "ipc_fused", "ipc_fused_bcast", "ipc_wide", "ipc_bcast_wide"}

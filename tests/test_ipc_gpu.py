@@ -115,3 +115,20 @@ def test_ipc_window_too_large_for_one_mapping_fails_fast():
     r, rows = _run(2, "--size", str(360_000_000), "--rounds", "1", timeout=150)
     assert r.returncode != 0 and not rows
     assert "exceeds the 1920 MiB an IPC mapping is known to open" in r.stderr, r.stderr[-2000:]
+
+
+@pytest.mark.parametrize("threads", [512, 1024])
+@pytest.mark.parametrize("n,size,dtype,mode", [
+    (2, 1 << 20, "float32", "rotate"),       # even blocks, all four variants round by round
+    (3, 1 << 20, "float32", "alternate"),    # uneven blocks: scalar paths, pull / bcast
+    (2, 3 * (1 << 18) + 8, "bfloat16", "pull"),
+    (4, 1 << 24, "float32", "rotate"),       # many portions, grid cap in waves
+])
+def test_ipc_lane_wide_workgroups(threads, n, size, dtype, mode):
+    """AKKA_IPC_THREADS / set_ipc_mode(threads=...): the round kernels with
+    512- or 1024-thread workgroups give the same bitwise sums."""
+    r, rows = _run(n, "--size", str(size), "--dtype", dtype, "--mode", mode, "--rounds", "4",
+                   env={"AKKA_IPC_THREADS": str(threads)})
+    assert r.returncode == 0 and len(rows) == n, r.stderr[-3000:]
+    for d in rows:
+        assert all(d["exact"]) and d["ipc_error"] == 0, d
