@@ -230,3 +230,47 @@ def test_fast_path_offstream_read_is_flagged():
     rows = _run_fast(2, "p2p", "offstream")
     assert all(d["races"] > 0 for d in rows), rows
     assert any("caller.read" in m for d in rows for m in d["reports"])
+
+
+_UNIT = r'''
+import json, sys
+sys.path.insert(0, {root!r})
+import torch
+from akka_allreduce_amd.parallel.sim import SimCluster
+
+c = SimCluster(2, 64, 8)
+core = c.workers[0]._core
+a, b = core.create_stream(), core.create_stream()
+buf = torch.zeros(1024)
+p = buf.data_ptr()
+res = {{}}
+def count():
+    return core.race_count()
+core.declare_access(a, p, 64, True, "w1"); core.declare_access(a, p, 64, True, "w2")
+res["same_stream_ww"] = count()
+core.declare_access(a, p + 128, 64, False, "r1"); core.declare_access(b, p + 128, 64, False, "r2")
+res["two_streams_rr"] = count()
+core.declare_access(b, p, 32, True, "w3")
+res["two_streams_ww"] = count()
+core.sync_stream(a); core.sync_stream(b)
+core.declare_access(a, p, 64, True, "w4")
+res["after_host_sync"] = count()
+core.declare_access(b, p + 256, 64, True, "w5"); core.declare_access(a, p + 300, 8, False, "r3")
+res["partial_overlap_wr"] = count()
+print(json.dumps(res))
+'''
+
+
+def test_checker_unit_semantics():
+    """Same-stream order, read/read, unordered write/write, host-sync joins,
+    partial range overlap."""
+    import json
+
+    e = dict(os.environ)
+    e["AKKA_RACECHECK"] = "1"
+    r = subprocess.run([sys.executable, "-c", _UNIT.format(root=ROOT)], capture_output=True, text=True,
+                       timeout=120, env=e, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d == {"same_stream_ww": 0, "two_streams_rr": 0, "two_streams_ww": 1, "after_host_sync": 1,
+                 "partial_overlap_wr": 2}, d
