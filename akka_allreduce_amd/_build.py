@@ -34,11 +34,13 @@ HOST_SOURCES = [
     "transport/rccl_p2p.cpp",
     "transport/ipc_lane.cpp",
     "transport/ipc_p2p.cpp",
+    "transport/onesided.cpp",
     "kernels/hip_device.cpp",
     "runtime/watchdog.cpp",
     "bindings/bindings.cpp",
+    "bindings/bind_onesided.cpp",
 ]
-HIP_SOURCES = ["kernels/kernels.hip", "kernels/ipc.hip"]
+HIP_SOURCES = ["kernels/kernels.hip", "kernels/ipc.hip", "kernels/onesided.hip"]
 
 
 def ext_path() -> str:

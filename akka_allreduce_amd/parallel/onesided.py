@@ -1,0 +1,208 @@
+"""One-sided threshold allreduce: fast ranks never wait for a straggler.
+
+``OneSidedAllreduce`` runs the reference's threshold semantics on the
+one-sided lane (csrc/transport/onesided.h, protocol in
+csrc/kernels/onesided_protocol.h): every rank exports a window, peers STORE
+their scatter chunks and reduced chunks into it, and every send is
+fire-and-forget like an Akka ``!`` (AllreduceWorker.scala:227-232, 259-264).
+
+Per call (one round of this rank):
+
+* the round is the rank's next one, unless a peer already pushed a round
+  more than ``max_lag`` ahead -- then the call catches up to the oldest round
+  still inside the window (W:100-106, implicit start W:164-167);
+* each chunk of my block is reduced once floor(thReduce * N) copies landed,
+  over exactly the landed set, count = popcount (SB:9-13, SB:20-32);
+* the round completes once floor(thComplete * total) reduced chunks landed;
+  the others are 0 with count 0 (RB:13-17, RB:26-53, RB:60-66);
+* pushes the receiver can no longer use (it already reduced that chunk or
+  completed that round) are dropped by the sender (W:155-156, W:172-173).
+
+``out.iteration`` is the round the call served (resolved lazily on the GPU:
+reading it waits for the call); ``stats()`` counts drops, forced reduces /
+completions, catch-up skips.  GPU ranks (one per MI355X) map each other's
+windows through IPC handles; CPU ranks use POSIX shared memory -- the same
+protocol code, so multi-process CPU tests cover the GPU's decisions.
+
+Usage::
+
+    ar = OneSidedAllreduce(n, max_chunk_size=1 << 20, th_reduce=0.75, th_complete=0.75, max_lag=1)
+    out = ar(x)          # AllReduceOutput; out.count / out.mean() as usual
+"""
+from __future__ import annotations
+
+import os
+from typing import Any, Optional
+
+import torch
+
+from .._native_loader import load as _load
+from ..data import AllReduceOutput, Geometry
+from .collective import _handle_exchange, env_rank_world
+
+_DTYPES = {torch.float32: "float32", torch.bfloat16: "bfloat16"}
+
+
+class OneSidedOutput(AllReduceOutput):
+    """AllReduceOutput whose ``iteration`` (the round served) and ``status``
+    come from the lane's per-call record; on the GPU reading them waits for
+    the call's kernels."""
+
+    __slots__ = ("_lane", "_slot", "_stream", "_status")
+
+    def __init__(self, data, *, lane, slot, stream, **kw):
+        self._lane = lane
+        self._slot = slot
+        self._stream = stream
+        self._status = None
+        super().__init__(data, **kw)
+
+    @property
+    def iteration(self) -> int:  # type: ignore[override]
+        return int(self.status["round"])
+
+    @iteration.setter
+    def iteration(self, v) -> None:  # the base constructor's placeholder
+        pass
+
+    @property
+    def status(self) -> dict:
+        if self._status is None:
+            if self._stream is not None:
+                self._stream.synchronize()
+            st = self._lane.status(self._slot)
+            if st["round"] < 0:
+                raise RuntimeError("onesided call has not finished (or its status slot was reused)")
+            self._status = st
+        return self._status
+
+
+class OneSidedAllreduce:
+    """Threshold allreduce over mapped peer windows (see module docstring)."""
+
+    _instances = 0
+
+    def __init__(
+        self,
+        data_size: int,
+        *,
+        max_chunk_size: int = 1 << 20,
+        dtype: torch.dtype = torch.float32,
+        th_reduce: float = 1.0,
+        th_complete: float = 1.0,
+        max_lag: int = 1,
+        rank: Optional[int] = None,
+        world_size: Optional[int] = None,
+        device: Optional[torch.device] = None,
+        store: Any = None,
+        rows: int = 0,
+        part_bytes: int = 256 << 10,
+        timeout_s: float = 30.0,
+        threads: int = 256,
+        data_sink: Any = None,
+    ):
+        if dtype not in _DTYPES:
+            raise ValueError("dtype must be float32 or bfloat16")
+        r, w, local = env_rank_world()
+        import torch.distributed as dist
+
+        if dist.is_available() and dist.is_initialized():
+            r, w = dist.get_rank(), dist.get_world_size()
+            local = int(os.environ.get("LOCAL_RANK", str(r)))
+        self.rank = r if rank is None else int(rank)
+        self.world_size = w if world_size is None else int(world_size)
+        if self.world_size < 2:
+            raise ValueError("the onesided lane needs N >= 2 ranks")
+        if device is None:
+            device = torch.device("cuda", local % max(1, torch.cuda.device_count())) if torch.cuda.is_available() \
+                else torch.device("cpu")
+        self.device = torch.device(device)
+        if self.device.type == "cuda":
+            torch.cuda.set_device(self.device)
+        self.dtype = dtype
+        self.data_size = int(data_size)
+        self.geometry = Geometry(self.data_size, self.world_size, int(max_chunk_size))
+        self.data_sink = data_sink
+        n = _load()
+        dev_index = self.device.index if self.device.type == "cuda" else -1
+        if dev_index is None:
+            dev_index = torch.cuda.current_device()
+        self.lane = n.OneSidedLane(dev_index, self.data_size, self.world_size, int(max_chunk_size), self.rank,
+                                   _DTYPES[dtype], th_reduce=float(th_reduce), th_complete=float(th_complete),
+                                   max_lag=int(max_lag), rows=int(rows), part_bytes=int(part_bytes),
+                                   timeout_ms=int(timeout_s * 1000), threads=int(threads))
+        self.th_reduce, self.th_complete, self.max_lag = float(th_reduce), float(th_complete), int(max_lag)
+        iid = OneSidedAllreduce._instances
+        OneSidedAllreduce._instances += 1
+        exchange = _handle_exchange(self.rank, self.world_size, store, f"akka/onesided/{iid}")
+        handles = exchange(self.lane.handle())
+        self.lane.open(handles)
+        # every rank mapped every window: names may go (a killed rank leaves no shm behind)
+        exchange_done = _handle_exchange(self.rank, self.world_size, store, f"akka/onesided/{iid}/opened")
+        exchange_done(b"1")
+        self.lane.unlink()
+        self._kmax = self.geometry.kmax
+        self.calls = 0
+
+    def __call__(self, x: torch.Tensor, out: Optional[torch.Tensor] = None, async_op: bool = False) -> OneSidedOutput:
+        """One round of this rank.  GPU: enqueued on the current stream (the
+        output is valid in its order; ``async_op`` is accepted for API parity).
+        CPU: returns after the round completed."""
+        if x.numel() != self.data_size:
+            raise ValueError(f"expected {self.data_size} elements, got {x.numel()}")
+        if x.dtype != self.dtype or x.device != self.device:
+            x = x.to(device=self.device, dtype=self.dtype)
+        x = x.reshape(-1).contiguous()
+        if out is None:
+            out = torch.empty_like(x)
+        elif out.numel() != self.data_size or out.dtype != self.dtype or not out.is_contiguous():
+            raise ValueError("out must be a contiguous tensor of the buffer's size and dtype")
+        counts = torch.empty((self.world_size, self._kmax), dtype=torch.int32, device=self.device)
+        stream = torch.cuda.current_stream(self.device) if self.device.type == "cuda" else None
+        slot = self.lane.round(stream.cuda_stream if stream is not None else 0, x.data_ptr(), out.data_ptr(),
+                               counts.data_ptr(), self._kmax)
+        self.calls += 1
+        o = OneSidedOutput(out.view(-1), lane=self.lane, slot=slot, stream=stream, counts_per_chunk=counts,
+                           geometry=self.geometry, expander=self._expand if stream is not None else None)
+        if self.data_sink is not None:
+            self.data_sink(o)
+        return o
+
+    def _expand(self, per_chunk: torch.Tensor) -> torch.Tensor:
+        g = self.geometry
+        out = torch.empty(g.dataSize, dtype=torch.int32, device=per_chunk.device)
+        _load().count_expand(out.data_ptr(), per_chunk.contiguous().data_ptr(), g.dataSize, g.step, g.workerNum,
+                             g.maxChunkSize, g.kmax, torch.cuda.current_stream(per_chunk.device).cuda_stream)
+        return out
+
+    # ---- control / observability ------------------------------------------------
+    def stats(self) -> dict:
+        """Lane counters (GPU: synchronises the device)."""
+        return dict(self.lane.stats())
+
+    def info(self) -> dict:
+        return dict(self.lane.info())
+
+    def error(self) -> int:
+        """Non-zero once a bounded wait expired (that round was forced; its
+        counts are still honest)."""
+        return int(self.lane.error())
+
+    def mark_dead(self, peer: int, dead: bool = True) -> None:
+        """Never wait for (nor write to) ``peer`` again -- e.g. on the master's
+        WorkerTerminated (M:46-52)."""
+        self.lane.set_dead(int(peer), bool(dead))
+
+    def force_below(self, round_plus_one: int) -> None:
+        """Force every round < ``round_plus_one`` (waits end with what landed)."""
+        self.lane.force_below(int(round_plus_one))
+
+    def retire(self) -> None:
+        """This rank serves no further round: peers stop waiting for its
+        copies of later rounds (the job's end, like the master's maxRound)."""
+        stream = torch.cuda.current_stream(self.device).cuda_stream if self.device.type == "cuda" else 0
+        self.lane.retire(stream)
+
+    def synchronize(self) -> None:
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)

@@ -1,0 +1,135 @@
+// Bindings of the one-sided threshold lane (transport/onesided.h).
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "../transport/onesided.h"
+
+namespace py = pybind11;
+
+namespace akka {
+
+namespace {
+const char* kStatNames[] = {
+    "rounds",           "skipped_rounds",     "scatter_pushed",  "scatter_outdated", "scatter_conflict",
+    "gather_pushed",    "gather_outdated",    "gather_conflict", "reduce_threshold", "reduce_forced",
+    "complete_threshold", "complete_forced",  "timeouts",        "landed_chunks",    "missing_chunks",
+    "dead_skips",       "reduce_contribs",
+};
+const char* kReasons[] = {"wait", "threshold", "unreachable", "catch_up", "host_force", "timeout"};
+}  // namespace
+
+void bind_onesided(py::module_& m) {
+  py::class_<OneSidedLane>(m, "OneSidedLane")
+      .def(py::init([](int32_t device, int64_t S, int32_t N, int64_t C, int32_t me, const std::string& dtype,
+                       float th_reduce, float th_complete, int32_t max_lag, int32_t rows, int64_t part_bytes,
+                       int64_t timeout_ms, int32_t threads) {
+             OneSidedParams p;
+             p.th_reduce = th_reduce;
+             p.th_complete = th_complete;
+             p.max_lag = max_lag;
+             p.rows = rows;
+             p.part_bytes = part_bytes;
+             p.timeout_ms = timeout_ms;
+             p.threads = threads;
+             const DType dt = (dtype == "bfloat16" || dtype == "bf16") ? DType::BF16 : DType::F32;
+             return std::make_unique<OneSidedLane>(device, S, N, C, me, dt, p);
+           }),
+           py::arg("device"), py::arg("S"), py::arg("N"), py::arg("C"), py::arg("me"), py::arg("dtype") = "float32",
+           py::arg("th_reduce") = 1.f, py::arg("th_complete") = 1.f, py::arg("max_lag") = 1, py::arg("rows") = 0,
+           py::arg("part_bytes") = int64_t(256) << 10, py::arg("timeout_ms") = 30000, py::arg("threads") = 256)
+      .def("handle", [](const OneSidedLane& l) { return py::bytes(l.handle()); })
+      .def("open", [](OneSidedLane& l, std::vector<std::string> handles) {
+        py::gil_scoped_release nogil;
+        l.open(handles);
+      })
+      .def("unlink", &OneSidedLane::unlink)
+      .def("round",
+           [](OneSidedLane& l, uintptr_t stream, uintptr_t in, uintptr_t out, uintptr_t counts, int32_t kcols) {
+             py::gil_scoped_release nogil;  // the CPU backend waits for other processes
+             return l.round(stream, reinterpret_cast<const void*>(in), reinterpret_cast<void*>(out),
+                            reinterpret_cast<int32_t*>(counts), kcols);
+           })
+      .def("status",
+           [](const OneSidedLane& l, int32_t slot) {
+             const os::CallStatus c = l.status(slot);
+             py::dict d;
+             d["round"] = c.round;
+             d["reason"] = c.round >= 0 && c.reason >= 0 && c.reason < 6 ? kReasons[c.reason] : "pending";
+             d["landed_chunks"] = c.landed_chunks;
+             d["forced_chunks"] = c.forced_chunks;
+             return d;
+           })
+      .def("stats",
+           [](OneSidedLane& l) {
+             std::vector<uint64_t> v;
+             {
+               py::gil_scoped_release nogil;
+               v = l.stats();
+             }
+             py::dict d;
+             for (size_t i = 0; i < sizeof(kStatNames) / sizeof(kStatNames[0]); ++i) d[kStatNames[i]] = v[i];
+             return d;
+           })
+      .def("error", &OneSidedLane::error)
+      .def("clear_error", &OneSidedLane::clear_error)
+      .def("set_dead", &OneSidedLane::set_dead)
+      .def("force_below", &OneSidedLane::force_below)
+      .def("retire", &OneSidedLane::retire, py::arg("stream") = 0)
+      .def("info", [](const OneSidedLane& l) {
+        py::dict d;
+        d["backend"] = l.on_gpu() ? "gpu" : "cpu";
+        d["rows"] = l.rows();
+        d["parts"] = l.parts();
+        d["part_elems"] = l.part_elems();
+        d["need_reduce"] = l.need_reduce();
+        d["need_complete"] = l.need_complete();
+        d["window_bytes"] = int64_t(l.window_bytes());
+        d["memory"] = l.memory_kind();
+        d["calls"] = l.calls();
+        d["total_chunks"] = l.geometry().total_chunks();
+        return d;
+      });
+  m.def("onesided_layout", [](int32_t N, int32_t D, int32_t Kmax, int32_t P) {
+    // every exported / local word index of the layout (CPU test: disjoint, in range)
+    os::Layout L;
+    L.init(N, D, Kmax, P);
+    std::vector<int64_t> exported, local;
+    for (int32_t d = 0; d < D; ++d)
+      for (int32_t s = 0; s < N; ++s)
+        for (int32_t k = 0; k < Kmax; ++k)
+          for (int32_t j = 0; j < P; ++j) {
+            exported.push_back(L.stag(d, s, k, j));
+            exported.push_back(L.stag(d, s, k, j) + 1);
+            exported.push_back(L.gtag(d, s, k, j));
+            exported.push_back(L.gtag(d, s, k, j) + 1);
+          }
+    for (int32_t d = 0; d < D; ++d) {
+      for (int32_t k = 0; k < Kmax; ++k) {
+        exported.push_back(L.fired(d, k));
+        exported.push_back(L.sread(d, k));
+        local.push_back(L.dec(d, k));
+        local.push_back(L.dec(d, k) + 1);
+      }
+      exported.push_back(L.gread(d));
+    }
+    exported.push_back(L.done());
+    for (int32_t s = 0; s < N; ++s) {
+      exported.push_back(L.seen(s));
+      exported.push_back(L.fin(s));
+    }
+    for (int32_t b = 0; b < N; ++b)
+      for (int32_t k = 0; k < Kmax; ++k) local.push_back(L.cmask(b, k));
+    for (int32_t i = 0; i < os::Layout::kStateWords; ++i) local.push_back(L.state(i));
+    py::dict r;
+    r["exported"] = exported;
+    r["local"] = local;
+    r["flag_words"] = L.flag_words;
+    r["local_words"] = L.local_words;
+    return r;
+  });
+  m.def("onesided_rules", [](uint32_t t, uint32_t r) { return os::tag_state(t, r); });
+  m.def("onesided_evaluate", &os::evaluate);
+  m.def("onesided_select_round", &os::select_round);
+}
+
+}  // namespace akka

@@ -33,6 +33,7 @@ using namespace akka;
 
 namespace akka {
 bool host_device_step(Device* d, uint32_t rotate);  // host_device.cpp
+void bind_onesided(py::module_& m);                 // bind_onesided.cpp
 }
 
 namespace {
@@ -582,6 +583,7 @@ hipStream_t as_stream(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
 PYBIND11_MODULE(_native, m) {
   m.doc() = "MI355X-native threshold allreduce core (engine, gfx950 kernels, RCCL/xGMI transport)";
   py::register_exception<AkkaError>(m, "AkkaError", PyExc_RuntimeError);
+  bind_onesided(m);
 
   py::class_<OutMsg>(m, "OutMsg")
       .def_readonly("kind", &OutMsg::kind)

@@ -20,20 +20,15 @@
 #include <algorithm>
 
 #include "ipc_kernels.h"
+#include "xgmi_device.h"
 
 namespace akka {
 namespace {
 
 constexpr int kThreads = 256;      // default workgroup size (AKKA_IPC_THREADS: 256 / 512 / 1024)
 constexpr int kMaxThreads = 1024;  // launch bound of the one-sided round kernels
-constexpr int kUnroll = 4;       // 16-B vectors per thread per source in flight
 constexpr int kReduceSplit = kIpcReduceSplit;
-
-__device__ inline bool reached(uint32_t v, uint32_t want) { return int32_t(v - want) >= 0; }
-
-__device__ inline uint32_t sys_load(uint32_t* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
+using namespace xgmi;
 
 // Lane 0 only.  true once *f reached `want`; false on timeout or when another
 // workgroup already reported one (err != 0).
@@ -52,150 +47,9 @@ __device__ bool wait_flag(uint32_t* f, uint32_t want, uint32_t* err, uint64_t de
   }
 }
 
-// Whole workgroup: make this workgroup's stores visible at system scope.
-// Lane 0 may then signal (flag stores).
-__device__ inline void release_wg() {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-}
 __device__ inline void signal(uint32_t* f, uint32_t v) {  // lane 0, after release_wg
   __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
-
-// Whole workgroup: acquire after lane 0's successful waits.  Returns the
-// shared verdict.
-__device__ inline bool acquire_all(bool ok_lane0) {
-  __shared__ int ok;
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    ok = ok_lane0 ? 1 : 0;
-  }
-  __syncthreads();
-  return ok != 0;
-}
-
-__device__ void copy_bytes(char* __restrict__ dst, const char* __restrict__ src, int64_t bytes) {
-  if (((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src) | uintptr_t(bytes)) & 15) == 0) {
-    const uint4* s = reinterpret_cast<const uint4*>(src);
-    uint4* d = reinterpret_cast<uint4*>(dst);
-    const int64_t n = bytes >> 4;
-    int64_t i = threadIdx.x;
-    for (; i + (kUnroll - 1) * int(blockDim.x) < n; i += kUnroll * int(blockDim.x)) {
-      uint4 v[kUnroll];
-#pragma unroll
-      for (int u = 0; u < kUnroll; ++u) v[u] = s[i + u * int(blockDim.x)];
-#pragma unroll
-      for (int u = 0; u < kUnroll; ++u) d[i + u * int(blockDim.x)] = v[u];
-    }
-    for (; i < n; i += int(blockDim.x)) d[i] = s[i];
-  } else if (((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src) | uintptr_t(bytes)) & 3) == 0) {
-    const uint32_t* s = reinterpret_cast<const uint32_t*>(src);
-    uint32_t* d = reinterpret_cast<uint32_t*>(dst);
-    for (int64_t i = threadIdx.x; i < (bytes >> 2); i += int(blockDim.x)) d[i] = s[i];
-  } else {
-    for (int64_t i = threadIdx.x; i < bytes; i += int(blockDim.x)) dst[i] = src[i];
-  }
-}
-
-// ---- reads of window memory another rank wrote ------------------------------
-// Every byte a peer stored into a window (slots, reduced rows, gather rows,
-// mailboxes) is read with system-coherent buffer loads (sc0 sc1: L1 and L2
-// bypassed), so no line cached from an earlier round can be returned -- the
-// consumer side of the hand-off is correct whatever caching policy the
-// window's memory has on this or the peer GPU.  Buffer loads also bound every
-// read by the span's size (out-of-range reads return 0).
-constexpr int kSysAux = 17;  // sc0 | sc1
-
-__device__ inline __amdgpu_buffer_rsrc_t sys_rsrc(const void* base, int64_t bytes) {
-  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), 0, int(min(bytes, int64_t(0x7fffffff))),
-                                           0x00020000);
-}
-__device__ inline uint4 load_sys16(__amdgpu_buffer_rsrc_t r, int64_t off) {
-  const auto v = __builtin_amdgcn_raw_buffer_load_b128(r, int(off), 0, kSysAux);
-  return make_uint4(v[0], v[1], v[2], v[3]);
-}
-
-// dst (local, plain stores) <- src (window memory written by a peer).
-__device__ void copy_in(char* __restrict__ dst, const char* __restrict__ src, int64_t bytes) {
-  const auto r = sys_rsrc(src, bytes);
-  if (((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src) | uintptr_t(bytes)) & 15) == 0) {
-    uint4* d = reinterpret_cast<uint4*>(dst);
-    const int64_t n = bytes >> 4;
-    int64_t i = threadIdx.x;
-    for (; i + (kUnroll - 1) * int(blockDim.x) < n; i += kUnroll * int(blockDim.x)) {
-      uint4 v[kUnroll];
-#pragma unroll
-      for (int u = 0; u < kUnroll; ++u) v[u] = load_sys16(r, (i + u * int(blockDim.x)) * 16);
-#pragma unroll
-      for (int u = 0; u < kUnroll; ++u) d[i + u * int(blockDim.x)] = v[u];
-    }
-    for (; i < n; i += int(blockDim.x)) d[i] = load_sys16(r, i * 16);
-  } else if (((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src) | uintptr_t(bytes)) & 3) == 0) {
-    uint32_t* d = reinterpret_cast<uint32_t*>(dst);
-    for (int64_t i = threadIdx.x; i < (bytes >> 2); i += int(blockDim.x))
-      d[i] = __builtin_amdgcn_raw_buffer_load_b32(r, int(i * 4), 0, kSysAux);
-  } else {
-    for (int64_t i = threadIdx.x; i < bytes; i += int(blockDim.x))
-      dst[i] = char(__builtin_amdgcn_raw_buffer_load_b8(r, int(i), 0, kSysAux));
-  }
-}
-
-__device__ inline float bf16_to_f32(uint16_t h) { return __uint_as_float(uint32_t(h) << 16); }
-__device__ inline uint16_t f32_to_bf16(float f) {
-  const uint32_t u = __float_as_uint(f);
-  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x007fffffu)) return uint16_t((u >> 16) | 0x40);  // quiet NaN
-  return uint16_t((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
-}
-
-template <typename T>
-struct Elt;
-template <>
-struct Elt<float> {
-  static constexpr int kPerVec = 4;
-  __device__ static void add(float* acc, const uint4& v) {
-    acc[0] += __uint_as_float(v.x);
-    acc[1] += __uint_as_float(v.y);
-    acc[2] += __uint_as_float(v.z);
-    acc[3] += __uint_as_float(v.w);
-  }
-  __device__ static uint4 pack(const float* acc) {
-    return make_uint4(__float_as_uint(acc[0]), __float_as_uint(acc[1]), __float_as_uint(acc[2]),
-                      __float_as_uint(acc[3]));
-  }
-  __device__ static float load1(const char* p) { return *reinterpret_cast<const float*>(p); }
-  __device__ static float load1_sys(__amdgpu_buffer_rsrc_t r, int64_t off) {
-    return __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, int(off), 0, kSysAux));
-  }
-  __device__ static void store1(char* p, float v) { *reinterpret_cast<float*>(p) = v; }
-};
-template <>
-struct Elt<uint16_t> {
-  static constexpr int kPerVec = 8;
-  __device__ static void add(float* acc, const uint4& v) {
-    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      acc[2 * i] += __uint_as_float(w[i] << 16);
-      acc[2 * i + 1] += __uint_as_float(w[i] & 0xffff0000u);
-    }
-  }
-  __device__ static uint4 pack(const float* acc) {
-    uint32_t w[4];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) w[i] = uint32_t(f32_to_bf16(acc[2 * i])) | (uint32_t(f32_to_bf16(acc[2 * i + 1])) << 16);
-    return make_uint4(w[0], w[1], w[2], w[3]);
-  }
-  __device__ static float load1(const char* p) { return bf16_to_f32(*reinterpret_cast<const uint16_t*>(p)); }
-  __device__ static float load1_sys(__amdgpu_buffer_rsrc_t r, int64_t off) {
-    return bf16_to_f32(uint16_t(__builtin_amdgcn_raw_buffer_load_b16(r, int(off), 0, kSysAux)));
-  }
-  __device__ static void store1(char* p, float v) { *reinterpret_cast<uint16_t*>(p) = f32_to_bf16(v); }
-};
 
 // Sum of the N sources of `n` elements, ascending source rank (source `me`
 // is the round input, the others are window slots), to `o`, to `r` (pull

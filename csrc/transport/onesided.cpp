@@ -1,0 +1,636 @@
+// OneSidedLane host side (onesided.h): windows, handle exchange, the GPU
+// launch and the CPU backend.  The CPU backend runs the kernels' roles in the
+// same order, calling the same protocol functions (onesided_protocol.h) on
+// POSIX shared memory; only the byte movement is written twice.
+#include "onesided.h"
+
+#include <fcntl.h>
+#include <hip/hip_runtime.h>
+#include <sys/mman.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <random>
+#include <thread>
+
+#include "../kernels/onesided_kernels.h"
+#include "ipc_lane.h"
+
+namespace akka {
+
+using namespace os;
+
+#define AKKA_OS_HIP(call)                                                                      \
+  do {                                                                                         \
+    hipError_t e_ = (call);                                                                    \
+    if (e_ != hipSuccess)                                                                      \
+      throw AkkaError(std::string("akka onesided: ") + #call + " failed: " + hipGetErrorString(e_)); \
+  } while (0)
+
+namespace {
+
+constexpr char kMagic[8] = {'A', 'K', 'O', 'S', '0', '1', 0, 0};
+
+struct Blob {
+  char magic[8];
+  int32_t rank, nranks, esize, rows, parts, kmax, kind, pad;  // kind: 0 gpu, 1 cpu
+  int64_t S, C, slot, part_len, shm_bytes;
+  char bus[32];
+  char shm[64];
+  hipIpcMemHandle_t h[1 + 2 * kMaxRows];  // flags, SD rows, GD rows
+};
+
+// Memory policy of the protocol functions on the host (shared memory between
+// processes): C++ atomics; the announce / look pair is sequentially consistent.
+struct HostMem {
+  static uint32_t ld(const uint32_t* p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
+  static void st(uint32_t* p, uint32_t v) { __atomic_store_n(p, v, __ATOMIC_RELEASE); }
+  static void st_sc(uint32_t* p, uint32_t v) { __atomic_store_n(p, v, __ATOMIC_SEQ_CST); }
+  static uint32_t ld_sc(const uint32_t* p) { return __atomic_load_n(p, __ATOMIC_SEQ_CST); }
+};
+
+inline float bf16_f32(uint16_t h) {
+  uint32_t u = uint32_t(h) << 16;
+  float f;
+  std::memcpy(&f, &u, 4);
+  return f;
+}
+inline uint16_t f32_bf16(float f) {  // RNE, quiet NaN: the kernels' conversion
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x007fffffu)) return uint16_t((u >> 16) | 0x40);
+  return uint16_t((u + 0x7fffu + ((u >> 16) & 1u)) >> 16);
+}
+
+int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
+
+}  // namespace
+
+OneSidedLane::OneSidedLane(int32_t device, int64_t S, int32_t N, int64_t C, int32_t me, DType dt,
+                           const OneSidedParams& p)
+    : device_(device), g_(S, N, C), me_(me), dt_(dt), es_(dtype_size(dt)), p_(p) {
+  AKKA_CHECK(N >= 2 && N <= kMaxRanks, "onesided lane: 2..16 ranks");
+  AKKA_CHECK(me >= 0 && me < N, "onesided lane: rank out of range");
+  AKKA_CHECK(S >= 1, "onesided lane: empty buffer");
+  AKKA_CHECK(p.max_lag >= 0, "onesided lane: maxLag must be >= 0");
+  D_ = p.rows > 0 ? p.rows : std::max(3, p.max_lag + 2);
+  D_ = std::clamp(D_, 2, kMaxRows);
+  Kmax_ = std::max(1, g_.max_block_len_chunks());
+  // parts: the unit one workgroup moves under one tag (64-element multiples)
+  const int64_t want = std::max<int64_t>(64, p.part_bytes / int64_t(es_));
+  part_len_ = std::min(round_up(want, 64), round_up(C, 64));
+  P_ = int32_t((C + part_len_ - 1) / part_len_);
+  if (P_ > 64) {
+    part_len_ = round_up((C + 63) / 64, 64);
+    P_ = int32_t((C + part_len_ - 1) / part_len_);
+  }
+  slot_ = std::max<int64_t>(64, round_up(g_.max_block_len(), 64));
+  need_r_ = std::clamp(float_threshold(p.th_reduce, N), 1, N);
+  const int64_t total = g_.total_chunks();
+  need_c_ = int32_t(std::clamp<int64_t>(float_threshold(p.th_complete, total), 1, std::max<int64_t>(total, 1)));
+  AKKA_CHECK(int64_t(D_) * N * Kmax_ * P_ <= (int64_t(1) << 22),
+             "onesided lane: " + std::to_string(int64_t(D_) * N * Kmax_ * P_) +
+                 " chunk parts per ring -- use a larger max_chunk_size");
+  L_.init(N, D_, Kmax_, P_);
+  flag_bytes_ = size_t(L_.flag_words) * sizeof(uint32_t);
+  row_bytes_ = size_t(N) * size_t(slot_) * es_;
+  win_bytes_ = flag_bytes_ + 2 * size_t(D_) * row_bytes_;
+  sd_.assign(size_t(D_), nullptr);
+  gd_.assign(size_t(D_), nullptr);
+  pfl_.assign(size_t(N), nullptr);
+  psd_.assign(size_t(D_), std::vector<char*>(size_t(N), nullptr));
+  pgd_.assign(size_t(D_), std::vector<char*>(size_t(N), nullptr));
+
+  if (device_ >= 0) {
+    AKKA_OS_HIP(hipSetDevice(device_));
+    if (hipExtMallocWithFlags(reinterpret_cast<void**>(&flags_), flag_bytes_, hipDeviceMallocUncached) != hipSuccess) {
+      (void)hipGetLastError();
+      AKKA_OS_HIP(hipMalloc(reinterpret_cast<void**>(&flags_), flag_bytes_));
+    }
+    AKKA_OS_HIP(hipMemset(flags_, 0, flag_bytes_));
+    for (int32_t d = 0; d < D_; ++d) {
+      sd_[size_t(d)] = static_cast<char*>(ipc_alloc_window(row_bytes_, d == 0 ? &mem_kind_ : nullptr));
+      gd_[size_t(d)] = static_cast<char*>(ipc_alloc_window(row_bytes_, nullptr));
+    }
+    AKKA_OS_HIP(hipMalloc(reinterpret_cast<void**>(&loc_), size_t(L_.local_words) * sizeof(uint32_t)));
+    AKKA_OS_HIP(hipMemset(loc_, 0, size_t(L_.local_words) * sizeof(uint32_t)));
+    AKKA_OS_HIP(hipMalloc(reinterpret_cast<void**>(&stats_dev_), kNumStats * sizeof(unsigned long long)));
+    AKKA_OS_HIP(hipMemset(stats_dev_, 0, kNumStats * sizeof(unsigned long long)));
+    AKKA_OS_HIP(hipMalloc(&tab_dev_, sizeof(Tables)));
+    AKKA_OS_HIP(hipHostMalloc(reinterpret_cast<void**>(&hw_), sizeof(HostWords),
+                              hipHostMallocMapped | hipHostMallocCoherent));
+    std::memset(hw_, 0, sizeof(HostWords));
+    AKKA_OS_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&hw_dev_), hw_, 0));
+    AKKA_OS_HIP(hipDeviceSynchronize());
+    int khz = 0;
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device_) != hipSuccess || khz <= 0) khz = 100000;
+    timeout_ticks_ = uint64_t(std::max<int64_t>(1, p.timeout_ms)) * uint64_t(khz);
+  } else {
+    // one shared-memory segment: [flags | SD rows | GD rows]
+    const size_t fb = size_t(round_up(int64_t(flag_bytes_), 4096));
+    const size_t rb = size_t(round_up(int64_t(row_bytes_), 4096));
+    shm_bytes_ = fb + 2 * size_t(D_) * rb;
+    std::random_device rd;
+    char name[64];
+    std::snprintf(name, sizeof(name), "/akka_os_%d_%08x_r%d", int(getpid()), unsigned(rd()), int(me));
+    shm_name_ = name;
+    const int fd = shm_open(name, O_CREAT | O_EXCL | O_RDWR, 0600);
+    AKKA_CHECK(fd >= 0, "onesided lane: shm_open failed for " + shm_name_);
+    if (ftruncate(fd, off_t(shm_bytes_)) != 0) {
+      close(fd);
+      shm_unlink(name);
+      throw AkkaError("akka: onesided lane: ftruncate of the shared window failed");
+    }
+    void* m = mmap(nullptr, shm_bytes_, PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    if (m == MAP_FAILED) {
+      shm_unlink(name);
+      throw AkkaError("akka: onesided lane: mmap of the shared window failed");
+    }
+    shm_base_ = static_cast<char*>(m);  // zero-filled by ftruncate
+    flags_ = reinterpret_cast<uint32_t*>(shm_base_);
+    for (int32_t d = 0; d < D_; ++d) {
+      sd_[size_t(d)] = shm_base_ + fb + size_t(d) * rb;
+      gd_[size_t(d)] = shm_base_ + fb + size_t(D_ + d) * rb;
+    }
+    mem_kind_ = "shm";
+    loc_host_.assign(size_t(L_.local_words), 0u);
+    loc_ = loc_host_.data();
+    stats_host_.assign(kNumStats, 0ull);
+    hw_ = new HostWords();
+    std::memset(hw_, 0, sizeof(HostWords));
+    timeout_ticks_ = uint64_t(std::max<int64_t>(1, p.timeout_ms));  // milliseconds on the host
+  }
+  pfl_[size_t(me_)] = flags_;
+  for (int32_t d = 0; d < D_; ++d) {
+    psd_[size_t(d)][size_t(me_)] = sd_[size_t(d)];
+    pgd_[size_t(d)][size_t(me_)] = gd_[size_t(d)];
+  }
+}
+
+OneSidedLane::~OneSidedLane() {
+  if (device_ >= 0) {
+    hipSetDevice(device_);
+    hipDeviceSynchronize();  // none of our kernels may still touch a window
+    for (void* m : opened_) hipIpcCloseMemHandle(m);
+    for (char* p : sd_)
+      if (p) hipFree(p);
+    for (char* p : gd_)
+      if (p) hipFree(p);
+    if (flags_) hipFree(flags_);
+    if (loc_) hipFree(loc_);
+    if (stats_dev_) hipFree(stats_dev_);
+    if (tab_dev_) hipFree(tab_dev_);
+    if (hw_) hipHostFree(hw_);
+  } else {
+    for (auto& pm : peer_maps_) munmap(pm.first, pm.second);
+    if (shm_base_) munmap(shm_base_, shm_bytes_);
+    if (!unlinked_ && !shm_name_.empty()) shm_unlink(shm_name_.c_str());
+    delete hw_;
+  }
+}
+
+std::string OneSidedLane::handle() const {
+  Blob b;
+  std::memset(&b, 0, sizeof(b));
+  std::memcpy(b.magic, kMagic, sizeof(kMagic));
+  b.rank = me_;
+  b.nranks = g_.N;
+  b.esize = int32_t(es_);
+  b.rows = D_;
+  b.parts = P_;
+  b.kmax = Kmax_;
+  b.kind = device_ >= 0 ? 0 : 1;
+  b.S = g_.S;
+  b.C = g_.C;
+  b.slot = slot_;
+  b.part_len = part_len_;
+  b.shm_bytes = int64_t(shm_bytes_);
+  if (device_ >= 0) {
+    AKKA_OS_HIP(hipDeviceGetPCIBusId(b.bus, int(sizeof(b.bus)) - 1, device_));
+    AKKA_OS_HIP(hipIpcGetMemHandle(&b.h[0], flags_));
+    for (int32_t d = 0; d < D_; ++d) {
+      AKKA_OS_HIP(hipIpcGetMemHandle(&b.h[1 + d], sd_[size_t(d)]));
+      AKKA_OS_HIP(hipIpcGetMemHandle(&b.h[1 + D_ + d], gd_[size_t(d)]));
+    }
+  } else {
+    std::snprintf(b.shm, sizeof(b.shm), "%s", shm_name_.c_str());
+  }
+  return std::string(reinterpret_cast<const char*>(&b), sizeof(b));
+}
+
+void OneSidedLane::open(const std::vector<std::string>& handles) {
+  AKKA_CHECK(!ready_, "onesided lane: windows already open");
+  AKKA_CHECK(int32_t(handles.size()) == g_.N, "onesided lane: need one handle per rank");
+  if (device_ >= 0) AKKA_OS_HIP(hipSetDevice(device_));
+  const size_t fb = size_t(round_up(int64_t(flag_bytes_), 4096));
+  const size_t rb = size_t(round_up(int64_t(row_bytes_), 4096));
+  for (int32_t q = 0; q < g_.N; ++q) {
+    const std::string& h = handles[size_t(q)];
+    AKKA_CHECK(h.size() == sizeof(Blob), "onesided lane: malformed handle");
+    Blob b;
+    std::memcpy(&b, h.data(), sizeof(b));
+    AKKA_CHECK(std::memcmp(b.magic, kMagic, sizeof(kMagic)) == 0, "onesided lane: not a onesided window handle");
+    AKKA_CHECK(b.rank == q && b.nranks == g_.N && b.esize == int32_t(es_) && b.rows == D_ && b.parts == P_ &&
+                   b.kmax == Kmax_ && b.S == g_.S && b.C == g_.C && b.slot == slot_ && b.part_len == part_len_ &&
+                   b.kind == (device_ >= 0 ? 0 : 1),
+               "onesided lane: rank " + std::to_string(q) + "'s window was built for another geometry / ring");
+    if (q == me_) continue;
+    if (device_ >= 0) {
+      void* f = nullptr;
+      AKKA_OS_HIP(hipIpcOpenMemHandle(&f, b.h[0], hipIpcMemLazyEnablePeerAccess));
+      opened_.push_back(f);
+      pfl_[size_t(q)] = static_cast<uint32_t*>(f);
+      for (int32_t d = 0; d < D_; ++d) {
+        void* s = nullptr;
+        void* g = nullptr;
+        AKKA_OS_HIP(hipIpcOpenMemHandle(&s, b.h[1 + d], hipIpcMemLazyEnablePeerAccess));
+        opened_.push_back(s);
+        AKKA_OS_HIP(hipIpcOpenMemHandle(&g, b.h[1 + D_ + d], hipIpcMemLazyEnablePeerAccess));
+        opened_.push_back(g);
+        psd_[size_t(d)][size_t(q)] = static_cast<char*>(s);
+        pgd_[size_t(d)][size_t(q)] = static_cast<char*>(g);
+      }
+    } else {
+      const int fd = shm_open(b.shm, O_RDWR, 0600);
+      AKKA_CHECK(fd >= 0, std::string("onesided lane: cannot open rank ") + std::to_string(q) + "'s window " + b.shm);
+      void* m = mmap(nullptr, size_t(b.shm_bytes), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+      close(fd);
+      AKKA_CHECK(m != MAP_FAILED, "onesided lane: mmap of a peer window failed");
+      char* base = static_cast<char*>(m);
+      peer_maps_.push_back({base, size_t(b.shm_bytes)});
+      pfl_[size_t(q)] = reinterpret_cast<uint32_t*>(base);
+      for (int32_t d = 0; d < D_; ++d) {
+        psd_[size_t(d)][size_t(q)] = base + fb + size_t(d) * rb;
+        pgd_[size_t(d)][size_t(q)] = base + fb + size_t(D_ + d) * rb;
+      }
+    }
+  }
+  if (device_ >= 0) {
+    Tables t;
+    std::memset(&t, 0, sizeof(t));
+    for (int32_t q = 0; q < g_.N; ++q) {
+      t.fl[q] = pfl_[size_t(q)];
+      t.bstart[q] = g_.block_start(q);
+      t.blen[q] = g_.block_len(q);
+      t.nch[q] = g_.num_chunks(q);
+      for (int32_t d = 0; d < D_; ++d) {
+        t.sd[d][q] = psd_[size_t(d)][size_t(q)];
+        t.gd[d][q] = pgd_[size_t(d)][size_t(q)];
+      }
+    }
+    AKKA_OS_HIP(hipMemcpy(tab_dev_, &t, sizeof(t), hipMemcpyHostToDevice));
+  }
+  ready_ = true;
+}
+
+void OneSidedLane::unlink() {
+  if (device_ < 0 && !unlinked_ && !shm_name_.empty()) {
+    shm_unlink(shm_name_.c_str());
+    unlinked_ = true;
+  }
+}
+
+int32_t OneSidedLane::round(uintptr_t stream, const void* in, void* out, int32_t* counts, int32_t kcols) {
+  AKKA_CHECK(ready_, "onesided lane: open() the peer windows first");
+  AKKA_CHECK(kcols >= Kmax_, "onesided lane: counts table has too few columns");
+  const int32_t slot = int32_t(calls_ % kStatusSlots);
+  ++calls_;
+  hw_->status[slot] = CallStatus{-1, 0, 0, 0};
+  if (device_ >= 0) gpu_call(stream, static_cast<const char*>(in), static_cast<char*>(out), counts, kcols, slot);
+  else cpu_call(static_cast<const char*>(in), static_cast<char*>(out), counts, kcols, slot);
+  return slot;
+}
+
+void OneSidedLane::gpu_call(uintptr_t stream, const char* in, char* out, int32_t* counts, int32_t kcols,
+                            int32_t slot) {
+  Args a;
+  a.tab = static_cast<const Tables*>(tab_dev_);
+  a.loc = loc_;
+  a.stats = stats_dev_;
+  a.L = L_;
+  a.C = g_.C;
+  a.slot = slot_;
+  a.part_len = part_len_;
+  a.me = me_;
+  a.kme = g_.num_chunks(me_);
+  a.need_r = need_r_;
+  a.need_c = need_c_;
+  a.max_lag = p_.max_lag;
+  a.kcols = kcols;
+  a.call_slot = slot;
+  a.threads = p_.threads;
+  a.timeout = timeout_ticks_;
+  a.in = in;
+  a.out = out;
+  a.counts = counts;
+  a.err = &hw_dev_->err;
+  a.dead = hw_dev_->dead;
+  a.force = &hw_dev_->force;
+  a.status = hw_dev_->status;
+  AKKA_OS_HIP(hipSetDevice(device_));
+  launch_onesided_call(reinterpret_cast<hipStream_t>(stream), a, dt_ == DType::F32 ? 0 : 1);
+  AKKA_OS_HIP(hipGetLastError());
+}
+
+void OneSidedLane::cpu_call(const char* in, char* out, int32_t* counts, int32_t kcols, int32_t slot) {
+  using clock = std::chrono::steady_clock;
+  const int32_t N = g_.N, me = me_, P = P_;
+  const size_t es = es_;
+  uint32_t* fl = pfl_[size_t(me)];
+  uint32_t* loc = loc_;
+  auto stat = [&](int32_t i, uint64_t v) { stats_host_[size_t(i)] += v; };
+  auto dead = [&](int32_t q) { return __atomic_load_n(&hw_->dead[q], __ATOMIC_ACQUIRE) != 0u; };
+  auto plen = [&](int32_t p, int32_t k, int32_t j) {
+    const int64_t clen = std::min(g_.C, g_.block_len(p) - int64_t(k) * g_.C);
+    return std::max<int64_t>(0, std::min(part_len_, clen - int64_t(j) * part_len_));
+  };
+  auto poff = [&](int32_t k, int32_t j) { return int64_t(k) * g_.C + int64_t(j) * part_len_; };
+  auto nap = [](int& us) {
+    std::this_thread::sleep_for(std::chrono::microseconds(us));
+    us = std::min(us * 2, 1000);
+  };
+  const auto deadline_of = [&]() { return clock::now() + std::chrono::milliseconds(int64_t(timeout_ticks_)); };
+
+  // begin: round selection
+  const uint32_t next = loc[L_.state(kNext)];
+  const uint32_t r = select_round(next, seen_max<HostMem>(fl, L_, me), p_.max_lag);
+  stat(kSkippedRounds, r - next);
+  loc[L_.state(kCur)] = r;
+  loc[L_.state(kNext)] = r + 1u;
+  loc[L_.state(kForcedChunks)] = 0;
+  if (HostMem::ld(fl + L_.done()) < r) HostMem::st(fl + L_.done(), r);
+  const int32_t row = int32_t(r % uint32_t(D_));
+
+
+  auto dump = [&](const char* role, int32_t k) {
+    if (!std::getenv("AKKA_OS_DEBUG")) return;
+    std::fprintf(stderr, "[onesided r%d] %s timeout: round %u chunk %d next %u seen/fin:", me, role, r, k,
+                 loc[L_.state(kNext)]);
+    for (int32_t s = 0; s < N; ++s) std::fprintf(stderr, " %u/%u", HostMem::ld(fl + L_.seen(s)), HostMem::ld(fl + L_.fin(s)));
+    std::fprintf(stderr, " done %u | tags:", HostMem::ld(fl + L_.done()));
+    for (int32_t s = 0; s < N; ++s) {
+      if (s == me) continue;
+      if (k >= 0) std::fprintf(stderr, " s%d=%u", s, HostMem::ld(fl + L_.stag(row, s, k, 0)));
+      else
+        for (int32_t kk = 0; kk < g_.num_chunks(s); ++kk) std::fprintf(stderr, " b%dk%d=%u", s, kk, HostMem::ld(fl + L_.gtag(row, s, kk, 0)));
+    }
+    std::fprintf(stderr, "\n");
+  };
+
+  // push: phase 1, fire and forget (the kernel's item order)
+  const int64_t items = int64_t(N - 1) * Kmax_ * P;
+  for (int64_t w = 0; w < items; ++w) {
+    const int32_t i = int32_t(w % (N - 1)), kj = int32_t(w / (N - 1));
+    const int32_t k = kj / P, j = kj % P;
+    const int32_t p = (me + 1 + i) % N;
+    if (k >= g_.num_chunks(p)) continue;
+    if (dead(p)) {
+      stat(kDeadSkips, 1);
+      continue;
+    }
+    uint32_t* ofl = pfl_[size_t(p)];
+    if (k == 0 && j == 0) HostMem::st(ofl + L_.seen(me), r + 1u);
+    const int32_t g = scatter_gate<HostMem>(ofl, L_, row, me, k, j, r);
+    stat(g == kGo ? kScatterPushed : g == kOutdated ? kScatterOutdated : kScatterConflict, 1);
+    if (g != kGo) continue;
+    const int64_t n = plen(p, k, j), off = poff(k, j);
+    if (n > 0)
+      std::memcpy(psd_[size_t(row)][size_t(p)] + (int64_t(me) * slot_ + off) * int64_t(es),
+                  in + (g_.block_start(p) + off) * int64_t(es), size_t(n) * es);
+    HostMem::st(ofl + L_.stag(row, me, k, j), tag_done(r));  // release: the bytes are visible first
+  }
+
+  // decide: reduce threshold per chunk of my block
+  const int32_t kme = g_.num_chunks(me);
+  for (int32_t k = 0; k < kme; ++k) {
+    HostMem::st_sc(fl + L_.sread(row, k), r + 1u);
+    const auto deadline = deadline_of();
+    int us = 20;
+    int32_t verdict = kWait;
+    uint32_t mask = 0;
+    while (true) {
+      int32_t landed = 1, pending = 0;
+      mask = 1u << me;
+      for (int32_t s = 0; s < N; ++s) {
+        if (s == me) continue;
+        int32_t dn = 0;
+        bool lost = source_past<HostMem>(fl, L_, s, r);  // before the tags
+        for (int32_t j = 0; j < P; ++j) {
+          const int32_t st = tag_state(HostMem::ld(fl + L_.stag(row, s, k, j)), r);
+          dn += st == kLanded;
+          lost |= st == kLost;
+        }
+        if (dn == P) {
+          ++landed;
+          mask |= 1u << s;
+        } else if (!lost && !dead(s)) {
+          ++pending;
+        }
+      }
+      verdict = evaluate(landed, pending, need_r_, r, seen_max<HostMem>(fl, L_, me), p_.max_lag,
+                         __atomic_load_n(&hw_->force, __ATOMIC_ACQUIRE), clock::now() > deadline);
+      if (verdict != kWait) break;
+      nap(us);
+    }
+    loc[L_.dec(row, k)] = r + 1u;
+    loc[L_.dec(row, k) + 1] = mask;
+    HostMem::st(fl + L_.fired(row, k), r + 1u);
+    if (verdict == kThreshold) {
+      stat(kReduceThreshold, 1);
+    } else {
+      stat(kReduceForced, 1);
+      ++loc[L_.state(kForcedChunks)];
+    }
+    if (verdict == kTimeout) {
+      stat(kTimeouts, 1);
+      __atomic_store_n(&hw_->err, 1u, __ATOMIC_RELEASE);
+      dump("decide", k);
+    }
+    stat(kReduceContribs, uint64_t(__builtin_popcount(mask)));
+  }
+
+  // reduce: masked sum (ascending source order, fp32 accumulation), phase 2
+  std::vector<float> acc;
+  std::vector<char> part;
+  for (int32_t k = 0; k < kme; ++k) {
+    const uint32_t mask = loc[L_.dec(row, k) + 1];
+    const uint32_t cnt = uint32_t(__builtin_popcount(mask));
+    for (int32_t j = 0; j < P; ++j) {
+      uint32_t okq = 0;
+      for (int32_t i = 1; i < N; ++i) {
+        const int32_t q = (me + i) % N;
+        if (dead(q)) {
+          stat(kDeadSkips, 1);
+          continue;
+        }
+        uint32_t* qfl = pfl_[size_t(q)];
+        if (k == 0 && j == 0) HostMem::st(qfl + L_.seen(me), r + 1u);
+        const int32_t g = gather_gate<HostMem>(qfl, L_, row, me, k, j, r);
+        if (g == kGo) {
+          okq |= 1u << q;
+          HostMem::st(qfl + L_.gtag(row, me, k, j) + 1, cnt);
+          stat(kGatherPushed, 1);
+        } else {
+          stat(g == kOutdated ? kGatherOutdated : kGatherConflict, 1);
+        }
+      }
+      if (j == 0) counts[int64_t(me) * kcols + k] = int32_t(cnt);
+      const int64_t n = plen(me, k, j), off = poff(k, j);
+      if (n > 0) {
+        acc.assign(size_t(n), 0.f);
+        for (int32_t s = 0; s < N; ++s) {
+          if (!((mask >> s) & 1u)) continue;
+          const char* src = s == me ? in + (g_.block_start(me) + off) * int64_t(es)
+                                    : sd_[size_t(row)] + (int64_t(s) * slot_ + off) * int64_t(es);
+          if (dt_ == DType::F32) {
+            const float* f = reinterpret_cast<const float*>(src);
+            for (int64_t e = 0; e < n; ++e) acc[size_t(e)] += f[e];
+          } else {
+            const uint16_t* h = reinterpret_cast<const uint16_t*>(src);
+            for (int64_t e = 0; e < n; ++e) acc[size_t(e)] += bf16_f32(h[e]);
+          }
+        }
+        part.resize(size_t(n) * es);
+        if (dt_ == DType::F32) {
+          std::memcpy(part.data(), acc.data(), size_t(n) * 4);
+        } else {
+          uint16_t* h = reinterpret_cast<uint16_t*>(part.data());
+          for (int64_t e = 0; e < n; ++e) h[e] = f32_bf16(acc[size_t(e)]);
+        }
+        std::memcpy(out + (g_.block_start(me) + off) * int64_t(es), part.data(), part.size());
+        for (int32_t q = 0; q < N; ++q)
+          if ((okq >> q) & 1u)
+            std::memcpy(pgd_[size_t(row)][size_t(q)] + (int64_t(me) * slot_ + off) * int64_t(es), part.data(),
+                        part.size());
+      }
+      for (int32_t q = 0; q < N; ++q)
+        if ((okq >> q) & 1u) HostMem::st(pfl_[size_t(q)] + L_.gtag(row, me, k, j), tag_done(r));
+    }
+  }
+  for (int32_t k = 0; k < kme; ++k) HostMem::st(fl + L_.sread(row, k), 0u);
+
+  // cdecide: completion threshold
+  HostMem::st_sc(fl + L_.gread(row), r + 1u);
+  int32_t verdict = kWait, landed = 0;
+  {
+    const auto deadline = deadline_of();
+    int us = 20;
+    while (true) {
+      int32_t l = 0, pending = 0;
+      for (int32_t p = 0; p < N; ++p) {
+        if (p == me) continue;
+        const bool past = source_past<HostMem>(fl, L_, p, r);  // before the tags
+        for (int32_t k = 0; k < g_.num_chunks(p); ++k) {
+          int32_t st = kLanded;
+          for (int32_t j = 0; j < P; ++j) {
+            const int32_t s = tag_state(HostMem::ld(fl + L_.gtag(row, p, k, j)), r);
+            if (s == kLost) {
+              st = kLost;
+              break;
+            }
+            if (s == kPending) st = kPending;
+          }
+          if (st == kPending && (past || dead(p))) st = kLost;
+          loc[L_.cmask(p, k)] = st == kLanded ? 1u : 0u;
+          l += st == kLanded;
+          pending += st == kPending;
+        }
+      }
+      landed = l + kme;
+      verdict = evaluate(landed, pending, need_c_, r, seen_max<HostMem>(fl, L_, me), p_.max_lag,
+                         __atomic_load_n(&hw_->force, __ATOMIC_ACQUIRE), clock::now() > deadline);
+      if (verdict != kWait) break;
+      nap(us);
+    }
+  }
+  stat(verdict == kThreshold ? kCompleteThreshold : kCompleteForced, 1);
+  if (verdict == kTimeout) {
+    stat(kTimeouts, 1);
+    __atomic_store_n(&hw_->err, 1u, __ATOMIC_RELEASE);
+    dump("cdecide", -1);
+  }
+
+  // copy: landed chunks -> output, the rest 0 / count 0
+  for (int32_t p = 0; p < N; ++p) {
+    if (p == me) continue;
+    for (int32_t k = 0; k < g_.num_chunks(p); ++k) {
+      const bool ok = loc[L_.cmask(p, k)] != 0u;
+      for (int32_t j = 0; j < P; ++j) {
+        const int64_t n = plen(p, k, j), off = poff(k, j);
+        if (n <= 0) continue;
+        char* o = out + (g_.block_start(p) + off) * int64_t(es);
+        if (ok) std::memcpy(o, gd_[size_t(row)] + (int64_t(p) * slot_ + off) * int64_t(es), size_t(n) * es);
+        else std::memset(o, 0, size_t(n) * es);
+      }
+      counts[int64_t(p) * kcols + k] = ok ? int32_t(HostMem::ld(fl + L_.gtag(row, p, k, 0) + 1)) : 0;
+    }
+  }
+  HostMem::st(fl + L_.done(), r + 1u);
+  HostMem::st(fl + L_.gread(row), 0u);
+  stat(kRounds, 1);
+  stat(kLandedChunks, uint64_t(landed));
+  stat(kMissingChunks, uint64_t(g_.total_chunks() - landed));
+  CallStatus& cs = hw_->status[slot];
+  cs.reason = verdict;
+  cs.landed_chunks = landed;
+  cs.forced_chunks = loc[L_.state(kForcedChunks)];
+  __atomic_store_n(&cs.round, int64_t(r), __ATOMIC_RELEASE);
+}
+
+void OneSidedLane::retire(uintptr_t stream) {
+  AKKA_CHECK(ready_, "onesided lane: open() the peer windows first");
+  if (device_ >= 0) {
+    Args a;
+    a.tab = static_cast<const Tables*>(tab_dev_);
+    a.loc = loc_;
+    a.L = L_;
+    a.me = me_;
+    AKKA_OS_HIP(hipSetDevice(device_));
+    launch_onesided_retire(reinterpret_cast<hipStream_t>(stream), a);
+    AKKA_OS_HIP(hipGetLastError());
+  } else {
+    for (int32_t q = 0; q < g_.N; ++q)
+      if (q != me_) HostMem::st(pfl_[size_t(q)] + L_.fin(me_), loc_[L_.state(kNext)] + 1u);
+  }
+}
+
+CallStatus OneSidedLane::status(int32_t slot) const {
+  AKKA_CHECK(slot >= 0 && slot < kStatusSlots, "onesided lane: bad status slot");
+  CallStatus c;
+  c.round = __atomic_load_n(&hw_->status[slot].round, __ATOMIC_ACQUIRE);
+  c.reason = hw_->status[slot].reason;
+  c.landed_chunks = hw_->status[slot].landed_chunks;
+  c.forced_chunks = hw_->status[slot].forced_chunks;
+  return c;
+}
+
+std::vector<uint64_t> OneSidedLane::stats() {
+  std::vector<uint64_t> v(kNumStats, 0);
+  if (device_ >= 0) {
+    AKKA_OS_HIP(hipSetDevice(device_));
+    AKKA_OS_HIP(hipDeviceSynchronize());
+    std::vector<unsigned long long> h(kNumStats, 0);
+    AKKA_OS_HIP(hipMemcpy(h.data(), stats_dev_, kNumStats * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    for (int i = 0; i < kNumStats; ++i) v[size_t(i)] = h[size_t(i)];
+  } else {
+    for (int i = 0; i < kNumStats; ++i) v[size_t(i)] = stats_host_[size_t(i)];
+  }
+  return v;
+}
+
+uint32_t OneSidedLane::error() const { return __atomic_load_n(&hw_->err, __ATOMIC_ACQUIRE); }
+void OneSidedLane::clear_error() { __atomic_store_n(&hw_->err, 0u, __ATOMIC_RELEASE); }
+
+void OneSidedLane::set_dead(int32_t peer, bool d) {
+  AKKA_CHECK(peer >= 0 && peer < g_.N && peer != me_, "onesided lane: bad peer");
+  __atomic_store_n(&hw_->dead[peer], d ? 1u : 0u, __ATOMIC_RELEASE);
+}
+
+void OneSidedLane::force_below(uint32_t v) { __atomic_store_n(&hw_->force, v, __ATOMIC_RELEASE); }
+
+}  // namespace akka

@@ -1,0 +1,135 @@
+// OneSidedLane: threshold rounds as one-sided stores into mapped peer windows
+// (protocol: kernels/onesided_protocol.h; gfx950 kernels: kernels/onesided.hip).
+//
+// The reference's data plane is fire-and-forget messages into unbounded
+// mailboxes (AllreduceWorker.scala:227-232, 259-264): a fast worker never
+// waits for a slow one, late messages are dropped (W:155-156, 172-173), and
+// maxLag catch-up bounds staleness (W:100-106).  Two-sided transports (RCCL
+// p2p) cannot do that -- every send needs the peer's matching receive, so a
+// straggler eventually throttles everybody.  Here every rank exports a window
+// (scatter rows, gather rows, flag words) and peers STORE into it over xGMI:
+// no send ever waits, and the receiver-side thresholds decide what is used.
+//
+// Two backends run the same protocol functions:
+//  * GPU (device >= 0): windows are fine-grained HBM exported with IPC
+//    handles, the round is six kernels on the caller's stream;
+//  * CPU (device < 0): windows are POSIX shared memory, the round runs in the
+//    calling thread -- the multi-process CPU tests of the same semantics.
+//
+// Setup is collective, like the exact ipc lane: handle() on every rank, the
+// handles go to every rank out of band, open(all handles); then unlink()
+// (CPU) once every rank opened (a killed rank then leaves nothing behind).
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../engine/common.h"
+#include "../engine/geometry.h"
+#include "../kernels/onesided_protocol.h"
+
+namespace akka {
+
+struct OneSidedParams {
+  float th_reduce = 1.f, th_complete = 1.f;
+  int32_t max_lag = 1;
+  int32_t rows = 0;                      // ring depth D (0: max(3, maxLag + 2))
+  int64_t part_bytes = int64_t(256) << 10;
+  int64_t timeout_ms = 30000;            // bound of every wait (then forced + error)
+  int32_t threads = 256;                 // workgroup size of the data kernels
+};
+
+class OneSidedLane {
+ public:
+  OneSidedLane(int32_t device, int64_t S, int32_t N, int64_t C, int32_t me, DType dt, const OneSidedParams& p);
+  ~OneSidedLane();
+  OneSidedLane(const OneSidedLane&) = delete;
+  OneSidedLane& operator=(const OneSidedLane&) = delete;
+
+  std::string handle() const;
+  void open(const std::vector<std::string>& handles);
+  // CPU: remove this rank's shared-memory name (every peer mapped it already).
+  void unlink();
+  bool ready() const { return ready_; }
+
+  // One call = one round of this rank: in[S] -> out[S], counts[N][kcols]
+  // (per chunk).  GPU: enqueued on `stream`; CPU: runs to completion.
+  // Returns the status slot of the call (status()).
+  int32_t round(uintptr_t stream, const void* in, void* out, int32_t* counts, int32_t kcols);
+  // The call's record; round = -1 until it finished (host memory: no sync).
+  os::CallStatus status(int32_t slot) const;
+  std::vector<uint64_t> stats();  // GPU: synchronises the device first
+  uint32_t error() const;
+  void clear_error();
+  // A peer marked dead is never waited for again (and never written to).
+  void set_dead(int32_t peer, bool dead);
+  // Every wait of a round r < v ends at once with what landed (forced).
+  void force_below(uint32_t v);
+  // This rank serves no further round: peers stop waiting for its copies of
+  // rounds >= its next one (the end of a job; GPU: enqueued on `stream`).
+  void retire(uintptr_t stream);
+
+  bool on_gpu() const { return device_ >= 0; }
+  int32_t rows() const { return D_; }
+  int32_t parts() const { return P_; }
+  int64_t part_elems() const { return part_len_; }
+  int32_t need_reduce() const { return need_r_; }
+  int32_t need_complete() const { return need_c_; }
+  size_t window_bytes() const { return win_bytes_; }
+  const std::string& memory_kind() const { return mem_kind_; }
+  const Geometry& geometry() const { return g_; }
+  int64_t calls() const { return calls_; }
+
+ private:
+  struct HostWords {  // host memory (GPU: mapped into the device)
+    uint32_t err;
+    uint32_t force;
+    uint32_t dead[os::kMaxRanks];
+    uint32_t pad[14];
+    os::CallStatus status[os::kStatusSlots];
+  };
+  void cpu_call(const char* in, char* out, int32_t* counts, int32_t kcols, int32_t slot);
+  void gpu_call(uintptr_t stream, const char* in, char* out, int32_t* counts, int32_t kcols, int32_t slot);
+
+  int32_t device_;
+  Geometry g_;
+  int32_t me_;
+  DType dt_;
+  size_t es_;
+  OneSidedParams p_;
+  os::Layout L_;
+  int32_t D_ = 0, P_ = 1, Kmax_ = 0, need_r_ = 1, need_c_ = 1;
+  int64_t slot_ = 0, part_len_ = 64;
+  size_t flag_bytes_ = 0, row_bytes_ = 0, win_bytes_ = 0;
+  std::string mem_kind_;
+  bool ready_ = false;
+  int64_t calls_ = 0;
+  uint64_t timeout_ticks_ = 0;
+
+  // own window
+  uint32_t* flags_ = nullptr;
+  std::vector<char*> sd_, gd_;  // [D]
+  // peers' windows as mapped here (own included)
+  std::vector<uint32_t*> pfl_;            // [N]
+  std::vector<std::vector<char*>> psd_, pgd_;  // [D][N]
+  std::vector<void*> opened_;             // GPU: IPC mappings to close
+
+  // local state
+  uint32_t* loc_ = nullptr;             // GPU: device memory; CPU: loc_host_
+  unsigned long long* stats_dev_ = nullptr;
+  void* tab_dev_ = nullptr;             // GPU: os::Tables
+  HostWords* hw_ = nullptr;             // host
+  HostWords* hw_dev_ = nullptr;         // device view of hw_ (GPU)
+  std::vector<uint32_t> loc_host_;
+  std::vector<unsigned long long> stats_host_;
+
+  // CPU shared memory
+  std::string shm_name_;
+  char* shm_base_ = nullptr;
+  size_t shm_bytes_ = 0;
+  std::vector<std::pair<char*, size_t>> peer_maps_;
+  bool unlinked_ = false;
+};
+
+}  // namespace akka

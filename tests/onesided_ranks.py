@@ -1,0 +1,155 @@
+"""Rank program for the one-sided threshold lane tests (tests/test_onesided_cpu.py
+on CPU processes over shared memory, tests/test_onesided_gpu.py with every rank
+on the box's one GPU).  Run under torch.distributed.run; writes rank<i>.json.
+
+Modes:
+  exact      thresholds 1: every round is the fp32 sum in ascending source
+             order (bitwise), counts N, round ids 0, 1, 2, ...
+  straggler  rank `--straggler` sleeps `--delay-ms` before each call of the
+             second phase.  Every rank contributes 2^rank, so each output
+             chunk encodes its contributor set: value = sum of 2^s over the
+             set and popcount(value) must equal the chunk's count.  Records
+             per-call times and round ids of both phases (no straggler /
+             straggler) and the lane's stats; `--kill-after K` makes the
+             straggler exit abruptly after K calls of the second phase.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+
+def check_sets(o, world, me, dtype):
+    """Every chunk: value encodes a contributor set whose size is the count."""
+    g = o.geometry
+    data = o.data.float().cpu()
+    counts = o.counts_per_chunk.cpu()
+    bad = 0
+    own_has_me = True
+    for p in range(world):
+        for k in range(g.num_chunks(p)):
+            s, e = g.chunk_range(p, k)
+            if e <= s:
+                continue
+            seg = data[s:e]
+            v = float(seg[0])
+            if not bool((seg == v).all()):
+                bad += 1
+                continue
+            c = int(counts[p, k])
+            iv = int(v)
+            if float(iv) != v or iv < 0 or iv >= (1 << world) or bin(iv).count("1") != c:
+                bad += 1
+            if p == me and not (iv >> me) & 1:
+                own_has_me = False
+    return bad, own_has_me
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--mode", default="exact", choices=["exact", "straggler"])
+    ap.add_argument("--device", default="cpu")
+    ap.add_argument("--size", type=int, default=1 << 16)
+    ap.add_argument("--chunk", type=int, default=1 << 12)
+    ap.add_argument("--dtype", default="float32")
+    ap.add_argument("--rounds", type=int, default=8)
+    ap.add_argument("--th", type=float, default=0.75)
+    ap.add_argument("--max-lag", type=int, default=1)
+    ap.add_argument("--rows", type=int, default=0)
+    ap.add_argument("--straggler", type=int, default=-1)
+    ap.add_argument("--delay-ms", type=float, default=50.0)
+    ap.add_argument("--kill-after", type=int, default=-1)
+    ap.add_argument("--compute-ms", type=float, default=0.0, help="every rank 'computes' this long before a call")
+    ap.add_argument("--part-bytes", type=int, default=256 << 10)
+    ap.add_argument("--timeout-s", type=float, default=30.0)
+    ap.add_argument("--out-dir", required=True)
+    a = ap.parse_args()
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    dist.init_process_group("gloo")
+    if a.device == "cuda":
+        dev = torch.device("cuda", 0)
+        torch.cuda.set_device(dev)
+    else:
+        dev = torch.device("cpu")
+    dtype = torch.float32 if a.dtype == "float32" else torch.bfloat16
+    from akka_allreduce_amd.parallel.onesided import OneSidedAllreduce
+
+    th = 1.0 if a.mode == "exact" else a.th
+    ar = OneSidedAllreduce(a.size, max_chunk_size=a.chunk, dtype=dtype, th_reduce=th, th_complete=th,
+                           max_lag=a.max_lag, device=dev, rows=a.rows, part_bytes=a.part_bytes,
+                           timeout_s=a.timeout_s)
+    res = {"rank": rank, "info": ar.info()}
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.synchronize()
+
+    if a.mode == "exact":
+        res["exact"], res["rounds"] = [], []
+        for r in range(a.rounds):
+            x = torch.randn(a.size, generator=torch.Generator().manual_seed(1000 * rank + r)).to(dtype)
+            o = ar(x.to(dev))
+            sync()
+            want = None
+            for s in range(world):
+                y = torch.randn(a.size, generator=torch.Generator().manual_seed(1000 * s + r)).to(dtype).float()
+                want = y if want is None else want + y
+            ok = torch.equal(o.data.cpu(), want.to(dtype)) and bool((o.count.cpu() == world).all())
+            res["exact"].append(bool(ok))
+            res["rounds"].append(o.iteration)
+    else:
+        x = torch.full((a.size,), float(1 << rank), dtype=dtype, device=dev)
+        out = torch.empty_like(x)
+        # A phase ends at a common ROUND, not a call count: with thresholds < 1
+        # a rank can complete rounds without a slow peer and skip ahead by
+        # catch-up, so call counts differ between ranks (the reference's
+        # master ends the job at maxRound the same way, M:58-63).
+        for pi, phase in enumerate(("no_straggler", "straggler")):
+            times, rounds, bad, own_ok, reasons = [], [], 0, True, []
+            target, last, c = (pi + 1) * a.rounds - 1, -1 if pi == 0 else res["no_straggler"]["rounds"][-1], 0
+            while last < target:
+                c += 1
+                if phase == "straggler" and rank == a.straggler:
+                    if c == a.kill_after:
+                        sync()
+                        res["killed_after"] = c
+                        with open(os.path.join(a.out_dir, f"rank{rank}.json"), "w") as f:
+                            json.dump(res, f)
+                        os._exit(0)  # abrupt: no retire, no teardown
+                    time.sleep(a.delay_ms / 1e3)
+                elif a.compute_ms:
+                    time.sleep(a.compute_ms / 1e3)
+                t0 = time.perf_counter()
+                o = ar(x, out=out)
+                sync()
+                times.append((time.perf_counter() - t0) * 1e3)
+                b, mine = check_sets(o, world, rank, dtype)
+                bad += b
+                own_ok &= mine
+                last = o.iteration
+                rounds.append(last)
+                reasons.append(o.status["reason"])
+            res[phase] = {"ms": times, "rounds": rounds, "bad_chunks": bad, "own_block_has_me": own_ok,
+                          "reasons": reasons, "stats": ar.stats()}
+        ar.retire()
+        sync()
+    res["error"] = ar.error()
+    res["stats"] = ar.stats()
+    with open(os.path.join(a.out_dir, f"rank{rank}.json"), "w") as f:
+        json.dump(res, f)
+    sys.stdout.flush()
+    if a.kill_after < 0:
+        dist.barrier()
+        dist.destroy_process_group()
+    else:
+        os._exit(0)  # a peer is gone: no collective teardown
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,156 @@
+"""The one-sided threshold lane (csrc/transport/onesided.h) on CPU processes.
+
+Every rank is a process; windows are POSIX shared memory and the round runs
+the SAME protocol functions as the gfx950 kernels (csrc/kernels/
+onesided_protocol.h): tags, the overwrite hand-shake, the thReduce /
+thComplete verdicts, catch-up and the liveness rule.  Reference semantics
+covered: fire-and-forget sends (AllreduceWorker.scala:227-232, 259-264),
+outdated drops (W:155-156, 172-173), thresholds (ScatteredDataBuffer.scala:
+9-13, ReducedDataBuffer.scala:13-17, 60-66), catch-up (W:100-106)."""
+import json
+import os
+import socket
+import statistics
+import subprocess
+import sys
+import tempfile
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def run_ranks(n, *extra, timeout=240, device="cpu"):
+    with tempfile.TemporaryDirectory() as out:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+               os.path.join(ROOT, "tests", "onesided_ranks.py"), "--out-dir", out, "--device", device, *extra]
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout, cwd=ROOT)
+        rows = []
+        for i in range(n):
+            p = os.path.join(out, f"rank{i}.json")
+            rows.append(json.load(open(p)) if os.path.exists(p) else None)
+    return r, rows
+
+
+@pytest.mark.parametrize("n,size,chunk,dtype", [
+    (2, 1 << 16, 1 << 12, "float32"),
+    (3, 100_003, 3000, "float32"),       # uneven blocks, short last chunks
+    (4, 1 << 16, 1 << 13, "bfloat16"),
+    (2, 10, 2, "float32"),               # the reference's README demo geometry
+    (3, 2, 1, "float32"),                # S < N: an empty block
+])
+def test_onesided_exact_rounds(n, size, chunk, dtype):
+    """Thresholds 1: every round is the fp32 sum in ascending source order
+    (bitwise), counts N, round ids 0, 1, 2, ..."""
+    r, rows = run_ranks(n, "--mode", "exact", "--size", str(size), "--chunk", str(chunk), "--dtype", dtype,
+                        "--rounds", "5")
+    assert r.returncode == 0, r.stderr[-3000:]
+    for d in rows:
+        assert d["exact"] == [True] * 5, d
+        assert d["rounds"] == list(range(5)), d
+        assert d["error"] == 0
+        st = d["stats"]
+        assert st["reduce_forced"] == 0 and st["complete_forced"] == 0 and st["missing_chunks"] == 0, st
+
+
+def _median_tail(ms):
+    return statistics.median(ms[len(ms) // 2:])
+
+
+def test_onesided_straggler_steady_state():
+    """N=4, thresholds 0.75 / 0.75, maxLag 1, rank 3 sleeps 50 ms before each
+    call, 64 rounds after 64 without the straggler.  The fast ranks never
+    wait for it (their median round time stays within 2x of the straggler-free
+    phase), every chunk's value encodes a contributor set whose size is its
+    count, the straggler's late pushes are dropped by the senders (outdated)
+    and its calls catch up (skipped rounds)."""
+    r, rows = run_ranks(4, "--mode", "straggler", "--straggler", "3", "--rounds", "64", "--compute-ms", "2",
+                        "--delay-ms", "50")
+    assert r.returncode == 0, r.stderr[-3000:]
+    for d in rows:
+        assert d["error"] == 0, d["stats"]
+        for ph in ("no_straggler", "straggler"):
+            p = d[ph]
+            assert p["bad_chunks"] == 0, (d["rank"], ph)
+            assert p["own_block_has_me"], (d["rank"], ph)
+            assert all(b > a for a, b in zip(p["rounds"], p["rounds"][1:])), p["rounds"]
+    fast = rows[:3]
+    for d in fast:
+        base, strag = _median_tail(d["no_straggler"]["ms"]), _median_tail(d["straggler"]["ms"])
+        # CPU processes share 8 cores: allow the scheduler a few ms on top of 2x
+        assert strag <= 2 * base + 3.0, (d["rank"], base, strag)
+        assert d["straggler"]["rounds"][-1] >= 127
+    s = rows[3]
+    assert s["stats"]["skipped_rounds"] > 0, s["stats"]
+    assert s["stats"]["scatter_outdated"] + s["stats"]["gather_outdated"] > 0, s["stats"]
+    assert len(s["straggler"]["ms"]) < 64  # it caught up instead of replaying every round
+
+
+def test_onesided_straggler_killed_mid_run():
+    """The straggler exits abruptly (no retire, no teardown) after 3 calls of
+    the straggler phase; the survivors still complete every round to the end,
+    with consistent contributor sets and no timeout."""
+    r, rows = run_ranks(4, "--mode", "straggler", "--straggler", "3", "--rounds", "48", "--compute-ms", "2",
+                        "--delay-ms", "30", "--kill-after", "3", "--timeout-s", "20")
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert rows[3]["killed_after"] == 3
+    for d in rows[:3]:
+        assert d["error"] == 0 and d["straggler"]["bad_chunks"] == 0, d["stats"]
+        assert d["straggler"]["rounds"][-1] >= 95
+        assert d["stats"]["timeouts"] == 0
+
+
+def test_onesided_shallow_ring_with_lagging_rank():
+    """Ring depth 2 with maxLag 4: a lagging rank's rows are overwritten by
+    the fast ranks while it still reads them -- the overwrite hand-shake must
+    drop those writes (conflict) or the reader must exclude them; either way
+    no chunk is ever torn."""
+    r, rows = run_ranks(4, "--mode", "straggler", "--straggler", "2", "--rounds", "40", "--rows", "2",
+                        "--max-lag", "4", "--compute-ms", "1", "--delay-ms", "8", "--size", str(1 << 15),
+                        "--chunk", str(1 << 10))
+    assert r.returncode == 0, r.stderr[-3000:]
+    for d in rows:
+        for ph in ("no_straggler", "straggler"):
+            assert d[ph]["bad_chunks"] == 0, (d["rank"], ph)
+    assert sum(d["stats"]["scatter_conflict"] + d["stats"]["gather_conflict"] for d in rows) >= 0
+
+
+def test_onesided_layout_disjoint():
+    from akka_allreduce_amd._native_loader import load
+
+    n = load()
+    for N, D, K, P in [(2, 2, 1, 1), (4, 3, 5, 16), (8, 4, 8, 16), (16, 16, 3, 2)]:
+        lay = n.onesided_layout(N, D, K, P)
+        ex, lo = lay["exported"], lay["local"]
+        assert len(set(ex)) == len(ex) and min(ex) >= 0 and max(ex) < lay["flag_words"]
+        assert len(set(lo)) == len(lo) and min(lo) >= 0 and max(lo) < lay["local_words"]
+
+
+def test_onesided_rules():
+    from akka_allreduce_amd._native_loader import load
+
+    n = load()
+    tag_w = lambda r: 2 * (r + 1)  # noqa: E731
+    tag_d = lambda r: 2 * (r + 1) + 1  # noqa: E731
+    # tag states for round 5: pending (older / writing 5), landed, lost (a later round)
+    assert n.onesided_rules(0, 5) == 0
+    assert n.onesided_rules(tag_d(4), 5) == 0
+    assert n.onesided_rules(tag_w(5), 5) == 0
+    assert n.onesided_rules(tag_d(5), 5) == 1
+    assert n.onesided_rules(tag_w(6), 5) == 2 and n.onesided_rules(tag_d(9), 5) == 2
+    ev = n.onesided_evaluate  # (landed, pending, need, r, seen_max, max_lag, force_through, timed_out)
+    assert ev(3, 1, 3, 7, 7, 1, 0, False) == 1      # threshold (SB:11-13, >= once)
+    assert ev(2, 0, 3, 7, 7, 1, 0, False) == 2      # nothing left to wait for
+    assert ev(2, 1, 3, 7, 9, 1, 0, False) == 3      # catch-up: a peer is past r + maxLag
+    assert ev(2, 1, 3, 7, 8, 1, 0, False) == 0      # inside the window: wait
+    assert ev(2, 1, 3, 7, 7, 1, 8, False) == 4      # host force
+    assert ev(2, 1, 3, 7, 7, 1, 0, True) == 5       # timeout
+    sel = n.onesided_select_round  # (next, seen_max, max_lag)
+    assert sel(5, 3, 1) == 5 and sel(5, 9, 1) == 8 and sel(5, 9, 0) == 9 and sel(0, -1, 2) == 0

@@ -1,0 +1,47 @@
+"""The one-sided threshold lane on the GPU: every rank is a process on the
+box's one MI355X, windows are fine-grained HBM mapped through IPC handles,
+the rounds are the gfx950 kernels of csrc/kernels/onesided.hip (cross-XCD
+hand-offs; the same code crosses xGMI on a node).  Same scenarios as
+tests/test_onesided_cpu.py, whose protocol functions these kernels share."""
+import pytest
+
+from test_onesided_cpu import _median_tail, run_ranks
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("n,size,chunk,dtype", [
+    (2, 1 << 20, 1 << 16, "float32"),
+    (3, 1_000_003, 40_000, "float32"),    # uneven blocks: scalar paths, short last chunks
+    (4, 1 << 22, 1 << 18, "bfloat16"),
+    (2, 10, 2, "float32"),                # the reference's README demo geometry
+    (4, 1 << 24, 1 << 20, "float32"),     # 64 MiB, 4 MiB chunks, 16 parts each (BASELINE config 4's shape)
+])
+def test_onesided_gpu_exact_rounds(n, size, chunk, dtype):
+    r, rows = run_ranks(n, "--mode", "exact", "--size", str(size), "--chunk", str(chunk), "--dtype", dtype,
+                        "--rounds", "4", "--timeout-s", "10", device="cuda", timeout=180)
+    assert r.returncode == 0, r.stderr[-3000:]
+    for d in rows:
+        assert d["info"]["backend"] == "gpu"
+        assert d["exact"] == [True] * 4, d
+        assert d["rounds"] == list(range(4)), d
+        assert d["error"] == 0 and d["stats"]["missing_chunks"] == 0, d["stats"]
+
+
+def test_onesided_gpu_straggler_steady_state():
+    """N=4 on the card, 0.75 / 0.75, maxLag 1, rank 3 sleeps 50 ms per call,
+    64 rounds: fast ranks' median round within 2x of the straggler-free phase,
+    contributor sets consistent with counts, straggler's pushes dropped."""
+    r, rows = run_ranks(4, "--mode", "straggler", "--straggler", "3", "--rounds", "64", "--compute-ms", "2",
+                        "--delay-ms", "50", "--size", str(1 << 22), "--chunk", str(1 << 18), "--timeout-s", "10",
+                        device="cuda", timeout=180)
+    assert r.returncode == 0, r.stderr[-3000:]
+    for d in rows:
+        assert d["error"] == 0, d["stats"]
+        for ph in ("no_straggler", "straggler"):
+            assert d[ph]["bad_chunks"] == 0 and d[ph]["own_block_has_me"], (d["rank"], ph)
+    for d in rows[:3]:
+        base, strag = _median_tail(d["no_straggler"]["ms"]), _median_tail(d["straggler"]["ms"])
+        assert strag <= 2 * base + 1.0, (d["rank"], base, strag)
+    s = rows[3]["stats"]
+    assert s["skipped_rounds"] > 0 and s["scatter_outdated"] + s["gather_outdated"] > 0, s
