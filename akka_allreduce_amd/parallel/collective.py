@@ -14,21 +14,25 @@ Usage::
     out = ar(x)          # AllReduceOutput; out.data is valid in stream order
 
 ``lane`` picks how exact-threshold rounds (thReduce = thComplete = 1) move:
-``"auto"`` runs them as RCCL reduce-scatter + all-gather (two calls a round,
-RCCL's own xGMI schedules) when the buffer splits evenly, else the
-chunk-pipelined p2p schedule; ``"p2p"`` always uses the p2p schedule,
-``"collective"`` always the whole-round lane.  Rounds with thresholds < 1
-always take the p2p schedule (their outcome depends on arrival order).
+``"auto"`` / ``"p2p"`` run the chunk-pipelined p2p schedule with the gfx950
+reduce, ``"ipc"`` the one-sided kernels over mapped peer windows (after
+``enable_ipc``), ``"collective"`` RCCL's own reduce-scatter + all-gather -- a
+comparator only, never chosen automatically (``tune`` picks among the
+framework's lanes).  Rounds with thresholds < 1 always take the p2p schedule
+(their outcome depends on arrival order).
 
 ``th_allreduce`` adds the reference's third straggler knob, the master's
 round pacing (M:54-63): a rank starts round r only once ``thAllreduce * N``
 ranks completed round r-1 (counters in the job's TCPStore, no master
 process).  ``None`` (default): each rank paces itself.
 
-``transport="reactive"`` selects the straggler-tolerant data path
+``transport="onesided"`` is the straggler-tolerant path of choice
+(parallel/onesided.py, csrc/transport/onesided.h): every send is a store into
+the receiver's mapped window, so no rank ever waits for a slow one, in steady
+state.  ``transport="reactive"`` is the two-sided alternative
 (csrc/transport/reactive_link.h): one stream + one RCCL pair communicator per
-peer, arrivals polled from events, so with thresholds < 1 a rank completes
-rounds without waiting for slow peers (the reference's semantics).  It runs
+peer, arrivals polled from events; a lagging peer pins one send slot per
+round, so after the slot pool (16) the fast ranks run at its pace.  It runs
 N+2 streams per process: set ``GPU_MAX_HW_QUEUES`` (<= 32) to at least N+4
 before the first HIP call, or parked streams share hardware queues.
 """
@@ -168,8 +172,24 @@ class ThresholdAllreduce:
         th_allreduce: Optional[float] = None,
         data_plane: str = "rccl",
     ):
+        if transport == "onesided":
+            # thresholds over mapped peer windows: no send ever waits for a
+            # peer (parallel/onesided.py, csrc/transport/onesided.h)
+            if th_allreduce is not None:
+                raise ValueError("the onesided transport paces rounds by catch-up (maxLag), not thAllreduce")
+            from ..utils.faults import env_straggler_delay
+            from .onesided import OneSidedAllreduce
+
+            self._os = OneSidedAllreduce(data_size, max_chunk_size=max_chunk_size, dtype=dtype, th_reduce=th_reduce,
+                                         th_complete=th_complete, max_lag=max_lag, rank=rank, world_size=world_size,
+                                         device=device, store=store, data_sink=data_sink)
+            self.rank, self.world_size, self.device = self._os.rank, self._os.world_size, self._os.device
+            self.transport, self.worker, self.pacer, self.store = "onesided", None, None, store
+            self.data_size, self._round = int(data_size), 0
+            self.fault_delay_s = env_straggler_delay(self.rank)
+            return
         if transport not in ("stream", "reactive"):
-            raise ValueError("transport must be 'stream' or 'reactive'")
+            raise ValueError("transport must be 'stream', 'reactive' or 'onesided'")
         if data_plane not in ("rccl", "ipc", "ipc_p2p"):
             raise ValueError("data_plane must be 'rccl', 'ipc' or 'ipc_p2p'")
         if data_plane == "ipc" and (transport != "stream" or th_reduce < 1.0 or th_complete < 1.0):
@@ -262,6 +282,9 @@ class ThresholdAllreduce:
 
             time.sleep(self.fault_delay_s)
         r = self._round
+        if self.transport == "onesided":
+            self._round += 1
+            return self._os(x, out=out)
         if self.pacer is not None:
             self.pacer.wait_start(r, self.worker.poll if self.transport == "reactive" else None)
         out = self.worker.allreduce(x, async_op=async_op, out=out)
@@ -382,7 +405,10 @@ class ThresholdAllreduce:
         cands = list(candidates) if candidates is not None else None
         if cands is None:
             spec = self.worker.transport_spec or ("",)
-            cands = [] if spec[0] == "none" else ["collective", "p2p", "p2p_block"]  # "none": ipc-only job
+            # framework lanes only: the p2p schedule (gfx950 reduce) and the
+            # one-sided ipc kernels.  RCCL's own reduce-scatter + all-gather
+            # ("collective") is a comparator, never a candidate.  "none": ipc-only job
+            cands = [] if spec[0] == "none" else ["p2p", "p2p_block"]
             if self.device.type == "cuda" and try_ipc:
                 if not ipc_open:
                     err = None
@@ -448,11 +474,22 @@ class ThresholdAllreduce:
         return res
 
     def state(self) -> dict:
+        if self.transport == "onesided":
+            return {"link": {"lane": "onesided", "onesided": {**self._os.info(), "stats": self._os.stats()}},
+                    "stats": {"rounds_forced": self._os.stats()["complete_forced"]}}
         return self.worker.state()
+
+    def retire(self) -> None:
+        """Onesided transport: this rank serves no further round (the job's end)."""
+        if self.transport == "onesided":
+            self._os.retire()
 
     def synchronize(self) -> None:
         """Drain the reactive transport's in-flight transfers, then wait for
         this rank's queued device work."""
+        if self.transport == "onesided":
+            self._os.synchronize()
+            return
         self.drain()
         self.worker.synchronize()
 
@@ -465,6 +502,8 @@ class ThresholdAllreduce:
         on their own; there it only bounds the in-flight work.)"""
         import time
 
+        if self.transport == "onesided":
+            return  # nothing in flight between calls: every send completed inside its call
         core = self.worker._core
         if not core.reactive():
             return

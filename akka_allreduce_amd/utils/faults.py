@@ -119,8 +119,8 @@ def env_phase_stall(rank: int, phase: str) -> None:
     this rank and ``AKKA_FAULT_STALL_PHASE`` names the phase: a rank that never
     posts its side of a collective (tests the phase watchdog's failure line).
     ``AKKA_FAULT_STALL_MODE=raise`` raises instead (a rank-local error)."""
-    want = os.environ.get("AKKA_FAULT_STALL_RANK")
-    if want is None or int(want) != int(rank) or os.environ.get("AKKA_FAULT_STALL_PHASE") != phase:
+    want = os.environ.get("AKKA_FAULT_STALL_RANK")  # a rank, or "all"
+    if want is None or (want != "all" and int(want) != int(rank)) or os.environ.get("AKKA_FAULT_STALL_PHASE") != phase:
         return
     if os.environ.get("AKKA_FAULT_STALL_MODE") == "raise":
         raise RuntimeError(f"injected fault on rank {rank} in phase {phase}")

@@ -137,6 +137,26 @@ class PhaseGuard:
         self.phase = None
         return result
 
+    def try_run(self, phase: str, seconds: float, fn: Callable[[], Any]) -> tuple:
+        """Like ``run``, but an error that every rank AGREES on is returned
+        (result, {rank: error}) instead of ending the job, so the caller can
+        fall back (bench.py: RCCL init failing everywhere -> the ipc lane).  A
+        hang still ends the job at the deadline; no beacon is raised, so ranks
+        that fail a little later still reach the agreement."""
+        self.enter(phase, seconds)
+        err = None
+        result = None
+        progress(f"rank {self.rank}: phase {phase} (deadline {seconds:g} s, fallback allowed)")
+        try:
+            result = fn()
+        except Exception as e:
+            err = f"{type(e).__name__}: {e}"[:600]
+        errors = self._gather(phase, err) if self.world > 1 else ({self.rank: err} if err else {})
+        self.disarm()
+        self.history.append(phase if not errors else f"{phase}:failed")
+        self.phase = None
+        return result, errors
+
     def raise_beacon(self, phase: str, err: str) -> None:
         if not self.beacon_path:
             return

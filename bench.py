@@ -57,7 +57,11 @@ def parse():
     p.add_argument("--extras-only", default="", help="comma list of extra configs to run (cfg1,cfg3,cfg4,cfg5)")
     p.add_argument("--cfg4-size-mb", type=float, default=64.0, help="config 4 buffer (MiB)")
     p.add_argument("--cfg4-delay-ms", type=float, default=50.0, help="config 4 straggler delay per round")
-    p.add_argument("--cfg4-rounds", type=int, default=10)
+    p.add_argument("--cfg4-rounds", type=int, default=64,
+                   help="rounds per phase of config 4 (steady state: far more rounds than any buffering)")
+    p.add_argument("--cfg4-transport", choices=["onesided", "reactive"], default="onesided",
+                   help="config 4 data path: onesided (stores into mapped peer windows, no send ever waits) or "
+                        "reactive (RCCL pair communicators, two-sided)")
     p.add_argument("--extras-deadline-s", type=float, default=240.0,
                    help="give up on the extra configs after this many seconds (the headline line is still printed)")
     p.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
@@ -125,8 +129,98 @@ class _Skip(Exception):
     pass
 
 
-def run_cfg4(world: int, rank: int, dev, barrier, size_mb: float, delay_ms: float, rounds: int,
-             data_plane: str = "rccl") -> dict:
+def run_cfg4(world: int, rank: int, dev, barrier, size_mb: float, delay_ms: float, rounds: int) -> dict:
+    """BASELINE config 4 on the one-sided lane (transport="onesided",
+    csrc/transport/onesided.h): thReduce = thComplete = 0.75, maxLag 1, rank
+    N-1 an induced straggler.  Every send is a store into the receiver's
+    window, so the fast ranks never wait for the straggler -- in steady state,
+    not only until a buffer pool runs out (reference: fire-and-forget sends
+    W:227-232 / 259-264, outdated drops W:155-156 / 172-173, thresholds
+    SB:9-13 / RB:13-17, catch-up W:100-106).
+
+    Two phases of `rounds` rounds each, each ending at a common ROUND (with
+    thresholds < 1 ranks skip rounds by catch-up, so their call counts
+    differ): without the straggler, then with rank N-1 sleeping `delay_ms`
+    before each call.  Per phase: the fast ranks' median and p90 ms per call
+    over the second half (worst fast rank), their mean contributor count, the
+    straggler's calls and catch-up skips, drops and forced reduces."""
+    import statistics
+
+    import torch
+    import torch.distributed as dist
+
+    from akka_allreduce_amd.parallel import ThresholdAllreduce
+
+    esize = 4
+    S = int(size_mb * (1 << 20)) // esize
+    C = max(1, min(S, (4 << 20) // esize))
+    ar = ThresholdAllreduce(S, max_chunk_size=C, th_reduce=0.75, th_complete=0.75, max_lag=1, device=dev,
+                            transport="onesided")
+    run_cfg4.keep = ar  # type: ignore[attr-defined]
+    straggler = world - 1
+    g = torch.Generator(device=dev).manual_seed(77 + rank)
+    x = torch.randn(S, device=dev, generator=g)
+    out = torch.empty_like(x)
+    res = {"thresholds": [1.0, 0.75, 0.75], "max_lag": 1, "straggler_rank": straggler, "straggler_delay_ms": delay_ms,
+           "rounds_per_phase": rounds, "buffer_bytes": S * esize, "chunk_bytes": C * esize, "transport": "onesided",
+           "lane": ar.state()["link"]["onesided"]}
+    res["lane"].pop("stats", None)
+
+    def sync():
+        if dev.type == "cuda":
+            torch.cuda.current_stream(dev).synchronize()
+
+    last = -1
+    for pi, key in enumerate(("no_straggler", "with_straggler")):
+        target = (pi + 1) * rounds - 1
+        st0 = ar._os.stats()
+        ms, cnt, calls = [], [], 0
+        while last < target:
+            if key == "with_straggler" and rank == straggler:
+                time.sleep(delay_ms / 1e3)
+            t0 = time.perf_counter()
+            o = ar(x, out=out)
+            sync()
+            ms.append((time.perf_counter() - t0) * 1e3)
+            last = o.iteration
+            cnt.append(float(o.count.float().mean()))
+            calls += 1
+        st1 = ar._os.stats()
+        tail = sorted(ms[len(ms) // 2:])
+        mine = {"median_ms": statistics.median(tail), "p90_ms": tail[min(len(tail) - 1, int(0.9 * len(tail)))],
+                "calls": calls, "mean_count": sum(cnt) / len(cnt),
+                **{k: st1[k] - st0[k] for k in ("skipped_rounds", "scatter_outdated", "gather_outdated",
+                                                 "scatter_conflict", "gather_conflict", "reduce_forced",
+                                                 "complete_forced", "timeouts")}}
+        allv = [None] * world
+        dist.all_gather_object(allv, mine)
+        fast = [v for i, v in enumerate(allv) if i != straggler]
+        res[key] = {
+            "fast_rank_median_ms_per_round": round(max(v["median_ms"] for v in fast), 4),
+            "fast_rank_p90_ms_per_round": round(max(v["p90_ms"] for v in fast), 4),
+            "fast_rank_mean_count": round(sum(v["mean_count"] for v in fast) / len(fast), 4),
+            "fast_rank_calls": [v["calls"] for v in fast],
+            "straggler_calls": allv[straggler]["calls"],
+            "straggler_median_ms_per_call": round(allv[straggler]["median_ms"], 4),
+            "catch_up_skipped_rounds": sum(v["skipped_rounds"] for v in allv),
+            "outdated_pushes_dropped": sum(v["scatter_outdated"] + v["gather_outdated"] for v in allv),
+            "straggler_outdated_pushes_dropped": allv[straggler]["scatter_outdated"] + allv[straggler]["gather_outdated"],
+            "conflict_drops": sum(v["scatter_conflict"] + v["gather_conflict"] for v in allv),
+            "forced_chunk_reduces": sum(v["reduce_forced"] for v in allv),
+            "forced_completions": sum(v["complete_forced"] for v in allv),
+            "timeouts": sum(v["timeouts"] for v in allv),
+        }
+    a, b = res["no_straggler"], res["with_straggler"]
+    res["fast_rank_slowdown"] = round(b["fast_rank_median_ms_per_round"] / max(1e-9, a["fast_rank_median_ms_per_round"]),
+                                      3)
+    ar.retire()  # the job's end: nobody waits for this rank's later rounds
+    sync()
+    barrier()
+    return res
+
+
+def run_cfg4_reactive(world: int, rank: int, dev, barrier, size_mb: float, delay_ms: float, rounds: int,
+                      data_plane: str = "rccl") -> dict:
     """BASELINE config 4: threshold allreduce at thReduce = thComplete = 0.75,
     maxLag 1, with rank N-1 an induced straggler (sleeps ``delay_ms`` before
     each round), on the straggler-tolerant reactive transport (one pair
@@ -146,7 +240,7 @@ def run_cfg4(world: int, rank: int, dev, barrier, size_mb: float, delay_ms: floa
     C = max(1, min(S, (4 << 20) // esize))
     ar = ThresholdAllreduce(S, max_chunk_size=C, th_reduce=0.75, th_complete=0.75, max_lag=1, device=dev,
                             transport="reactive", data_plane=data_plane)
-    run_cfg4.keep = ar  # type: ignore[attr-defined]
+    run_cfg4_reactive.keep = ar  # type: ignore[attr-defined]
     straggler = world - 1
     g = torch.Generator(device=dev).manual_seed(77 + rank)
     x = torch.randn(S, device=dev, generator=g)
@@ -272,7 +366,8 @@ def apply_lane_choice(ar, name) -> None:
 
 
 def run_extras(world: int, dev, barrier, which=("cfg1", "cfg3", "cfg4", "cfg5"), rank: int = 0,
-               cfg4_size_mb: float = 64.0, cfg4_delay_ms: float = 50.0, cfg4_rounds: int = 10,
+               cfg4_size_mb: float = 64.0, cfg4_delay_ms: float = 50.0, cfg4_rounds: int = 64,
+               cfg4_transport: str = "onesided",
                lane: str | None = None, data_plane: str = "rccl") -> dict:
     """BASELINE config 3 (8-rank bf16, 1 GB buffer, link-sized chunks),
     config 4 (threshold 0.75/0.75 + straggler, N>1 only) and config 5 (2-layer
@@ -293,23 +388,17 @@ def run_extras(world: int, dev, barrier, which=("cfg1", "cfg3", "cfg4", "cfg5"),
     if "cfg4" in which and world > 1:
         progress(f"rank {rank}: extra cfg4")
         try:
-            # thresholds < 1 need a two-sided transport: RCCL pair communicators, or
-            # the mailbox p2p over mapped memory when the job runs without RCCL
-            res["cfg4_threshold_straggler"] = run_cfg4(world, rank, dev, barrier, cfg4_size_mb, cfg4_delay_ms,
-                                                       cfg4_rounds,
-                                                       data_plane="rccl" if data_plane == "rccl" else "ipc_p2p")
+            if cfg4_transport == "onesided":
+                res["cfg4_threshold_straggler"] = run_cfg4(world, rank, dev, barrier, cfg4_size_mb, cfg4_delay_ms,
+                                                           cfg4_rounds)
+            else:
+                # the two-sided alternative: RCCL pair communicators, or the
+                # mailbox p2p over mapped memory when the job runs without RCCL
+                res["cfg4_threshold_straggler"] = run_cfg4_reactive(
+                    world, rank, dev, barrier, cfg4_size_mb, cfg4_delay_ms, cfg4_rounds,
+                    data_plane="rccl" if data_plane == "rccl" else "ipc_p2p")
         except Exception as e:
             res["cfg4_error"] = f"{type(e).__name__}: {e}"[:300]
-            if data_plane == "rccl" and dev.type == "cuda":
-                # the pair communicators failed: the same schedule over the
-                # mailbox p2p in mapped peer memory (no RCCL)
-                try:
-                    r4 = run_cfg4(world, rank, dev, barrier, cfg4_size_mb, cfg4_delay_ms, cfg4_rounds,
-                                  data_plane="ipc_p2p")
-                    r4["data_plane"] = "ipc_p2p (after the RCCL attempt failed)"
-                    res["cfg4_threshold_straggler"] = r4
-                except Exception as e2:
-                    res["cfg4_error_ipc_p2p"] = f"{type(e2).__name__}: {e2}"[:300]
     try:
         if "cfg3" not in which:
             raise _Skip()
@@ -487,7 +576,23 @@ def main() -> int:
                                   device=dev, transport=args.transport, lane=args.lane,
                                   data_plane=args.data_plane)
 
-    ar = guard.run("rccl_init", dl, rccl_init)
+    # RCCL failing on EVERY rank (agreed) does not cost the headline: the job
+    # is rebuilt in this same process on the ipc data plane (one-sided xGMI,
+    # no RCCL communicator at all) and the line says so.  A failure on some
+    # ranks only, or a hang, still ends the job with the failure line.
+    ar, init_errors = guard.try_run("rccl_init", dl, rccl_init)
+    rccl_fallback = None
+    if init_errors:
+        if (len(init_errors) == world and world > 1 and args.data_plane == "rccl" and dev.type == "cuda"
+                and args.transport == "stream"):
+            rccl_fallback = {"rccl_init_errors": {str(k): v[:200] for k, v in init_errors.items()},
+                             "data_plane": "ipc"}
+            args.data_plane = "ipc"
+            ar = guard.run("ipc_init", dl, lambda: ThresholdAllreduce(
+                S, max_chunk_size=C, dtype=dtype, max_lag=args.max_lag, broadcast_lag=args.bcast_lag, device=dev,
+                data_plane="ipc"))
+        else:
+            guard.fail("rccl_init", "error", init_errors)
 
     def identity():
         me = _identity(ar, dev)
@@ -698,6 +803,10 @@ def main() -> int:
         "rccl_version": _rccl_version() if rccl_kind else None,
         "rank_devices": ranks,
         "lane": lane_used,
+        # the headline's lane is one of the framework's (p2p schedule with the
+        # gfx950 reduce, or the one-sided ipc kernels) unless --lane collective
+        # forced RCCL's own reduce-scatter + all-gather
+        "lane_is_framework": lane_used != "collective",
         "other_lane": lane_other,
         "lane_select": lane_sel,
         "rccl_allreduce_algbw_GBps": round(rccl, 3) if rccl else None,
@@ -714,6 +823,8 @@ def main() -> int:
     })
     if rccl_err:
         line["rccl_compare_error"] = rccl_err
+    if rccl_fallback:
+        line["rccl_fallback"] = rccl_fallback
     if os.environ.get("AKKA_SHARE_GPU") == "1" and world > 1:
         line["data"] += "; N ranks sharing ONE GPU (rehearsal of the N-rank flow, not the metric)"
     if world == 1:
@@ -735,7 +846,8 @@ def main() -> int:
         guard.arm(args.extras_deadline_s, late, exit_code=0 if ok in (None, True) else 1)
         which = tuple(args.extras_only.split(",")) if args.extras_only else ("cfg1", "cfg3", "cfg4", "cfg5")
         line["extra_configs"] = run_extras(world, dev, barrier, which, rank, args.cfg4_size_mb,
-                                           args.cfg4_delay_ms, args.cfg4_rounds, lane=chosen_lane,
+                                           args.cfg4_delay_ms, args.cfg4_rounds, cfg4_transport=args.cfg4_transport,
+                                           lane=chosen_lane,
                                            data_plane=args.data_plane)
         if chosen_lane and world > 1:
             line["extra_configs"]["lane"] = chosen_lane

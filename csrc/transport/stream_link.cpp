@@ -210,8 +210,10 @@ bool StreamLink::bulk_round(int32_t r) {
   if (N < 2) return false;  // a local round is already one pass
   AKKA_CHECK(p2p_->nranks() == N && p2p_->rank() == dp_->me(), "p2p communicator does not match the worker geometry");
   const bool native = p2p_->has_collectives() && g.S == int64_t(N) * g.step;
+  // Auto = the framework's own p2p schedule (gfx950 reduce); RCCL's
+  // reduce-scatter + all-gather runs only when asked for by name.
   if (lane_ == Lane::Ipc) ipc_round(r);
-  else if (lane_ == Lane::Collective || (lane_ == Lane::Auto && native)) collective_round(r, native);
+  else if (lane_ == Lane::Collective) collective_round(r, native);
   else exact_steps(r);
   p2p_->check();
   stats_.rounds++;

@@ -49,8 +49,9 @@ struct StreamLinkStats {
 //             buffer when the geometry is even (S == N * step), otherwise a
 //             whole-block direct exchange (one grouped p2p per phase around
 //             one N-way reduce);
-//  Auto       Collective when the transport has native collectives and the
-//             geometry is even, else P2P;
+//  Auto       P2P: the framework's own schedule.  (Until round 2 Auto picked
+//             RCCL's collectives when the geometry was even; they are now a
+//             comparator that runs only when asked for by name.)
 //  Ipc        one-sided xGMI loads/stores between mapped windows (ipc_lane.h),
 //             once set_ipc() handed the link an opened IpcLane.
 // Exact rounds never go through the engine's per-chunk message flow: their

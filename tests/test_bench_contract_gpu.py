@@ -61,7 +61,7 @@ def test_bench_multirank_on_one_card(plane):
         port = s.getsockname()[1]
     n = 4 if plane == "ipc_p2p" else 2
     extra = ["--extras", "on", "--extras-only", "cfg4", "--cfg4-size-mb", "4", "--cfg4-delay-ms", "40",
-             "--cfg4-rounds", "4"] if plane == "ipc_p2p" else ["--extras", "off"]
+             "--cfg4-rounds", "48"] if plane == "ipc_p2p" else ["--extras", "off"]
     env = dict(os.environ, AKKA_SHARE_GPU="1", GPU_MAX_HW_QUEUES="8")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
                         "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
@@ -79,9 +79,36 @@ def test_bench_multirank_on_one_card(plane):
     assert all(sel[k]["exact"] is True for k in cands), sel
     assert d["lane"] == sel["chosen"]
     if plane == "ipc_p2p":
-        assert {"collective", "p2p", "p2p_block", "ipc", "ipc_bcast", "ipc_fused", "ipc_fused_bcast", "ipc_wide",
-                "ipc_bcast_wide"} <= set(cands)
+        assert {"p2p", "p2p_block", "ipc", "ipc_bcast", "ipc_fused", "ipc_fused_bcast", "ipc_wide",
+                "ipc_bcast_wide"} <= set(cands) and "collective" not in cands
+        assert d["lane_is_framework"] is True
         c4 = d["extra_configs"]["cfg4_threshold_straggler"]
-        assert c4["fast_rank_ms_per_round_with_straggler"] < c4["straggler_ms_per_round_with_straggler"], c4
+        w = c4["with_straggler"]
+        assert c4["transport"] == "onesided" and w["timeouts"] == 0, c4
+        assert w["fast_rank_median_ms_per_round"] < 40 / 4 and w["catch_up_skipped_rounds"] > 0, c4
     else:
         assert set(cands) == {"ipc", "ipc_bcast", "ipc_fused", "ipc_fused_bcast", "ipc_wide", "ipc_bcast_wide"}
+
+
+def test_bench_rccl_init_failure_falls_back_to_ipc():
+    """RCCL init raising on EVERY rank (injected: AKKA_FAULT_STALL_RANK=all,
+    phase rccl_init, mode raise) does not cost the headline: the job is rebuilt
+    in the same processes on the ipc data plane and the line says so."""
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, AKKA_SHARE_GPU="1", GPU_MAX_HW_QUEUES="8", AKKA_FAULT_STALL_RANK="all",
+               AKKA_FAULT_STALL_PHASE="rccl_init", AKKA_FAULT_STALL_MODE="raise")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+                        "--gpus", "2", "--steps", "3", "--warmup", "1", "--size-mb", "16", "--compare-rccl", "off",
+                        "--extras", "off"], capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip().startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert d["rccl_fallback"]["data_plane"] == "ipc" and set(d["rccl_fallback"]["rccl_init_errors"]) == {"0", "1"}
+    assert d["config"]["data_plane"] == "ipc" and d["lane"].startswith("ipc") and d["lane_is_framework"] is True
+    assert d["exact"] is True and d["value"] > 0

@@ -36,6 +36,12 @@ def run_ranks(n, *extra, timeout=240, device="cpu"):
         for i in range(n):
             p = os.path.join(out, f"rank{i}.json")
             rows.append(json.load(open(p)) if os.path.exists(p) else None)
+    keep = os.environ.get("AKKA_TEST_KEEP")  # evidence runs: keep every rank's record
+    if keep:
+        os.makedirs(keep, exist_ok=True)
+        tag = "_".join(a.lstrip("-") for a in extra if not a.startswith("/"))[:120].replace("/", "")
+        with open(os.path.join(keep, f"onesided_{device}_n{n}_{tag}.json"), "w") as f:
+            json.dump({"args": list(extra), "rc": r.returncode, "rows": rows}, f)
     return r, rows
 
 
