@@ -39,6 +39,7 @@ HOST_SOURCES = [
     "runtime/watchdog.cpp",
     "bindings/bindings.cpp",
     "bindings/bind_onesided.cpp",
+    "bindings/bind_probe.cpp",
 ]
 HIP_SOURCES = ["kernels/kernels.hip", "kernels/ipc.hip", "kernels/onesided.hip"]
 

@@ -34,6 +34,7 @@ using namespace akka;
 namespace akka {
 bool host_device_step(Device* d, uint32_t rotate);  // host_device.cpp
 void bind_onesided(py::module_& m);                 // bind_onesided.cpp
+void bind_probe(py::module_& m);                    // bind_probe.cpp
 }
 
 namespace {
@@ -584,6 +585,7 @@ PYBIND11_MODULE(_native, m) {
   m.doc() = "MI355X-native threshold allreduce core (engine, gfx950 kernels, RCCL/xGMI transport)";
   py::register_exception<AkkaError>(m, "AkkaError", PyExc_RuntimeError);
   bind_onesided(m);
+  bind_probe(m);
 
   py::class_<OutMsg>(m, "OutMsg")
       .def_readonly("kind", &OutMsg::kind)

@@ -45,3 +45,18 @@ def test_onesided_gpu_straggler_steady_state():
         assert strag <= 2 * base + 1.0, (d["rank"], base, strag)
     s = rows[3]["stats"]
     assert s["skipped_rounds"] > 0 and s["scatter_outdated"] + s["gather_outdated"] > 0, s
+
+
+def test_onesided_gpu_straggler_killed_mid_run():
+    """The straggler process exits abruptly (os._exit: no retire, no
+    teardown) after 3 calls of the straggler phase while the survivors keep
+    storing into its (still mapped) window: they complete every round to the
+    end, contributor sets consistent, no timeout."""
+    r, rows = run_ranks(4, "--mode", "straggler", "--straggler", "3", "--rounds", "48", "--compute-ms", "2",
+                        "--delay-ms", "30", "--kill-after", "3", "--size", str(1 << 20), "--chunk", str(1 << 16),
+                        "--timeout-s", "10", device="cuda", timeout=180)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert rows[3]["killed_after"] == 3
+    for d in rows[:3]:
+        assert d["error"] == 0 and d["straggler"]["bad_chunks"] == 0, d["stats"]
+        assert d["straggler"]["rounds"][-1] >= 95 and d["stats"]["timeouts"] == 0
