@@ -115,6 +115,7 @@ class RoundPacer:
 
         self.store = store
         self.prefix = prefix
+        self.world = int(world)
         self.need = float(np.float32(world) * np.float32(th_allreduce))
         self.timeout = timeout
         self.waited_s = 0.0
@@ -147,6 +148,16 @@ class RoundPacer:
         if dt > 1e-4:
             self.waits += 1
         self.waited_s += dt
+        # Key r-1 is read only by ranks starting round r.  The last of the N
+        # ranks to pass here removes it (and its own pass counter), so the
+        # store hosted by rank 0 does not grow by a key per round forever.
+        passed = f"{self.prefix}/passed/{r - 1}"
+        if self.store.add(passed, 1) >= self.world:
+            for k in (key, passed):
+                try:
+                    self.store.delete_key(k)
+                except Exception:  # noqa: BLE001 - a store without deletion keeps the keys
+                    pass
 
 
 class ThresholdAllreduce:
@@ -416,9 +427,7 @@ class ThresholdAllreduce:
                         self.enable_ipc()
                     except Exception as e:  # noqa: BLE001 - the ipc lanes are skipped
                         err = f"{type(e).__name__}: {e}"[:200]
-                    flag = torch.tensor([0 if err else 1])
-                    dist.all_reduce(flag, op=dist.ReduceOp.MIN)
-                    ipc_open = bool(flag.item())
+                    ipc_open = self._agree_max([1.0 if err else 0.0])[0] == 0.0
                     if not ipc_open:
                         res["ipc"] = {"exact": None, "ms": None,
                                       "error": err or "another rank could not open its windows"}
@@ -444,24 +453,25 @@ class ThresholdAllreduce:
             ok, ms, err = False, 0.0, None
             try:
                 self.use_lane(name)
-                ok = exact(1) and exact(2)
-                if ok:
+                # every rank runs the same rounds whatever its local verdicts:
+                # a rank that skipped rounds would leave its peers waiting
+                e1 = exact(1)
+                e2 = exact(2)
+                o = self(x, async_op=cuda, out=buf)
+                o.wait()
+                sync()
+                t0 = time.perf_counter()
+                for _ in range(rounds):  # the ranks are coupled by the rounds themselves
                     o = self(x, async_op=cuda, out=buf)
-                    o.wait()
-                    sync()
-                    t0 = time.perf_counter()
-                    for _ in range(rounds):  # the ranks are coupled by the rounds themselves
-                        o = self(x, async_op=cuda, out=buf)
-                    o.wait()
-                    sync()
-                    ms = (time.perf_counter() - t0) / rounds * 1e3
-                    ok = exact(3)
+                o.wait()
+                sync()
+                ms = (time.perf_counter() - t0) / rounds * 1e3
+                ok = e1 and e2 and exact(3)
             except Exception as e:  # noqa: BLE001 - the candidate is rejected
                 ok, err = False, f"{type(e).__name__}: {e}"[:160]
-            t = torch.tensor([0.0 if ok else 1.0, ms], dtype=torch.float64)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            good = float(t[0].item()) == 0.0
-            res[name] = {"exact": good, "ms": round(float(t[1].item()), 4) if good else None}
+            bad, worst = self._agree_max([0.0 if ok else 1.0, ms])
+            good = bad == 0.0
+            res[name] = {"exact": good, "ms": round(worst, 4) if good else None}
             if err:
                 res[name]["error"] = err
         good = [n for n in cands if res[n]["exact"]]
@@ -472,6 +482,30 @@ class ThresholdAllreduce:
         res["chosen"] = pick
         self.tuned = res
         return res
+
+    def _agree_max(self, vals: list) -> list:
+        """Element-wise max over ranks of a few floats.  Over the job's store
+        when one was given; else over torch.distributed with a tensor the
+        default group's backend can reduce (a CUDA tensor for nccl = RCCL,
+        which has no CPU path; a CPU tensor for gloo)."""
+        import json
+
+        vals = [float(v) for v in vals]
+        if self.world_size < 2:
+            return vals
+        if self.store is not None:
+            seq = getattr(self, "_agree_seq", 0)
+            self._agree_seq = seq + 1
+            key = f"akka/agree/{self._iid}/{seq}"
+            self.store.set(f"{key}/{self.rank}", json.dumps(vals))
+            rows = [json.loads(bytes(self.store.get(f"{key}/{i}")).decode()) for i in range(self.world_size)]
+            return [max(r[j] for r in rows) for j in range(len(vals))]
+        import torch.distributed as dist
+
+        dev = self.device if (dist.get_backend() == "nccl" and self.device.type == "cuda") else torch.device("cpu")
+        t = torch.tensor(vals, dtype=torch.float64 if dev.type == "cpu" else torch.float32, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return [float(v) for v in t.cpu().tolist()]
 
     def state(self) -> dict:
         if self.transport == "onesided":

@@ -517,6 +517,9 @@ void DataPlane::finalize(int32_t round, const std::vector<uint8_t>& landed) {
       if (b.counts) dev_->zero(cs, b.counts + size_t(j) * kmax_ + k0, size_t(k - k0) * sizeof(int32_t));
     }
   }
+  // a round of a lane that failed (a wait timed out / the lane was aborted)
+  // never comes back as exact: its counts read 0 everywhere
+  if (poison_flag_ && b.counts) dev_->poison_counts_if(cs, poison_flag_, b.counts, size_t(g_.N) * kmax_);
   if (b.exec_on_producer) {
     dev_->flush(cs);  // the round's launch must not wait for the next round to merge into
     b.done_lazy = true;

@@ -75,6 +75,9 @@ class DataPlane {
   // --- phase 2 receive side --------------------------------------------------
   void store_reduced(int32_t round, int32_t src, int32_t k, const Payload& p);
   void set_count(int32_t round, int32_t block, int32_t k, int32_t count);
+  // Error word of the lane that moves the next rounds (nullptr: none): a
+  // round finalized while it is set gets all-zero counts (ipc lane failure).
+  void set_poison_flag(const uint32_t* f) { poison_flag_ = f; }
   // Copy host-known counts of the given blocks into the round's counts tensor.
   void upload_counts(int32_t round, const std::vector<int32_t>& blocks, StreamH s);
 
@@ -204,6 +207,7 @@ class DataPlane {
   // counts upload / finalize skip the wait for the caller's hand-over point,
   // i.e. the round-2 counts-fill race comes back.
   bool fault_skip_output_wait_ = false;
+  const uint32_t* poison_flag_ = nullptr;
   int32_t max_slots_ = 0;
   std::vector<SendSlot> slots_;
   std::map<int32_t, size_t> slot_of_;

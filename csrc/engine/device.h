@@ -83,6 +83,9 @@ class Device {
   virtual void copy(StreamH s, void* dst, const void* src, size_t bytes, CopyKind kind) = 0;
   virtual void zero(StreamH s, void* dst, size_t bytes) = 0;
   virtual void fill_i32(StreamH s, int32_t* dst, int32_t value, size_t n) = 0;
+  // counts[0..n) = 0 if *flag != 0 when the stream gets there (a failed
+  // one-sided round).  Host devices never run those rounds.
+  virtual void poison_counts_if(StreamH, const uint32_t* /*flag*/, int32_t* /*counts*/, size_t /*n*/) {}
   // Issue any work held back on `s` (reduce launches kept open for merging).
   virtual void flush(StreamH) {}
 

@@ -217,6 +217,11 @@ class HipDevice final : public Device {
     flush_if(s);
     AKKA_HIP(hipMemsetD32Async(dst, value, n, static_cast<hipStream_t>(s)));
   }
+  void poison_counts_if(StreamH s, const uint32_t* flag, int32_t* counts, size_t n) override {
+    if (!n) return;
+    flush_if(s);
+    launch_poison_counts(static_cast<hipStream_t>(s), flag, counts, int64_t(n));
+  }
   void flush(StreamH s) override { flush_if(s); }
 
  private:

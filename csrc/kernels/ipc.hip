@@ -12,9 +12,11 @@
 // compiler may drop its own when it proves the scoreboard empty, letting the
 // flag overtake the write-back (MI355X_MICROARCH.md, compiler hazard).
 // Every wait is bounded (wall clock, `timeout` ticks): on expiry the waiting
-// workgroup sets the window's error word, skips its data work and still
-// signals, so every grid drains and no GPU is ever left spinning; the round is
-// then reported as failed (IpcLane::error) and must not be trusted.
+// workgroup sets this rank's error word and the abort word of EVERY rank's
+// flag area (wait_flag), skips its data work and still signals, so every grid
+// drains and no GPU is ever left spinning.  Every rank's later waits fail on
+// the abort word, its round's counts are poisoned to 0 behind the round
+// (DataPlane::finalize), and its next round on the lane raises.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -30,16 +32,35 @@ constexpr int kMaxThreads = 1024;  // launch bound of the one-sided round kernel
 constexpr int kReduceSplit = kIpcReduceSplit;
 using namespace xgmi;
 
-// Lane 0 only.  true once *f reached `want`; false on timeout or when another
-// workgroup already reported one (err != 0).
-__device__ bool wait_flag(uint32_t* f, uint32_t want, uint32_t* err, uint64_t deadline) {
+// Lane 0 only.  true once *f reached `want` and no rank aborted the lane.
+// On timeout this rank ABORTS the lane: the abort word of every rank's flag
+// area is set before this workgroup signals anything (its release orders the
+// stores), so a peer that sees one of this rank's flags also sees the abort
+// and never consumes data this rank did not produce.  A peer's abort, or an
+// earlier timeout of this rank, makes every later wait fail too; the failed
+// round's counts are then poisoned to 0 (DataPlane::finalize) and the next
+// round on the lane raises.
+__device__ bool wait_flag(const IpcArgs& a, uint32_t* f, uint32_t want, uint64_t deadline) {
+  uint32_t* abort_me = a.flags[a.me] + ipc_flag_error(a.N, a.nportions);
   uint32_t spins = 0;
   while (true) {
-    if (reached(sys_load(f), want)) return true;
+    if (reached(sys_load(f), want)) {
+      // a producer that aborted stored the abort before its flag (release)
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      if (sys_load(abort_me) != 0) {
+        sys_store(a.err, 1u);
+        return false;
+      }
+      return true;
+    }
     if ((++spins & 63) == 0) {
-      if (sys_load(err) != 0) return false;
+      if (sys_load(a.err) != 0 || sys_load(abort_me) != 0) {
+        sys_store(a.err, 1u);
+        return false;
+      }
       if (wall_clock64() > deadline) {
-        __hip_atomic_store(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        sys_store(a.err, 1u);
+        for (int32_t p = 0; p < a.N; ++p) sys_store(a.flags[p] + ipc_flag_error(a.N, a.nportions), 1u);
         return false;
       }
     }
@@ -143,14 +164,13 @@ __device__ void reduce_item(const IpcArgs& a, int32_t j, int32_t part) {
   constexpr int ES = sizeof(T);
   const int32_t me = a.me, N = a.N, np = a.nportions;
   uint32_t* fl = a.flags[me];
-  uint32_t* err = a.err;
   // each item's part of its portion (a multiple of 64 elements)
   const int64_t per = ((a.portion / kReduceSplit) + 63) / 64 * 64;
   bool ok = true;
   if (threadIdx.x == 0) {
     const uint64_t deadline = wall_clock64() + a.timeout;
     for (int32_t s = 0; s < N && ok; ++s)
-      if (s != me) ok = wait_flag(fl + ipc_flag_push(s, j, np), a.round, err, deadline);
+      if (s != me) ok = wait_flag(a, fl + ipc_flag_push(s, j, np), a.round, deadline);
   }
   ok = acquire_all(ok);
   const int64_t e0 = int64_t(j) * a.portion;
@@ -180,14 +200,13 @@ __device__ void reduce_item(const IpcArgs& a, int32_t j, int32_t part) {
 template <int ES>
 __device__ void phase2_item(const IpcArgs& a, int32_t j, int32_t p) {
   const int32_t me = a.me, N = a.N, np = a.nportions;
-  uint32_t* err = a.err;
   bool ok = true;
   if (threadIdx.x == 0) {
     const uint64_t deadline = wall_clock64() + a.timeout;
     for (int32_t part = 0; part < kReduceSplit && ok; ++part)
-      ok = wait_flag(a.bcast ? a.flags[me] + ipc_flag_gather(p, j, part, N, np)
+      ok = wait_flag(a, a.bcast ? a.flags[me] + ipc_flag_gather(p, j, part, N, np)
                              : a.flags[p] + ipc_flag_reduced(j, part, N, np),
-                     a.round, err, deadline);
+                     a.round, deadline);
   }
   ok = acquire_all(ok);
   const int64_t e0 = int64_t(j) * a.portion;
@@ -291,11 +310,16 @@ __device__ bool wait_flag_p2p(uint32_t* f, uint32_t want, uint32_t* err, const u
   }
 }
 
-// grid = nqueues * wpp.  Workgroup (queue, w) moves part w of every piece of
-// every op of its queue, in order.
+// grid = nqueues * wpg.  Workgroup (queue, w0) moves parts w0, w0 + wpg, ...
+// (< wpp) of every piece of every op of its queue, pieces in order.  Every
+// wait of a send is on an EARLIER piece of the peer and every wait of a
+// receive on the same piece of a send, so with all workgroups resident no
+// cycle of waits exists however the parts are grouped (ipc_p2p_resident_wgs
+// bounds the grid).
 __global__ __launch_bounds__(kThreads) void ipc_p2p_kernel(IpcP2PArgs a) {
-  const int32_t qi = int32_t(blockIdx.x) / a.wpp;
-  const int32_t w = int32_t(blockIdx.x) % a.wpp;
+  const int32_t wpg = a.wpg > 0 ? a.wpg : a.wpp;
+  const int32_t qi = int32_t(blockIdx.x) / wpg;
+  const int32_t w0 = int32_t(blockIdx.x) % wpg;
   const int32_t me = a.me;
   for (int32_t oi = a.qstart[qi]; oi < a.qstart[qi + 1]; ++oi) {
     const IpcP2POp op = a.ops[oi];
@@ -307,36 +331,38 @@ __global__ __launch_bounds__(kThreads) void ipc_p2p_kernel(IpcP2PArgs a) {
       const int64_t pb0 = k * a.piece;
       const int64_t pbytes = min(a.piece, op.bytes - pb0);
       const int64_t part = ((pbytes + a.wpp - 1) / a.wpp + 15) / 16 * 16;
-      const int64_t b0 = min(pbytes, int64_t(w) * part), b1 = min(pbytes, b0 + part);
-      bool ok = true;
-      if (op.send) {
-        if (threadIdx.x == 0 && seq >= uint32_t(a.nslots)) {
-          const uint64_t deadline = wall_clock64() + a.timeout;
-          ok = wait_flag_p2p(a.flags[me] + ipc_p2p_flag_consumed(peer, ch, slot, w, a.N, a.nch, a.nslots, a.wpp),
-                             seq - uint32_t(a.nslots) + 1u, a.err, a.dead, peer, deadline);
+      for (int32_t w = w0; w < a.wpp; w += wpg) {
+        const int64_t b0 = min(pbytes, int64_t(w) * part), b1 = min(pbytes, b0 + part);
+        bool ok = true;
+        if (op.send) {
+          if (threadIdx.x == 0 && seq >= uint32_t(a.nslots)) {
+            const uint64_t deadline = wall_clock64() + a.timeout;
+            ok = wait_flag_p2p(a.flags[me] + ipc_p2p_flag_consumed(peer, ch, slot, w, a.N, a.nch, a.nslots, a.wpp),
+                               seq - uint32_t(a.nslots) + 1u, a.err, a.dead, peer, deadline);
+          }
+          ok = acquire_all(ok);
+          if (ok && b1 > b0)
+            copy_bytes(a.mbox[peer] + ipc_p2p_box(me, ch, slot, a.nch, a.nslots) * a.piece + b0, op.buf + pb0 + b0,
+                       b1 - b0);
+          release_wg();
+          if (threadIdx.x == 0)
+            signal(a.flags[peer] + ipc_p2p_flag_written(me, ch, slot, w, a.nch, a.nslots, a.wpp), seq + 1u);
+        } else {
+          if (threadIdx.x == 0) {
+            const uint64_t deadline = wall_clock64() + a.timeout;
+            ok = wait_flag_p2p(a.flags[me] + ipc_p2p_flag_written(peer, ch, slot, w, a.nch, a.nslots, a.wpp),
+                               seq + 1u, a.err, a.dead, peer, deadline);
+          }
+          ok = acquire_all(ok);
+          if (ok && b1 > b0)
+            copy_in(op.buf + pb0 + b0, a.mbox[me] + ipc_p2p_box(peer, ch, slot, a.nch, a.nslots) * a.piece + b0,
+                    b1 - b0);
+          release_wg();
+          if (threadIdx.x == 0)
+            signal(a.flags[peer] + ipc_p2p_flag_consumed(me, ch, slot, w, a.N, a.nch, a.nslots, a.wpp), seq + 1u);
         }
-        ok = acquire_all(ok);
-        if (ok && b1 > b0)
-          copy_bytes(a.mbox[peer] + ipc_p2p_box(me, ch, slot, a.nch, a.nslots) * a.piece + b0, op.buf + pb0 + b0,
-                     b1 - b0);
-        release_wg();
-        if (threadIdx.x == 0)
-          signal(a.flags[peer] + ipc_p2p_flag_written(me, ch, slot, w, a.nch, a.nslots, a.wpp), seq + 1u);
-      } else {
-        if (threadIdx.x == 0) {
-          const uint64_t deadline = wall_clock64() + a.timeout;
-          ok = wait_flag_p2p(a.flags[me] + ipc_p2p_flag_written(peer, ch, slot, w, a.nch, a.nslots, a.wpp),
-                             seq + 1u, a.err, a.dead, peer, deadline);
-        }
-        ok = acquire_all(ok);
-        if (ok && b1 > b0)
-          copy_in(op.buf + pb0 + b0, a.mbox[me] + ipc_p2p_box(peer, ch, slot, a.nch, a.nslots) * a.piece + b0,
-                  b1 - b0);
-        release_wg();
-        if (threadIdx.x == 0)
-          signal(a.flags[peer] + ipc_p2p_flag_consumed(me, ch, slot, w, a.N, a.nch, a.nslots, a.wpp), seq + 1u);
+        __syncthreads();  // `ok` is rewritten by the next part
       }
-      __syncthreads();  // `ok` is rewritten by the next piece
     }
   }
 }
@@ -345,7 +371,15 @@ __global__ __launch_bounds__(kThreads) void ipc_p2p_kernel(IpcP2PArgs a) {
 
 void launch_ipc_p2p_group(hipStream_t s, const IpcP2PArgs& a) {
   if (a.nqueues <= 0) return;
-  hipLaunchKernelGGL(ipc_p2p_kernel, dim3(unsigned(a.nqueues * a.wpp)), dim3(kThreads), 0, s, a);
+  const int32_t wpg = a.wpg > 0 ? a.wpg : a.wpp;
+  hipLaunchKernelGGL(ipc_p2p_kernel, dim3(unsigned(a.nqueues * wpg)), dim3(kThreads), 0, s, a);
+}
+
+int32_t ipc_p2p_resident_wgs(int32_t device) {
+  int bpm = 0, cus = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpm, ipc_p2p_kernel, kThreads, 0) != hipSuccess) bpm = 4;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) cus = 256;
+  return std::max(1, bpm) * std::max(1, cus);
 }
 
 void launch_ipc_round(hipStream_t s, const IpcArgs& a, DType dt) {

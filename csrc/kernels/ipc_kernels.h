@@ -99,7 +99,8 @@ struct IpcP2PArgs {
   uint32_t* err;                  // host-pinned: set on a timed-out wait or a dead peer
   const uint32_t* dead;           // host-pinned [N]: peers aborted by the host
   int64_t piece;
-  int32_t nslots, wpp, nch, N, me, nops, nqueues, pad;
+  int32_t nslots, wpp, nch, N, me, nops, nqueues;
+  int32_t wpg;  // workgroups per queue actually launched (<= wpp; each serves parts w, w + wpg, ...)
   uint64_t timeout;
   int16_t qstart[kIpcP2PMaxOps + 1];  // ops of queue i: [qstart[i], qstart[i+1]), in issue order
   IpcP2POp ops[kIpcP2PMaxOps];
@@ -124,6 +125,10 @@ __host__ __device__ inline size_t ipc_p2p_flag_bytes(int32_t N, int32_t nch, int
 // workgroups that walk its ops in order; all queues run concurrently (the
 // group semantics of a grouped send/recv).
 void launch_ipc_p2p_group(hipStream_t s, const IpcP2PArgs& a);
+// Workgroups of the group kernel the device can hold at once (occupancy x
+// CUs): every workgroup of a group must be resident together (a queue's
+// workgroup may wait on a peer's, which waits on another of this group).
+int32_t ipc_p2p_resident_wgs(int32_t device);
 
 // Enqueue one round on `s`: push, reduce, then pull (bcast = 0) or, with
 // bcast = 1, the reducer writes its rows into every peer's gather slot and a

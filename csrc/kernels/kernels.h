@@ -27,6 +27,9 @@ void launch_count_expand(hipStream_t s, int32_t* out, const int32_t* counts, int
 // `axpy`: dst += alpha * that mean (fused SGD update).
 void launch_count_mean(hipStream_t s, void* dst, const void* src, const int32_t* counts, int64_t S, int64_t step,
                        int32_t N, int64_t C, int32_t kmax, DType dt, bool axpy = false, float alpha = 0.f);
+// counts[0..n) = 0 if *flag != 0 (read when the kernel runs): poisons the
+// counts of a one-sided round whose waits failed.
+void launch_poison_counts(hipStream_t s, const uint32_t* flag, int32_t* counts, int64_t n);
 // Standalone kernels for tests/bench: out = a (+ b ...) via a pointer table on device.
 ReduceImpl reduce_impl_from_env();
 const char* reduce_impl_name(ReduceImpl i);

@@ -551,6 +551,22 @@ void launch_reduce(hipStream_t s, const ReduceSpec& spec, DType dt, ReduceImpl i
   }
 }
 
+namespace {
+// A failed one-sided round (ipc lane wait timed out / aborted): every count
+// of the round becomes 0, so the output is never handed back as exact.
+__global__ void poison_counts_kernel(const uint32_t* flag, int32_t* counts, int64_t n) {
+  if (__hip_atomic_load(const_cast<uint32_t*>(flag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0) return;
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
+    counts[i] = 0;
+}
+}  // namespace
+
+void launch_poison_counts(hipStream_t s, const uint32_t* flag, int32_t* counts, int64_t n) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(poison_counts_kernel, dim3(unsigned(std::min<int64_t>(64, (n + 255) / 256))), dim3(256), 0, s,
+                     flag, counts, n);
+}
+
 void launch_count_expand(hipStream_t s, int32_t* out, const int32_t* counts, int64_t S, int64_t step, int32_t N,
                          int64_t C, int32_t kmax) {
   if (S <= 0) return;

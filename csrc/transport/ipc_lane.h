@@ -79,6 +79,8 @@ class IpcLane {
   // error_now() as far as the kernels got (no synchronisation).
   uint32_t error();
   uint32_t error_now() const;
+  // device view of the host-mapped error word (the poison flag of the rounds)
+  const uint32_t* error_word_device() const { return err_dev_; }
   int32_t nportions() const { return nportions_; }
   int64_t portion_elems() const { return portion_; }
   size_t window_bytes() const { return data_bytes_; }

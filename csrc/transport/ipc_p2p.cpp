@@ -68,6 +68,11 @@ class IpcP2P final : public P2P {
     // workgroups per piece: 32 keeps more copies in flight (-6 % per 256 MiB round
     // vs 8 on 4 ranks sharing a card, profiles/r02/ipc_p2p)
     wpp_ = int32_t(std::clamp<int64_t>(env_i64("AKKA_IPC_P2P_WGS", 32), 1, 64));
+    // A group's workgroups must all be resident at once; keep the grid within
+    // half of what the device holds (the other half: other kernels, other
+    // ranks sharing the card in tests) by giving each queue fewer workgroups
+    // than parts when needed (each then serves several parts).
+    grid_cap_ = std::max(1, ipc_p2p_resident_wgs(device_) / 2);
     mbox_bytes_ = size_t(n_) * kChannels * size_t(nslots_) * size_t(piece_);
     flag_bytes_ = ipc_p2p_flag_bytes(n_, kChannels, nslots_, wpp_);
     mbox_ = static_cast<char*>(ipc_alloc_window(mbox_bytes_, &mem_kind_));  // fine-grained (ipc_lane.h)
@@ -169,6 +174,7 @@ class IpcP2P final : public P2P {
     a.timeout = timeout_;
     a.nops = int32_t(plan.ops.size());
     a.nqueues = int32_t(plan.qstart.size()) - 1;
+    a.wpg = std::clamp(grid_cap_ / std::max(1, a.nqueues), 1, wpp_);
     std::copy(plan.ops.begin(), plan.ops.end(), a.ops);
     for (size_t i = 0; i < plan.qstart.size(); ++i) a.qstart[i] = int16_t(plan.qstart[i]);
     launch_ipc_p2p_group(static_cast<hipStream_t>(stream), a);
@@ -190,7 +196,7 @@ class IpcP2P final : public P2P {
  private:
   int32_t rank_, n_, device_;
   int64_t piece_ = 0;
-  int32_t nslots_ = 4, wpp_ = 32;
+  int32_t nslots_ = 4, wpp_ = 32, grid_cap_ = 1024;
   size_t mbox_bytes_ = 0, flag_bytes_ = 0;
   char* mbox_ = nullptr;
   std::string mem_kind_;

@@ -212,6 +212,7 @@ bool StreamLink::bulk_round(int32_t r) {
   const bool native = p2p_->has_collectives() && g.S == int64_t(N) * g.step;
   // Auto = the framework's own p2p schedule (gfx950 reduce); RCCL's
   // reduce-scatter + all-gather runs only when asked for by name.
+  dp_->set_poison_flag(lane_ == Lane::Ipc && ipc_ ? ipc_->error_word_device() : nullptr);
   if (lane_ == Lane::Ipc) ipc_round(r);
   else if (lane_ == Lane::Collective) collective_round(r, native);
   else exact_steps(r);

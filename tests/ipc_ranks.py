@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=4)
     ap.add_argument("--dtype", default="float32")
     ap.add_argument("--skip-rank", type=int, default=-1, help="this rank runs only round 0 (a missing peer)")
+    ap.add_argument("--late-rank", type=int, default=-1, help="this rank sleeps --late-s before round 1")
+    ap.add_argument("--late-s", type=float, default=0.0)
     ap.add_argument("--time", action="store_true")
     ap.add_argument("--mode", default="pull", choices=["pull", "bcast", "alternate", "fused", "fused_bcast", "rotate"])
     ap.add_argument("--out-dir", default="", help="write rank<i>.json there (stdout lines of ranks interleave)")
@@ -49,6 +51,10 @@ def main():
     for r in range(a.rounds):
         if r > 0 and rank == a.skip_rank:
             break
+        if r == 1 and rank == a.late_rank:
+            import time
+
+            time.sleep(a.late_s)  # arrives after the peers' waits timed out
         if a.mode != "pull":
             variants = [("pull", False), ("bcast", False), ("pull", True), ("bcast", True)]
             mode, fused = {"bcast": ("bcast", False), "fused": ("pull", True), "fused_bcast": ("bcast", True),
@@ -74,8 +80,9 @@ def main():
         torch.cuda.synchronize()
         want = expected(a.size, world, r, dtype, 5)
         res["exact"].append(bool(torch.equal(o.data.cpu(), want)) and bool((o.count.cpu() == world).all()))
+        res.setdefault("counts_all_zero", []).append(bool((o.counts_per_chunk.cpu() == 0).all()))
     res["ipc_error"] = ar.ipc_error()
-    if a.skip_rank >= 0 and rank != a.skip_rank and res["ipc_error"]:
+    if ((a.skip_rank >= 0 and rank != a.skip_rank) or a.late_rank >= 0) and res["ipc_error"]:
         # the next round on this lane refuses to run (like an RCCL async error)
         try:
             ar(torch.zeros(a.size, device=dev, dtype=dtype))

@@ -95,6 +95,22 @@ def test_ipc_lane_missing_peer_times_out_cleanly():
     assert rows[1]["exact"] == [True]
 
 
+def test_ipc_lane_late_rank_poisons_the_round_everywhere():
+    """Rank 1 arrives at round 1 only after rank 0's waits timed out (0.5 s),
+    e.g. a rank busy with a checkpoint.  Rank 0 aborts the lane for everyone
+    (abort word in every rank's flag area, stored before any of its flags),
+    so rank 1 does not consume rank 0's never-written reduced rows either:
+    on BOTH ranks round 1's counts are all 0 (never handed back as exact),
+    ipc_error is set, and the next round raises."""
+    r, rows = _run(2, "--size", str(1 << 16), "--rounds", "2", "--late-rank", "1", "--late-s", "2.0",
+                   env={"AKKA_IPC_TIMEOUT_MS": "500"})
+    assert r.returncode == 0, r.stderr[-3000:]
+    for d in rows:
+        assert d["exact"][0] is True and d["counts_all_zero"] == [False, True], d
+        assert d["exact"][1] is False and d["ipc_error"] != 0, d
+        assert d["next_round_raised"] is True, d
+
+
 def test_ipc_round_waits_for_callers_pending_work_on_its_buffers():
     """The round's output and counts are carved from a block that a pending
     kernel on the caller's stream still writes (the caching allocator reuses

@@ -41,7 +41,12 @@ def _rank_main(rank, world, port, th_allreduce, rounds, nap, q):
             ar(torch.full((S,), float(rank + 1)))
         elapsed = time.monotonic() - t0
         ar.drain(60.0)
-        q.put((rank, elapsed, ar.pacer.waits, None))
+        dist.barrier()  # every rank passed every round's start
+        # pacing keys of rounds everyone passed are gone (only the last round's stays)
+        store = ar.pacer.store
+        left = [r for r in range(rounds - 1)
+                if store.check([f"{ar.pacer.prefix}/{r}"]) or store.check([f"{ar.pacer.prefix}/passed/{r}"])]
+        q.put((rank, elapsed, ar.pacer.waits, None if not left else f"pacing keys left for rounds {left}"))
         dist.barrier()
         dist.destroy_process_group()
     except Exception as e:  # pragma: no cover
