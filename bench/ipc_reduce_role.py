@@ -1,0 +1,44 @@
+"""Bandwidth of the exact ipc round's reduce role alone (csrc/kernels/ipc.hip,
+ipc_reduce_role_bench): one process, local fine-grained windows with every
+push flag pre-set, so the kernel only waits zero times and sums.  Bytes per
+launch: N x block read (N-1 window slots + the rank's own input) + 2 x block
+written (output block + `reduced` row, pull mode).  Compares system-coherent
+slot loads (sc0 sc1, the default) with plain loads behind the acquire.
+
+    python bench/ipc_reduce_role.py [--n 2,4,8] [--block-mb 4,32] [--threads 256,1024]
+"""
+import argparse
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", default="2,4,8")
+    ap.add_argument("--block-mb", default="4,32")
+    ap.add_argument("--threads", default="256,1024")
+    ap.add_argument("--modes", default="sys,plain")
+    ap.add_argument("--dtype", default="float32")
+    ap.add_argument("--iters", type=int, default=20)
+    a = ap.parse_args()
+    from akka_allreduce_amd._native_loader import load
+
+    n = load()
+    es = 4 if a.dtype == "float32" else 2
+    for N in [int(x) for x in a.n.split(",")]:
+        for mb in [float(x) for x in a.block_mb.split(",")]:
+            block = int(mb * (1 << 20)) // es
+            for th in [int(x) for x in a.threads.split(",")]:
+                for mode in a.modes.split(","):
+                    ms = n.ipc_reduce_role_bench(N, block, 512 << 10, a.dtype, mode == "plain", a.iters, th, 0)
+                    rd, wr = N * block * es, 2 * block * es
+                    print(json.dumps({"N": N, "block_mb": mb, "threads": th, "loads": mode, "dtype": a.dtype,
+                                      "us": round(ms * 1e3, 2), "read_bytes": rd, "write_bytes": wr,
+                                      "TBps": round((rd + wr) / (ms * 1e-3) / 1e12, 3)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -76,6 +76,64 @@ __device__ inline void signal(uint32_t* f, uint32_t v) {  // lane 0, after relea
 // is the round input, the others are window slots), to `o`, to `r` (pull
 // mode) or, with gather_off >= 0 (bcast mode), to every peer's window at
 // byte offset gather_off.
+// Vector body with the source count NS known at compile time: every thread
+// issues all NS x U 16-byte loads of an iteration before the first add (the
+// standalone reduce kernel's structure, kernels.hip), U = 16 / NS vectors per
+// source, so ~16 loads are in flight per lane whatever N is.  Slot loads are
+// system-coherent buffer loads (sc0 sc1), or -- `plain_slots`, measured
+// against them -- plain loads behind the workgroup's system-scope acquire.
+// Same summation order as the runtime-N body (ascending source), so the
+// result is bitwise identical.
+template <typename T, int NS>
+__device__ void reduce_vec_n(const IpcArgs& a, const char* mine, const char* slots, int64_t slot_bytes, char* o,
+                             char* r, int64_t gather_off, int64_t n) {
+  constexpr int PV = Elt<T>::kPerVec;
+  constexpr int U = NS >= 16 ? 1 : (16 / NS);
+  const int me = a.me;
+  const bool bc = gather_off >= 0;
+  const bool plain = a.plain_slots != 0;
+  const int64_t nv = n / PV;
+  const int bd = int(blockDim.x);
+  for (int64_t i0 = threadIdx.x; i0 < nv; i0 += int64_t(U) * bd) {
+    uint4 v[NS][U];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      if (s == me || plain) {
+        const uint4* src = reinterpret_cast<const uint4*>(s == me ? mine : slots + int64_t(s) * slot_bytes);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int64_t i = i0 + int64_t(u) * bd;
+          v[s][u] = i < nv ? src[i] : make_uint4(0, 0, 0, 0);
+        }
+      } else {
+        const auto rs = sys_rsrc(slots + int64_t(s) * slot_bytes, n * int64_t(sizeof(T)));
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[s][u] = load_sys16(rs, (i0 + int64_t(u) * bd) * 16);  // 0 past the end
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + int64_t(u) * bd;
+      float acc[PV];
+#pragma unroll
+      for (int e = 0; e < PV; ++e) acc[e] = 0.f;
+#pragma unroll
+      for (int s = 0; s < NS; ++s) Elt<T>::add(acc, v[s][u]);
+      if (i < nv) {
+        const uint4 w = Elt<T>::pack(acc);
+        reinterpret_cast<uint4*>(o)[i] = w;
+        if (bc) {
+#pragma unroll
+          for (int p = 0; p < NS; ++p)
+            if (p != me) reinterpret_cast<uint4*>(a.gdata[p] + gather_off)[i] = w;
+        } else {
+          reinterpret_cast<uint4*>(r)[i] = w;
+        }
+      }
+    }
+  }
+}
+
 template <typename T>
 __device__ void reduce_span(const IpcArgs& a, const char* mine, const char* slots, int64_t slot_bytes, char* o,
                             char* r, int64_t gather_off, int64_t n) {
@@ -86,6 +144,17 @@ __device__ void reduce_span(const IpcArgs& a, const char* mine, const char* slot
   bool vec = ((uintptr_t(mine) | uintptr_t(slots) | uintptr_t(slot_bytes) | uintptr_t(o) | uintptr_t(r) |
                uintptr_t(bc ? gather_off : 0) | uintptr_t(n * ES)) & 15) == 0;
   if (vec) {
+    switch (N) {  // the node's rank counts: compile-time source loops
+      case 2: return reduce_vec_n<T, 2>(a, mine, slots, slot_bytes, o, r, gather_off, n);
+      case 3: return reduce_vec_n<T, 3>(a, mine, slots, slot_bytes, o, r, gather_off, n);
+      case 4: return reduce_vec_n<T, 4>(a, mine, slots, slot_bytes, o, r, gather_off, n);
+      case 5: return reduce_vec_n<T, 5>(a, mine, slots, slot_bytes, o, r, gather_off, n);
+      case 6: return reduce_vec_n<T, 6>(a, mine, slots, slot_bytes, o, r, gather_off, n);
+      case 7: return reduce_vec_n<T, 7>(a, mine, slots, slot_bytes, o, r, gather_off, n);
+      case 8: return reduce_vec_n<T, 8>(a, mine, slots, slot_bytes, o, r, gather_off, n);
+      case 16: return reduce_vec_n<T, 16>(a, mine, slots, slot_bytes, o, r, gather_off, n);
+      default: break;
+    }
     const int64_t nv = n / PV;
     for (int64_t i0 = threadIdx.x; i0 < nv; i0 += kUnroll * int(blockDim.x)) {
       float acc[kUnroll][PV];
@@ -386,6 +455,92 @@ void launch_ipc_round(hipStream_t s, const IpcArgs& a, DType dt) {
   if (a.N < 2) return;
   if (dt == DType::F32) launch_round<float>(s, a);
   else launch_round<uint16_t>(s, a);
+}
+
+}  // namespace akka
+
+namespace akka {
+
+// Microbenchmark of the reduce role alone (one process, local fine-grained
+// windows, every push flag pre-set): the in-round reduce's bandwidth, with
+// system-coherent slot loads or plain ones (`plain`).  Pull mode: reads
+// N x block, writes the output block and the `reduced` row.  Returns ms per
+// launch over `iters` launches.
+double ipc_reduce_role_bench(int32_t N, int64_t block, int64_t portion_bytes, DType dt, bool plain, int32_t iters,
+                             int32_t threads, int32_t device) {
+  auto ok = [](hipError_t e, const char* w) {
+    if (e != hipSuccess) throw AkkaError(std::string("akka ipc bench: ") + w + ": " + hipGetErrorString(e));
+  };
+  ok(hipSetDevice(device), "set device");
+  const int64_t es = dt == DType::F32 ? 4 : 2;
+  const int64_t slot = (block + 63) / 64 * 64;
+  const int64_t portion = std::max<int64_t>(1024, portion_bytes / es / 1024 * 1024);
+  const int32_t np = int32_t((block + portion - 1) / portion);
+  char *data = nullptr, *gdata = nullptr, *in = nullptr, *out = nullptr;
+  uint32_t *flags = nullptr, *err = nullptr, *err_dev = nullptr;
+  ok(hipExtMallocWithFlags(reinterpret_cast<void**>(&data), size_t(N * slot * es), hipDeviceMallocFinegrained), "data");
+  ok(hipExtMallocWithFlags(reinterpret_cast<void**>(&gdata), size_t((N + 1) * slot * es), hipDeviceMallocFinegrained),
+     "gdata");
+  ok(hipExtMallocWithFlags(reinterpret_cast<void**>(&flags), ipc_flag_bytes(N, np), hipDeviceMallocUncached), "flags");
+  ok(hipMalloc(&in, size_t(N * block * es)), "in");
+  ok(hipMalloc(&out, size_t(N * block * es)), "out");
+  ok(hipHostMalloc(reinterpret_cast<void**>(&err), 4, hipHostMallocMapped | hipHostMallocCoherent), "err");
+  *err = 0;
+  ok(hipHostGetDevicePointer(reinterpret_cast<void**>(&err_dev), err, 0), "err dev");
+  ok(hipMemset(data, 0x3c, size_t(N * slot * es)), "fill");
+  ok(hipMemset(in, 0x3c, size_t(N * block * es)), "fill");
+  ok(hipMemset(flags, 0, ipc_flag_bytes(N, np)), "flags");
+  ok(hipMemsetD32(reinterpret_cast<hipDeviceptr_t>(flags), 1, size_t(N) * np * kIpcFlagStride), "push flags");
+  IpcArgs a;
+  std::memset(&a, 0, sizeof(a));
+  for (int32_t p = 0; p < N; ++p) {
+    a.data[p] = data;
+    a.gdata[p] = gdata;
+    a.flags[p] = flags;
+    a.bstart[p] = int64_t(p) * block;
+    a.blen[p] = block;
+  }
+  a.slot = slot;
+  a.portion = portion;
+  a.nportions = np;
+  a.max_wgs = 1024;
+  a.N = N;
+  a.me = 0;
+  a.threads = threads;
+  a.plain_slots = plain ? 1 : 0;
+  a.round = 1;
+  a.timeout = uint64_t(1) << 40;
+  a.in = in;
+  a.out = out;
+  a.err = err_dev;
+  const int32_t nt = (threads == 512 || threads == 1024) ? threads : kThreads;
+  const int32_t cap = std::max(1, a.max_wgs * kThreads / nt);
+  const unsigned grid = unsigned(std::min(np * kReduceSplit, cap));
+  hipEvent_t e0, e1;
+  ok(hipEventCreate(&e0), "event");
+  ok(hipEventCreate(&e1), "event");
+  auto launch = [&]() {
+    if (dt == DType::F32) hipLaunchKernelGGL(ipc_reduce_kernel<float>, dim3(grid), dim3(unsigned(nt)), 0, nullptr, a);
+    else hipLaunchKernelGGL(ipc_reduce_kernel<uint16_t>, dim3(grid), dim3(unsigned(nt)), 0, nullptr, a);
+  };
+  for (int i = 0; i < 3; ++i) launch();
+  ok(hipEventRecord(e0, nullptr), "record");
+  for (int i = 0; i < iters; ++i) launch();
+  ok(hipEventRecord(e1, nullptr), "record");
+  ok(hipEventSynchronize(e1), "sync");
+  float ms = 0.f;
+  ok(hipEventElapsedTime(&ms, e0, e1), "elapsed");
+  const uint32_t e = *err;
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  hipFree(data);
+  hipFree(gdata);
+  hipFree(flags);
+  hipFree(in);
+  hipFree(out);
+  hipHostFree(err);
+  if (e != 0) throw AkkaError("akka ipc bench: a wait failed");
+  return double(ms) / std::max(1, iters);
 }
 
 }  // namespace akka

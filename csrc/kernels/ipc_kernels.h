@@ -48,6 +48,7 @@ struct IpcArgs {
   int32_t fused = 0;  // 1: push, reduce and phase 2 as roles of ONE launch (pipelined by portion)
   int32_t N = 0, me = 0;
   int32_t threads = 256;    // workgroup size of the round's kernels (256 / 512 / 1024)
+  int32_t plain_slots = 0;  // measurement only: plain slot loads behind the acquire instead of sc0 sc1 loads
   uint32_t round = 0;       // this round's id (1, 2, ... identical on every rank)
   uint64_t timeout = 0;     // per wait, in wall-clock ticks (100 MHz)
   const char* in = nullptr;  // round input [S]
@@ -129,6 +130,10 @@ void launch_ipc_p2p_group(hipStream_t s, const IpcP2PArgs& a);
 // CUs): every workgroup of a group must be resident together (a queue's
 // workgroup may wait on a peer's, which waits on another of this group).
 int32_t ipc_p2p_resident_wgs(int32_t device);
+
+// Microbenchmark of the exact round's reduce role alone (ipc.hip): ms per launch.
+double ipc_reduce_role_bench(int32_t N, int64_t block, int64_t portion_bytes, DType dt, bool plain, int32_t iters,
+                             int32_t threads, int32_t device);
 
 // Enqueue one round on `s`: push, reduce, then pull (bcast = 0) or, with
 // bcast = 1, the reducer writes its rows into every peer's gather slot and a
