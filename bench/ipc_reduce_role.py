@@ -23,6 +23,8 @@ def main() -> None:
     ap.add_argument("--modes", default="sys,plain")
     ap.add_argument("--dtype", default="float32")
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--kinds", default="fine", help="window memory: fine,coarse,uncached")
+    ap.add_argument("--portion-kb", default="512", help="portion sizes (KiB): 4 reduce workgroups per portion")
     a = ap.parse_args()
     from akka_allreduce_amd._native_loader import load
 
@@ -31,13 +33,17 @@ def main() -> None:
     for N in [int(x) for x in a.n.split(",")]:
         for mb in [float(x) for x in a.block_mb.split(",")]:
             block = int(mb * (1 << 20)) // es
-            for th in [int(x) for x in a.threads.split(",")]:
-                for mode in a.modes.split(","):
-                    ms = n.ipc_reduce_role_bench(N, block, 512 << 10, a.dtype, mode == "plain", a.iters, th, 0)
-                    rd, wr = N * block * es, 2 * block * es
-                    print(json.dumps({"N": N, "block_mb": mb, "threads": th, "loads": mode, "dtype": a.dtype,
-                                      "us": round(ms * 1e3, 2), "read_bytes": rd, "write_bytes": wr,
-                                      "TBps": round((rd + wr) / (ms * 1e-3) / 1e12, 3)}), flush=True)
+            for kind in a.kinds.split(","):
+                for pk in [int(x) for x in a.portion_kb.split(",")]:
+                    for th in [int(x) for x in a.threads.split(",")]:
+                        for mode in a.modes.split(","):
+                            ms = n.ipc_reduce_role_bench(N, block, pk << 10, a.dtype, mode == "plain", a.iters, th,
+                                                         0, kind)
+                            rd, wr = N * block * es, 2 * block * es
+                            print(json.dumps({"N": N, "block_mb": mb, "kind": kind, "portion_kb": pk, "threads": th,
+                                              "loads": mode, "dtype": a.dtype, "us": round(ms * 1e3, 2),
+                                              "read_bytes": rd, "write_bytes": wr,
+                                              "TBps": round((rd + wr) / (ms * 1e-3) / 1e12, 3)}), flush=True)
 
 
 if __name__ == "__main__":

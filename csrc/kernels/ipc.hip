@@ -467,7 +467,7 @@ namespace akka {
 // N x block, writes the output block and the `reduced` row.  Returns ms per
 // launch over `iters` launches.
 double ipc_reduce_role_bench(int32_t N, int64_t block, int64_t portion_bytes, DType dt, bool plain, int32_t iters,
-                             int32_t threads, int32_t device) {
+                             int32_t threads, int32_t device, int32_t win_kind) {
   auto ok = [](hipError_t e, const char* w) {
     if (e != hipSuccess) throw AkkaError(std::string("akka ipc bench: ") + w + ": " + hipGetErrorString(e));
   };
@@ -478,9 +478,14 @@ double ipc_reduce_role_bench(int32_t N, int64_t block, int64_t portion_bytes, DT
   const int32_t np = int32_t((block + portion - 1) / portion);
   char *data = nullptr, *gdata = nullptr, *in = nullptr, *out = nullptr;
   uint32_t *flags = nullptr, *err = nullptr, *err_dev = nullptr;
-  ok(hipExtMallocWithFlags(reinterpret_cast<void**>(&data), size_t(N * slot * es), hipDeviceMallocFinegrained), "data");
-  ok(hipExtMallocWithFlags(reinterpret_cast<void**>(&gdata), size_t((N + 1) * slot * es), hipDeviceMallocFinegrained),
-     "gdata");
+  // window memory kind: 0 fine-grained (the lane's default), 1 coarse (hipMalloc), 2 uncached
+  auto walloc = [&](char** p, size_t bytes, const char* what) {
+    if (win_kind == 1) ok(hipMalloc(reinterpret_cast<void**>(p), bytes), what);
+    else ok(hipExtMallocWithFlags(reinterpret_cast<void**>(p), bytes,
+                                  win_kind == 2 ? hipDeviceMallocUncached : hipDeviceMallocFinegrained), what);
+  };
+  walloc(&data, size_t(N * slot * es), "data");
+  walloc(&gdata, size_t((N + 1) * slot * es), "gdata");
   ok(hipExtMallocWithFlags(reinterpret_cast<void**>(&flags), ipc_flag_bytes(N, np), hipDeviceMallocUncached), "flags");
   ok(hipMalloc(&in, size_t(N * block * es)), "in");
   ok(hipMalloc(&out, size_t(N * block * es)), "out");
