@@ -112,20 +112,30 @@ class Node:
         self._stop.set()
         self.mailbox.put(None)
         try:
+            self._srv.shutdown(socket.SHUT_RDWR)  # wakes the accept loop (close alone does not)
+        except OSError:
+            pass
+        try:
             self._srv.close()
         except OSError:
             pass
+        # every access to _conns holds _conn_lock: a sender thread (heartbeats)
+        # connecting while the node stops must not change the dict under this
+        # loop ("dictionary changed size during iteration" in stop())
         with self._conn_lock:
-            for s in self._conns.values():
-                try:
-                    s.close()
-                except OSError:
-                    pass
+            conns = list(self._conns.values())
             self._conns.clear()
+        for s in conns:
+            try:
+                s.close()
+            except OSError:
+                pass
 
     def join(self, timeout: Optional[float] = None) -> None:
         end = None if timeout is None else time.time() + timeout
         for t in self._threads:
+            if t is threading.current_thread():
+                continue  # stop() from inside a handler: nothing to wait for here
             t.join(None if end is None else max(0.0, end - time.time()))
 
     @property
@@ -137,20 +147,28 @@ class Node:
         if address == self.address:
             self.mailbox.put(msg)
             return
+        if self._stop.is_set():
+            return  # a stopped node sends nothing (and opens no new connection)
         frame = wire.encode(msg, self.addr_of)
         with self._conn_lock:
             lock = self._send_locks.setdefault(address, threading.Lock())
         with lock:
             try:
-                s = self._conns.get(address)
+                with self._conn_lock:
+                    s = self._conns.get(address)
                 if s is None:
                     s = socket.create_connection(parse_addr(address), timeout=10.0)
                     s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
                     s.settimeout(None)
-                    self._conns[address] = s
+                    with self._conn_lock:
+                        if self._stop.is_set():
+                            s.close()
+                            return
+                        self._conns[address] = s
                 s.sendall(frame)
             except OSError as e:
-                self._conns.pop(address, None)
+                with self._conn_lock:
+                    self._conns.pop(address, None)
                 log.warning("%s: send to %s failed: %s", self.name, address, e)
                 if self.on_send_failure:
                     self.on_send_failure(address, e)

@@ -190,8 +190,15 @@ class MasterProcess:
     def wait(self, timeout: Optional[float] = None) -> bool:
         return self.finished.wait(timeout)
 
-    def stop(self) -> None:
+    def stop(self, join_s: float = 5.0) -> None:
+        """Stop the node and wait (bounded) for its threads: a dispatch thread
+        still inside native engine code when the interpreter exits would be
+        torn down mid-call (pthread_exit unwinding through C++ frames aborts
+        the process)."""
         self.node.stop()
+        self.node.join(join_s)
+        if self._fd is not threading.current_thread():
+            self._fd.join(join_s)
 
 
 def start_master(thresholds: ThresholdConfig, data: DataConfig, workers: WorkerConfig, **kw) -> MasterProcess:
@@ -262,9 +269,14 @@ class WorkerProcess:
     def wait(self, timeout: Optional[float] = None) -> bool:
         return self.stopped.wait(timeout)
 
-    def stop(self) -> None:
+    def stop(self, join_s: float = 5.0) -> None:
+        """Stop and wait (bounded) for the node's and the heartbeat's threads
+        (see MasterProcess.stop)."""
         self.stopped.set()
         self.node.stop()
+        self.node.join(join_s)
+        if self._hb is not threading.current_thread():
+            self._hb.join(join_s)
 
 
 def start_worker(master_address: str, data_size: int, *, checkpoint: int = 50, assert_multiple: int = 0,
