@@ -35,13 +35,14 @@ HOST_SOURCES = [
     "transport/ipc_lane.cpp",
     "transport/ipc_p2p.cpp",
     "transport/onesided.cpp",
+    "transport/link_probe.cpp",
     "kernels/hip_device.cpp",
     "runtime/watchdog.cpp",
     "bindings/bindings.cpp",
     "bindings/bind_onesided.cpp",
     "bindings/bind_probe.cpp",
 ]
-HIP_SOURCES = ["kernels/kernels.hip", "kernels/ipc.hip", "kernels/onesided.hip"]
+HIP_SOURCES = ["kernels/kernels.hip", "kernels/ipc.hip", "kernels/onesided.hip", "kernels/probe.hip"]
 
 
 def ext_path() -> str:

@@ -62,6 +62,10 @@ def parse():
     p.add_argument("--cfg4-transport", choices=["onesided", "reactive"], default="onesided",
                    help="config 4 data path: onesided (stores into mapped peer windows, no send ever waits) or "
                         "reactive (RCCL pair communicators, two-sided)")
+    p.add_argument("--link-probe", choices=["on", "off"], default="on",
+                   help="N>1: measure every ordered pair's push / pull bandwidth after the headline (untimed)")
+    p.add_argument("--link-probe-mib", type=float, default=64.0)
+    p.add_argument("--link-probe-deadline-s", type=float, default=120.0)
     p.add_argument("--extras-deadline-s", type=float, default=240.0,
                    help="give up on the extra configs after this many seconds (the headline line is still printed)")
     p.add_argument("--device", choices=["cuda", "cpu"], default="cuda",
@@ -833,6 +837,35 @@ def main() -> int:
     else:
         # direct scatter/broadcast moves S/N per link per phase: algbw <= N*L/2
         line["xgmi_bound_algbw_GBps"] = round(world * XGMI_LINK_GBPS / 2, 1)
+
+    # Per-link probe (N>1, untimed, after the headline): every ordered pair's
+    # remote-write (push) and remote-read (pull) bandwidth through mapped
+    # memory, and every rank to all peers at once.  It validates the ~153 GB/s
+    # per xGMI link behind xgmi_bound_algbw_GBps.  Bounded like the extras: a
+    # hang prints the headline line with link_probe_error instead.
+    if world > 1 and args.link_probe == "on":
+        late = dict(line)
+        late["link_probe_error"] = f"link probe not done after {args.link_probe_deadline_s:g} s; skipped"
+        guard.arm(args.link_probe_deadline_s, late, exit_code=0 if ok in (None, True) else 1)
+        progress_msg = f"rank {rank}: link probe"
+        from akka_allreduce_amd.utils.phases import progress
+
+        progress(progress_msg)
+        try:
+            from akka_allreduce_amd.utils.link_probe import probe_links
+
+            probe = probe_links(rank, world, dev, mib=args.link_probe_mib, iters=3)
+            if rank == 0:
+                if dev.type != "cuda":
+                    probe["note"] = "CPU shared memory (gloo rehearsal): not a link measurement"
+                elif os.environ.get("AKKA_SHARE_GPU") == "1":
+                    probe["note"] = "ranks share ONE GPU: copies inside one card's HBM, not xGMI"
+                else:
+                    probe["note"] = "one rank per GPU: each pair is an xGMI link"
+                line["link_probe"] = probe
+        except Exception as e:  # noqa: BLE001 - the probe must never cost the headline
+            line["link_probe_error"] = f"{type(e).__name__}: {e}"[:200]
+        guard.disarm()
 
     # The other BASELINE configs at the same N, measured after the headline
     # (each guarded so it cannot cost the line).  The native watchdog bounds

@@ -3,6 +3,7 @@
 // opens, and how long it takes).
 #include <hip/hip_runtime.h>
 #include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
 
 #include <chrono>
 #include <cstring>
@@ -10,6 +11,7 @@
 
 #include "../engine/common.h"
 #include "../kernels/ipc_kernels.h"
+#include "../transport/link_probe.h"
 
 namespace py = pybind11;
 
@@ -22,6 +24,21 @@ void check(hipError_t e, const char* what) {
 }  // namespace
 
 void bind_probe(py::module_& m) {
+  py::class_<LinkProbe>(m, "LinkProbe")
+      .def(py::init<int32_t, int32_t, int32_t, int64_t>(), py::arg("device"), py::arg("rank"), py::arg("nranks"),
+           py::arg("bytes"))
+      .def("handle", [](const LinkProbe& p) { return py::bytes(p.handle()); })
+      .def("open", &LinkProbe::open)
+      .def("unlink", &LinkProbe::unlink)
+      .def("bytes", &LinkProbe::bytes)
+      .def("push", [](LinkProbe& p, std::vector<int32_t> peers, int32_t iters) {
+        py::gil_scoped_release nogil;
+        return p.push(peers, iters);
+      })
+      .def("pull", [](LinkProbe& p, std::vector<int32_t> peers, int32_t iters) {
+        py::gil_scoped_release nogil;
+        return p.pull(peers, iters);
+      });
   m.def("ipc_probe_export", [](int32_t device, int64_t bytes, const std::string& kind) {
     check(hipSetDevice(device), "hipSetDevice");
     void* p = nullptr;

@@ -78,6 +78,9 @@ def test_bench_multirank_on_one_card(plane):
     cands = [k for k in sel if k != "chosen"]
     assert all(sel[k]["exact"] is True for k in cands), sel
     assert d["lane"] == sel["chosen"]
+    lp = d["link_probe"]  # the N x N matrix, labelled: ranks share one card, not xGMI
+    assert "share ONE GPU" in lp["note"] and len(lp["push_GBps"]) == n and len(lp["pull_GBps"][0]) == n
+    assert all(lp["push_GBps"][i][j] > 0 for i in range(n) for j in range(n) if i != j)
     if plane == "ipc_p2p":
         assert {"p2p", "p2p_block", "ipc", "ipc_bcast", "ipc_fused", "ipc_fused_bcast", "ipc_wide",
                 "ipc_bcast_wide"} <= set(cands) and "collective" not in cands

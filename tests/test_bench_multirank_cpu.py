@@ -57,6 +57,14 @@ def test_bench_multirank_line(n, transport):
     # gloo has no native collectives: auto keeps the chunk schedule, and the
     # whole-round lane is measured as the other lane (stream transport only)
     assert d["lane"] == "p2p" and d["lane_is_framework"] is True
+    # per-link probe: an N x N matrix per direction (row = source), no diagonal
+    lp = d["link_probe"]
+    for key in ("push_GBps", "pull_GBps"):
+        m = lp[key]
+        assert len(m) == n and all(len(row) == n for row in m)
+        assert all((m[i][j] is None) == (i == j) for i in range(n) for j in range(n))
+        assert all(m[i][j] > 0 for i in range(n) for j in range(n) if i != j)
+    assert len(lp["all_peers_push_GBps_per_rank"]) == n and "not a link measurement" in lp["note"]
     if transport == "stream":
         assert d["other_lane"]["lane"] == "collective" and d["other_lane"]["algbw_GBps"] > 0
 
