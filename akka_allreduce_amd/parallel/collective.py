@@ -182,6 +182,8 @@ class ThresholdAllreduce:
         lane: str = "auto",
         th_allreduce: Optional[float] = None,
         data_plane: str = "rccl",
+        share_transport_with: Optional["ThresholdAllreduce"] = None,
+        ipc_capacity: int = 0,
     ):
         if transport == "onesided":
             # thresholds over mapped peer windows: no send ever waits for a
@@ -226,7 +228,18 @@ class ThresholdAllreduce:
             if have < need:
                 raise RuntimeError(f"reactive transport at N={self.world_size} needs GPU_MAX_HW_QUEUES >= {need} "
                                    f"(have {have}); export it (<= 32) before the first HIP call")
-        if self.device.type == "cuda" and data_plane == "ipc" and self.world_size > 1:
+        share = share_transport_with if self.world_size > 1 else None
+        if share is not None:
+            # ride on another engine's transport: one communicator (and one set
+            # of device streams) for every engine of the job, e.g. one per DDP
+            # bucket size (WorkerCore.adopt_transport)
+            if (share.transport != transport or share.device != self.device or share.world_size != self.world_size
+                    or share.rank != self.rank or getattr(share, "data_plane", data_plane) != data_plane):
+                raise ValueError("share_transport_with: the engines differ in transport, device, rank or data plane")
+            if self.device.type == "cuda":
+                torch.cuda.set_device(self.device)
+            spec = ("shared", share.worker)
+        elif self.device.type == "cuda" and data_plane == "ipc" and self.world_size > 1:
             torch.cuda.set_device(self.device)
             spec = ("none", self.rank, self.world_size)
         elif self.device.type == "cuda" and data_plane == "ipc_p2p" and self.world_size > 1:
@@ -259,6 +272,9 @@ class ThresholdAllreduce:
                                      int(data_size), int(max_chunk_size)))
         self.data_size = int(data_size)
         self.store = store
+        self.data_plane = data_plane
+        self._share = share
+        self._ipc_capacity = int(ipc_capacity)
         self._iid = ThresholdAllreduce._instances
         self._ipc_epoch = 0
         if data_plane == "ipc" and self.world_size > 1:
@@ -326,7 +342,10 @@ class ThresholdAllreduce:
         # blocked in the collective
         err = None
         try:
-            mine = self.worker.ipc_handle()
+            # windows sized for ipc_capacity; an engine sharing another's
+            # transport reuses that engine's windows when they fit (IpcLane)
+            share = self._share.worker if (self._share is not None and self._share.worker is not None) else None
+            mine = self.worker.ipc_handle(self._ipc_capacity, share)
         except Exception as e:  # noqa: BLE001 - re-raised below, after the exchange
             mine, err = b"", e
         if self.store is not None:
@@ -348,10 +367,11 @@ class ThresholdAllreduce:
             raise RuntimeError(f"enable_ipc: ranks {missing} could not create their ipc windows")
         self.worker.ipc_open(handles)
 
-    def set_ipc_mode(self, mode: str, fused: bool = False, threads: int = 0) -> None:
+    def set_ipc_mode(self, mode: str, fused: bool = False, threads: int = 0, lite: Optional[bool] = None) -> None:
         """Phase 2 of the ipc lane: ``"pull"`` or ``"bcast"``, optionally ``fused``
-        into one launch, with ``threads`` per workgroup (AllreduceWorker.ipc_set_mode)."""
-        self.worker.ipc_set_mode(mode, fused, threads)
+        into one launch, with ``threads`` per workgroup, ``lite`` fence-free
+        hand-offs (AllreduceWorker.ipc_set_mode)."""
+        self.worker.ipc_set_mode(mode, fused, threads, lite)
 
     def ipc_error(self) -> int:
         """Non-zero once a wait of the ipc lane timed out (synchronises)."""
@@ -370,27 +390,32 @@ class ThresholdAllreduce:
         self.worker.set_graphs(on)
 
     # ---- lane tuning -------------------------------------------------------
-    LANES = {  # candidate -> (lane, exact transfer-unit bytes or -1, ipc mode, ipc fused, ipc workgroup size)
-        "collective": ("collective", -1, None, False, 0),
-        "p2p": ("p2p", -1, None, False, 0),
-        "p2p_block": ("p2p", 1 << 40, None, False, 0),
-        "ipc": ("ipc", -1, "pull", False, 256),
-        "ipc_bcast": ("ipc", -1, "bcast", False, 256),
-        "ipc_fused": ("ipc", -1, "pull", True, 256),
-        "ipc_fused_bcast": ("ipc", -1, "bcast", True, 256),
+    LANES = {  # candidate -> (lane, exact transfer-unit bytes or -1, ipc mode, ipc fused, ipc workgroup size, lite)
+        "collective": ("collective", -1, None, False, 0, False),
+        "p2p": ("p2p", -1, None, False, 0, False),
+        "p2p_block": ("p2p", 1 << 40, None, False, 0, False),
+        "ipc": ("ipc", -1, "pull", False, 256, False),
+        "ipc_bcast": ("ipc", -1, "bcast", False, 256, False),
+        "ipc_fused": ("ipc", -1, "pull", True, 256, False),
+        "ipc_fused_bcast": ("ipc", -1, "bcast", True, 256, False),
         # 1024-thread workgroups: 4x the loads / stores in flight per CU when a
         # rank has its GPU to itself (profiles/r02/ipc: -10 % at N=2 on one card)
-        "ipc_wide": ("ipc", -1, "pull", False, 1024),
-        "ipc_bcast_wide": ("ipc", -1, "bcast", False, 1024),
+        "ipc_wide": ("ipc", -1, "pull", False, 1024, False),
+        "ipc_bcast_wide": ("ipc", -1, "bcast", False, 1024, False),
+        # fence-free hand-offs: write-through window stores, system-coherent
+        # loads, no buffer_wbl2 / buffer_inv per portion (IpcLane::set_lite)
+        "ipc_lite": ("ipc", -1, "pull", False, 1024, True),
+        "ipc_bcast_lite": ("ipc", -1, "bcast", False, 1024, True),
+        "ipc_fused_lite": ("ipc", -1, "pull", True, 1024, True),
     }
 
     def use_lane(self, name: str) -> None:
         """Switch to a named lane candidate (see LANES); every rank must do the
         same at the same round."""
-        ln, unit, mode, fused, threads = self.LANES[name]
+        ln, unit, mode, fused, threads, lite = self.LANES[name]
         self.set_lane(ln)
         if ln == "ipc":
-            self.set_ipc_mode(mode, fused, threads)
+            self.set_ipc_mode(mode, fused, threads, lite)
         elif self.world_size > 1:
             self.set_exact_unit_bytes(unit)
 
@@ -432,7 +457,8 @@ class ThresholdAllreduce:
                         res["ipc"] = {"exact": None, "ms": None,
                                       "error": err or "another rank could not open its windows"}
                 if ipc_open:
-                    cands += ["ipc", "ipc_bcast", "ipc_fused", "ipc_fused_bcast", "ipc_wide", "ipc_bcast_wide"]
+                    cands += ["ipc", "ipc_bcast", "ipc_fused", "ipc_fused_bcast", "ipc_wide", "ipc_bcast_wide",
+                              "ipc_lite", "ipc_bcast_lite", "ipc_fused_lite"]
         S, N, r = self.data_size, self.world_size, self.rank
         dtype = self.worker.dtype
         x = torch.randn(S, device=self.device).to(dtype)

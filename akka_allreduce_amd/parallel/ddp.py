@@ -29,12 +29,22 @@ class ThresholdHookState:
     like DDP's own allreduce hook.  ``th_allreduce``: master-style round
     pacing across ranks (see ThresholdAllreduce).  ``data_plane="ipc"``: exact
     rounds on the one-sided xGMI lane, no RCCL communicator (ThresholdAllreduce).
-    ``tune`` (exact thresholds): each bucket size's engine measures every exact
-    lane once when it is created and keeps the fastest (ThresholdAllreduce.tune)."""
+    ``tune`` (exact thresholds): the hook's first engine measures every exact
+    lane once and keeps the fastest; later engines take the same lane
+    (ThresholdAllreduce.tune).
+
+    One transport per hook: the engines of the different bucket sizes share
+    the first engine's device streams and communicator
+    (``share_transport_with``), so a job holds ONE RCCL communicator however
+    many bucket shapes DDP produces, and every bucket's round is ordered on the
+    same streams in the bucket order every rank sees.  With the ipc data plane
+    the engines also share the first engine's window memory when it is large
+    enough (``ipc_capacity``: the window is sized for ``bucket_cap_mb``)."""
 
     def __init__(self, *, th_reduce: float = 1.0, th_complete: float = 1.0, max_lag: int = 2,
                  max_chunk_size: int = 1 << 20, transport: str = "stream", broadcast_lag: int = 2,
-                 async_op: bool = True, th_allreduce=None, data_plane: str = "rccl", tune: bool = False):
+                 async_op: bool = True, th_allreduce=None, data_plane: str = "rccl", tune: bool = False,
+                 bucket_cap_mb: float = 25.0):
         self.kw = dict(th_reduce=th_reduce, th_complete=th_complete, max_lag=max_lag, max_chunk_size=max_chunk_size,
                        transport=transport, broadcast_lag=broadcast_lag, th_allreduce=th_allreduce,
                        data_plane=data_plane)
@@ -43,16 +53,33 @@ class ThresholdHookState:
         self.async_op = async_op
         self.async_rounds = 0
         self.tune = tune and th_reduce >= 1.0 and th_complete >= 1.0
+        self.bucket_cap_bytes = int(bucket_cap_mb * (1 << 20))
+        self.first: Dict[Tuple[torch.dtype, torch.device], ThresholdAllreduce] = {}
+        self.lane = None  # tuned lane, applied to every engine
 
     def engine(self, t: torch.Tensor) -> ThresholdAllreduce:
         key = (t.numel(), t.dtype, t.device)
         ar = self.engines.get(key)
         if ar is None:
-            ar = ThresholdAllreduce(t.numel(), dtype=t.dtype, device=t.device, **self.kw)
-            if self.tune and ar.world_size > 1 and ar.transport == "stream":
-                ar.tune()  # collective: every rank creates this engine at the same bucket
+            first = self.first.get((t.dtype, t.device))
+            cap = max(t.numel(), self.bucket_cap_bytes // t.element_size())
+            ar = ThresholdAllreduce(t.numel(), dtype=t.dtype, device=t.device, share_transport_with=first,
+                                    ipc_capacity=cap, **self.kw)
+            if first is None:
+                self.first[(t.dtype, t.device)] = ar
+            if ar.world_size > 1 and ar.transport == "stream":
+                if self.tune and self.lane is None:
+                    self.lane = ar.tune()["chosen"]  # collective: every rank creates this engine at the same bucket
+                elif self.lane is not None:  # tuned once per hook: later engines take the same lane
+                    if self.lane.startswith("ipc") and not ar.state().get("link", {}).get("ipc"):
+                        ar.enable_ipc()  # collective, like the engine's creation
+                    ar.use_lane(self.lane)
             self.engines[key] = ar
         return ar
+
+    def transports(self) -> int:
+        """Distinct transports (communicators) the hook's engines use."""
+        return len({ar.worker._core.transport_id() for ar in self.engines.values() if ar.worker is not None})
 
 
 # (real annotations, not postponed strings: DDP checks them)

@@ -94,6 +94,8 @@ class AllreduceWorker:
         # host streams are queues this process runs: the simulator steps them,
         # async-callback (gloo) workers step them in poll()
         deferred = bool(transport_spec and transport_spec[0] in ("sim", "async_callback"))
+        if transport_spec and transport_spec[0] == "shared":
+            deferred = transport_spec[1]._deferred  # the adopted device's kind
         self._deferred = deferred
         dev_index = self.device.index if self.device.type == "cuda" else -1
         self._core = n.WorkerCore(self, transport, dev_index, _DTYPES[dtype], deferred, broadcast_lag)
@@ -215,6 +217,10 @@ class AllreduceWorker:
             # in-process data planes handed out by the control plane (tests /
             # single-process clusters): the hub is shared by every worker
             self.transport_spec = (tinfo["kind"], tinfo["hub"], int(m.destId))
+        if self.transport_spec and self.transport_spec[0] == "shared" and not self.initialized:
+            # this engine rides on another engine's transport (device streams +
+            # communicator): ThresholdAllreduce(share_transport_with=...)
+            self._core.adopt_transport(self.transport_spec[1]._core)
         first = self._core.init(int(m.destId), int(m.workerNum), float(m.thReduce), float(m.thComplete),
                                 int(m.maxLag), int(m.dataSize), int(m.maxChunkSize), peers)
         self.peers = dict(m.workers)
@@ -290,6 +296,8 @@ class AllreduceWorker:
         elif kind == "none":  # ipc-only data plane: exact rounds on the one-sided lane
             _, rank, nranks = spec
             self._core.connect_none(int(rank), int(nranks))
+        elif kind == "shared":  # another engine's transport (adopted before init)
+            self._core.connect_adopted()
         else:
             raise ValueError(f"unknown transport spec {spec!r}")
 
@@ -376,10 +384,12 @@ class AllreduceWorker:
         self._core.set_exact_unit_bytes(int(nbytes))
 
     # ---- one-sided xGMI lane (csrc/transport/ipc_lane.h) ----
-    def ipc_handle(self) -> bytes:
+    def ipc_handle(self, capacity: int = 0, share: Optional["AllreduceWorker"] = None) -> bytes:
         """Create this rank's window (once) and return its handle, to be
-        exchanged with every rank of the job (ipc_open)."""
-        return bytes(self._core.ipc_handle())
+        exchanged with every rank of the job (ipc_open).  ``capacity``: size
+        the windows for that many elements; ``share``: an engine on the same
+        (adopted) transport whose windows to reuse when large enough."""
+        return bytes(self._core.ipc_handle(int(capacity), share._core if share is not None else None))
 
     def ipc_open(self, handles: list) -> None:
         """Map every other rank's window; ``handles[i]`` is rank i's
@@ -391,14 +401,15 @@ class AllreduceWorker:
         (synchronises the device)."""
         return int(self._core.ipc_error())
 
-    def ipc_set_mode(self, mode: str, fused: bool = False, threads: int = 0) -> None:
+    def ipc_set_mode(self, mode: str, fused: bool = False, threads: int = 0, lite: Optional[bool] = None) -> None:
         """Phase 2 of the ipc lane: ``"pull"`` (every rank reads the reduced
         rows over xGMI) or ``"bcast"`` (each reducer writes its rows into every
         peer's window); ``fused``: the three phases as roles of one launch,
         pipelined by portion; ``threads``: workgroup size of the round's
-        kernels (256 / 512 / 1024, 0 keeps it).  Every rank must switch at the
-        same round."""
-        self._core.ipc_set_mode(mode, bool(fused), int(threads))
+        kernels (256 / 512 / 1024, 0 keeps it); ``lite``: fence-free hand-offs
+        (write-through window stores, system-coherent loads; None keeps it).
+        Every rank must switch at the same round."""
+        self._core.ipc_set_mode(mode, bool(fused), int(threads), -1 if lite is None else int(bool(lite)))
 
     def ipc_close(self) -> None:
         self._core.ipc_close()

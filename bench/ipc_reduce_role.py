@@ -20,7 +20,8 @@ def main() -> None:
     ap.add_argument("--n", default="2,4,8")
     ap.add_argument("--block-mb", default="4,32")
     ap.add_argument("--threads", default="256,1024")
-    ap.add_argument("--modes", default="sys,plain")
+    ap.add_argument("--modes", default="sys,plain,lite", help="sys: sc0 sc1 slot loads + fences; plain: plain slot "
+                    "loads behind the acquire; lite: sc loads, write-through window stores, no fences")
     ap.add_argument("--dtype", default="float32")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--kinds", default="fine", help="window memory: fine,coarse,uncached")
@@ -38,7 +39,7 @@ def main() -> None:
                     for th in [int(x) for x in a.threads.split(",")]:
                         for mode in a.modes.split(","):
                             ms = n.ipc_reduce_role_bench(N, block, pk << 10, a.dtype, mode == "plain", a.iters, th,
-                                                         0, kind)
+                                                         0, kind, mode == "lite")
                             rd, wr = N * block * es, 2 * block * es
                             print(json.dumps({"N": N, "block_mb": mb, "kind": kind, "portion_kb": pk, "threads": th,
                                               "loads": mode, "dtype": a.dtype, "us": round(ms * 1e3, 2),

@@ -94,7 +94,8 @@ class WorkerCore final : public EngineHost {
     stream_link_.reset();
     reactive_link_.reset();
     dp_.reset();
-    p2p_.reset();
+    p2p_.reset();  // (a shared transport lives on in the engines that still hold it)
+    adopted_p2p_.reset();
     dev_.reset();
   }
 
@@ -113,8 +114,10 @@ class WorkerCore final : public EngineHost {
     for (auto& kv : peers) pe.push_back({kv.first, kv.second});
     bool first = engine_->init(p, pe);
     if (!first) return false;
-    if (device_idx_ < 0) dev_ = make_host_device(deferred_);
-    else dev_ = make_hip_device(device_idx_, true);
+    if (!dev_) {  // (adopt_transport may have handed us a shared device)
+      if (device_idx_ < 0) dev_ = make_host_device(deferred_);
+      else dev_ = make_hip_device(device_idx_, true);
+    }
     dp_ = std::make_unique<DataPlane>(dev_.get(), engine_->geometry(), id, max_lag + 1, dt_);
     if (link_kind_ == "outbox") {
       outbox_ = std::make_unique<OutboxLink>(id);
@@ -207,11 +210,41 @@ class WorkerCore final : public EngineHost {
     p2p_ = std::make_unique<NullP2P>(rank, nranks);
     make_stream_link();
   }
+  // Several engines of one job (e.g. one per DDP bucket size) share ONE
+  // transport: the device (its comm / compute streams) and the P2P object
+  // (RCCL communicator, ipc-only null transport, gloo callbacks).  Every
+  // engine's rounds are then ordered on the same streams, in the order the
+  // caller issues them -- identical on every rank -- which is what RCCL
+  // needs of ops sharing a communicator and what lets engines share window
+  // memory (IpcLane::share).  Call adopt_transport before init, then
+  // connect_adopted instead of a connect_* call.
+  void adopt_transport(WorkerCore& other) {
+    AKKA_CHECK(!dev_ && !p2p_, "adopt_transport: call it before init");
+    AKKA_CHECK(other.dev_ && other.p2p_, "adopt_transport: the other engine has no connected transport");
+    AKKA_CHECK(other.link_kind_ == link_kind_ && other.device_idx_ == device_idx_ && other.deferred_ == deferred_,
+               "adopt_transport: the engines differ in link kind or device");
+    dev_ = other.dev_;
+    adopted_p2p_ = other.p2p_;
+  }
+  void connect_adopted() {
+    AKKA_CHECK(adopted_p2p_, "connect_adopted: adopt_transport first");
+    AKKA_CHECK(adopted_p2p_->nranks() == engine_->geometry().N && adopted_p2p_->rank() == engine_->id(),
+               "connect_adopted: the shared transport was built for another rank / size");
+    p2p_ = adopted_p2p_;
+    if (link_kind_ == "reactive") make_reactive_link();
+    else make_stream_link();
+  }
+  // Identity of the transport object (engines sharing one report the same).
+  uintptr_t transport_id() const { return reinterpret_cast<uintptr_t>(p2p_.get()); }
   // ---- one-sided xGMI lane (ipc_lane.h) ----
-  py::bytes ipc_handle() {
+  // `capacity`: size the windows for a buffer of that many elements; `share`:
+  // an engine on the same (adopted) transport whose open lane's windows this
+  // one reuses when they are large enough (IpcLane).
+  py::bytes ipc_handle(int64_t capacity, WorkerCore* share) {
     AKKA_CHECK(stream_link_ && dp_, "ipc_handle: scheduled (stream) transport, after init");
+    const IpcLane* other = (share && share->stream_link_) ? share->stream_link_->ipc() : nullptr;
     if (!ipc_pending_)
-      ipc_pending_ = std::make_unique<IpcLane>(dev_.get(), dp_->geometry(), dp_->me(), dt_);
+      ipc_pending_ = std::make_unique<IpcLane>(dev_.get(), dp_->geometry(), dp_->me(), dt_, capacity, other);
     return py::bytes(ipc_pending_->handle());
   }
   void ipc_open(std::vector<std::string> handles) {
@@ -227,7 +260,7 @@ class WorkerCore final : public EngineHost {
     py::gil_scoped_release nogil;
     return stream_link_->ipc()->error();
   }
-  void ipc_set_mode(const std::string& mode, bool fused, int32_t threads) {
+  void ipc_set_mode(const std::string& mode, bool fused, int32_t threads, int32_t lite) {
     AKKA_CHECK(stream_link_ && stream_link_->ipc(), "ipc_set_mode: the ipc lane is not open");
     AKKA_CHECK(mode == "pull" || mode == "bcast", "ipc mode must be 'pull' or 'bcast'");
     AKKA_CHECK(threads == 0 || threads == 256 || threads == 512 || threads == 1024,
@@ -235,6 +268,7 @@ class WorkerCore final : public EngineHost {
     stream_link_->ipc()->set_bcast(mode == "bcast");
     stream_link_->ipc()->set_fused(fused);
     if (threads) stream_link_->ipc()->set_threads(threads);
+    if (lite >= 0) stream_link_->ipc()->set_lite(lite != 0);
   }
   void ipc_close() {
     ipc_pending_.reset();
@@ -401,12 +435,15 @@ class WorkerCore final : public EngineHost {
         is["portions"] = ipc->nportions();
         is["portion_bytes"] = ipc->portion_elems() * int64_t(dtype_size(dt_));
         is["window_bytes"] = int64_t(ipc->window_bytes());
+        is["shares_windows"] = ipc->shares_windows();
+        is["windows_id"] = int64_t(ipc->windows_id());
         is["max_wgs"] = ipc->max_wgs();
         is["ranks_on_this_gpu"] = ipc->ranks_on_this_gpu();
         is["rounds"] = ipc->stats().rounds;
         is["bcast_rounds"] = ipc->stats().bcast_rounds;
         is["mode"] = ipc->bcast() ? "bcast" : "pull";
         is["fused"] = ipc->fused();
+        is["lite"] = ipc->lite();
         is["memory"] = ipc->memory_kind();
         is["bytes_pushed"] = ipc->stats().bytes_pushed;
         is["bytes_pulled"] = ipc->stats().bytes_pulled;
@@ -567,9 +604,10 @@ class WorkerCore final : public EngineHost {
   std::set<std::string> tags_;  // stable storage of declared access tags
   int32_t lag_;
   DType dt_ = DType::F32;
-  std::unique_ptr<Device> dev_;
+  std::shared_ptr<Device> dev_;  // shared between engines that adopt one transport
   std::unique_ptr<DataPlane> dp_;
-  std::unique_ptr<P2P> p2p_;
+  std::shared_ptr<P2P> p2p_;
+  std::shared_ptr<P2P> adopted_p2p_;
   std::unique_ptr<StreamLink> stream_link_;
   std::unique_ptr<ReactiveLink> reactive_link_;
   bool self_drive_ = false;
@@ -669,14 +707,17 @@ PYBIND11_MODULE(_native, m) {
       .def("set_exact_unit_bytes", &WorkerCore::set_exact_unit_bytes)
       .def("connect_none", &WorkerCore::connect_none)
       .def("connect_ipc_p2p", &WorkerCore::connect_ipc_p2p)
+      .def("adopt_transport", &WorkerCore::adopt_transport)
+      .def("connect_adopted", &WorkerCore::connect_adopted)
+      .def("transport_id", &WorkerCore::transport_id)
       .def("p2p_handle", &WorkerCore::p2p_handle)
       .def("p2p_open", &WorkerCore::p2p_open)
-      .def("ipc_handle", &WorkerCore::ipc_handle)
+      .def("ipc_handle", &WorkerCore::ipc_handle, py::arg("capacity") = 0, py::arg("share") = nullptr)
       .def("ipc_open", &WorkerCore::ipc_open)
       .def("ipc_error", &WorkerCore::ipc_error)
       .def("ipc_close", &WorkerCore::ipc_close)
       .def("ipc_set_mode", &WorkerCore::ipc_set_mode, py::arg("mode"), py::arg("fused") = false,
-           py::arg("threads") = 0)
+           py::arg("threads") = 0, py::arg("lite") = -1)
       .def("scatter_count", &WorkerCore::scatter_count)
       .def("reduced_arrivals", &WorkerCore::reduced_arrivals);
 

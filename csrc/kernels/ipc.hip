@@ -121,11 +121,17 @@ __device__ void reduce_vec_n(const IpcArgs& a, const char* mine, const char* slo
       for (int s = 0; s < NS; ++s) Elt<T>::add(acc, v[s][u]);
       if (i < nv) {
         const uint4 w = Elt<T>::pack(acc);
-        reinterpret_cast<uint4*>(o)[i] = w;
+        reinterpret_cast<uint4*>(o)[i] = w;  // my output: read by this rank only
+        // window bytes (read by peers): write-through with `lite`, else plain + release
         if (bc) {
 #pragma unroll
-          for (int p = 0; p < NS; ++p)
-            if (p != me) reinterpret_cast<uint4*>(a.gdata[p] + gather_off)[i] = w;
+          for (int p = 0; p < NS; ++p) {
+            if (p == me) continue;
+            if (a.lite) store_sys16(sys_rsrc(a.gdata[p] + gather_off, nv * 16), i * 16, w);
+            else reinterpret_cast<uint4*>(a.gdata[p] + gather_off)[i] = w;
+          }
+        } else if (a.lite) {
+          store_sys16(sys_rsrc(r, nv * 16), i * 16, w);
         } else {
           reinterpret_cast<uint4*>(r)[i] = w;
         }
@@ -134,8 +140,10 @@ __device__ void reduce_vec_n(const IpcArgs& a, const char* mine, const char* slo
   }
 }
 
+// Returns whether the window bytes it stored need a release fence before the
+// flag (plain stores), i.e. false only for the write-through `lite` bodies.
 template <typename T>
-__device__ void reduce_span(const IpcArgs& a, const char* mine, const char* slots, int64_t slot_bytes, char* o,
+__device__ bool reduce_span(const IpcArgs& a, const char* mine, const char* slots, int64_t slot_bytes, char* o,
                             char* r, int64_t gather_off, int64_t n) {
   constexpr int ES = sizeof(T);
   constexpr int PV = Elt<T>::kPerVec;
@@ -144,15 +152,16 @@ __device__ void reduce_span(const IpcArgs& a, const char* mine, const char* slot
   bool vec = ((uintptr_t(mine) | uintptr_t(slots) | uintptr_t(slot_bytes) | uintptr_t(o) | uintptr_t(r) |
                uintptr_t(bc ? gather_off : 0) | uintptr_t(n * ES)) & 15) == 0;
   if (vec) {
+    const bool fenced = !a.lite;
     switch (N) {  // the node's rank counts: compile-time source loops
-      case 2: return reduce_vec_n<T, 2>(a, mine, slots, slot_bytes, o, r, gather_off, n);
-      case 3: return reduce_vec_n<T, 3>(a, mine, slots, slot_bytes, o, r, gather_off, n);
-      case 4: return reduce_vec_n<T, 4>(a, mine, slots, slot_bytes, o, r, gather_off, n);
-      case 5: return reduce_vec_n<T, 5>(a, mine, slots, slot_bytes, o, r, gather_off, n);
-      case 6: return reduce_vec_n<T, 6>(a, mine, slots, slot_bytes, o, r, gather_off, n);
-      case 7: return reduce_vec_n<T, 7>(a, mine, slots, slot_bytes, o, r, gather_off, n);
-      case 8: return reduce_vec_n<T, 8>(a, mine, slots, slot_bytes, o, r, gather_off, n);
-      case 16: return reduce_vec_n<T, 16>(a, mine, slots, slot_bytes, o, r, gather_off, n);
+      case 2: reduce_vec_n<T, 2>(a, mine, slots, slot_bytes, o, r, gather_off, n); return fenced;
+      case 3: reduce_vec_n<T, 3>(a, mine, slots, slot_bytes, o, r, gather_off, n); return fenced;
+      case 4: reduce_vec_n<T, 4>(a, mine, slots, slot_bytes, o, r, gather_off, n); return fenced;
+      case 5: reduce_vec_n<T, 5>(a, mine, slots, slot_bytes, o, r, gather_off, n); return fenced;
+      case 6: reduce_vec_n<T, 6>(a, mine, slots, slot_bytes, o, r, gather_off, n); return fenced;
+      case 7: reduce_vec_n<T, 7>(a, mine, slots, slot_bytes, o, r, gather_off, n); return fenced;
+      case 8: reduce_vec_n<T, 8>(a, mine, slots, slot_bytes, o, r, gather_off, n); return fenced;
+      case 16: reduce_vec_n<T, 16>(a, mine, slots, slot_bytes, o, r, gather_off, n); return fenced;
       default: break;
     }
     const int64_t nv = n / PV;
@@ -209,6 +218,7 @@ __device__ void reduce_span(const IpcArgs& a, const char* mine, const char* slot
       }
     }
   }
+  return true;  // plain window stores (runtime-N or scalar body): release before the flag
 }
 
 // ---- the three phases of a round, one work item each ----------------------
@@ -218,11 +228,32 @@ template <int ES>
 __device__ void push_item(const IpcArgs& a, int32_t j, int32_t p) {
   const int64_t e0 = int64_t(j) * a.portion;
   const int64_t n = max(int64_t(0), min(a.portion, a.blen[p] - e0));
-  if (n > 0)
-    copy_bytes(a.data[p] + (int64_t(a.me) * a.slot + e0) * ES, a.in + (a.bstart[p] + e0) * ES, n * ES);
-  release_wg();
+  char* dst = a.data[p] + (int64_t(a.me) * a.slot + e0) * ES;
+  const char* src = a.in + (a.bstart[p] + e0) * ES;
+  const bool lite = a.lite && ((uintptr_t(dst) | uintptr_t(src) | uintptr_t(n * ES)) & 15) == 0;
+  if (n > 0) {
+    if (lite) copy_out_sys(dst, src, n * ES);  // write-through: no release fence needed
+    else copy_bytes(dst, src, n * ES);
+  }
+  if (lite) drain_wg();
+  else release_wg();
   if (threadIdx.x == 0) signal(a.flags[p] + ipc_flag_push(a.me, j, a.nportions), a.round);
   __syncthreads();
+}
+
+// After the flag waits: every lane's verdict combined; without `lite` lane 0
+// also runs the system-scope acquire (with `lite` every read of the handed-off
+// bytes is a system-coherent load, which needs none).
+__device__ inline bool settle_waits(const IpcArgs& a, bool ok) {
+  ok = __syncthreads_and(ok ? 1 : 0) != 0;
+  if (!a.lite) {
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+  }
+  return ok;
 }
 
 // Part `part` of portion j of my block: wait for every peer's push of it, sum,
@@ -236,22 +267,24 @@ __device__ void reduce_item(const IpcArgs& a, int32_t j, int32_t part) {
   // each item's part of its portion (a multiple of 64 elements)
   const int64_t per = ((a.portion / kReduceSplit) + 63) / 64 * 64;
   bool ok = true;
-  if (threadIdx.x == 0) {
-    const uint64_t deadline = wall_clock64() + a.timeout;
-    for (int32_t s = 0; s < N && ok; ++s)
-      if (s != me) ok = wait_flag(a, fl + ipc_flag_push(s, j, np), a.round, deadline);
+  {
+    // every peer's push flag polled by a lane of its own: the waits overlap
+    const int32_t s = int32_t(threadIdx.x);
+    if (s < N && s != me) ok = wait_flag(a, fl + ipc_flag_push(s, j, np), a.round, wall_clock64() + a.timeout);
   }
-  ok = acquire_all(ok);
+  ok = settle_waits(a, ok);
   const int64_t e0 = int64_t(j) * a.portion;
   const int64_t n = max(int64_t(0), min(a.portion, a.blen[me] - e0));
   const int64_t p0 = min(n, part * per), p1 = min(n, p0 + per);
+  bool fenced = !a.lite;
   if (ok && p1 > p0) {
     const int64_t e = e0 + p0;
-    reduce_span<T>(a, a.in + (a.bstart[me] + e) * ES, a.data[me] + e * ES, a.slot * ES,
-                   a.out + (a.bstart[me] + e) * ES, a.gdata[me] + e * ES,
-                   a.bcast ? (int64_t(1 + me) * a.slot + e) * ES : int64_t(-1), p1 - p0);
+    fenced = reduce_span<T>(a, a.in + (a.bstart[me] + e) * ES, a.data[me] + e * ES, a.slot * ES,
+                            a.out + (a.bstart[me] + e) * ES, a.gdata[me] + e * ES,
+                            a.bcast ? (int64_t(1 + me) * a.slot + e) * ES : int64_t(-1), p1 - p0);
   }
-  release_wg();
+  if (fenced) release_wg();  // (uniform: the alignment of an item is the same for every thread)
+  else drain_wg();
   if (threadIdx.x == 0) {
     if (a.bcast) {
       for (int32_t p = 0; p < N; ++p)
@@ -270,14 +303,14 @@ template <int ES>
 __device__ void phase2_item(const IpcArgs& a, int32_t j, int32_t p) {
   const int32_t me = a.me, N = a.N, np = a.nportions;
   bool ok = true;
-  if (threadIdx.x == 0) {
-    const uint64_t deadline = wall_clock64() + a.timeout;
-    for (int32_t part = 0; part < kReduceSplit && ok; ++part)
+  {
+    const int32_t part = int32_t(threadIdx.x);  // one lane per reduce part: the waits overlap
+    if (part < kReduceSplit)
       ok = wait_flag(a, a.bcast ? a.flags[me] + ipc_flag_gather(p, j, part, N, np)
-                             : a.flags[p] + ipc_flag_reduced(j, part, N, np),
-                     a.round, deadline);
+                                : a.flags[p] + ipc_flag_reduced(j, part, N, np),
+                     a.round, wall_clock64() + a.timeout);
   }
-  ok = acquire_all(ok);
+  ok = settle_waits(a, ok);
   const int64_t e0 = int64_t(j) * a.portion;
   const int64_t n = max(int64_t(0), min(a.portion, a.blen[p] - e0));
   const char* src = a.bcast ? a.gdata[me] + (int64_t(1 + p) * a.slot + e0) * ES
@@ -467,7 +500,7 @@ namespace akka {
 // N x block, writes the output block and the `reduced` row.  Returns ms per
 // launch over `iters` launches.
 double ipc_reduce_role_bench(int32_t N, int64_t block, int64_t portion_bytes, DType dt, bool plain, int32_t iters,
-                             int32_t threads, int32_t device, int32_t win_kind) {
+                             int32_t threads, int32_t device, int32_t win_kind, bool lite) {
   auto ok = [](hipError_t e, const char* w) {
     if (e != hipSuccess) throw AkkaError(std::string("akka ipc bench: ") + w + ": " + hipGetErrorString(e));
   };
@@ -513,6 +546,7 @@ double ipc_reduce_role_bench(int32_t N, int64_t block, int64_t portion_bytes, DT
   a.me = 0;
   a.threads = threads;
   a.plain_slots = plain ? 1 : 0;
+  a.lite = lite ? 1 : 0;
   a.round = 1;
   a.timeout = uint64_t(1) << 40;
   a.in = in;
@@ -536,14 +570,14 @@ double ipc_reduce_role_bench(int32_t N, int64_t block, int64_t portion_bytes, DT
   float ms = 0.f;
   ok(hipEventElapsedTime(&ms, e0, e1), "elapsed");
   const uint32_t e = *err;
-  hipEventDestroy(e0);
-  hipEventDestroy(e1);
-  hipFree(data);
-  hipFree(gdata);
-  hipFree(flags);
-  hipFree(in);
-  hipFree(out);
-  hipHostFree(err);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  (void)hipFree(data);
+  (void)hipFree(gdata);
+  (void)hipFree(flags);
+  (void)hipFree(in);
+  (void)hipFree(out);
+  (void)hipHostFree(err);
   if (e != 0) throw AkkaError("akka ipc bench: a wait failed");
   return double(ms) / std::max(1, iters);
 }

@@ -49,6 +49,7 @@ struct IpcArgs {
   int32_t N = 0, me = 0;
   int32_t threads = 256;    // workgroup size of the round's kernels (256 / 512 / 1024)
   int32_t plain_slots = 0;  // measurement only: plain slot loads behind the acquire instead of sc0 sc1 loads
+  int32_t lite = 0;         // fence-free hand-offs: write-through window stores + drained flags (xgmi_device.h)
   uint32_t round = 0;       // this round's id (1, 2, ... identical on every rank)
   uint64_t timeout = 0;     // per wait, in wall-clock ticks (100 MHz)
   const char* in = nullptr;  // round input [S]
@@ -134,7 +135,7 @@ int32_t ipc_p2p_resident_wgs(int32_t device);
 // Microbenchmark of the exact round's reduce role alone (ipc.hip): ms per launch.
 // win_kind: 0 fine-grained, 1 coarse, 2 uncached window memory.
 double ipc_reduce_role_bench(int32_t N, int64_t block, int64_t portion_bytes, DType dt, bool plain, int32_t iters,
-                             int32_t threads, int32_t device, int32_t win_kind = 0);
+                             int32_t threads, int32_t device, int32_t win_kind = 0, bool lite = false);
 
 // Enqueue one round on `s`: push, reduce, then pull (bcast = 0) or, with
 // bcast = 1, the reducer writes its rows into every peer's gather slot and a

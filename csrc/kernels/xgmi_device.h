@@ -123,6 +123,47 @@ __device__ inline void copy_in(char* __restrict__ dst, const char* __restrict__ 
   }
 }
 
+// ---- fence-free hand-offs ("lite") -------------------------------------------
+// Producer: every byte a consumer will read goes out as a system-coherent
+// (sc0 sc1, write-through) store; each storing wave waits for its stores
+// (s_waitcnt vmcnt(0)), the workgroup meets at a barrier, lane 0 stores the
+// flag.  Consumer: lane(s) poll the flag(s); after the barrier every load of
+// the bytes is a system-coherent load.  No buffer_wbl2 / buffer_inv at all --
+// MI355X_MICROARCH.md's "handoff-flag" / "publish-large" forms (write-through
+// stores + drained flag; sc loads in place of the acquire), at system scope.
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+__device__ inline void store_sys16(__amdgpu_buffer_rsrc_t r, int64_t off, const uint4& v) {
+  u32x4 w;
+  w[0] = v.x;
+  w[1] = v.y;
+  w[2] = v.z;
+  w[3] = v.w;
+  __builtin_amdgcn_raw_buffer_store_b128(w, r, int(off), 0, kSysAux);
+}
+
+// dst (a window, read by a peer) <- src (local), 16-byte aligned.
+__device__ inline void copy_out_sys(char* __restrict__ dst, const char* __restrict__ src, int64_t bytes) {
+  const auto r = sys_rsrc(dst, bytes);
+  const uint4* s = reinterpret_cast<const uint4*>(src);
+  const int64_t n = bytes >> 4;
+  int64_t i = threadIdx.x;
+  for (; i + (kUnroll - 1) * int(blockDim.x) < n; i += kUnroll * int(blockDim.x)) {
+    uint4 v[kUnroll];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) v[u] = s[i + u * int(blockDim.x)];
+#pragma unroll
+    for (int u = 0; u < kUnroll; ++u) store_sys16(r, (i + u * int(blockDim.x)) * 16, v[u]);
+  }
+  for (; i < n; i += int(blockDim.x)) store_sys16(r, i * 16, s[i]);
+}
+
+// Whole workgroup: every wave's stores performed, then lane 0 may signal.
+__device__ inline void drain_wg() {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+}
+
 __device__ inline void zero_bytes(char* __restrict__ dst, int64_t bytes) {
   if (((reinterpret_cast<uintptr_t>(dst) | uintptr_t(bytes)) & 15) == 0) {
     uint4* d = reinterpret_cast<uint4*>(dst);

@@ -20,11 +20,11 @@ namespace akka {
 
 namespace {
 
-constexpr char kMagic[8] = {'A', 'K', 'I', 'P', 'C', '0', '2', 0};
+constexpr char kMagic[8] = {'A', 'K', 'I', 'P', 'C', '0', '3', 0};
 
 struct HandleBlob {  // what handle() serialises
   char magic[8];
-  int32_t rank, nranks, esize, pad;
+  int32_t rank, nranks, esize, shared;  // shared: the windows are another lane's (only flags travel)
   int64_t S, slot, portion;
   char bus[32];  // PCI bus id of the rank's GPU: ranks sharing a card (tests) share its CUs
   hipIpcMemHandle_t data, gdata, flags;
@@ -54,7 +54,16 @@ void* ipc_alloc_window(size_t bytes, std::string* kind) {
   return p;
 }
 
-IpcLane::IpcLane(Device* dev, const Geometry& g, int32_t me, DType dt)
+IpcWindows::~IpcWindows() {
+  if (!dev) return;
+  hipSetDevice(dev->device_index());
+  hipDeviceSynchronize();  // no kernel of any lane may still touch a window
+  for (void* m : opened) hipIpcCloseMemHandle(m);
+  if (data) hipFree(data);
+  if (gdata) hipFree(gdata);
+}
+
+IpcLane::IpcLane(Device* dev, const Geometry& g, int32_t me, DType dt, int64_t capacity, const IpcLane* share)
     : dev_(dev), g_(g), me_(me), dt_(dt), es_(dtype_size(dt)) {
   AKKA_CHECK(dev_ && !dev_->is_host(), "ipc lane needs a HIP device");
   AKKA_CHECK(g_.N >= 2 && g_.N <= kIpcMaxRanks, "ipc lane: 2..16 ranks");
@@ -68,22 +77,46 @@ IpcLane::IpcLane(Device* dev, const Geometry& g, int32_t me, DType dt)
   const int64_t pbytes = std::max<int64_t>(4096, env_i64("AKKA_IPC_PORTION_BYTES", int64_t(512) << 10));
   portion_ = std::max<int64_t>(1024, (pbytes / int64_t(es_)) / 1024 * 1024);
   nportions_ = int32_t(std::max<int64_t>(1, (maxb + portion_ - 1) / portion_));
-  // Two allocations (inbound slots | reduced + gather slots), each one IPC
-  // mapping.  hipIpcOpenMemHandle of a 2.5 GiB mapping hung on the test box
-  // (1.9 GiB opened at once; profiles/r02/ipc/README.md): refuse larger ones
-  // up front, every rank alike (the sizes are a function of the geometry),
-  // so the job keeps its other exact lanes instead of hanging in open().
-  in_bytes_ = size_t(g_.N) * size_t(slot_) * es_;
-  out_bytes_ = size_t(g_.N + 1) * size_t(slot_) * es_;
-  data_bytes_ = in_bytes_ + out_bytes_;
-  AKKA_CHECK(std::max(in_bytes_, out_bytes_) <= kIpcMaxWindowBytes,
-             "ipc lane: window part of " + std::to_string(std::max(in_bytes_, out_bytes_) >> 20) +
-                 " MiB exceeds the " + std::to_string(kIpcMaxWindowBytes >> 20) +
-                 " MiB an IPC mapping is known to open (buffer too large for this N; use the collective / p2p "
-                 "lanes)");
+  const size_t need_in = size_t(g_.N) * size_t(slot_) * es_;
+  const size_t need_out = size_t(g_.N + 1) * size_t(slot_) * es_;
+  if (share && share->win_ && share->win_->open && share->win_->N == g_.N && share->win_->me == me_ &&
+      share->dev_ == dev_ && share->win_->in_bytes >= need_in && share->win_->out_bytes >= need_out) {
+    win_ = share->win_;  // this geometry fits the shared windows
+    shared_windows_ = true;
+  } else {
+    // Windows sized for `capacity` elements (>= this buffer) so that lanes of
+    // engines that share this one's transport can share them too.  Every part
+    // stays below the 2 GiB IPC boundary (kIpcMaxWindowBytes), every rank
+    // alike (the sizes are a function of the geometry), so the job keeps its
+    // other exact lanes instead of hanging in open().
+    const int64_t cap = std::max<int64_t>(capacity, g_.S);
+    const int64_t cap_slot = std::max<int64_t>(slot_, ((cap + g_.N - 1) / g_.N + 63) / 64 * 64);
+    size_t in_bytes = size_t(g_.N) * size_t(cap_slot) * es_;
+    size_t out_bytes = size_t(g_.N + 1) * size_t(cap_slot) * es_;
+    if (std::max(in_bytes, out_bytes) > kIpcMaxWindowBytes) {  // capacity too ambitious: just this buffer
+      in_bytes = need_in;
+      out_bytes = need_out;
+    }
+    AKKA_CHECK(std::max(in_bytes, out_bytes) <= kIpcMaxWindowBytes,
+               "ipc lane: window part of " + std::to_string(std::max(in_bytes, out_bytes) >> 20) +
+                   " MiB exceeds the " + std::to_string(kIpcMaxWindowBytes >> 20) +
+                   " MiB an IPC mapping opens (allocations of 2 GiB or more hang in hipIpcOpenMemHandle; buffer too "
+                   "large for this N: use the p2p lanes)");
+    auto w = std::make_shared<IpcWindows>();
+    w->N = g_.N;
+    w->me = me_;
+    w->in_bytes = in_bytes;
+    w->out_bytes = out_bytes;
+    w->data = static_cast<char*>(ipc_alloc_window(in_bytes, &w->kind));
+    w->gdata = static_cast<char*>(ipc_alloc_window(out_bytes, nullptr));
+    w->dev = dev_;  // set last: a throw above leaves nothing for the destructor to free twice
+    w->peer_data.assign(size_t(g_.N), nullptr);
+    w->peer_gdata.assign(size_t(g_.N), nullptr);
+    w->peer_data[size_t(me_)] = w->data;
+    w->peer_gdata[size_t(me_)] = w->gdata;
+    win_ = std::move(w);
+  }
   flag_bytes_ = ipc_flag_bytes(g_.N, nportions_);
-  data_ = static_cast<char*>(ipc_alloc_window(in_bytes_, &mem_kind_));
-  gdata_ = static_cast<char*>(ipc_alloc_window(out_bytes_, nullptr));
   // Flags uncached: every poll and every signal goes to memory.
   if (hipExtMallocWithFlags(reinterpret_cast<void**>(&flags_), flag_bytes_, hipDeviceMallocUncached) != hipSuccess) {
     (void)hipGetLastError();
@@ -102,27 +135,18 @@ IpcLane::IpcLane(Device* dev, const Geometry& g, int32_t me, DType dt)
   timeout_ticks_ = uint64_t(std::max<int64_t>(1, env_i64("AKKA_IPC_TIMEOUT_MS", 10000))) * uint64_t(khz);
   threads_ = int32_t(env_i64("AKKA_IPC_THREADS", 256));
   if (threads_ != 512 && threads_ != 1024) threads_ = 256;
-  peer_data_.assign(size_t(g_.N), nullptr);
-  peer_gdata_.assign(size_t(g_.N), nullptr);
+  lite_ = env_i64("AKKA_IPC_LITE", 0) != 0;
   peer_flags_.assign(size_t(g_.N), nullptr);
-  peer_data_[size_t(me_)] = data_;
-  peer_gdata_[size_t(me_)] = gdata_;
   peer_flags_[size_t(me_)] = flags_;
 }
 
 IpcLane::~IpcLane() {
   hipSetDevice(dev_->device_index());
   hipDeviceSynchronize();  // no kernel of ours may still touch a window
-  for (int32_t p = 0; p < g_.N; ++p) {
-    if (p == me_) continue;
-    if (peer_data_[size_t(p)]) hipIpcCloseMemHandle(peer_data_[size_t(p)]);
-    if (peer_gdata_[size_t(p)]) hipIpcCloseMemHandle(peer_gdata_[size_t(p)]);
-    if (peer_flags_[size_t(p)]) hipIpcCloseMemHandle(peer_flags_[size_t(p)]);
-  }
-  if (data_) hipFree(data_);
-  if (gdata_) hipFree(gdata_);
+  for (void* m : opened_flags_) hipIpcCloseMemHandle(m);
   if (flags_) hipFree(flags_);
   if (err_host_) hipHostFree(err_host_);
+  // win_: freed by its last owner (IpcWindows::~IpcWindows)
 }
 
 std::string IpcLane::handle() const {
@@ -132,12 +156,15 @@ std::string IpcLane::handle() const {
   b.rank = me_;
   b.nranks = g_.N;
   b.esize = int32_t(es_);
+  b.shared = shared_windows_ ? 1 : 0;
   b.S = g_.S;
   b.slot = slot_;
   b.portion = portion_;
   AKKA_IPC_HIP(hipDeviceGetPCIBusId(b.bus, int(sizeof(b.bus)) - 1, dev_->device_index()));
-  AKKA_IPC_HIP(hipIpcGetMemHandle(&b.data, data_));
-  AKKA_IPC_HIP(hipIpcGetMemHandle(&b.gdata, gdata_));
+  if (!shared_windows_) {
+    AKKA_IPC_HIP(hipIpcGetMemHandle(&b.data, win_->data));
+    AKKA_IPC_HIP(hipIpcGetMemHandle(&b.gdata, win_->gdata));
+  }
   AKKA_IPC_HIP(hipIpcGetMemHandle(&b.flags, flags_));
   return std::string(reinterpret_cast<const char*>(&b), sizeof(b));
 }
@@ -158,18 +185,26 @@ void IpcLane::open(const std::vector<std::string>& handles) {
     AKKA_CHECK(b.rank == p && b.nranks == g_.N && b.esize == int32_t(es_) && b.S == g_.S && b.slot == slot_ &&
                    b.portion == portion_,
                "ipc lane: rank " + std::to_string(p) + "'s window was built for another geometry");
+    AKKA_CHECK((b.shared != 0) == shared_windows_,
+               "ipc lane: rank " + std::to_string(p) + " shares windows where this rank does not (or the reverse)");
     if (std::strncmp(b.bus, mybus, sizeof(mybus)) == 0) ++sharers;
     if (p == me_) continue;
-    void* d = nullptr;
-    void* gd = nullptr;
+    if (!shared_windows_) {
+      void* d = nullptr;
+      void* gd = nullptr;
+      AKKA_IPC_HIP(hipIpcOpenMemHandle(&d, b.data, hipIpcMemLazyEnablePeerAccess));
+      win_->opened.push_back(d);
+      AKKA_IPC_HIP(hipIpcOpenMemHandle(&gd, b.gdata, hipIpcMemLazyEnablePeerAccess));
+      win_->opened.push_back(gd);
+      win_->peer_data[size_t(p)] = static_cast<char*>(d);
+      win_->peer_gdata[size_t(p)] = static_cast<char*>(gd);
+    }
     void* f = nullptr;
-    AKKA_IPC_HIP(hipIpcOpenMemHandle(&d, b.data, hipIpcMemLazyEnablePeerAccess));
-    AKKA_IPC_HIP(hipIpcOpenMemHandle(&gd, b.gdata, hipIpcMemLazyEnablePeerAccess));
     AKKA_IPC_HIP(hipIpcOpenMemHandle(&f, b.flags, hipIpcMemLazyEnablePeerAccess));
-    peer_data_[size_t(p)] = static_cast<char*>(d);
-    peer_gdata_[size_t(p)] = static_cast<char*>(gd);
+    opened_flags_.push_back(f);
     peer_flags_[size_t(p)] = static_cast<uint32_t*>(f);
   }
+  win_->open = true;
   // Grid cap of the waiting kernels: their parked workgroups must leave room
   // for the other ranks' push kernels when several ranks share one card.
   max_wgs_ = int32_t(std::max<int64_t>(64, env_i64("AKKA_IPC_MAX_WGS", 1024) / std::max(1, sharers)));
@@ -182,8 +217,8 @@ void IpcLane::round(StreamH s, const void* in, void* out) {
   IpcArgs a;
   std::memset(&a, 0, sizeof(a));
   for (int32_t p = 0; p < g_.N; ++p) {
-    a.data[p] = peer_data_[size_t(p)];
-    a.gdata[p] = peer_gdata_[size_t(p)];
+    a.data[p] = win_->peer_data[size_t(p)];
+    a.gdata[p] = win_->peer_gdata[size_t(p)];
     a.flags[p] = peer_flags_[size_t(p)];
     a.bstart[p] = g_.block_start(p);
     a.blen[p] = g_.block_len(p);
@@ -195,6 +230,7 @@ void IpcLane::round(StreamH s, const void* in, void* out) {
   a.threads = threads_;
   a.bcast = bcast_ ? 1 : 0;
   a.fused = fused_ ? 1 : 0;
+  a.lite = lite_ ? 1 : 0;
   a.N = g_.N;
   a.me = me_;
   a.round = ++round_;

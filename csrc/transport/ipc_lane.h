@@ -24,6 +24,7 @@
 #pragma once
 
 #include <cstdint>
+#include <memory>
 #include <string>
 #include <vector>
 
@@ -40,16 +41,45 @@ namespace akka {
 // `kind` reports what was allocated.
 void* ipc_alloc_window(size_t bytes, std::string* kind);
 
-// Largest part of a window the lane builds (one allocation, one IPC handle).
-constexpr size_t kIpcMaxWindowBytes = size_t(1920) << 20;
+// Largest allocation the lanes export (one allocation, one IPC handle).
+// hipIpcOpenMemHandle of an allocation of 2^31 bytes or more hangs on the
+// ROCm 7.2 / MI355X pool, whatever its memory kind (fine, uncached and coarse
+// all hang at 2048 MiB and all open at 2047 MiB in 0.3 ms:
+// profiles/r03/ipc_open/) -- a 2 GiB boundary, so every part stays below it.
+constexpr size_t kIpcMaxWindowBytes = size_t(2047) << 20;
 
 struct IpcLaneStats {
   int64_t rounds = 0, bcast_rounds = 0, bytes_pushed = 0, bytes_pulled = 0;
 };
 
+// The big part of a rank's window (inbound slots | reduced row + gather
+// slots) and every peer's as mapped in this process.  Lanes of engines that
+// share one transport (same device streams, rounds issued in the same order
+// on every rank) share it: every round of any of them starts only after this
+// rank's previous round finished reading peers' windows and every peer
+// finished reading this rank's slots (the lanes' flag protocol), so one set of
+// windows serves every geometry that fits (IpcLane's `share`).
+struct IpcWindows {
+  Device* dev = nullptr;
+  int32_t N = 0, me = 0;
+  size_t in_bytes = 0, out_bytes = 0;
+  char* data = nullptr;
+  char* gdata = nullptr;
+  std::vector<char*> peer_data, peer_gdata;  // [N] (own = data / gdata)
+  std::vector<void*> opened;
+  std::string kind;
+  bool open = false;
+  ~IpcWindows();
+};
+
 class IpcLane {
  public:
-  IpcLane(Device* dev, const Geometry& g, int32_t me, DType dt);
+  // `capacity` (elements, 0: S): size the windows for a buffer this large, so
+  // that later lanes of smaller (or equal) geometry can share them; `share`:
+  // use that lane's windows when they are large enough (then this lane only
+  // allocates and exchanges its own flag area).
+  IpcLane(Device* dev, const Geometry& g, int32_t me, DType dt, int64_t capacity = 0,
+          const IpcLane* share = nullptr);
   ~IpcLane();
   IpcLane(const IpcLane&) = delete;
   IpcLane& operator=(const IpcLane&) = delete;
@@ -73,6 +103,12 @@ class IpcLane {
   // flight per CU when one rank has the GPU to itself.
   void set_threads(int32_t t) { threads_ = (t == 512 || t == 1024) ? t : 256; }
   int32_t threads() const { return threads_; }
+  // Fence-free hand-offs (xgmi_device.h "lite"): window bytes stored
+  // write-through (sc0 sc1), flags after a drain, consumers' system-coherent
+  // loads in place of the acquire -- no buffer_wbl2 / buffer_inv per item.
+  // Every rank must use the same setting in a round (AKKA_IPC_LITE).
+  void set_lite(bool on) { lite_ = on; }
+  bool lite() const { return lite_; }
   // Enqueue one exact round on `s`: in[S] from every rank summed into out[S].
   void round(StreamH s, const void* in, void* out);
   // The error word (a wait timed out): error() after draining the device,
@@ -83,8 +119,11 @@ class IpcLane {
   const uint32_t* error_word_device() const { return err_dev_; }
   int32_t nportions() const { return nportions_; }
   int64_t portion_elems() const { return portion_; }
-  size_t window_bytes() const { return data_bytes_; }
-  const std::string& memory_kind() const { return mem_kind_; }
+  size_t window_bytes() const { return win_ ? win_->in_bytes + win_->out_bytes : 0; }
+  const std::string& memory_kind() const { return win_->kind; }
+  bool shares_windows() const { return shared_windows_; }
+  // Identity of the window memory (lanes sharing windows report the same).
+  uintptr_t windows_id() const { return reinterpret_cast<uintptr_t>(win_.get()); }
   int32_t max_wgs() const { return max_wgs_; }
   int32_t ranks_on_this_gpu() const { return sharers_; }
   const IpcLaneStats& stats() const { return stats_; }
@@ -97,21 +136,20 @@ class IpcLane {
   size_t es_;
   int64_t slot_ = 0, portion_ = 0;
   int32_t nportions_ = 0;
-  size_t data_bytes_ = 0, flag_bytes_ = 0, in_bytes_ = 0, out_bytes_ = 0;
-  char* data_ = nullptr;   // inbound slots
-  char* gdata_ = nullptr;  // reduced row + gather slots
-  uint32_t* flags_ = nullptr;
+  size_t flag_bytes_ = 0;
+  std::shared_ptr<IpcWindows> win_;  // inbound slots + reduced / gather rows (maybe shared)
+  bool shared_windows_ = false;
+  uint32_t* flags_ = nullptr;        // this lane's own flag area (never shared)
   uint32_t* err_host_ = nullptr;  // host-mapped error word
   uint32_t* err_dev_ = nullptr;
-  std::vector<char*> peer_data_;      // [N] mapped windows (own = data_)
-  std::vector<char*> peer_gdata_;     // [N] mapped reduced / gather parts (own = gdata_)
   std::vector<uint32_t*> peer_flags_; // [N]
+  std::vector<void*> opened_flags_;
   uint32_t round_ = 0;
   int32_t max_wgs_ = 1024, sharers_ = 1;
   int32_t threads_ = 256;  // workgroup size of the round kernels (AKKA_IPC_THREADS)
   uint64_t timeout_ticks_ = 0;
   bool ready_ = false;
-  bool bcast_ = false, fused_ = false;
+  bool bcast_ = false, fused_ = false, lite_ = false;
   std::string mem_kind_;
   IpcLaneStats stats_;
 };

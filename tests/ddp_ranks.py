@@ -40,9 +40,11 @@ def main():
     torch.cuda.synchronize()
     flat = torch.cat([p.detach().reshape(-1).float().cpu() for p in model.parameters()])
     errs = [ar.ipc_error() for ar in state.engines.values()]
-    chosen = [getattr(ar, "tuned", {}).get("chosen") for ar in state.engines.values()]
+    # tuned once per hook (the first engine), every engine on the chosen lane
+    chosen = [state.lane] if a.tune else []
+    windows = sorted({ar.state()["link"]["ipc"]["windows_id"] for ar in state.engines.values()})
     torch.save({"flat": flat, "buckets": len(state.engines), "rounds": state.rounds, "ipc_errors": errs,
-                "chosen": chosen},
+                "chosen": chosen, "transports": state.transports(), "window_sets": len(windows)},
                os.path.join(a.out_dir, f"rank{rank}.pt"))
     dist.barrier()
     dist.destroy_process_group()

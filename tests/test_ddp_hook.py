@@ -23,18 +23,20 @@ def _train(use_hook, rank, world):
     from akka_allreduce_amd.parallel.ddp import ThresholdHookState, threshold_allreduce_hook
 
     torch.manual_seed(0)
-    model = torch.nn.Sequential(torch.nn.Linear(32, 64), torch.nn.ReLU(), torch.nn.Linear(64, 8))
-    # small bucket cap -> several buckets of different sizes
-    ddp = DDP(model, bucket_cap_mb=0.004)
+    # ~1.7 MB of parameters; DDP's first bucket is 1 MiB, and after its bucket
+    # rebuild (first step) a 0.3 MB cap gives several buckets of different sizes
+    model = torch.nn.Sequential(torch.nn.Linear(256, 512), torch.nn.ReLU(), torch.nn.Linear(512, 512),
+                                torch.nn.ReLU(), torch.nn.Linear(512, 64))
+    ddp = DDP(model, bucket_cap_mb=0.3)
     state = None
     if use_hook:
-        state = ThresholdHookState(max_chunk_size=100)
+        state = ThresholdHookState(max_chunk_size=4096)
         ddp.register_comm_hook(state, threshold_allreduce_hook)
     opt = torch.optim.SGD(ddp.parameters(), lr=0.1)
     g = torch.Generator().manual_seed(100 + rank)
     for _ in range(3):
-        x = torch.randn(16, 32, generator=g)
-        y = torch.randn(16, 8, generator=g)
+        x = torch.randn(16, 256, generator=g)
+        y = torch.randn(16, 64, generator=g)
         opt.zero_grad()
         torch.nn.functional.mse_loss(ddp(x), y).backward()
         opt.step()
@@ -50,11 +52,11 @@ def _main(rank, world, port, q):
         ref, _ = _train(False, rank, world)
         got, st = _train(True, rank, world)
         ok = all(torch.allclose(a, b, rtol=1e-5, atol=1e-6) for a, b in zip(ref, got))
-        q.put((rank, ok, st.rounds, len(st.engines)))
+        q.put((rank, ok, st.rounds, len(st.engines), st.transports()))
         dist.barrier()
         dist.destroy_process_group()
     except Exception as e:  # pragma: no cover
-        q.put((rank, False, repr(e), 0))
+        q.put((rank, False, repr(e), 0, 0))
 
 
 def test_ddp_hook_matches_stock_ddp():
@@ -67,6 +69,7 @@ def test_ddp_hook_matches_stock_ddp():
     res = sorted(q.get(timeout=240) for _ in range(2))
     for p in procs:
         p.join(timeout=60)
-    for rank, ok, rounds, engines in res:
+    for rank, ok, rounds, engines, transports in res:
         assert ok, (rank, rounds)
-        assert rounds >= 3 and engines >= 1  # one round per bucket per step
+        assert rounds >= 3 and engines >= 3  # one round per bucket per step, >= 3 bucket sizes
+        assert transports == 1  # every bucket size's engine rides on ONE transport (communicator)

@@ -95,9 +95,11 @@ def test_torch_ddp_hook_multiprocess(tune):
         res = [torch.load(os.path.join(out, f"rank{i}.pt"), weights_only=True) for i in range(n)]
     for d in res:
         assert d["ipc_errors"] and all(e == 0 for e in d["ipc_errors"])
-        if tune:  # every bucket engine tuned, the same choice on every rank
+        if tune:  # tuned once per hook, the same choice on every rank
             assert all(c and c.startswith("ipc") for c in d["chosen"]) and d["chosen"] == res[0]["chosen"]
         assert d["buckets"] >= 1 and d["rounds"] >= steps
+        # every bucket size's engine on ONE transport and ONE set of window memory
+        assert d["transports"] == 1 and d["window_sets"] == 1, d
         assert torch.equal(d["flat"], res[0]["flat"])
     want = _reference(n, steps, torch.device("cuda", 0))
     torch.testing.assert_close(res[0]["flat"], want, rtol=1e-4, atol=1e-5)

@@ -133,6 +133,23 @@ def test_ipc_window_too_large_for_one_mapping_fails_fast():
     assert "exceeds the 1920 MiB an IPC mapping is known to open" in r.stderr, r.stderr[-2000:]
 
 
+@pytest.mark.parametrize("n,size,dtype,mode", [
+    (2, 1 << 20, "float32", "rotate"),       # even blocks, all four variants round by round
+    (3, 1 << 20, "float32", "alternate"),    # uneven blocks: scalar paths keep their fences
+    (2, 3 * (1 << 18) + 8, "bfloat16", "rotate"),
+    (4, 1 << 24, "float32", "rotate"),       # many portions
+])
+def test_ipc_lane_lite_handoffs(n, size, dtype, mode):
+    """AKKA_IPC_LITE=1: fence-free hand-offs (write-through window stores,
+    drained flags, system-coherent loads) give the same bitwise sums, across
+    XCDs of the card, in every phase-2 mode."""
+    r, rows = _run(n, "--size", str(size), "--dtype", dtype, "--mode", mode, "--rounds", "4",
+                   env={"AKKA_IPC_LITE": "1", "AKKA_IPC_THREADS": "1024"})
+    assert r.returncode == 0 and len(rows) == n, r.stderr[-3000:]
+    for d in rows:
+        assert all(d["exact"]) and d["ipc_error"] == 0 and d["ipc"]["lite"] is True, d
+
+
 @pytest.mark.parametrize("threads", [512, 1024])
 @pytest.mark.parametrize("n,size,dtype,mode", [
     (2, 1 << 20, "float32", "rotate"),       # even blocks, all four variants round by round

@@ -90,8 +90,9 @@ def test_onesided_straggler_steady_state():
     fast = rows[:3]
     for d in fast:
         base, strag = _median_tail(d["no_straggler"]["ms"]), _median_tail(d["straggler"]["ms"])
-        # CPU processes share 8 cores: allow the scheduler a few ms on top of 2x
-        assert strag <= 2 * base + 3.0, (d["rank"], base, strag)
+        # CPU processes share 8 cores (and other tests' workers under xdist):
+        # allow the scheduler a few ms on top of 2x
+        assert strag <= 2 * base + 5.0, (d["rank"], base, strag)
         assert d["straggler"]["rounds"][-1] >= 127
     s = rows[3]
     assert s["stats"]["skipped_rounds"] > 0, s["stats"]
