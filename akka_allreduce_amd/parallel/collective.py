@@ -39,6 +39,7 @@ before the first HIP call, or parked streams share hardware queues.
 from __future__ import annotations
 
 import os
+import time
 from typing import Any, Optional
 
 import torch
@@ -365,7 +366,9 @@ class ThresholdAllreduce:
         missing = [i for i, h in enumerate(handles) if not h]
         if missing:
             raise RuntimeError(f"enable_ipc: ranks {missing} could not create their ipc windows")
+        t0 = time.perf_counter()
         self.worker.ipc_open(handles)
+        self.ipc_open_s = time.perf_counter() - t0  # mapping the peers' windows (no rendezvous in it)
 
     def set_ipc_mode(self, mode: str, fused: bool = False, threads: int = 0, lite: Optional[bool] = None) -> None:
         """Phase 2 of the ipc lane: ``"pull"`` or ``"bcast"``, optionally ``fused``

@@ -26,6 +26,7 @@ def main() -> None:
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--kinds", default="fine", help="window memory: fine,coarse,uncached")
     ap.add_argument("--portion-kb", default="512", help="portion sizes (KiB): 4 reduce workgroups per portion")
+    ap.add_argument("--max-wgs", default="1024", help="grid caps, in 256-thread workgroups (AKKA_IPC_MAX_WGS)")
     a = ap.parse_args()
     from akka_allreduce_amd._native_loader import load
 
@@ -37,14 +38,15 @@ def main() -> None:
             for kind in a.kinds.split(","):
                 for pk in [int(x) for x in a.portion_kb.split(",")]:
                     for th in [int(x) for x in a.threads.split(",")]:
-                        for mode in a.modes.split(","):
-                            ms = n.ipc_reduce_role_bench(N, block, pk << 10, a.dtype, mode == "plain", a.iters, th,
-                                                         0, kind, mode == "lite")
-                            rd, wr = N * block * es, 2 * block * es
-                            print(json.dumps({"N": N, "block_mb": mb, "kind": kind, "portion_kb": pk, "threads": th,
-                                              "loads": mode, "dtype": a.dtype, "us": round(ms * 1e3, 2),
-                                              "read_bytes": rd, "write_bytes": wr,
-                                              "TBps": round((rd + wr) / (ms * 1e-3) / 1e12, 3)}), flush=True)
+                        for cap in [int(x) for x in a.max_wgs.split(",")]:
+                            for mode in a.modes.split(","):
+                                ms = n.ipc_reduce_role_bench(N, block, pk << 10, a.dtype, mode == "plain", a.iters,
+                                                             th, 0, kind, mode == "lite", cap)
+                                rd, wr = N * block * es, 2 * block * es
+                                print(json.dumps({"N": N, "block_mb": mb, "kind": kind, "portion_kb": pk,
+                                                  "threads": th, "max_wgs": cap, "loads": mode, "dtype": a.dtype,
+                                                  "us": round(ms * 1e3, 2), "read_bytes": rd, "write_bytes": wr,
+                                                  "TBps": round((rd + wr) / (ms * 1e-3) / 1e12, 3)}), flush=True)
 
 
 if __name__ == "__main__":

@@ -71,14 +71,14 @@ void bind_probe(py::module_& m) {
   });
   m.def("ipc_reduce_role_bench", [](int32_t N, int64_t block, int64_t portion_bytes, const std::string& dtype,
                                     bool plain, int32_t iters, int32_t threads, int32_t device, const std::string& kind,
-                                    bool lite) {
+                                    bool lite, int32_t max_wgs) {
     const int32_t wk = kind == "coarse" ? 1 : kind == "uncached" ? 2 : 0;
     py::gil_scoped_release nogil;
     return ipc_reduce_role_bench(N, block, portion_bytes, dtype == "bfloat16" ? DType::BF16 : DType::F32, plain, iters,
-                                 threads, device, wk, lite);
+                                 threads, device, wk, lite, max_wgs);
   }, py::arg("N"), py::arg("block"), py::arg("portion_bytes") = int64_t(512) << 10, py::arg("dtype") = "float32",
      py::arg("plain") = false, py::arg("iters") = 20, py::arg("threads") = 256, py::arg("device") = 0,
-     py::arg("kind") = "fine", py::arg("lite") = false);
+     py::arg("kind") = "fine", py::arg("lite") = false, py::arg("max_wgs") = 1024);
   m.def("ipc_probe_close", [](uintptr_t p) { check(hipIpcCloseMemHandle(reinterpret_cast<void*>(p)), "close"); });
   m.def("ipc_probe_free", [](uintptr_t p) { check(hipFree(reinterpret_cast<void*>(p)), "free"); });
 }

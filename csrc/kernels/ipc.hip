@@ -121,7 +121,9 @@ __device__ void reduce_vec_n(const IpcArgs& a, const char* mine, const char* slo
       for (int s = 0; s < NS; ++s) Elt<T>::add(acc, v[s][u]);
       if (i < nv) {
         const uint4 w = Elt<T>::pack(acc);
-        reinterpret_cast<uint4*>(o)[i] = w;  // my output: read by this rank only
+        // my output: read by this rank only, after the round -- streamed past
+        // the caches so it does not evict the slots still to be read
+        store_nt16(reinterpret_cast<uint4*>(o) + i, w);
         // window bytes (read by peers): write-through with `lite`, else plain + release
         if (bc) {
 #pragma unroll
@@ -500,7 +502,7 @@ namespace akka {
 // N x block, writes the output block and the `reduced` row.  Returns ms per
 // launch over `iters` launches.
 double ipc_reduce_role_bench(int32_t N, int64_t block, int64_t portion_bytes, DType dt, bool plain, int32_t iters,
-                             int32_t threads, int32_t device, int32_t win_kind, bool lite) {
+                             int32_t threads, int32_t device, int32_t win_kind, bool lite, int32_t max_wgs) {
   auto ok = [](hipError_t e, const char* w) {
     if (e != hipSuccess) throw AkkaError(std::string("akka ipc bench: ") + w + ": " + hipGetErrorString(e));
   };
@@ -541,7 +543,7 @@ double ipc_reduce_role_bench(int32_t N, int64_t block, int64_t portion_bytes, DT
   a.slot = slot;
   a.portion = portion;
   a.nportions = np;
-  a.max_wgs = 1024;
+  a.max_wgs = std::max(64, max_wgs);
   a.N = N;
   a.me = 0;
   a.threads = threads;

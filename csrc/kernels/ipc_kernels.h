@@ -133,9 +133,11 @@ void launch_ipc_p2p_group(hipStream_t s, const IpcP2PArgs& a);
 int32_t ipc_p2p_resident_wgs(int32_t device);
 
 // Microbenchmark of the exact round's reduce role alone (ipc.hip): ms per launch.
-// win_kind: 0 fine-grained, 1 coarse, 2 uncached window memory.
+// win_kind: 0 fine-grained, 1 coarse, 2 uncached window memory; max_wgs: the
+// grid cap in 256-thread workgroups (IpcArgs::max_wgs).
 double ipc_reduce_role_bench(int32_t N, int64_t block, int64_t portion_bytes, DType dt, bool plain, int32_t iters,
-                             int32_t threads, int32_t device, int32_t win_kind = 0, bool lite = false);
+                             int32_t threads, int32_t device, int32_t win_kind = 0, bool lite = false,
+                             int32_t max_wgs = 1024);
 
 // Enqueue one round on `s`: push, reduce, then pull (bcast = 0) or, with
 // bcast = 1, the reducer writes its rows into every peer's gather slot and a

@@ -142,6 +142,17 @@ __device__ inline void store_sys16(__amdgpu_buffer_rsrc_t r, int64_t off, const 
   __builtin_amdgcn_raw_buffer_store_b128(w, r, int(off), 0, kSysAux);
 }
 
+// Streaming (nontemporal) 16-byte store of local memory nobody reads before
+// the kernel ends: it does not evict the lines still to be read.
+__device__ inline void store_nt16(uint4* p, const uint4& v) {
+  u32x4 w;
+  w[0] = v.x;
+  w[1] = v.y;
+  w[2] = v.z;
+  w[3] = v.w;
+  __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(p));
+}
+
 // dst (a window, read by a peer) <- src (local), 16-byte aligned.
 __device__ inline void copy_out_sys(char* __restrict__ dst, const char* __restrict__ src, int64_t bytes) {
   const auto r = sys_rsrc(dst, bytes);

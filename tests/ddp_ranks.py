@@ -12,22 +12,36 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 
+def build_model(name: str) -> torch.nn.Module:
+    """``mlp``: the 2-layer MLP.  ``deep``: 3 linear layers (~1.6 MB); with a
+    0.3 MB bucket cap DDP's buckets take 3 distinct sizes over the first steps
+    (before and after its bucket rebuild) -> 3 bucket engines per hook."""
+    from akka_allreduce_amd.models.mlp import MLP
+
+    if name == "mlp":
+        return MLP(256, 512, 10)
+    return torch.nn.Sequential(torch.nn.Linear(256, 512), torch.nn.ReLU(), torch.nn.Linear(512, 512),
+                               torch.nn.ReLU(), torch.nn.Linear(512, 10))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out-dir", required=True)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--tune", action="store_true")
+    ap.add_argument("--model", choices=["mlp", "deep"], default="mlp")
+    ap.add_argument("--bucket-mb", type=float, default=0.25)
     a = ap.parse_args()
     rank = int(os.environ["RANK"])
     dist.init_process_group("gloo")
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    from akka_allreduce_amd.models.mlp import MLP, synthetic_batch
+    from akka_allreduce_amd.models.mlp import synthetic_batch
     from akka_allreduce_amd.parallel.ddp import ThresholdHookState, threshold_allreduce_hook
 
     torch.manual_seed(0)
-    model = torch.nn.parallel.DistributedDataParallel(MLP(256, 512, 10).to(dev), device_ids=[0],
-                                                      bucket_cap_mb=0.25)
+    model = torch.nn.parallel.DistributedDataParallel(build_model(a.model).to(dev), device_ids=[0],
+                                                      bucket_cap_mb=a.bucket_mb)
     state = ThresholdHookState(data_plane="ipc", max_chunk_size=1 << 14, tune=a.tune)
     model.register_comm_hook(state, threshold_allreduce_hook)
     opt = torch.optim.SGD(model.parameters(), lr=0.1)

@@ -47,7 +47,8 @@ def main():
     from akka_allreduce_amd.parallel import ThresholdAllreduce
 
     ar = ThresholdAllreduce(a.size, max_chunk_size=max(1, a.size // 16), dtype=dtype, device=dev, data_plane="ipc")
-    res = {"rank": rank, "exact": [], "lane": ar.state()["link"]["lane"]}
+    res = {"rank": rank, "exact": [], "lane": ar.state()["link"]["lane"],
+           "ipc_open_s": getattr(ar, "ipc_open_s", None)}
     for r in range(a.rounds):
         if r > 0 and rank == a.skip_rank:
             break

@@ -23,11 +23,14 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-def _reference(n, steps, dev):
-    from akka_allreduce_amd.models.mlp import MLP, synthetic_batch
+def _reference(n, steps, dev, model_name="mlp"):
+    from akka_allreduce_amd.models.mlp import synthetic_batch
+
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from ddp_ranks import build_model
 
     torch.manual_seed(0)
-    model = MLP(256, 512, 10).to(dev)
+    model = build_model(model_name).to(dev)
     for s in range(steps):
         grads = None
         for r in range(n):
@@ -77,17 +80,19 @@ def _round_diagnosis(res, n, steps) -> str:
     return "\n".join(lines)
 
 
-@pytest.mark.parametrize("tune", [False, True])
-def test_torch_ddp_hook_multiprocess(tune):
+@pytest.mark.parametrize("tune,model", [(False, "mlp"), (True, "mlp"), (True, "deep")])
+def test_torch_ddp_hook_multiprocess(tune, model):
     """torch DDP with the comm hook on the ipc data plane, 2 processes: the
     hook's rounds average every bucket across the processes (same result as
-    the mean-gradient reference), several buckets -> several allreduce
-    engines, all created collectively inside backward."""
+    the mean-gradient reference), several bucket sizes -> several allreduce
+    engines, all created collectively inside backward, all on one transport
+    and one window set, tuned once."""
     n, steps = 2, 3
     with tempfile.TemporaryDirectory() as out:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
                "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
-               os.path.join(ROOT, "tests", "ddp_ranks.py"), "--out-dir", out, "--steps", str(steps)]
+               os.path.join(ROOT, "tests", "ddp_ranks.py"), "--out-dir", out, "--steps", str(steps),
+               "--model", model, "--bucket-mb", "0.3" if model == "deep" else "0.25"]
         if tune:
             cmd.append("--tune")
         r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT)
@@ -97,9 +102,9 @@ def test_torch_ddp_hook_multiprocess(tune):
         assert d["ipc_errors"] and all(e == 0 for e in d["ipc_errors"])
         if tune:  # tuned once per hook, the same choice on every rank
             assert all(c and c.startswith("ipc") for c in d["chosen"]) and d["chosen"] == res[0]["chosen"]
-        assert d["buckets"] >= 1 and d["rounds"] >= steps
+        assert d["buckets"] >= (3 if model == "deep" else 1) and d["rounds"] >= steps
         # every bucket size's engine on ONE transport and ONE set of window memory
         assert d["transports"] == 1 and d["window_sets"] == 1, d
         assert torch.equal(d["flat"], res[0]["flat"])
-    want = _reference(n, steps, torch.device("cuda", 0))
+    want = _reference(n, steps, torch.device("cuda", 0), model)
     torch.testing.assert_close(res[0]["flat"], want, rtol=1e-4, atol=1e-5)

@@ -124,13 +124,25 @@ def test_ipc_round_waits_for_callers_pending_work_on_its_buffers():
 
 
 def test_ipc_window_too_large_for_one_mapping_fails_fast():
-    """A window beyond what one IPC mapping is known to open (an open of a
-    2.5 GiB window hung on the test box) is refused at construction on every
-    rank, with a message, instead of hanging in hipIpcOpenMemHandle."""
-    # N=2 fp32: slot = S/2 elements; the reduced + gather part is 3 slots
+    """A window part of 2 GiB or more (allocations that size hang in
+    hipIpcOpenMemHandle, whatever the memory kind: profiles/r03/ipc_open/) is
+    refused at construction on every rank, with a message, instead of
+    hanging."""
+    # N=2 fp32: slot = S/2 elements; the reduced + gather part is 3 slots = 2160 MiB
     r, rows = _run(2, "--size", str(360_000_000), "--rounds", "1", timeout=150)
     assert r.returncode != 0 and not rows
-    assert "exceeds the 1920 MiB an IPC mapping is known to open" in r.stderr, r.stderr[-2000:]
+    assert "exceeds the 2047 MiB an IPC mapping opens" in r.stderr, r.stderr[-2000:]
+
+
+def test_ipc_config3_window_opens_fast():
+    """BASELINE config 3's buffer (1 GiB bf16) at N=2: 1.5 GiB window parts,
+    below the 2 GiB boundary, map in well under a second and the round is
+    exact."""
+    r, rows = _run(2, "--size", str(1 << 29), "--dtype", "bfloat16", "--rounds", "1", timeout=200)
+    assert r.returncode == 0 and len(rows) == 2, r.stderr[-3000:]
+    for d in rows:
+        assert d["exact"] == [True] and d["ipc_error"] == 0, d
+        assert d["ipc_open_s"] is not None and d["ipc_open_s"] < 1.0, d
 
 
 @pytest.mark.parametrize("n,size,dtype,mode", [
