@@ -821,7 +821,8 @@ def main() -> int:
                       "xgmi-mailbox-p2p" if args.data_plane == "ipc_p2p" else
                       "rccl-pair-reactive" if ar.transport == "reactive" else "rccl-p2p-xgmi")
         if world > 1 and dev.type == "cuda" else ("gloo-p2p" if world > 1 else "local"),
-        "data_plane": args.data_plane,
+        # N=1 moves nothing between ranks: no data plane runs
+        "data_plane": args.data_plane if world > 1 else "none (local reduce pass)",
         "async_op": args.async_op,
         "output": "fresh tensor per round" if args.fresh_out else "preallocated, reused",
     })
@@ -834,6 +835,8 @@ def main() -> int:
     if world == 1:
         line["note"] = ("N=1 has no peer: the round is one local reduce pass (input -> output), HBM-bound; "
                         "N>1 is xGMI-bound, compare it with rccl_allreduce_algbw_GBps")
+        line["host_us_note"] = ("N=1: host time of one launch on the caller's stream; at N>1 it is the engine's "
+                                "per-round scheduling (transfers + reduces), not comparable")
     else:
         # direct scatter/broadcast moves S/N per link per phase: algbw <= N*L/2
         line["xgmi_bound_algbw_GBps"] = round(world * XGMI_LINK_GBPS / 2, 1)

@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "ipc_kernels.h"
 #include "xgmi_device.h"
@@ -144,7 +145,9 @@ __device__ void reduce_vec_n(const IpcArgs& a, const char* mine, const char* slo
 
 // Returns whether the window bytes it stored need a release fence before the
 // flag (plain stores), i.e. false only for the write-through `lite` bodies.
-template <typename T>
+// NS > 0: the kernel was instantiated for N == NS (one kernel per node rank
+// count, so each gets the registers of its own body only); NS == 0: any N.
+template <typename T, int NS>
 __device__ bool reduce_span(const IpcArgs& a, const char* mine, const char* slots, int64_t slot_bytes, char* o,
                             char* r, int64_t gather_off, int64_t n) {
   constexpr int ES = sizeof(T);
@@ -154,17 +157,9 @@ __device__ bool reduce_span(const IpcArgs& a, const char* mine, const char* slot
   bool vec = ((uintptr_t(mine) | uintptr_t(slots) | uintptr_t(slot_bytes) | uintptr_t(o) | uintptr_t(r) |
                uintptr_t(bc ? gather_off : 0) | uintptr_t(n * ES)) & 15) == 0;
   if (vec) {
-    const bool fenced = !a.lite;
-    switch (N) {  // the node's rank counts: compile-time source loops
-      case 2: reduce_vec_n<T, 2>(a, mine, slots, slot_bytes, o, r, gather_off, n); return fenced;
-      case 3: reduce_vec_n<T, 3>(a, mine, slots, slot_bytes, o, r, gather_off, n); return fenced;
-      case 4: reduce_vec_n<T, 4>(a, mine, slots, slot_bytes, o, r, gather_off, n); return fenced;
-      case 5: reduce_vec_n<T, 5>(a, mine, slots, slot_bytes, o, r, gather_off, n); return fenced;
-      case 6: reduce_vec_n<T, 6>(a, mine, slots, slot_bytes, o, r, gather_off, n); return fenced;
-      case 7: reduce_vec_n<T, 7>(a, mine, slots, slot_bytes, o, r, gather_off, n); return fenced;
-      case 8: reduce_vec_n<T, 8>(a, mine, slots, slot_bytes, o, r, gather_off, n); return fenced;
-      case 16: reduce_vec_n<T, 16>(a, mine, slots, slot_bytes, o, r, gather_off, n); return fenced;
-      default: break;
+    if constexpr (NS > 0) {
+      reduce_vec_n<T, NS>(a, mine, slots, slot_bytes, o, r, gather_off, n);
+      return !a.lite;
     }
     const int64_t nv = n / PV;
     for (int64_t i0 = threadIdx.x; i0 < nv; i0 += kUnroll * int(blockDim.x)) {
@@ -261,7 +256,7 @@ __device__ inline bool settle_waits(const IpcArgs& a, bool ok) {
 // Part `part` of portion j of my block: wait for every peer's push of it, sum,
 // write my output block and my `reduced` row (pull mode) or every peer's
 // gather slot [me] (bcast mode), then signal.
-template <typename T>
+template <typename T, int NS>
 __device__ void reduce_item(const IpcArgs& a, int32_t j, int32_t part) {
   constexpr int ES = sizeof(T);
   const int32_t me = a.me, N = a.N, np = a.nportions;
@@ -281,9 +276,9 @@ __device__ void reduce_item(const IpcArgs& a, int32_t j, int32_t part) {
   bool fenced = !a.lite;
   if (ok && p1 > p0) {
     const int64_t e = e0 + p0;
-    fenced = reduce_span<T>(a, a.in + (a.bstart[me] + e) * ES, a.data[me] + e * ES, a.slot * ES,
-                            a.out + (a.bstart[me] + e) * ES, a.gdata[me] + e * ES,
-                            a.bcast ? (int64_t(1 + me) * a.slot + e) * ES : int64_t(-1), p1 - p0);
+    fenced = reduce_span<T, NS>(a, a.in + (a.bstart[me] + e) * ES, a.data[me] + e * ES, a.slot * ES,
+                                a.out + (a.bstart[me] + e) * ES, a.gdata[me] + e * ES,
+                                a.bcast ? (int64_t(1 + me) * a.slot + e) * ES : int64_t(-1), p1 - p0);
   }
   if (fenced) release_wg();  // (uniform: the alignment of an item is the same for every thread)
   else drain_wg();
@@ -336,10 +331,13 @@ __global__ __launch_bounds__(kMaxThreads) void ipc_push_kernel(IpcArgs a) {
   for (int32_t w = blockIdx.x; w < items; w += gridDim.x) push_item<ES>(a, w / (a.N - 1), item_peer(a, w));
 }
 
-template <typename T>
-__global__ __launch_bounds__(kMaxThreads) void ipc_reduce_kernel(IpcArgs a) {
+// One instantiation per (dtype, rank count, launch bound): a 1024-thread bound
+// caps a thread at 128 VGPRs, a 256-thread one lets the N-source body keep
+// every load in registers (occupancy then follows its real VGPR count).
+template <typename T, int NS, int LB>
+__global__ __launch_bounds__(LB) void ipc_reduce_kernel(IpcArgs a) {
   const int32_t items = a.nportions * kReduceSplit;
-  for (int32_t w = blockIdx.x; w < items; w += gridDim.x) reduce_item<T>(a, w / kReduceSplit, w % kReduceSplit);
+  for (int32_t w = blockIdx.x; w < items; w += gridDim.x) reduce_item<T, NS>(a, w / kReduceSplit, w % kReduceSplit);
 }
 
 template <int ES>
@@ -356,7 +354,7 @@ __global__ __launch_bounds__(kMaxThreads) void ipc_phase2_kernel(IpcArgs a) {
 // dispatched in id order (per XCD), pushers never wait, reducers wait only on
 // (remote) pushers and phase-2 workgroups only on (remote) reducers -- every
 // role depends on roles with lower ids only.
-template <typename T>
+template <typename T, int NS>
 __global__ __launch_bounds__(kMaxThreads) void ipc_fused_kernel(IpcArgs a, int32_t gp, int32_t gr) {
   constexpr int ES = sizeof(T);
   const int32_t b = blockIdx.x;
@@ -365,7 +363,7 @@ __global__ __launch_bounds__(kMaxThreads) void ipc_fused_kernel(IpcArgs a, int32
     for (int32_t w = b; w < items; w += gp) push_item<ES>(a, w / (a.N - 1), item_peer(a, w));
   } else if (b < gp + gr) {
     const int32_t items = a.nportions * kReduceSplit;
-    for (int32_t w = b - gp; w < items; w += gr) reduce_item<T>(a, w / kReduceSplit, w % kReduceSplit);
+    for (int32_t w = b - gp; w < items; w += gr) reduce_item<T, NS>(a, w / kReduceSplit, w % kReduceSplit);
   } else {
     const int32_t gq = int32_t(gridDim.x) - gp - gr;
     const int32_t items = a.nportions * (a.N - 1);
@@ -373,7 +371,32 @@ __global__ __launch_bounds__(kMaxThreads) void ipc_fused_kernel(IpcArgs a, int32
   }
 }
 
-template <typename T>
+template <typename T, int NS>
+void launch_reduce(hipStream_t s, const IpcArgs& a, unsigned grid, unsigned nt) {
+  if (nt <= unsigned(kThreads))
+    hipLaunchKernelGGL((ipc_reduce_kernel<T, NS, kThreads>), dim3(grid), dim3(nt), 0, s, a);
+  else
+    hipLaunchKernelGGL((ipc_reduce_kernel<T, NS, kMaxThreads>), dim3(grid), dim3(nt), 0, s, a);
+}
+
+// Calls f(std::integral_constant<int, NS>) with NS = N for the node's rank
+// counts (2..8, 16) and NS = 0 (runtime N) otherwise.
+template <typename F>
+void with_ns(int32_t N, F&& f) {
+  switch (N) {
+    case 2: return f(std::integral_constant<int, 2>{});
+    case 3: return f(std::integral_constant<int, 3>{});
+    case 4: return f(std::integral_constant<int, 4>{});
+    case 5: return f(std::integral_constant<int, 5>{});
+    case 6: return f(std::integral_constant<int, 6>{});
+    case 7: return f(std::integral_constant<int, 7>{});
+    case 8: return f(std::integral_constant<int, 8>{});
+    case 16: return f(std::integral_constant<int, 16>{});
+    default: return f(std::integral_constant<int, 0>{});
+  }
+}
+
+template <typename T, int NS>
 void launch_round(hipStream_t s, const IpcArgs& a) {
   constexpr int ES = sizeof(T);
   // workgroup size and the waiting kernels' grid cap (given in 256-thread
@@ -388,11 +411,11 @@ void launch_round(hipStream_t s, const IpcArgs& a) {
     const int32_t gp = std::max(1, int32_t(int64_t(budget) * push_items / total));
     const int32_t gr = std::max(1, int32_t(int64_t(budget) * red_items / total));
     const int32_t gq = std::max(1, budget - gp - gr);
-    hipLaunchKernelGGL(ipc_fused_kernel<T>, dim3(unsigned(gp + gr + gq)), dim3(unsigned(nt)), 0, s, a, gp, gr);
+    hipLaunchKernelGGL((ipc_fused_kernel<T, NS>), dim3(unsigned(gp + gr + gq)), dim3(unsigned(nt)), 0, s, a, gp, gr);
     return;
   }
   hipLaunchKernelGGL(ipc_push_kernel<ES>, dim3(unsigned(push_items)), dim3(unsigned(nt)), 0, s, a);
-  hipLaunchKernelGGL(ipc_reduce_kernel<T>, dim3(unsigned(std::min(red_items, cap))), dim3(unsigned(nt)), 0, s, a);
+  launch_reduce<T, NS>(s, a, unsigned(std::min(red_items, cap)), unsigned(nt));
   hipLaunchKernelGGL(ipc_phase2_kernel<ES>, dim3(unsigned(std::min(push_items, cap))), dim3(unsigned(nt)), 0, s, a);
 }
 
@@ -488,8 +511,10 @@ int32_t ipc_p2p_resident_wgs(int32_t device) {
 
 void launch_ipc_round(hipStream_t s, const IpcArgs& a, DType dt) {
   if (a.N < 2) return;
-  if (dt == DType::F32) launch_round<float>(s, a);
-  else launch_round<uint16_t>(s, a);
+  with_ns(a.N, [&](auto ns) {
+    if (dt == DType::F32) launch_round<float, decltype(ns)::value>(s, a);
+    else launch_round<uint16_t, decltype(ns)::value>(s, a);
+  });
 }
 
 }  // namespace akka
@@ -561,8 +586,10 @@ double ipc_reduce_role_bench(int32_t N, int64_t block, int64_t portion_bytes, DT
   ok(hipEventCreate(&e0), "event");
   ok(hipEventCreate(&e1), "event");
   auto launch = [&]() {
-    if (dt == DType::F32) hipLaunchKernelGGL(ipc_reduce_kernel<float>, dim3(grid), dim3(unsigned(nt)), 0, nullptr, a);
-    else hipLaunchKernelGGL(ipc_reduce_kernel<uint16_t>, dim3(grid), dim3(unsigned(nt)), 0, nullptr, a);
+    with_ns(N, [&](auto ns) {
+      if (dt == DType::F32) launch_reduce<float, decltype(ns)::value>(nullptr, a, grid, unsigned(nt));
+      else launch_reduce<uint16_t, decltype(ns)::value>(nullptr, a, grid, unsigned(nt));
+    });
   };
   for (int i = 0; i < 3; ++i) launch();
   ok(hipEventRecord(e0, nullptr), "record");

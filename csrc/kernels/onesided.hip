@@ -182,7 +182,65 @@ __global__ __launch_bounds__(kWaitThreads) void os_decide_kernel(Args a) {
 // Sources in ascending rank order (the exact lanes' order): my own input
 // (plain loads), peers' SD slots (system-coherent loads).  Destinations: my
 // output block (local) and GD[row][me] of every peer in `okq`.
-template <typename T>
+// Vector body with the rank count NS known at compile time: every thread
+// issues the loads of all landed sources (U = 16 / NS vectors each) before the
+// first add, as the exact lanes' reduce does; a source outside `mask` reads as
+// zeros without a load (the branch is uniform).  Same ascending-source order as
+// the runtime-N body, so the sums are bitwise identical.
+template <typename T, int NS>
+__device__ void masked_sum_n(const Args& a, const char* mine, const char* sd, char* o, int64_t goff, int32_t row,
+                             uint32_t mask, uint32_t okq, int64_t off, int64_t n) {
+  constexpr int ES = sizeof(T);
+  constexpr int PV = Elt<T>::kPerVec;
+  // <= 4 vectors per source: beyond that the mask-dependent bodies of small N
+  // spill at the 1024-thread bound (128 VGPRs)
+  constexpr int U = NS >= 16 ? 1 : (16 / NS > 4 ? 4 : 16 / NS);
+  const int32_t me = a.me;
+  const int64_t nv = n / PV;
+  const int bd = int(blockDim.x);
+  for (int64_t i0 = threadIdx.x; i0 < nv; i0 += int64_t(U) * bd) {
+    uint4 v[NS][U];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      if (!((mask >> s) & 1u)) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[s][u] = make_uint4(0, 0, 0, 0);
+      } else if (s == me) {
+        const uint4* src = reinterpret_cast<const uint4*>(mine);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int64_t i = i0 + int64_t(u) * bd;
+          v[s][u] = i < nv ? src[i] : make_uint4(0, 0, 0, 0);
+        }
+      } else {
+        const auto rs = sys_rsrc(sd + (int64_t(s) * a.slot + off) * ES, n * ES);
+#pragma unroll
+        for (int u = 0; u < U; ++u) v[s][u] = load_sys16(rs, (i0 + int64_t(u) * bd) * 16);  // 0 past the end
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + int64_t(u) * bd;
+      float acc[PV];
+#pragma unroll
+      for (int e = 0; e < PV; ++e) acc[e] = 0.f;
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+        if ((mask >> s) & 1u) Elt<T>::add(acc, v[s][u]);
+      if (i < nv) {
+        const uint4 w = Elt<T>::pack(acc);
+        store_nt16(reinterpret_cast<uint4*>(o) + i, w);  // my output: not read again in this kernel
+#pragma unroll
+        for (int q = 0; q < NS; ++q)
+          if ((okq >> q) & 1u) reinterpret_cast<uint4*>(a.tab->gd[row][q] + goff)[i] = w;
+      }
+    }
+  }
+}
+
+// NS > 0: instantiated for N == NS (one reduce kernel per node rank count);
+// NS == 0: any N.
+template <typename T, int NS>
 __device__ void masked_sum(const Args& a, int32_t row, uint32_t mask, uint32_t okq, int64_t off, int64_t n) {
   constexpr int ES = sizeof(T);
   constexpr int PV = Elt<T>::kPerVec;
@@ -194,6 +252,10 @@ __device__ void masked_sum(const Args& a, int32_t row, uint32_t mask, uint32_t o
   const uintptr_t al = uintptr_t(mine) | uintptr_t(o) | uintptr_t(n * ES) | uintptr_t(goff) | uintptr_t(off * ES) |
                        uintptr_t(a.slot * ES);
   if ((al & 15) == 0) {
+    if constexpr (NS > 0) {
+      masked_sum_n<T, NS>(a, mine, sd, o, goff, row, mask, okq, off, n);
+      return;
+    }
     const int64_t nv = n / PV;
     for (int64_t i0 = threadIdx.x; i0 < nv; i0 += kUnroll * int(blockDim.x)) {
       float acc[kUnroll][PV];
@@ -245,8 +307,8 @@ __device__ void masked_sum(const Args& a, int32_t row, uint32_t mask, uint32_t o
   }
 }
 
-template <typename T>
-__global__ __launch_bounds__(kMaxThreads) void os_reduce_kernel(Args a) {
+template <typename T, int NS, int LB>
+__global__ __launch_bounds__(LB) void os_reduce_kernel(Args a) {
   const Layout& L = a.L;
   const int32_t N = L.N, P = L.P, me = a.me;
   const int32_t kme = a.tab->nch[me];
@@ -285,7 +347,7 @@ __global__ __launch_bounds__(kMaxThreads) void os_reduce_kernel(Args a) {
     }
     __syncthreads();
     const int64_t n = part_len_of(a, me, k, j);
-    if (n > 0) masked_sum<T>(a, row, mask_s, okq_s, part_off(a, k, j), n);
+    if (n > 0) masked_sum<T, NS>(a, row, mask_s, okq_s, part_off(a, k, j), n);
     release_wg();
     if (threadIdx.x == 0) {
       for (int32_t q = 0; q < N; ++q)
@@ -435,6 +497,29 @@ __global__ void os_retire_kernel(Args a) {
 
 int32_t grid_for(int64_t items, int32_t cap) { return int32_t(std::max<int64_t>(1, std::min<int64_t>(items, cap))); }
 
+// The reduce kernel for this call's rank count (2..8, 16; else runtime N) and
+// workgroup size (a 256-thread launch bound leaves the body all its VGPRs).
+template <typename T, int NS>
+void launch_reduce_ns(hipStream_t s, const Args& a, unsigned grid, unsigned nt) {
+  if (nt <= 256u) hipLaunchKernelGGL((os_reduce_kernel<T, NS, 256>), dim3(grid), dim3(nt), 0, s, a);
+  else hipLaunchKernelGGL((os_reduce_kernel<T, NS, kMaxThreads>), dim3(grid), dim3(nt), 0, s, a);
+}
+
+template <typename T>
+void launch_reduce(hipStream_t s, const Args& a, unsigned grid, unsigned nt) {
+  switch (a.L.N) {
+    case 2: return launch_reduce_ns<T, 2>(s, a, grid, nt);
+    case 3: return launch_reduce_ns<T, 3>(s, a, grid, nt);
+    case 4: return launch_reduce_ns<T, 4>(s, a, grid, nt);
+    case 5: return launch_reduce_ns<T, 5>(s, a, grid, nt);
+    case 6: return launch_reduce_ns<T, 6>(s, a, grid, nt);
+    case 7: return launch_reduce_ns<T, 7>(s, a, grid, nt);
+    case 8: return launch_reduce_ns<T, 8>(s, a, grid, nt);
+    case 16: return launch_reduce_ns<T, 16>(s, a, grid, nt);
+    default: return launch_reduce_ns<T, 0>(s, a, grid, nt);
+  }
+}
+
 template <typename T>
 void launch_call(hipStream_t s, const Args& a) {
   constexpr int ES = sizeof(T);
@@ -444,8 +529,7 @@ void launch_call(hipStream_t s, const Args& a) {
   hipLaunchKernelGGL(os_push_kernel<ES>, dim3(unsigned(grid_for(peer_items, 8192))), dim3(unsigned(nt)), 0, s, a);
   if (a.kme > 0) {
     hipLaunchKernelGGL(os_decide_kernel, dim3(unsigned(a.kme)), dim3(kWaitThreads), 0, s, a);
-    hipLaunchKernelGGL(os_reduce_kernel<T>, dim3(unsigned(grid_for(int64_t(a.kme) * a.L.P, 8192))), dim3(unsigned(nt)),
-                       0, s, a);
+    launch_reduce<T>(s, a, unsigned(grid_for(int64_t(a.kme) * a.L.P, 8192)), unsigned(nt));
   }
   hipLaunchKernelGGL(os_cdecide_kernel, dim3(1), dim3(kWaitThreads), 0, s, a);
   hipLaunchKernelGGL(os_copy_kernel<ES>, dim3(unsigned(grid_for(peer_items, 8192))), dim3(unsigned(nt)), 0, s, a);
