@@ -6,10 +6,10 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 R=$(pwd)
-O=$R/gpurun_out/pmc_ipc
+O=$R/gpurun_out/${PMC_OUT:-pmc_ipc}
 mkdir -p $O
 cd /tmp && export TMPDIR=/tmp
-ARGS="$R/bench/ipc_reduce_role.py --n 2,8 --block-mb 32 --threads 256 --modes sys,plain --iters 3"
+ARGS="$R/bench/ipc_reduce_role.py ${PMC_BENCH_ARGS:---n 2,8 --block-mb 32 --threads 256 --modes sys,plain} --iters 3"
 i=0
 for C in "TCC_EA0_RDREQ_sum TCC_EA0_RDREQ_128B_sum TCC_EA0_RDREQ_64B_sum TCC_EA0_RDREQ_32B_sum" \
          "TCC_EA0_WRREQ_sum TCC_EA0_WRREQ_64B_sum TCC_EA0_RDREQ_DRAM_sum"; do
