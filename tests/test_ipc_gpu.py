@@ -150,6 +150,8 @@ def test_ipc_config3_window_opens_fast():
     (3, 1 << 20, "float32", "alternate"),    # uneven blocks: scalar paths keep their fences
     (2, 3 * (1 << 18) + 8, "bfloat16", "rotate"),
     (4, 1 << 24, "float32", "rotate"),       # many portions
+    (8, 1 << 22, "float32", "rotate"),       # a node's rank count: the N=8 reduce kernels
+    (8, 1 << 22, "bfloat16", "rotate"),
 ])
 def test_ipc_lane_lite_handoffs(n, size, dtype, mode):
     """AKKA_IPC_LITE=1: fence-free hand-offs (write-through window stores,

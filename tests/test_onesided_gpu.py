@@ -16,6 +16,8 @@ pytestmark = pytest.mark.gpu
     (4, 1 << 22, 1 << 18, "bfloat16"),
     (2, 10, 2, "float32"),                # the reference's README demo geometry
     (4, 1 << 24, 1 << 20, "float32"),     # 64 MiB, 4 MiB chunks, 16 parts each (BASELINE config 4's shape)
+    (8, 1 << 22, 1 << 17, "float32"),     # a node's rank count: the N=8 masked-sum kernel
+    (8, 1 << 22, 1 << 17, "bfloat16"),
 ])
 def test_onesided_gpu_exact_rounds(n, size, chunk, dtype):
     r, rows = run_ranks(n, "--mode", "exact", "--size", str(size), "--chunk", str(chunk), "--dtype", dtype,
