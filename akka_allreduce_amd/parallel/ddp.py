@@ -10,8 +10,11 @@ so creation is collective-safe).  The bucket is replaced by the mean over the
 contributors that made it into the round (per-element ``count``), which is
 what DDP's default hook computes at thresholds 1 (sum / world size) and stays
 unbiased when a straggler's gradients are missing (``count`` lets
-a consumer average partial sums).  With ``transport="reactive"`` on GPUs the
-fast ranks do not wait for slow ones.
+a consumer average partial sums).  With ``transport="onesided"`` the fast
+ranks never wait for a live straggler (device-side thresholds over mapped
+windows, parallel/onesided.py; one window set per bucket size, since each
+lane's round tags are its own); ``transport="reactive"`` is the RCCL
+alternative, bounded by its send-slot pool.
 """
 from typing import Dict, Tuple
 

@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--tune", action="store_true")
     ap.add_argument("--model", choices=["mlp", "deep"], default="mlp")
     ap.add_argument("--bucket-mb", type=float, default=0.25)
+    ap.add_argument("--transport", choices=["stream", "onesided"], default="stream")
     a = ap.parse_args()
     rank = int(os.environ["RANK"])
     dist.init_process_group("gloo")
@@ -42,7 +43,7 @@ def main():
     torch.manual_seed(0)
     model = torch.nn.parallel.DistributedDataParallel(build_model(a.model).to(dev), device_ids=[0],
                                                       bucket_cap_mb=a.bucket_mb)
-    state = ThresholdHookState(data_plane="ipc", max_chunk_size=1 << 14, tune=a.tune)
+    state = ThresholdHookState(data_plane="ipc", max_chunk_size=1 << 14, tune=a.tune, transport=a.transport)
     model.register_comm_hook(state, threshold_allreduce_hook)
     opt = torch.optim.SGD(model.parameters(), lr=0.1)
     for s in range(a.steps):
@@ -53,10 +54,14 @@ def main():
         opt.step()
     torch.cuda.synchronize()
     flat = torch.cat([p.detach().reshape(-1).float().cpu() for p in model.parameters()])
-    errs = [ar.ipc_error() for ar in state.engines.values()]
+    if a.transport == "onesided":  # one lane (window set) per bucket size
+        errs = [ar._os.error() for ar in state.engines.values()]
+        windows = list(state.engines)
+    else:
+        errs = [ar.ipc_error() for ar in state.engines.values()]
+        windows = sorted({ar.state()["link"]["ipc"]["windows_id"] for ar in state.engines.values()})
     # tuned once per hook (the first engine), every engine on the chosen lane
     chosen = [state.lane] if a.tune else []
-    windows = sorted({ar.state()["link"]["ipc"]["windows_id"] for ar in state.engines.values()})
     torch.save({"flat": flat, "buckets": len(state.engines), "rounds": state.rounds, "ipc_errors": errs,
                 "chosen": chosen, "transports": state.transports(), "window_sets": len(windows)},
                os.path.join(a.out_dir, f"rank{rank}.pt"))

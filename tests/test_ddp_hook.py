@@ -17,7 +17,7 @@ def _free_port() -> int:
     return p
 
 
-def _train(use_hook, rank, world):
+def _train(use_hook, rank, world, **hook_kw):
     from torch.nn.parallel import DistributedDataParallel as DDP
 
     from akka_allreduce_amd.parallel.ddp import ThresholdHookState, threshold_allreduce_hook
@@ -30,7 +30,7 @@ def _train(use_hook, rank, world):
     ddp = DDP(model, bucket_cap_mb=0.3)
     state = None
     if use_hook:
-        state = ThresholdHookState(max_chunk_size=4096)
+        state = ThresholdHookState(max_chunk_size=4096, **hook_kw)
         ddp.register_comm_hook(state, threshold_allreduce_hook)
     opt = torch.optim.SGD(ddp.parameters(), lr=0.1)
     g = torch.Generator().manual_seed(100 + rank)
@@ -43,14 +43,14 @@ def _train(use_hook, rank, world):
     return [p.detach().clone() for p in model.parameters()], state
 
 
-def _main(rank, world, port, q):
+def _main(rank, world, port, q, hook_kw):
     try:
         os.environ["MASTER_ADDR"] = "127.0.0.1"
         os.environ["MASTER_PORT"] = str(port)
         torch.set_num_threads(1)
         dist.init_process_group("gloo", rank=rank, world_size=world)
         ref, _ = _train(False, rank, world)
-        got, st = _train(True, rank, world)
+        got, st = _train(True, rank, world, **hook_kw)
         ok = all(torch.allclose(a, b, rtol=1e-5, atol=1e-6) for a, b in zip(ref, got))
         q.put((rank, ok, st.rounds, len(st.engines), st.transports()))
         dist.barrier()
@@ -59,17 +59,30 @@ def _main(rank, world, port, q):
         q.put((rank, False, repr(e), 0, 0))
 
 
-def test_ddp_hook_matches_stock_ddp():
+def _run(hook_kw):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_main, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_main, args=(r, 2, port, q, hook_kw)) for r in range(2)]
     for p in procs:
         p.start()
     res = sorted(q.get(timeout=240) for _ in range(2))
     for p in procs:
         p.join(timeout=60)
-    for rank, ok, rounds, engines, transports in res:
+    return res
+
+
+def test_ddp_hook_matches_stock_ddp():
+    for rank, ok, rounds, engines, transports in _run({}):
         assert ok, (rank, rounds)
         assert rounds >= 3 and engines >= 3  # one round per bucket per step, >= 3 bucket sizes
         assert transports == 1  # every bucket size's engine rides on ONE transport (communicator)
+
+
+def test_ddp_hook_onesided_matches_stock_ddp():
+    """The hook on the one-sided lane (thresholds 1: every contributor, so
+    the same mean as DDP's allreduce); on the CPU the windows are shared
+    memory running the GPU kernels' protocol."""
+    for rank, ok, rounds, engines, _ in _run({"transport": "onesided"}):
+        assert ok, (rank, rounds)
+        assert rounds >= 3 and engines >= 3

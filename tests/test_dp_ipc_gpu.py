@@ -108,3 +108,24 @@ def test_torch_ddp_hook_multiprocess(tune, model):
         assert torch.equal(d["flat"], res[0]["flat"])
     want = _reference(n, steps, torch.device("cuda", 0), model)
     torch.testing.assert_close(res[0]["flat"], want, rtol=1e-4, atol=1e-5)
+
+
+def test_torch_ddp_hook_onesided_multiprocess():
+    """The DDP hook on the one-sided threshold lane (thresholds 1 here, so
+    every bucket's mean must equal the mean-gradient reference), 2 processes,
+    3 bucket sizes."""
+    n, steps = 2, 3
+    with tempfile.TemporaryDirectory() as out:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+               os.path.join(ROOT, "tests", "ddp_ranks.py"), "--out-dir", out, "--steps", str(steps),
+               "--model", "deep", "--bucket-mb", "0.3", "--transport", "onesided"]
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT)
+        assert r.returncode == 0, r.stderr[-3000:]
+        res = [torch.load(os.path.join(out, f"rank{i}.pt"), weights_only=True) for i in range(n)]
+    for d in res:
+        assert d["ipc_errors"] and all(e == 0 for e in d["ipc_errors"]), d
+        assert d["buckets"] >= 3 and d["rounds"] >= steps
+        assert torch.equal(d["flat"], res[0]["flat"])
+    want = _reference(n, steps, torch.device("cuda", 0), "deep")
+    torch.testing.assert_close(res[0]["flat"], want, rtol=1e-4, atol=1e-5)
