@@ -57,6 +57,19 @@ __device__ inline bool acquire_all(bool ok_lane0) {
   return ok != 0;
 }
 
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// Streaming (nontemporal) 16-byte store of local memory nobody reads before
+// the kernel ends: it does not evict the lines still to be read.
+__device__ inline void store_nt16(uint4* p, const uint4& v) {
+  u32x4 w;
+  w[0] = v.x;
+  w[1] = v.y;
+  w[2] = v.z;
+  w[3] = v.w;
+  __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(p));
+}
+
 // dst <- src with plain loads and stores (src is this rank's own memory).
 __device__ inline void copy_bytes(char* __restrict__ dst, const char* __restrict__ src, int64_t bytes) {
   if (((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src) | uintptr_t(bytes)) & 15) == 0) {
@@ -98,7 +111,8 @@ __device__ inline uint4 load_sys16(__amdgpu_buffer_rsrc_t r, int64_t off) {
   return make_uint4(v[0], v[1], v[2], v[3]);
 }
 
-// dst (local, plain stores) <- src (window memory written by a peer).
+// dst (local, streamed past the caches: the round's output, read after the
+// round) <- src (window memory written by a peer).
 __device__ inline void copy_in(char* __restrict__ dst, const char* __restrict__ src, int64_t bytes) {
   const auto r = sys_rsrc(src, bytes);
   if (((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src) | uintptr_t(bytes)) & 15) == 0) {
@@ -110,9 +124,9 @@ __device__ inline void copy_in(char* __restrict__ dst, const char* __restrict__ 
 #pragma unroll
       for (int u = 0; u < kUnroll; ++u) v[u] = load_sys16(r, (i + u * int(blockDim.x)) * 16);
 #pragma unroll
-      for (int u = 0; u < kUnroll; ++u) d[i + u * int(blockDim.x)] = v[u];
+      for (int u = 0; u < kUnroll; ++u) store_nt16(d + i + u * int(blockDim.x), v[u]);
     }
-    for (; i < n; i += int(blockDim.x)) d[i] = load_sys16(r, i * 16);
+    for (; i < n; i += int(blockDim.x)) store_nt16(d + i, load_sys16(r, i * 16));
   } else if (((reinterpret_cast<uintptr_t>(dst) | reinterpret_cast<uintptr_t>(src) | uintptr_t(bytes)) & 3) == 0) {
     uint32_t* d = reinterpret_cast<uint32_t*>(dst);
     for (int64_t i = threadIdx.x; i < (bytes >> 2); i += int(blockDim.x))
@@ -131,8 +145,6 @@ __device__ inline void copy_in(char* __restrict__ dst, const char* __restrict__ 
 // the bytes is a system-coherent load.  No buffer_wbl2 / buffer_inv at all --
 // MI355X_MICROARCH.md's "handoff-flag" / "publish-large" forms (write-through
 // stores + drained flag; sc loads in place of the acquire), at system scope.
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-
 __device__ inline void store_sys16(__amdgpu_buffer_rsrc_t r, int64_t off, const uint4& v) {
   u32x4 w;
   w[0] = v.x;
@@ -140,17 +152,6 @@ __device__ inline void store_sys16(__amdgpu_buffer_rsrc_t r, int64_t off, const 
   w[2] = v.z;
   w[3] = v.w;
   __builtin_amdgcn_raw_buffer_store_b128(w, r, int(off), 0, kSysAux);
-}
-
-// Streaming (nontemporal) 16-byte store of local memory nobody reads before
-// the kernel ends: it does not evict the lines still to be read.
-__device__ inline void store_nt16(uint4* p, const uint4& v) {
-  u32x4 w;
-  w[0] = v.x;
-  w[1] = v.y;
-  w[2] = v.z;
-  w[3] = v.w;
-  __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(p));
 }
 
 // dst (a window, read by a peer) <- src (local), 16-byte aligned.

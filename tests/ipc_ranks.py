@@ -33,6 +33,9 @@ def main():
     ap.add_argument("--late-rank", type=int, default=-1, help="this rank sleeps --late-s before round 1")
     ap.add_argument("--late-s", type=float, default=0.0)
     ap.add_argument("--time", action="store_true")
+    ap.add_argument("--time-mode", default="", choices=["", "pull", "bcast", "fused", "fused_bcast"],
+                    help="phase-2 mode of the timed rounds (--rounds 0 times without checking)")
+    ap.add_argument("--chunk", type=int, default=0, help="max chunk size (elements; default size / 16)")
     ap.add_argument("--mode", default="pull", choices=["pull", "bcast", "alternate", "fused", "fused_bcast", "rotate"])
     ap.add_argument("--out-dir", default="", help="write rank<i>.json there (stdout lines of ranks interleave)")
     ap.add_argument("--poison", action="store_true",
@@ -46,7 +49,8 @@ def main():
     dtype = torch.float32 if a.dtype == "float32" else torch.bfloat16
     from akka_allreduce_amd.parallel import ThresholdAllreduce
 
-    ar = ThresholdAllreduce(a.size, max_chunk_size=max(1, a.size // 16), dtype=dtype, device=dev, data_plane="ipc")
+    ar = ThresholdAllreduce(a.size, max_chunk_size=a.chunk or max(1, a.size // 16), dtype=dtype, device=dev,
+                            data_plane="ipc")
     res = {"rank": rank, "exact": [], "lane": ar.state()["link"]["lane"],
            "ipc_open_s": getattr(ar, "ipc_open_s", None)}
     for r in range(a.rounds):
@@ -94,6 +98,9 @@ def main():
     res["ipc_rounds"] = st["ipc_rounds"]
     res["ipc"] = st.get("ipc")
     if a.time and a.skip_rank < 0:
+        if a.time_mode:
+            ar.set_ipc_mode(*{"pull": ("pull", False), "bcast": ("bcast", False), "fused": ("pull", True),
+                              "fused_bcast": ("bcast", True)}[a.time_mode])
         x = torch.randn(a.size, device=dev).to(dtype)
         out = torch.empty_like(x)
         for _ in range(3):
