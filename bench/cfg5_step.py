@@ -1,0 +1,48 @@
+"""BASELINE config 5's step alone, one GPU (no peer: the allreduce is the
+local pass): MLP 4096-8192-1000, batch 256, DP-SGD through
+ThresholdAllreduce, fp32 or bf16 autocast.  For kernel traces:
+
+    rocprofv3 --kernel-trace --stats -d gpurun_out/cfg5 -- python3 bench/cfg5_step.py --dtype bf16
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--dtype", choices=["fp32", "bf16"], default="bf16")
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    a = ap.parse_args()
+    import torch
+
+    from akka_allreduce_amd.models.mlp import MLP, dp_sgd_step, synthetic_batch
+    from akka_allreduce_amd.parallel import ThresholdAllreduce
+    from akka_allreduce_amd.parallel.dp import GradientBucket
+
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    model = MLP(4096, 8192, 1000).to(dev)
+    bucket = GradientBucket(list(model.parameters()), flatten_params=True)
+    ar = ThresholdAllreduce(bucket.numel, max_chunk_size=(4 << 20) // 4, device=dev, rank=0, world_size=1)
+    x, y = synthetic_batch(256, 4096, 1000, device=dev, generator=torch.Generator(device=dev).manual_seed(1))
+    cd = torch.bfloat16 if a.dtype == "bf16" else None
+    for _ in range(a.warmup):
+        dp_sgd_step(model, x, y, 0.05, ar, bucket, sync_loss=False, compute_dtype=cd)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        dp_sgd_step(model, x, y, 0.05, ar, bucket, sync_loss=False, compute_dtype=cd)
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    print(json.dumps({"dtype": a.dtype, "steps": a.steps, "ms_per_step": round(dt / a.steps * 1e3, 4),
+                      "steps_per_s": round(a.steps / dt, 2)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

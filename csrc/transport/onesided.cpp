@@ -106,6 +106,11 @@ OneSidedLane::OneSidedLane(int32_t device, int64_t S, int32_t N, int64_t C, int3
   pgd_.assign(size_t(D_), std::vector<char*>(size_t(N), nullptr));
 
   if (device_ >= 0) {
+    // every row is one IPC allocation: refuse what hipIpcOpenMemHandle would hang on
+    AKKA_CHECK(row_bytes_ <= kIpcMaxWindowBytes,
+               "onesided lane: a window row of " + std::to_string(row_bytes_ >> 20) + " MiB exceeds the " +
+                   std::to_string(kIpcMaxWindowBytes >> 20) +
+                   " MiB an IPC mapping opens (allocations of 2 GiB or more hang in hipIpcOpenMemHandle)");
     AKKA_OS_HIP(hipSetDevice(device_));
     if (hipExtMallocWithFlags(reinterpret_cast<void**>(&flags_), flag_bytes_, hipDeviceMallocUncached) != hipSuccess) {
       (void)hipGetLastError();
