@@ -417,8 +417,13 @@ def run_extras(world: int, dev, barrier, which=("cfg1", "cfg3", "cfg4", "cfg5"),
         out = torch.empty_like(x)
         steps = 10
         dt = timed(lambda: ar(x, async_op=world > 1, out=out), steps, 3, world, barrier)
+        link = ar.state().get("link", {}) if ar.world_size > 1 else {}
+        ipc = link.get("ipc") or {}
         res["cfg3_bf16_1GiB_chunk8MiB"] = {"algbw_GBps": round(nbytes / (dt / steps) / 1e9, 3),
-                                           "ms_per_step": round(dt / steps * 1e3, 4)}
+                                           "ms_per_step": round(dt / steps * 1e3, 4), "lane": link.get("lane"),
+                                           "ipc_mode": {k: ipc.get(k) for k in ("mode", "fused", "lite", "max_wgs",
+                                                                                "portions", "rounds")}
+                                           if ipc else None}
         del x, out
     except _Skip:
         pass
