@@ -297,6 +297,8 @@ __global__ __launch_bounds__(kBlock) void count_expand_kernel(int32_t* __restric
 // averaging: one read of the sum, one read + write of the parameters).
 // dst may alias src (mean(out=data): a gradient bucket averaged in place);
 // each element is read before the same thread writes it, so no __restrict__.
+constexpr int kCmUnroll = 4;
+
 template <typename T, bool AXPY>
 __global__ __launch_bounds__(kBlock) void count_mean_kernel(T* dst, const T* src,
                                                             const int32_t* __restrict__ counts, int64_t S,
@@ -327,23 +329,38 @@ __global__ __launch_bounds__(kBlock) void count_mean_kernel(T* dst, const T* src
     }
     const v4u* s4 = reinterpret_cast<const v4u*>(src + a);
     v4u* d4 = reinterpret_cast<v4u*>(dst + a);
-    for (int64_t i = int64_t(blockIdx.y) * kBlock + threadIdx.x; i < nv; i += int64_t(kBlock) * gridDim.y) {
+    auto mean_vec = [&](const v4u& sv, const v4u& dv) {
       float acc[E];
 #pragma unroll
       for (int q = 0; q < E; ++q) acc[q] = 0.f;
-      add_vec(acc, s4[i], T{});
+      add_vec(acc, sv, T{});
 #pragma unroll
       for (int q = 0; q < E; ++q) acc[q] = v > 0 ? acc[q] / fv : 0.f;
       if constexpr (AXPY) {
         float p[E];
 #pragma unroll
         for (int q = 0; q < E; ++q) p[q] = 0.f;
-        add_vec(p, d4[i], T{});
+        add_vec(p, dv, T{});
 #pragma unroll
         for (int q = 0; q < E; ++q) acc[q] = p[q] + alpha * acc[q];
       }
-      d4[i] = pack_vec(acc);
+      return pack_vec(acc);
+    };
+    // kCmUnroll vectors per thread: every load of the group in flight before
+    // the first store (one vector at a time left the pass latency-bound)
+    constexpr int U = kCmUnroll;
+    const int64_t stride = int64_t(kBlock) * gridDim.y;
+    int64_t i = int64_t(blockIdx.y) * kBlock + threadIdx.x;
+    for (; i + (U - 1) * stride < nv; i += U * stride) {
+      v4u sv[U], dv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) sv[u] = s4[i + u * stride];
+#pragma unroll
+      for (int u = 0; u < U; ++u) dv[u] = AXPY ? d4[i + u * stride] : sv[u];
+#pragma unroll
+      for (int u = 0; u < U; ++u) d4[i + u * stride] = mean_vec(sv[u], dv[u]);
     }
+    for (; i < nv; i += stride) d4[i] = mean_vec(s4[i], AXPY ? d4[i] : s4[i]);
   }
 }
 

@@ -24,18 +24,22 @@ def _port() -> int:
 
 def main() -> None:
     ap = argparse.ArgumentParser()
-    ap.add_argument("--cases", required=True, help="N:size:dtype:mode:lite:threads[:chunk], comma separated")
+    ap.add_argument("--cases", required=True,
+                    help="N:size:dtype:mode:lite:threads[:chunk[:async[:pre_size]]], comma separated")
     ap.add_argument("--timeout", type=int, default=240)
     a = ap.parse_args()
     for case in a.cases.split(","):
         f = case.split(":")
         n, size, dtype, mode, lite, threads = int(f[0]), int(f[1]), f[2], f[3], f[4], f[5]
         chunk = int(f[6]) if len(f) > 6 else 0
+        async_op = len(f) > 7 and f[7] == "1"
+        pre = int(f[8]) if len(f) > 8 else 0
         with tempfile.TemporaryDirectory() as out:
             cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
                    "--master-addr", "127.0.0.1", "--master-port", str(_port()),
                    os.path.join(ROOT, "tests", "ipc_ranks.py"), "--out-dir", out, "--size", str(size),
-                   "--dtype", dtype, "--rounds", "0", "--time", "--time-mode", mode, "--chunk", str(chunk)]
+                   "--dtype", dtype, "--rounds", "0", "--time", "--time-mode", mode, "--chunk", str(chunk),
+                   "--pre-size", str(pre)] + (["--time-async"] if async_op else [])
             env = dict(os.environ, AKKA_IPC_LITE=lite, AKKA_IPC_THREADS=threads)
             r = subprocess.run(cmd, capture_output=True, text=True, timeout=a.timeout, cwd=ROOT, env=env)
             rows = []
@@ -45,7 +49,7 @@ def main() -> None:
                     with open(p) as fh:
                         rows.append(json.load(fh))
         line = {"N": n, "size": size, "dtype": dtype, "mode": mode, "lite": lite == "1", "threads": int(threads),
-                "chunk": chunk, "rc": r.returncode}
+                "chunk": chunk, "async": async_op, "pre_size": pre, "rc": r.returncode}
         if r.returncode == 0 and len(rows) == n:
             ms = max(d["ms_per_round"] for d in rows)
             es = 4 if dtype == "float32" else 2

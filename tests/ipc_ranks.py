@@ -36,6 +36,8 @@ def main():
     ap.add_argument("--time-mode", default="", choices=["", "pull", "bcast", "fused", "fused_bcast"],
                     help="phase-2 mode of the timed rounds (--rounds 0 times without checking)")
     ap.add_argument("--chunk", type=int, default=0, help="max chunk size (elements; default size / 16)")
+    ap.add_argument("--time-async", action="store_true", help="timed rounds with async_op=True")
+    ap.add_argument("--pre-size", type=int, default=0, help="run 5 rounds of another fp32 engine of this size first")
     ap.add_argument("--mode", default="pull", choices=["pull", "bcast", "alternate", "fused", "fused_bcast", "rotate"])
     ap.add_argument("--out-dir", default="", help="write rank<i>.json there (stdout lines of ranks interleave)")
     ap.add_argument("--poison", action="store_true",
@@ -49,6 +51,13 @@ def main():
     dtype = torch.float32 if a.dtype == "float32" else torch.bfloat16
     from akka_allreduce_amd.parallel import ThresholdAllreduce
 
+    pre = None
+    if a.pre_size:  # another engine in the process first (bench.py's headline before its extras)
+        pre = ThresholdAllreduce(a.pre_size, max_chunk_size=max(1, a.pre_size // 64), device=dev, data_plane="ipc")
+        px = torch.randn(a.pre_size, device=dev)
+        for _ in range(5):
+            pre(px, async_op=True).wait()
+        torch.cuda.synchronize()
     ar = ThresholdAllreduce(a.size, max_chunk_size=a.chunk or max(1, a.size // 16), dtype=dtype, device=dev,
                             data_plane="ipc")
     res = {"rank": rank, "exact": [], "lane": ar.state()["link"]["lane"],
@@ -103,8 +112,10 @@ def main():
                               "fused_bcast": ("bcast", True)}[a.time_mode])
         x = torch.randn(a.size, device=dev).to(dtype)
         out = torch.empty_like(x)
+        o = None
         for _ in range(3):
-            ar(x, out=out)
+            o = ar(x, out=out, async_op=a.time_async)
+        o.wait()
         torch.cuda.synchronize()
         dist.barrier()
         import time
@@ -112,7 +123,8 @@ def main():
         t0 = time.perf_counter()
         k = 10
         for _ in range(k):
-            ar(x, out=out)
+            o = ar(x, out=out, async_op=a.time_async)
+        o.wait()
         torch.cuda.synchronize()
         dist.barrier()
         res["ms_per_round"] = (time.perf_counter() - t0) / k * 1e3
