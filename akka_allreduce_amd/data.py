@@ -130,23 +130,31 @@ class AllReduceOutput:
                 and dst.device == d.device and dst.numel() == d.numel() and d.data_ptr() % 16 == 0
                 and dst.data_ptr() % 16 == 0)
 
-    def _count_mean(self, dst: torch.Tensor, axpy: bool, alpha: float) -> None:
+    def _count_mean(self, dst: torch.Tensor, axpy: bool, alpha: float, shadow: Optional[torch.Tensor] = None) -> None:
         from ._native_loader import load
 
         d, g = self.data, self.geometry
         pc = self.counts_per_chunk.contiguous()
         load().count_mean(dst.data_ptr(), d.data_ptr(), pc.data_ptr(), g.dataSize, g.step, g.workerNum,
                           g.maxChunkSize, g.kmax, "bfloat16" if d.dtype == torch.bfloat16 else "float32",
-                          torch.cuda.current_stream(d.device).cuda_stream, axpy, float(alpha))
+                          torch.cuda.current_stream(d.device).cuda_stream, axpy, float(alpha),
+                          shadow.data_ptr() if shadow is not None else 0)
 
-    def axpy_mean_(self, y: torch.Tensor, alpha: float) -> torch.Tensor:
+    def axpy_mean_(self, y: torch.Tensor, alpha: float, shadow: Optional[torch.Tensor] = None) -> torch.Tensor:
         """``y += alpha * mean()`` in one fused pass on the GPU (the SGD update
-        of a flat parameter buffer: alpha = -lr); ``y`` is updated in place."""
+        of a flat parameter buffer: alpha = -lr); ``y`` is updated in place.
+        ``shadow`` (bf16, same length as fp32 ``y``) also receives the updated
+        values, stored by the same pass (a separate cast off the fused path)."""
         self.wait()
-        if self._fused_ok(y):
-            self._count_mean(y, True, alpha)
+        if self._fused_ok(y) and (shadow is None or (
+                y.dtype == torch.float32 and shadow.dtype == torch.bfloat16 and shadow.is_contiguous()
+                and shadow.numel() == y.numel() and shadow.device == y.device and shadow.data_ptr() % 16 == 0)):
+            self._count_mean(y, True, alpha, shadow)
             return y
-        return y.add_(self.mean().view_as(y).to(y.dtype), alpha=alpha)
+        y.add_(self.mean().view_as(y).to(y.dtype), alpha=alpha)
+        if shadow is not None:
+            shadow.copy_(y.view_as(shadow))
+        return y
 
     def mean(self, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         """Element-wise average over the contributors that made it (0 where none).

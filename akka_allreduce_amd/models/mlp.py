@@ -14,6 +14,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..ops.colsum import colsum
 from ..parallel.dp import AllreduceFn, GradientBucket
 
 
@@ -34,13 +35,17 @@ class _LinearIntoBucket(torch.autograd.Function):
     gradient bucket's views (``p.grad``) instead of returning them to
     autograd: no bucket zeroing and no AccumulateGrad read-modify-write pass
     over the 167 MB of gradients per step.  Under autocast the GEMMs run in
-    the autocast dtype (bf16 MFMA) and the weight/bias stay fp32."""
+    the autocast dtype (bf16 MFMA) and the weight/bias stay fp32; ``ws`` /
+    ``bs`` are the bucket's bf16 shadows of w / b (written by the previous
+    step's fused update), used instead of casting w / b again."""
 
     @staticmethod
-    def forward(ctx, x, w, b, gw, gb):
+    def forward(ctx, x, w, b, gw, gb, ws=None, bs=None):
         dt = torch.get_autocast_dtype(x.device.type) if torch.is_autocast_enabled(x.device.type) else None
         with torch.autocast(device_type=x.device.type, enabled=False):
-            if dt is not None:
+            if dt is not None and ws is not None and bs is not None and ws.dtype == dt and bs.dtype == dt:
+                xc, wc, bc = x.to(dt), ws, bs
+            elif dt is not None:
                 xc, wc, bc = x.to(dt), w.to(dt), b.to(dt)
             else:
                 xc, wc, bc = x, w, b
@@ -54,9 +59,12 @@ class _LinearIntoBucket(torch.autograd.Function):
         xc, wc = ctx.saved_tensors
         go2 = go.reshape(-1, go.shape[-1]).to(wc.dtype)
         _mm_into(go2.t(), xc.reshape(-1, xc.shape[-1]), ctx.gw)
-        torch.sum(go2, 0, dtype=ctx.gb.dtype, out=ctx.gb)
+        if go2.is_cuda and go2.dtype == torch.bfloat16 and ctx.gb.dtype == torch.float32 and ctx.gb.is_contiguous():
+            colsum(go2, out=ctx.gb.view(-1))  # gfx950 column sum (ops/colsum.py)
+        else:
+            torch.sum(go2, 0, dtype=ctx.gb.dtype, out=ctx.gb)
         gx = (go2 @ wc).reshape(*go.shape[:-1], wc.shape[1]) if ctx.needs_input_grad[0] else None
-        return gx, None, None, None, None
+        return gx, None, None, None, None, None, None
 
 
 class MLP(nn.Module):
@@ -68,10 +76,14 @@ class MLP(nn.Module):
         # a bucket view); reset before it returns
         self.direct_grads = False
         self.last_step_direct = False
+        self.shadow_bucket: Optional[GradientBucket] = None  # set with direct_grads when bf16 shadows are current
 
     def _linear(self, fc: nn.Linear, x: torch.Tensor) -> torch.Tensor:
         if self.direct_grads and torch.is_grad_enabled():
-            return _LinearIntoBucket.apply(x, fc.weight, fc.bias, fc.weight.grad, fc.bias.grad)
+            sb = self.shadow_bucket
+            ws = sb.shadow_of(fc.weight) if sb is not None else None
+            bs = sb.shadow_of(fc.bias) if sb is not None else None
+            return _LinearIntoBucket.apply(x, fc.weight, fc.bias, fc.weight.grad, fc.bias.grad, ws, bs)
         return fc(x)
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
@@ -81,13 +93,16 @@ class MLP(nn.Module):
 def dp_sgd_step(model: nn.Module, x: torch.Tensor, y: torch.Tensor, lr: float,
                 allreduce: Optional[AllreduceFn], bucket: Optional[GradientBucket] = None,
                 sync_loss: bool = True, compute_dtype: Optional[torch.dtype] = None,
-                direct_grads: bool = True):
+                direct_grads: bool = True, shadow_weights: bool = True):
     """forward + backward + gradient allreduce (mean over contributors) + SGD
     update.  With a bucket built with ``flatten_params=True`` the averaging and
     the update are one fused pass.  ``sync_loss=False`` returns the loss as a
     device tensor (no host sync per step).  ``compute_dtype=torch.bfloat16``
     runs the forward/backward GEMMs on bf16 MFMA (autocast) while weights,
-    gradients, the allreduce and the update stay fp32."""
+    gradients, the allreduce and the update stay fp32; with
+    ``shadow_weights`` the fused update also stores the bf16 weight copy the
+    next step's GEMMs read (``GradientBucket.use_shadow``), so no step casts
+    the fp32 weights again."""
     if bucket is None:
         bucket = getattr(model, "_akka_bucket", None)
         if bucket is None:
@@ -106,7 +121,12 @@ def dp_sgd_step(model: nn.Module, x: torch.Tensor, y: torch.Tensor, lr: float,
             # (micro-batch accumulation, a later plain loss.backward()) must
             # accumulate as usual.
             model.direct_grads = True
+            # bf16 GEMMs read the bf16 weight copy the last fused update wrote
+            lowp = compute_dtype if (shadow_weights and compute_dtype is not None
+                                     and compute_dtype != torch.float32) else None
+            model.shadow_bucket = bucket if bucket.use_shadow(lowp) else None
         else:
+            bucket.use_shadow(None)
             bucket.zero_()
         if compute_dtype is not None and compute_dtype != torch.float32:
             with torch.autocast(device_type=x.device.type, dtype=compute_dtype):
@@ -117,6 +137,7 @@ def dp_sgd_step(model: nn.Module, x: torch.Tensor, y: torch.Tensor, lr: float,
     finally:
         if isinstance(model, MLP):
             model.direct_grads = False
+            model.shadow_bucket = None
             model.last_step_direct = direct
     bucket.sgd_from(allreduce, lr)
     return float(loss.detach()) if sync_loss else loss.detach()

@@ -35,6 +35,10 @@ class GradientBucket:
         self.numel = sum(p.numel() for p in self.params)
         self.flat = torch.zeros(self.numel, dtype=dt, device=dev)
         self.pflat: Optional[torch.Tensor] = None
+        # low-precision copy of pflat kept current by the fused update (use_shadow)
+        self.sflat: Optional[torch.Tensor] = None
+        self._shadow_on = False
+        self._shadow_versions: Optional[List[int]] = None
         if flatten_params and all(p.dtype == dt for p in self.params):
             self.pflat = torch.empty(self.numel, dtype=dt, device=dev)
         off = 0
@@ -49,6 +53,66 @@ class GradientBucket:
 
     def zero_(self) -> None:
         self.flat.zero_()
+
+    # ---- bf16 shadow weights -------------------------------------------------
+    # A bf16 forward under autocast casts every fp32 weight to bf16 each step
+    # (4 B read + 2 B written per parameter).  With flattened fp32 parameters
+    # the fused average + SGD pass (``count_mean`` kernel) can store the bf16
+    # copy of each updated parameter as it writes it, so the next forward reads
+    # that copy instead: the cast disappears from the step.
+    #
+    # The shadow is trusted only while nothing else touched the parameters: a
+    # torch in-place op on a parameter bumps its version counter, and any
+    # mismatch with the versions recorded at the last refresh re-copies the
+    # shadow (our kernel writes through raw pointers and bumps none).  Writes
+    # through ``p.data`` bypass the counter (torch's documented caveat): call
+    # ``invalidate_shadow()`` after such writes.
+
+    def use_shadow(self, dtype: Optional[torch.dtype]) -> bool:
+        """Keep a ``dtype`` copy of the parameters current from now on (None:
+        stop updating it).  Returns whether the shadow is in use."""
+        ok = (dtype is not None and dtype != self.flat.dtype and self.pflat is not None
+              and self.pflat.is_cuda and self.pflat.dtype == torch.float32 and dtype == torch.bfloat16
+              and self.params_bound())
+        if not ok:
+            self._shadow_on = False
+            return False
+        if self.sflat is None or self.sflat.dtype != dtype:
+            self.sflat = torch.empty(self.numel, dtype=dtype, device=self.pflat.device)
+            self._shadow_versions = None
+        if not self._shadow_on or self._shadow_versions != [p._version for p in self.params]:
+            self.sflat.copy_(self.pflat)
+            self._shadow_versions = [p._version for p in self.params]
+        self._shadow_on = True
+        return True
+
+    def invalidate_shadow(self) -> None:
+        self._shadow_versions = None
+
+    def shadow_of(self, p: torch.nn.Parameter) -> Optional[torch.Tensor]:
+        """The current low-precision copy of parameter ``p`` (None if the
+        shadow is not in use)."""
+        if not self._shadow_on or self.sflat is None:
+            return None
+        off = 0
+        for q in self.params:
+            if q is p:
+                return self.sflat[off:off + p.numel()].view_as(p)
+            off += q.numel()
+        return None
+
+    def params_bound(self) -> bool:
+        """Is every parameter still its view of ``pflat``?"""
+        if self.pflat is None:
+            return False
+        off = 0
+        es = self.pflat.element_size()
+        base = self.pflat.data_ptr()
+        for p in self.params:
+            if p.data_ptr() != base + off * es:
+                return False
+            off += p.numel()
+        return True
 
     def bound(self) -> bool:
         """Is every parameter's ``.grad`` still its view of ``flat``?"""
@@ -101,10 +165,15 @@ class GradientBucket:
             return None
         out = allreduce(self.flat)
         if self.pflat is not None and out.data.dtype == self.pflat.dtype:
-            out.axpy_mean_(self.pflat, -lr)
+            out.axpy_mean_(self.pflat, -lr, shadow=self.sflat if self._shadow_on else None)
         else:
             self.average_out(out)
             sgd_step(self.params, lr)
+            if self._shadow_on and self.sflat is not None:
+                self.sflat.copy_(self.pflat)
+        if self._shadow_on:
+            # versions after our own update (sgd_step's in-place adds bump them)
+            self._shadow_versions = [p._version for p in self.params]
         return out
 
     def average_out(self, out: AllReduceOutput) -> None:

@@ -18,6 +18,7 @@ def main() -> None:
     ap.add_argument("--dtype", choices=["fp32", "bf16"], default="bf16")
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--no-shadow", action="store_true", help="bf16: cast the fp32 weights every step")
     a = ap.parse_args()
     import torch
 
@@ -33,14 +34,14 @@ def main() -> None:
     x, y = synthetic_batch(256, 4096, 1000, device=dev, generator=torch.Generator(device=dev).manual_seed(1))
     cd = torch.bfloat16 if a.dtype == "bf16" else None
     for _ in range(a.warmup):
-        dp_sgd_step(model, x, y, 0.05, ar, bucket, sync_loss=False, compute_dtype=cd)
+        dp_sgd_step(model, x, y, 0.05, ar, bucket, sync_loss=False, compute_dtype=cd, shadow_weights=not a.no_shadow)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        dp_sgd_step(model, x, y, 0.05, ar, bucket, sync_loss=False, compute_dtype=cd)
+        dp_sgd_step(model, x, y, 0.05, ar, bucket, sync_loss=False, compute_dtype=cd, shadow_weights=not a.no_shadow)
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    print(json.dumps({"dtype": a.dtype, "steps": a.steps, "ms_per_step": round(dt / a.steps * 1e3, 4),
+    print(json.dumps({"dtype": a.dtype, "shadow": not a.no_shadow and cd is not None, "steps": a.steps, "ms_per_step": round(dt / a.steps * 1e3, 4),
                       "steps_per_s": round(a.steps / dt, 2)}), flush=True)
 
 

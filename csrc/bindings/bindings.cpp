@@ -116,7 +116,12 @@ class WorkerCore final : public EngineHost {
     if (!first) return false;
     if (!dev_) {  // (adopt_transport may have handed us a shared device)
       if (device_idx_ < 0) dev_ = make_host_device(deferred_);
-      else dev_ = make_hip_device(device_idx_, true);
+      else {
+        // AKKA_COMM_PRIORITY=normal: the comm stream at normal priority
+        // (measurement knob: which hardware queue pool the round lands in)
+        const char* pr = std::getenv("AKKA_COMM_PRIORITY");
+        dev_ = make_hip_device(device_idx_, !(pr && std::strcmp(pr, "normal") == 0));
+      }
     }
     dp_ = std::make_unique<DataPlane>(dev_.get(), engine_->geometry(), id, max_lag + 1, dt_);
     if (link_kind_ == "outbox") {
@@ -868,12 +873,21 @@ PYBIND11_MODULE(_native, m) {
                         S, step, N, C, kmax);
   });
   m.def("count_mean", [](uintptr_t dst, uintptr_t src, uintptr_t counts, int64_t S, int64_t step, int32_t N,
-                         int64_t C, int32_t kmax, std::string dtype, uintptr_t stream, bool axpy, float alpha) {
+                         int64_t C, int32_t kmax, std::string dtype, uintptr_t stream, bool axpy, float alpha,
+                         uintptr_t shadow) {
     launch_count_mean(as_stream(stream), reinterpret_cast<void*>(dst), reinterpret_cast<const void*>(src),
                       reinterpret_cast<const int32_t*>(counts), S, step, N, C, kmax,
-                      dtype == "bfloat16" ? DType::BF16 : DType::F32, axpy, alpha);
+                      dtype == "bfloat16" ? DType::BF16 : DType::F32, axpy, alpha, reinterpret_cast<void*>(shadow));
   }, py::arg("dst"), py::arg("src"), py::arg("counts"), py::arg("S"), py::arg("step"), py::arg("N"), py::arg("C"),
-     py::arg("kmax"), py::arg("dtype"), py::arg("stream"), py::arg("axpy") = false, py::arg("alpha") = 0.f);
+     py::arg("kmax"), py::arg("dtype"), py::arg("stream"), py::arg("axpy") = false, py::arg("alpha") = 0.f,
+     py::arg("shadow") = 0);
+  m.def("colsum_bf16", [](uintptr_t out, uintptr_t in, int64_t M, int64_t ncol, uintptr_t part, uintptr_t tickets,
+                          int32_t splits, uintptr_t stream, bool lite) {
+    launch_colsum_bf16(as_stream(stream), reinterpret_cast<float*>(out), reinterpret_cast<const void*>(in), M, ncol,
+                       reinterpret_cast<float*>(part), reinterpret_cast<uint32_t*>(tickets), splits, lite);
+  }, py::arg("out"), py::arg("in"), py::arg("M"), py::arg("ncol"), py::arg("part"), py::arg("tickets"),
+     py::arg("splits"), py::arg("stream"), py::arg("lite") = true);
+  m.def("colsum_row_splits", &colsum_row_splits);
   m.def("geometry", [](int64_t S, int32_t N, int64_t C) {
     Geometry g(S, N, C);
     py::dict d;

@@ -26,7 +26,14 @@ void launch_count_expand(hipStream_t s, int32_t* out, const int32_t* counts, int
 // dst = src / per-chunk count (0 where the count is 0), one pass; with
 // `axpy`: dst += alpha * that mean (fused SGD update).
 void launch_count_mean(hipStream_t s, void* dst, const void* src, const int32_t* counts, int64_t S, int64_t step,
-                       int32_t N, int64_t C, int32_t kmax, DType dt, bool axpy = false, float alpha = 0.f);
+                       int32_t N, int64_t C, int32_t kmax, DType dt, bool axpy = false, float alpha = 0.f,
+                       void* shadow = nullptr);
+// out[c] = sum_r in[r, c] (bf16 [M, ncol] row-major, fp32 out): the bias
+// gradient.  part: fp32 [splits, ncol] workspace; tickets: uint32
+// [ceil(ncol / 512)] zeroed once (each launch leaves them zero again).
+void launch_colsum_bf16(hipStream_t s, float* out, const void* in, int64_t M, int64_t ncol, float* part,
+                        uint32_t* tickets, int32_t splits, bool lite = true);
+int32_t colsum_row_splits(int64_t M, int64_t ncol);
 // counts[0..n) = 0 if *flag != 0 (read when the kernel runs): poisons the
 // counts of a one-sided round whose waits failed.
 void launch_poison_counts(hipStream_t s, const uint32_t* flag, int32_t* counts, int64_t n);

@@ -23,6 +23,7 @@
 #include <cstring>
 
 #include "kernels.h"
+#include "xgmi_device.h"
 
 namespace akka {
 
@@ -295,15 +296,19 @@ __global__ __launch_bounds__(kBlock) void count_expand_kernel(int32_t* __restric
 // Same region walk as count_expand (one wave-uniform count per region).
 // AXPY: dst[i] += alpha * mean[i] instead (the SGD update fused into the
 // averaging: one read of the sum, one read + write of the parameters).
+// SHADOW (fp32 AXPY only): the updated parameters are also stored as bf16 into
+// `shadow` (same element index), so a bf16 forward reads a weight copy the
+// update already wrote instead of casting 4 B/element again every step.
 // dst may alias src (mean(out=data): a gradient bucket averaged in place);
 // each element is read before the same thread writes it, so no __restrict__.
 constexpr int kCmUnroll = 4;
 
-template <typename T, bool AXPY>
+template <typename T, bool AXPY, bool SHADOW>
 __global__ __launch_bounds__(kBlock) void count_mean_kernel(T* dst, const T* src,
                                                             const int32_t* __restrict__ counts, int64_t S,
                                                             int64_t step, int32_t N, int64_t C, int32_t kmax,
-                                                            float alpha) {
+                                                            float alpha, unsigned short* __restrict__ shadow) {
+  static_assert(!SHADOW || (AXPY && std::is_same_v<T, float>), "shadow: fp32 SGD update only");
   constexpr int E = VecTraits<T>::kElems;
   const int64_t nregions = int64_t(N) * kmax;
   for (int64_t reg = blockIdx.x; reg < nregions; reg += gridDim.x) {
@@ -321,7 +326,9 @@ __global__ __launch_bounds__(kBlock) void count_mean_kernel(T* dst, const T* src
     const int64_t nv = (e - a) / E;
     auto one = [&](int64_t i) {
       const float m = v > 0 ? to_f(src[i]) / fv : 0.f;
-      dst[i] = from_f<T>(AXPY ? to_f(dst[i]) + alpha * m : m);
+      const float r = AXPY ? to_f(dst[i]) + alpha * m : m;
+      dst[i] = from_f<T>(r);
+      if constexpr (SHADOW) shadow[i] = from_f<unsigned short>(r);
     };
     if (blockIdx.y == 0) {
       for (int64_t i = s + threadIdx.x; i < a; i += kBlock) one(i);
@@ -329,7 +336,8 @@ __global__ __launch_bounds__(kBlock) void count_mean_kernel(T* dst, const T* src
     }
     const v4u* s4 = reinterpret_cast<const v4u*>(src + a);
     v4u* d4 = reinterpret_cast<v4u*>(dst + a);
-    auto mean_vec = [&](const v4u& sv, const v4u& dv) {
+    uint2* h2 = SHADOW ? reinterpret_cast<uint2*>(shadow + a) : nullptr;  // 4 bf16 per fp32 vector
+    auto mean_vec = [&](const v4u& sv, const v4u& dv, int64_t at) {
       float acc[E];
 #pragma unroll
       for (int q = 0; q < E; ++q) acc[q] = 0.f;
@@ -343,6 +351,9 @@ __global__ __launch_bounds__(kBlock) void count_mean_kernel(T* dst, const T* src
         add_vec(p, dv, T{});
 #pragma unroll
         for (int q = 0; q < E; ++q) acc[q] = p[q] + alpha * acc[q];
+      }
+      if constexpr (SHADOW) {
+        if constexpr (E == 4) h2[at] = make_uint2(pack_bf16x2(acc[0], acc[1]), pack_bf16x2(acc[2], acc[3]));
       }
       return pack_vec(acc);
     };
@@ -358,10 +369,114 @@ __global__ __launch_bounds__(kBlock) void count_mean_kernel(T* dst, const T* src
 #pragma unroll
       for (int u = 0; u < U; ++u) dv[u] = AXPY ? d4[i + u * stride] : sv[u];
 #pragma unroll
-      for (int u = 0; u < U; ++u) d4[i + u * stride] = mean_vec(sv[u], dv[u]);
+      for (int u = 0; u < U; ++u) d4[i + u * stride] = mean_vec(sv[u], dv[u], i + u * stride);
     }
-    for (; i < nv; i += stride) d4[i] = mean_vec(s4[i], AXPY ? d4[i] : s4[i]);
+    for (; i < nv; i += stride) d4[i] = mean_vec(s4[i], AXPY ? d4[i] : s4[i], i);
   }
+}
+
+// ---- column sum (the bias gradient of a linear layer) -------------------------
+// out[c] = sum_r in[r, c] for a row-major bf16 [M, Ncol] matrix, fp32
+// accumulation and output: db = sum over the batch of dY.  Each lane owns 8
+// adjacent columns (one 16-B load per row), a wave 512 columns, and the rows
+// of a column tile are split over `gridDim.y` workgroups (x 4 waves) so a
+// batch of a few hundred rows still spreads over the whole chip.  Each
+// workgroup leaves its fp32 partial row in `part[blockIdx.y]`; the last to
+// arrive at the tile's ticket sums the partials in row-split order
+// (deterministic: no float atomics) and re-arms the ticket for the next call.
+// Hand-off of the partial rows: LITE = write-through (sc0 sc1) stores, a
+// drained vmcnt and system-coherent loads in the last workgroup (no cache
+// write-back or invalidate); otherwise device-scope release / acquire fences.
+constexpr int kCsCols = 64 * 8;  // columns per workgroup (one wave's width)
+constexpr int kCsRows = 8;       // rows per lane in flight
+constexpr int kCsMaxSplits = 16;
+
+template <bool LITE>
+__global__ __launch_bounds__(kBlock) void colsum_bf16_kernel(float* __restrict__ out,
+                                                             const unsigned short* __restrict__ in, int64_t M,
+                                                             int64_t ncol, float* __restrict__ part,
+                                                             uint32_t* __restrict__ tickets, int32_t vec) {
+  __shared__ float red[kBlock / 64][kCsCols];
+  __shared__ uint32_t last;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t c0 = int64_t(blockIdx.x) * kCsCols + lane * 8;
+  const int64_t rows_per = (M + gridDim.y - 1) / gridDim.y;
+  const int64_t r0 = int64_t(blockIdx.y) * rows_per;
+  const int64_t r1 = r0 + rows_per < M ? r0 + rows_per : M;
+  float acc[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) acc[q] = 0.f;
+  if (vec && c0 + 8 <= ncol) {
+    // kCsRows rows in flight per lane before the adds
+    int64_t r = r0 + wave;
+    for (; r + 4 * (kCsRows - 1) < r1; r += 4 * kCsRows) {
+      v4u v[kCsRows];
+#pragma unroll
+      for (int u = 0; u < kCsRows; ++u) v[u] = *reinterpret_cast<const v4u*>(in + (r + 4 * u) * ncol + c0);
+#pragma unroll
+      for (int u = 0; u < kCsRows; ++u) add_vec(acc, v[u], (unsigned short)0);
+    }
+    for (; r < r1; r += 4) add_vec(acc, *reinterpret_cast<const v4u*>(in + r * ncol + c0), (unsigned short)0);
+  } else {
+    for (int64_t r = r0 + wave; r < r1; r += 4)
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        if (c0 + q < ncol) acc[q] += to_f(in[r * ncol + c0 + q]);
+  }
+  // the workgroup's 4 waves -> one partial row (acc[q] is column c0 + q)
+#pragma unroll
+  for (int q = 0; q < 8; ++q) red[wave][lane * 8 + q] = acc[q];
+  __syncthreads();
+  float* prow = part + int64_t(blockIdx.y) * ncol;
+  const auto prs = xgmi::sys_rsrc(part, int64_t(gridDim.y) * ncol * 4);
+  for (int i = threadIdx.x; i < kCsCols; i += kBlock) {
+    const int64_t c = int64_t(blockIdx.x) * kCsCols + i;
+    if (c >= ncol) continue;
+    const float v = red[0][i] + red[1][i] + red[2][i] + red[3][i];
+    if constexpr (LITE)
+      __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), prs, int((int64_t(blockIdx.y) * ncol + c) * 4), 0,
+                                            xgmi::kSysAux);
+    else
+      prow[c] = v;
+  }
+  if constexpr (LITE) {
+    xgmi::drain_wg();  // every wave's write-through stores performed
+  } else {
+    __threadfence();  // release: this workgroup's partial row before its ticket
+    __syncthreads();
+  }
+  if (threadIdx.x == 0)
+    last = __hip_atomic_fetch_add(&tickets[blockIdx.x], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                   gridDim.y - 1
+               ? 1u
+               : 0u;
+  __syncthreads();
+  if (!last) return;
+  if constexpr (!LITE) __threadfence();  // acquire: every partial row of this tile
+  // every partial of a column loaded before the first add (one memory
+  // latency for the combine, not one per split), summed in split order
+  for (int i = threadIdx.x; i < kCsCols; i += kBlock) {
+    const int64_t c = int64_t(blockIdx.x) * kCsCols + i;
+    if (c >= ncol) continue;
+    float v[kCsMaxSplits];
+#pragma unroll
+    for (int y = 0; y < kCsMaxSplits; ++y) {
+      v[y] = 0.f;
+      if (y < int(gridDim.y)) {
+        if constexpr (LITE)
+          v[y] = __uint_as_float(
+              __builtin_amdgcn_raw_buffer_load_b32(prs, int((int64_t(y) * ncol + c) * 4), 0, xgmi::kSysAux));
+        else
+          v[y] = part[int64_t(y) * ncol + c];
+      }
+    }
+    float sum = 0.f;
+#pragma unroll
+    for (int y = 0; y < kCsMaxSplits; ++y) sum += v[y];
+    out[c] = sum;
+  }
+  if (threadIdx.x == 0)  // re-armed for the next launch on this workspace
+    __hip_atomic_store(&tickets[blockIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 template <typename T, int NSRC, int POL, int UNROLL>
@@ -600,11 +715,41 @@ void launch_count_expand(hipStream_t s, int32_t* out, const int32_t* counts, int
   check_launch("count_expand");
 }
 
+int32_t colsum_row_splits(int64_t M, int64_t ncol) {
+  const int64_t tiles = (ncol + kCsCols - 1) / kCsCols;
+  // one workgroup per CU over the chip at most, >= 32 rows per workgroup
+  int64_t r = (kCUs + tiles - 1) / tiles;
+  const int64_t cap = M / 32;
+  if (r > cap) r = cap;
+  if (r > kCsMaxSplits) r = kCsMaxSplits;
+  return int32_t(r < 1 ? 1 : r);
+}
+
+void launch_colsum_bf16(hipStream_t s, float* out, const void* in, int64_t M, int64_t ncol, float* part,
+                        uint32_t* tickets, int32_t splits, bool lite) {
+  if (ncol <= 0) return;
+  AKKA_CHECK(M > 0 && splits >= 1 && splits <= kCsMaxSplits, "colsum: bad shape or row splits (1..16)");
+  const int64_t tiles = (ncol + kCsCols - 1) / kCsCols;
+  AKKA_CHECK(tiles < (int64_t(1) << 31), "colsum: too many columns");
+  // the partial rows are addressed through one buffer resource (32-bit offsets)
+  AKKA_CHECK(int64_t(splits) * ncol * 4 < (int64_t(1) << 31), "colsum: partial rows exceed 2 GiB");
+  const int vec = ((reinterpret_cast<uintptr_t>(in) & 15) == 0 && ncol % 8 == 0) ? 1 : 0;
+  if (lite)
+    hipLaunchKernelGGL(colsum_bf16_kernel<true>, dim3(uint32_t(tiles), uint32_t(splits)), dim3(kBlock), 0, s, out,
+                       static_cast<const unsigned short*>(in), M, ncol, part, tickets, vec);
+  else
+    hipLaunchKernelGGL(colsum_bf16_kernel<false>, dim3(uint32_t(tiles), uint32_t(splits)), dim3(kBlock), 0, s, out,
+                       static_cast<const unsigned short*>(in), M, ncol, part, tickets, vec);
+  check_launch("colsum_bf16");
+}
+
 void launch_count_mean(hipStream_t s, void* dst, const void* src, const int32_t* counts, int64_t S, int64_t step,
-                       int32_t N, int64_t C, int32_t kmax, DType dt, bool axpy, float alpha) {
+                       int32_t N, int64_t C, int32_t kmax, DType dt, bool axpy, float alpha, void* shadow) {
   if (S <= 0) return;
   AKKA_CHECK((reinterpret_cast<uintptr_t>(dst) & 15) == 0 && (reinterpret_cast<uintptr_t>(src) & 15) == 0,
              "count_mean: buffers must be 16-B aligned");
+  AKKA_CHECK(shadow == nullptr || (axpy && dt == DType::F32 && (reinterpret_cast<uintptr_t>(shadow) & 15) == 0),
+             "count_mean: a bf16 shadow needs the fp32 SGD update and a 16-B aligned buffer");
   const int64_t regions = int64_t(N) * kmax;
   int grid = int(regions < kMaxGrid ? regions : kMaxGrid);
   int split = int(kMaxGrid / grid);
@@ -612,15 +757,17 @@ void launch_count_mean(hipStream_t s, void* dst, const void* src, const int32_t*
   const int64_t useful = (per_region_vecs + kBlock - 1) / kBlock;
   if (split > useful) split = int(useful);
   if (split < 1) split = 1;
-#define AKKA_CM(T, AX)                                                                                       \
-  hipLaunchKernelGGL((count_mean_kernel<T, AX>), dim3(grid, split), dim3(kBlock), 0, s, static_cast<T*>(dst), \
-                     static_cast<const T*>(src), counts, S, step, N, C, kmax, alpha)
+#define AKKA_CM(T, AX, SH)                                                                                       \
+  hipLaunchKernelGGL((count_mean_kernel<T, AX, SH>), dim3(grid, split), dim3(kBlock), 0, s, static_cast<T*>(dst), \
+                     static_cast<const T*>(src), counts, S, step, N, C, kmax, alpha,                              \
+                     static_cast<unsigned short*>(shadow))
   if (dt == DType::F32) {
-    if (axpy) AKKA_CM(float, true);
-    else AKKA_CM(float, false);
+    if (shadow) AKKA_CM(float, true, true);
+    else if (axpy) AKKA_CM(float, true, false);
+    else AKKA_CM(float, false, false);
   } else {
-    if (axpy) AKKA_CM(unsigned short, true);
-    else AKKA_CM(unsigned short, false);
+    if (axpy) AKKA_CM(unsigned short, true, false);
+    else AKKA_CM(unsigned short, false, false);
   }
 #undef AKKA_CM
   check_launch("count_mean");

@@ -25,7 +25,8 @@ def _port() -> int:
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("--cases", required=True,
-                    help="N:size:dtype:mode:lite:threads[:chunk[:async[:pre_size]]], comma separated")
+                    help="N:size:dtype:mode:lite:threads[:chunk[:async[:pre_size[:pre_rounds[:pre_del]]]]], comma separated")
+    ap.add_argument("--env", default="", help="extra environment for every case, K=V;K=V")
     ap.add_argument("--timeout", type=int, default=240)
     a = ap.parse_args()
     for case in a.cases.split(","):
@@ -34,13 +35,17 @@ def main() -> None:
         chunk = int(f[6]) if len(f) > 6 else 0
         async_op = len(f) > 7 and f[7] == "1"
         pre = int(f[8]) if len(f) > 8 else 0
+        pre_rounds = int(f[9]) if len(f) > 9 else 5
+        pre_del = len(f) > 10 and f[10] == "1"
         with tempfile.TemporaryDirectory() as out:
             cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
                    "--master-addr", "127.0.0.1", "--master-port", str(_port()),
                    os.path.join(ROOT, "tests", "ipc_ranks.py"), "--out-dir", out, "--size", str(size),
                    "--dtype", dtype, "--rounds", "0", "--time", "--time-mode", mode, "--chunk", str(chunk),
-                   "--pre-size", str(pre)] + (["--time-async"] if async_op else [])
+                   "--pre-size", str(pre), "--pre-rounds", str(pre_rounds)] + (["--time-async"] if async_op else []) \
+                + (["--pre-del"] if pre_del else [])
             env = dict(os.environ, AKKA_IPC_LITE=lite, AKKA_IPC_THREADS=threads)
+            env.update(kv.split("=", 1) for kv in a.env.split(";") if kv)
             r = subprocess.run(cmd, capture_output=True, text=True, timeout=a.timeout, cwd=ROOT, env=env)
             rows = []
             for i in range(n):
@@ -49,7 +54,8 @@ def main() -> None:
                     with open(p) as fh:
                         rows.append(json.load(fh))
         line = {"N": n, "size": size, "dtype": dtype, "mode": mode, "lite": lite == "1", "threads": int(threads),
-                "chunk": chunk, "async": async_op, "pre_size": pre, "rc": r.returncode}
+                "chunk": chunk, "async": async_op, "pre_size": pre, "pre_rounds": pre_rounds, "pre_del": pre_del,
+                "env": a.env, "rc": r.returncode}
         if r.returncode == 0 and len(rows) == n:
             ms = max(d["ms_per_round"] for d in rows)
             es = 4 if dtype == "float32" else 2

@@ -38,6 +38,8 @@ def main():
     ap.add_argument("--chunk", type=int, default=0, help="max chunk size (elements; default size / 16)")
     ap.add_argument("--time-async", action="store_true", help="timed rounds with async_op=True")
     ap.add_argument("--pre-size", type=int, default=0, help="run 5 rounds of another fp32 engine of this size first")
+    ap.add_argument("--pre-rounds", type=int, default=5, help="rounds of the --pre-size engine")
+    ap.add_argument("--pre-del", action="store_true", help="delete the --pre-size engine before the timed one")
     ap.add_argument("--mode", default="pull", choices=["pull", "bcast", "alternate", "fused", "fused_bcast", "rotate"])
     ap.add_argument("--out-dir", default="", help="write rank<i>.json there (stdout lines of ranks interleave)")
     ap.add_argument("--poison", action="store_true",
@@ -55,9 +57,16 @@ def main():
     if a.pre_size:  # another engine in the process first (bench.py's headline before its extras)
         pre = ThresholdAllreduce(a.pre_size, max_chunk_size=max(1, a.pre_size // 64), device=dev, data_plane="ipc")
         px = torch.randn(a.pre_size, device=dev)
-        for _ in range(5):
+        for _ in range(a.pre_rounds):
             pre(px, async_op=True).wait()
         torch.cuda.synchronize()
+        if a.pre_del:
+            dist.barrier()  # every rank's pre rounds drained before any window goes
+            del pre, px
+            import gc
+
+            gc.collect()
+            pre = None
     ar = ThresholdAllreduce(a.size, max_chunk_size=a.chunk or max(1, a.size // 16), dtype=dtype, device=dev,
                             data_plane="ipc")
     res = {"rank": rank, "exact": [], "lane": ar.state()["link"]["lane"],

@@ -94,3 +94,33 @@ def test_rebind_keeps_foreign_gradient_values():
     assert not bucket.bound()
     assert bucket.rebind() and bucket.bound()
     torch.testing.assert_close(model.fc2.weight.grad, g)
+
+
+def test_colsum_cpu_matches_torch():
+    import torch
+
+    from akka_allreduce_amd.ops import colsum
+
+    x = torch.randn(37, 1003).to(torch.bfloat16)
+    torch.testing.assert_close(colsum(x), x.float().sum(0), rtol=1e-5, atol=1e-4)
+    out = torch.empty(1003)
+    assert colsum(x, out=out) is out
+
+
+def test_bucket_shadow_off_on_cpu():
+    """The bf16 weight shadow is a device feature: on the CPU the bucket says
+    no and the bf16 step casts as before."""
+    import torch
+
+    from akka_allreduce_amd.models.mlp import MLP, dp_sgd_step, synthetic_batch
+    from akka_allreduce_amd.parallel.dp import GradientBucket
+
+    torch.manual_seed(0)
+    model = MLP(32, 64, 5)
+    bucket = GradientBucket(list(model.parameters()), flatten_params=True)
+    assert bucket.params_bound()
+    assert not bucket.use_shadow(torch.bfloat16)
+    assert bucket.shadow_of(model.fc1.weight) is None
+    x, y = synthetic_batch(16, 32, 5, device="cpu")
+    dp_sgd_step(model, x, y, 0.1, None, bucket, compute_dtype=torch.bfloat16)
+    assert bucket.sflat is None
