@@ -15,6 +15,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from ..ops.colsum import colsum
+from ..ops.xent import cross_entropy
 from ..parallel.dp import AllreduceFn, GradientBucket
 
 
@@ -93,7 +94,7 @@ class MLP(nn.Module):
 def dp_sgd_step(model: nn.Module, x: torch.Tensor, y: torch.Tensor, lr: float,
                 allreduce: Optional[AllreduceFn], bucket: Optional[GradientBucket] = None,
                 sync_loss: bool = True, compute_dtype: Optional[torch.dtype] = None,
-                direct_grads: bool = True, shadow_weights: bool = True):
+                direct_grads: bool = True, shadow_weights: bool = True, fused_loss: bool = True):
     """forward + backward + gradient allreduce (mean over contributors) + SGD
     update.  With a bucket built with ``flatten_params=True`` the averaging and
     the update are one fused pass.  ``sync_loss=False`` returns the loss as a
@@ -108,6 +109,14 @@ def dp_sgd_step(model: nn.Module, x: torch.Tensor, y: torch.Tensor, lr: float,
         if bucket is None:
             bucket = GradientBucket(list(model.parameters()))
             model._akka_bucket = bucket  # type: ignore[attr-defined]
+    loss = _forward_backward(model, x, y, bucket, compute_dtype, direct_grads, shadow_weights, fused_loss)
+    bucket.sgd_from(allreduce, lr)
+    return float(loss.detach()) if sync_loss else loss.detach()
+
+
+def _forward_backward(model: nn.Module, x: torch.Tensor, y: torch.Tensor, bucket: GradientBucket,
+                      compute_dtype: Optional[torch.dtype], direct_grads: bool, shadow_weights: bool,
+                      fused_loss: bool, grad_seed: Optional[torch.Tensor] = None) -> torch.Tensor:
     # zero_grad() (set_to_none) or a reassigned .grad detaches a parameter
     # from the bucket: put the views back, or the allreduce would average a
     # buffer autograd no longer writes
@@ -130,17 +139,95 @@ def dp_sgd_step(model: nn.Module, x: torch.Tensor, y: torch.Tensor, lr: float,
             bucket.zero_()
         if compute_dtype is not None and compute_dtype != torch.float32:
             with torch.autocast(device_type=x.device.type, dtype=compute_dtype):
-                loss = F.cross_entropy(model(x), y)
+                logits = model(x)
+            # bf16 logits: the fused gfx950 loss (ops/xent.py), fp32 inside
+            loss = cross_entropy(logits, y) if fused_loss else F.cross_entropy(logits.float(), y)
         else:
             loss = F.cross_entropy(model(x), y)
-        loss.backward()
+        loss.backward(grad_seed)  # None: autograd's ones; a graph passes a preallocated seed (no fill kernel)
     finally:
         if isinstance(model, MLP):
             model.direct_grads = False
             model.shadow_bucket = None
             model.last_step_direct = direct
-    bucket.sgd_from(allreduce, lr)
-    return float(loss.detach()) if sync_loss else loss.detach()
+    return loss
+
+
+class GraphedDPStep:
+    """``dp_sgd_step`` with the forward + backward captured once in a HIP
+    graph (``torch.cuda.CUDAGraph``): a step is two input copies, one graph
+    replay, then the gradient allreduce and the fused average + SGD pass,
+    eagerly -- the allreduce keeps its own per-round host protocol (round
+    ids, peer flags), so it stays outside the graph.  The ~30 launches of
+    the forward/backward cost one replay instead of ~10 µs of host time each
+    (the step is otherwise host-bound at this size).
+
+    The graph bakes in every buffer: the bucket (gradients written directly
+    into it), the parameters, the bf16 shadow and the static batch.  Moving
+    any of them (``zero_grad(set_to_none=True)``, reassigning ``p.data``, a
+    different batch shape) raises; in-place parameter updates by torch are
+    fine (they refresh the shadow before the replay)."""
+
+    def __init__(self, model: "MLP", bucket: GradientBucket, x: torch.Tensor, y: torch.Tensor,
+                 compute_dtype: Optional[torch.dtype] = None, shadow_weights: bool = True, warmup: int = 3):
+        if not (x.is_cuda and isinstance(model, MLP)):
+            raise ValueError("GraphedDPStep: an MLP on a GPU")
+        if bucket.pflat is None or not bucket.bound() or not bucket.params_bound():
+            raise ValueError("GraphedDPStep: needs GradientBucket(flatten_params=True) bound to the model")
+        self.model, self.bucket = model, bucket
+        self.compute_dtype = compute_dtype
+        self.lowp = compute_dtype if (shadow_weights and compute_dtype is not None
+                                      and compute_dtype != torch.float32) else None
+        # the static batch: write the next batch into these (static_inputs())
+        # and the replay reads it in place, no copy
+        self.sx = x.detach().clone()
+        self.sy = y.detach().clone()
+        self._seed = torch.ones((), dtype=torch.float32, device=x.device)
+        self._ptrs = self._pointers()
+
+        def fb():
+            return _forward_backward(model, self.sx, self.sy, bucket, compute_dtype, True, shadow_weights, True,
+                                     grad_seed=self._seed)
+
+        # warm up and capture on ONE stream: the kernels' per-stream workspaces
+        # (colsum / cross-entropy tickets) are created, and zeroed, by the
+        # warmup, so the graph holds no fill for them
+        side = torch.cuda.Stream(device=x.device)
+        side.wait_stream(torch.cuda.current_stream(x.device))
+        with torch.cuda.stream(side):
+            for _ in range(warmup):
+                fb()
+        side.synchronize()
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph, stream=side):
+            self.loss = fb().detach()
+        torch.cuda.current_stream(x.device).wait_stream(side)
+        self._ptrs = self._pointers()  # the shadow exists now
+
+    def static_inputs(self):
+        """(x, y) buffers the graph reads: fill them with the next batch and
+        pass them to the call to skip the copies."""
+        return self.sx, self.sy
+
+    def _pointers(self):
+        b = self.bucket
+        return (b.flat.data_ptr(), b.pflat.data_ptr(), b.sflat.data_ptr() if b.sflat is not None else 0,
+                [p.data_ptr() for p in b.params], [p.grad.data_ptr() if p.grad is not None else 0 for p in b.params])
+
+    def __call__(self, x: torch.Tensor, y: torch.Tensor, lr: float, allreduce: Optional[AllreduceFn],
+                 sync_loss: bool = False):
+        b = self.bucket
+        if self._pointers() != self._ptrs:
+            raise RuntimeError("GraphedDPStep: a parameter, gradient or shadow buffer moved since the capture")
+        if b.use_shadow(self.lowp) != (self.lowp is not None and b.sflat is not None):
+            raise RuntimeError("GraphedDPStep: the bf16 shadow is no longer usable")
+        if x.data_ptr() != self.sx.data_ptr():
+            self.sx.copy_(x)
+        if y.data_ptr() != self.sy.data_ptr():
+            self.sy.copy_(y)
+        self.graph.replay()
+        b.sgd_from(allreduce, lr)
+        return float(self.loss) if sync_loss else self.loss
 
 
 def synthetic_batch(batch: int, d_in: int, n_classes: int, *, device, generator: Optional[torch.Generator] = None):

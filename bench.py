@@ -459,6 +459,17 @@ def run_extras(world: int, dev, barrier, which=("cfg1", "cfg3", "cfg4", "cfg5"),
         res["cfg5_mlp_dp_sgd_bf16"] = {"steps_per_s": round(steps / dt, 3),
                                        "samples_per_s": round(steps * batch * world / dt, 1),
                                        "compute_dtype": "bf16 autocast, fp32 master weights/grads"}
+        # same step with forward + backward replayed from a HIP graph (the
+        # allreduce and the fused update stay eager: GraphedDPStep)
+        from akka_allreduce_amd.models.mlp import GraphedDPStep
+
+        gstep = GraphedDPStep(model, bucket, xb, yb, compute_dtype=torch.bfloat16)
+        gx, gy = gstep.static_inputs()  # the synthetic batch lives in the graph's buffers
+        dt = timed(lambda: gstep(gx, gy, 0.05, ar), steps, 5, world, barrier)
+        res["cfg5_mlp_dp_sgd_bf16_graph"] = {"steps_per_s": round(steps / dt, 3),
+                                             "samples_per_s": round(steps * batch * world / dt, 1),
+                                             "compute_dtype": "bf16 autocast, fp32 master weights/grads; "
+                                                              "forward+backward as one HIP graph replay"}
     except _Skip:
         pass
     except Exception as e:

@@ -888,6 +888,18 @@ PYBIND11_MODULE(_native, m) {
   }, py::arg("out"), py::arg("in"), py::arg("M"), py::arg("ncol"), py::arg("part"), py::arg("tickets"),
      py::arg("splits"), py::arg("stream"), py::arg("lite") = true);
   m.def("colsum_row_splits", &colsum_row_splits);
+  m.def("xent_fwd", [](uintptr_t x, uintptr_t y, int64_t B, int64_t C, uintptr_t lse, uintptr_t rowloss, uintptr_t out,
+                       uintptr_t ticket, uintptr_t stream) {
+    launch_xent_fwd(as_stream(stream), reinterpret_cast<const void*>(x), reinterpret_cast<const int64_t*>(y), B, C,
+                    reinterpret_cast<float*>(lse), reinterpret_cast<float*>(rowloss), reinterpret_cast<float*>(out),
+                    reinterpret_cast<uint32_t*>(ticket));
+  });
+  m.def("xent_bwd", [](uintptr_t x, uintptr_t y, int64_t B, int64_t C, uintptr_t lse, uintptr_t stat, uintptr_t go,
+                       uintptr_t gx, uintptr_t stream) {
+    launch_xent_bwd(as_stream(stream), reinterpret_cast<const void*>(x), reinterpret_cast<const int64_t*>(y), B, C,
+                    reinterpret_cast<const float*>(lse), reinterpret_cast<const float*>(stat),
+                    reinterpret_cast<const float*>(go), reinterpret_cast<void*>(gx));
+  });
   m.def("geometry", [](int64_t S, int32_t N, int64_t C) {
     Geometry g(S, N, C);
     py::dict d;

@@ -34,6 +34,14 @@ void launch_count_mean(hipStream_t s, void* dst, const void* src, const int32_t*
 void launch_colsum_bf16(hipStream_t s, float* out, const void* in, int64_t M, int64_t ncol, float* part,
                         uint32_t* tickets, int32_t splits, bool lite = true);
 int32_t colsum_row_splits(int64_t M, int64_t ncol);
+// Cross entropy over bf16 logits [B, C] with int64 labels (mean over the rows
+// whose label is in [0, C)).  Forward: lse [B] fp32, rowloss [2B] fp32
+// workspace, out [2] = {loss, valid rows}, ticket: one uint32 zeroed once.
+// Backward: gx [B, C] bf16 = d(loss)/d(x) * go[0].
+void launch_xent_fwd(hipStream_t s, const void* x, const int64_t* y, int64_t B, int64_t C, float* lse,
+                     float* rowloss, float* out, uint32_t* ticket);
+void launch_xent_bwd(hipStream_t s, const void* x, const int64_t* y, int64_t B, int64_t C, const float* lse,
+                     const float* stat, const float* go, void* gx);
 // counts[0..n) = 0 if *flag != 0 (read when the kernel runs): poisons the
 // counts of a one-sided round whose waits failed.
 void launch_poison_counts(hipStream_t s, const uint32_t* flag, int32_t* counts, int64_t n);

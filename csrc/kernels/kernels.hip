@@ -479,6 +479,94 @@ __global__ __launch_bounds__(kBlock) void colsum_bf16_kernel(float* __restrict__
     __hip_atomic_store(&tickets[blockIdx.x], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// ---- fused cross entropy (the MLP's loss) -------------------------------------
+// Forward: one workgroup per row of bf16 logits [B, C]: lse = log sum exp,
+// loss_r = lse - x[y_r] (0 for a label outside [0, C): torch's ignore_index),
+// lse kept for the backward; the mean over the valid rows is combined by the
+// last-arriving workgroup (write-through per-row words, drained vmcnt, relaxed
+// ticket, system-coherent loads: the colsum hand-off) in row order.
+// Backward: grad[r, c] = (exp(x - lse_r) - [c == y_r]) * go / nvalid, bf16.
+// Replaces autocast's fp32 upcast + log_softmax + nll_loss (+ their
+// backwards and the bf16 downcast of the gradient): two launches instead of
+// six, logits read once per pass.
+__device__ __forceinline__ float block_reduce(float v, float* red, bool is_max) {
+  for (int o = 32; o > 0; o >>= 1) {
+    const float w = __shfl_xor(v, o, 64);
+    v = is_max ? fmaxf(v, w) : v + w;
+  }
+  __syncthreads();  // red may still be read by a previous reduction
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  float r = red[0];
+  for (int w = 1; w < int(blockDim.x >> 6); ++w) r = is_max ? fmaxf(r, red[w]) : r + red[w];
+  return r;
+}
+
+__global__ __launch_bounds__(kBlock) void xent_fwd_kernel(const unsigned short* __restrict__ x,
+                                                          const int64_t* __restrict__ y, int64_t B, int64_t C,
+                                                          float* __restrict__ lse, float* __restrict__ rowloss,
+                                                          float* __restrict__ out, uint32_t* __restrict__ ticket) {
+  __shared__ float red[kBlock / 64 + 1];
+  const int64_t r = blockIdx.x;
+  const unsigned short* row = x + r * C;
+  float m = -INFINITY;
+  for (int64_t c = threadIdx.x; c < C; c += kBlock) m = fmaxf(m, to_f(row[c]));
+  m = block_reduce(m, red, true);
+  float sum = 0.f;
+  for (int64_t c = threadIdx.x; c < C; c += kBlock) sum += __expf(to_f(row[c]) - m);
+  sum = block_reduce(sum, red, false);
+  const auto rs = xgmi::sys_rsrc(rowloss, B * 8);
+  if (threadIdx.x == 0) {
+    const float l = m + __logf(sum);
+    const int64_t t = y[r];
+    const bool valid = t >= 0 && t < C;
+    lse[r] = l;
+    // [loss, valid] per row, written through for the last arriver
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(valid ? l - to_f(row[t]) : 0.f), rs, int(r * 8), 0,
+                                          xgmi::kSysAux);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(valid ? 1.f : 0.f), rs, int(r * 8 + 4), 0,
+                                          xgmi::kSysAux);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    red[kBlock / 64] =
+        __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == uint32_t(B - 1) ? 1.f : 0.f;
+  }
+  __syncthreads();
+  if (red[kBlock / 64] == 0.f) return;
+  // last workgroup: mean over the valid rows, in row order per thread, then
+  // a fixed-order tree across threads (deterministic)
+  float ls = 0.f, nv = 0.f;
+  for (int64_t i = threadIdx.x; i < B; i += kBlock) {
+    ls += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, int(i * 8), 0, xgmi::kSysAux));
+    nv += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, int(i * 8 + 4), 0, xgmi::kSysAux));
+  }
+  ls = block_reduce(ls, red, false);
+  nv = block_reduce(nv, red, false);
+  if (threadIdx.x == 0) {
+    out[0] = nv > 0.f ? ls / nv : __uint_as_float(0x7fc00000u);  // torch: NaN when every row is ignored
+    out[1] = nv;
+    __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+__global__ __launch_bounds__(kBlock) void xent_bwd_kernel(const unsigned short* __restrict__ x,
+                                                          const int64_t* __restrict__ y, int64_t C,
+                                                          const float* __restrict__ lse,
+                                                          const float* __restrict__ stat,  // [loss, nvalid]
+                                                          const float* __restrict__ go,
+                                                          unsigned short* __restrict__ gx) {
+  const int64_t r = blockIdx.x;
+  const int64_t t = y[r];
+  const float nv = stat[1];
+  const float scale = (t >= 0 && t < C && nv > 0.f) ? go[0] / nv : 0.f;
+  const float l = lse[r];
+  const unsigned short* row = x + r * C;
+  unsigned short* g = gx + r * C;
+  for (int64_t c = threadIdx.x; c < C; c += kBlock) {
+    const float p = __expf(to_f(row[c]) - l) - (c == t ? 1.f : 0.f);
+    g[c] = from_f<unsigned short>(p * scale);
+  }
+}
+
 template <typename T, int NSRC, int POL, int UNROLL>
 void launch_vec_u(hipStream_t s, const SrcTable& t, v4u* dst, int64_t nvec, int blocks_per_cu) {
   const int64_t cap = int64_t(kCUs) * blocks_per_cu;
@@ -741,6 +829,22 @@ void launch_colsum_bf16(hipStream_t s, float* out, const void* in, int64_t M, in
     hipLaunchKernelGGL(colsum_bf16_kernel<false>, dim3(uint32_t(tiles), uint32_t(splits)), dim3(kBlock), 0, s, out,
                        static_cast<const unsigned short*>(in), M, ncol, part, tickets, vec);
   check_launch("colsum_bf16");
+}
+
+void launch_xent_fwd(hipStream_t s, const void* x, const int64_t* y, int64_t B, int64_t C, float* lse,
+                     float* rowloss, float* out, uint32_t* ticket) {
+  AKKA_CHECK(B >= 1 && C >= 1 && B < (int64_t(1) << 27), "xent: bad shape");
+  hipLaunchKernelGGL(xent_fwd_kernel, dim3(uint32_t(B)), dim3(kBlock), 0, s, static_cast<const unsigned short*>(x), y,
+                     B, C, lse, rowloss, out, ticket);
+  check_launch("xent_fwd");
+}
+
+void launch_xent_bwd(hipStream_t s, const void* x, const int64_t* y, int64_t B, int64_t C, const float* lse,
+                     const float* stat, const float* go, void* gx) {
+  AKKA_CHECK(B >= 1 && C >= 1, "xent: bad shape");
+  hipLaunchKernelGGL(xent_bwd_kernel, dim3(uint32_t(B)), dim3(kBlock), 0, s, static_cast<const unsigned short*>(x), y,
+                     C, lse, stat, go, static_cast<unsigned short*>(gx));
+  check_launch("xent_bwd");
 }
 
 void launch_count_mean(hipStream_t s, void* dst, const void* src, const int32_t* counts, int64_t S, int64_t step,

@@ -32,6 +32,7 @@ def test_bench_prints_one_baseline_line():
     ex = d["extra_configs"]
     assert ex["cfg3_bf16_1GiB_chunk8MiB"]["algbw_GBps"] > 0, ex
     assert ex["cfg5_mlp_dp_sgd"]["steps_per_s"] > 0, ex
+    assert ex["cfg5_mlp_dp_sgd_bf16_graph"]["steps_per_s"] > 0, ex
 
 
 def test_bench_extras_deadline_keeps_headline():

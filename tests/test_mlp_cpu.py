@@ -124,3 +124,14 @@ def test_bucket_shadow_off_on_cpu():
     x, y = synthetic_batch(16, 32, 5, device="cpu")
     dp_sgd_step(model, x, y, 0.1, None, bucket, compute_dtype=torch.bfloat16)
     assert bucket.sflat is None
+
+
+def test_cross_entropy_cpu_is_torch():
+    import torch
+    import torch.nn.functional as F
+
+    from akka_allreduce_amd.ops import cross_entropy
+
+    x = torch.randn(5, 7)
+    y = torch.tensor([0, 6, 2, 3, 1])
+    assert torch.equal(cross_entropy(x, y), F.cross_entropy(x, y))
