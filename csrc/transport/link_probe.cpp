@@ -15,7 +15,9 @@
 
 namespace akka {
 
-void launch_probe_copy(hipStream_t s, void* dst, const void* src, int64_t bytes, int32_t wgs);  // probe.hip
+// probe.hip: every (dst, src) pair of the table in one launch (<= 16 pairs)
+void launch_probe_copies(hipStream_t s, void* const* dst, const void* const* src, int32_t n, int64_t bytes,
+                         int32_t wgs);
 
 namespace {
 
@@ -46,11 +48,11 @@ LinkProbe::LinkProbe(int32_t device, int32_t rank, int32_t nranks, int64_t bytes
     AKKA_PROBE_HIP(hipMalloc(reinterpret_cast<void**>(&local_), size_t(bytes_)));
     AKKA_PROBE_HIP(hipMemset(buf_, 1, size_t(bytes_)));
     AKKA_PROBE_HIP(hipMemset(local_, 2, size_t(bytes_)));
-    for (int32_t i = 0; i < n_; ++i) {
-      hipStream_t s;
-      AKKA_PROBE_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-      streams_.push_back(s);
-    }
+    // ONE stream: the peers' copies share a launch (probe_copies_kernel), so the
+    // probe adds one hardware queue to the process, not one per peer
+    hipStream_t s;
+    AKKA_PROBE_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    streams_.push_back(s);
     AKKA_PROBE_HIP(hipDeviceSynchronize());
   } else {
     std::random_device rd;
@@ -153,17 +155,21 @@ double LinkProbe::run(const std::vector<int32_t>& peers, int32_t iters, bool pus
     return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   }
   AKKA_PROBE_HIP(hipSetDevice(device_));
-  // one stream per peer, every copy enqueued before timing ends; 1024
+  // every peer's copy in one launch per iteration (blockIdx.y = peer); 1024
   // workgroups per copy keep plenty of 16-byte requests in flight per link
+  AKKA_CHECK(peers.size() <= 16, "link probe: at most 16 peers per launch");
   const int32_t wgs = 1024;
+  std::vector<void*> dst(peers.size());
+  std::vector<const void*> src(peers.size());
+  for (size_t i = 0; i < peers.size(); ++i) {
+    const int32_t q = peers[i];
+    dst[i] = push ? static_cast<void*>(peer_[size_t(q)]) : static_cast<void*>(local_);
+    src[i] = push ? static_cast<const void*>(local_) : static_cast<const void*>(peer_[size_t(q)]);
+  }
+  hipStream_t s = static_cast<hipStream_t>(streams_[0]);
   auto enqueue = [&](int32_t reps) {
     for (int32_t it = 0; it < reps; ++it)
-      for (size_t i = 0; i < peers.size(); ++i) {
-        hipStream_t s = static_cast<hipStream_t>(streams_[i % streams_.size()]);
-        const int32_t q = peers[i];
-        if (push) launch_probe_copy(s, peer_[size_t(q)], local_, bytes_, wgs);
-        else launch_probe_copy(s, local_, peer_[size_t(q)], bytes_, wgs);
-      }
+      launch_probe_copies(s, dst.data(), src.data(), int32_t(peers.size()), bytes_, wgs);
   };
   enqueue(1);  // warm-up (mapping, TLB)
   AKKA_PROBE_HIP(hipDeviceSynchronize());
