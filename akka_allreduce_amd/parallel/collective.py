@@ -410,6 +410,10 @@ class ThresholdAllreduce:
         "ipc_lite": ("ipc", -1, "pull", False, 1024, True),
         "ipc_bcast_lite": ("ipc", -1, "bcast", False, 1024, True),
         "ipc_fused_lite": ("ipc", -1, "pull", True, 1024, True),
+        # phase 2 as remote WRITES in the fused, fence-free form: over xGMI a
+        # store can beat a remote read, which the shared-card rehearsals cannot
+        # show (both stay inside one card's HBM there)
+        "ipc_fused_bcast_lite": ("ipc", -1, "bcast", True, 1024, True),
     }
 
     def use_lane(self, name: str) -> None:
@@ -461,7 +465,7 @@ class ThresholdAllreduce:
                                       "error": err or "another rank could not open its windows"}
                 if ipc_open:
                     cands += ["ipc", "ipc_bcast", "ipc_fused", "ipc_fused_bcast", "ipc_wide", "ipc_bcast_wide",
-                              "ipc_lite", "ipc_bcast_lite", "ipc_fused_lite"]
+                              "ipc_lite", "ipc_bcast_lite", "ipc_fused_lite", "ipc_fused_bcast_lite"]
         S, N, r = self.data_size, self.world_size, self.rank
         dtype = self.worker.dtype
         x = torch.randn(S, device=self.device).to(dtype)

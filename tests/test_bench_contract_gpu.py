@@ -92,7 +92,7 @@ def test_bench_multirank_on_one_card(plane):
         assert w["fast_rank_median_ms_per_round"] < 40 / 4 and w["catch_up_skipped_rounds"] > 0, c4
     else:
         assert set(cands) == {"ipc", "ipc_bcast", "ipc_fused", "ipc_fused_bcast", "ipc_wide", "ipc_bcast_wide",
-                              "ipc_lite", "ipc_bcast_lite", "ipc_fused_lite"}
+                              "ipc_lite", "ipc_bcast_lite", "ipc_fused_lite", "ipc_fused_bcast_lite"}
 
 
 def test_bench_rccl_init_failure_falls_back_to_ipc():
