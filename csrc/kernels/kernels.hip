@@ -578,15 +578,18 @@ void launch_vec_u(hipStream_t s, const SrcTable& t, v4u* dst, int64_t nvec, int 
 template <typename T, int NSRC, int POL>
 void launch_vec_pol(hipStream_t s, const SrcTable& t, v4u* dst, int64_t nvec, int blocks_per_cu) {
   constexpr int U0 = NSRC <= 4 ? 4 : (NSRC <= 8 ? 2 : 1);
-  constexpr int UNROLL = POL == kBoth ? (U0 < 2 ? U0 : 2) : U0;
-  if constexpr (NSRC == 8 && POL == kNts && std::is_same<T, float>::value) {
-    // experiments (bench/reduce_kernel_bw.py sweeps): loads in flight per lane
+  // kBoth (big streams): 2 vectors per lane per source, but 4 for the
+  // one-source pass (1 GiB bf16: 5.69 vs 5.53 TB/s at 2 blocks/CU, pass V)
+  constexpr int UNROLL = POL == kBoth ? (NSRC == 1 ? 4 : (U0 < 2 ? U0 : 2)) : U0;
+  if constexpr ((NSRC == 8 && POL == kNts && std::is_same<T, float>::value) || (NSRC == 1 && POL == kBoth)) {
+    // experiments (bench/reduce_kernel_bw.py, bench/n1_bigcopy.py sweeps): loads in flight per lane
     static const int u = [] {
       const char* v = std::getenv("AKKA_VEC_UNROLL");
       return v ? std::atoi(v) : 0;
     }();
     if (u == 1) return launch_vec_u<T, NSRC, POL, 1>(s, t, dst, nvec, blocks_per_cu);
     if (u == 4) return launch_vec_u<T, NSRC, POL, 4>(s, t, dst, nvec, blocks_per_cu);
+    if (u == 8) return launch_vec_u<T, NSRC, POL, 8>(s, t, dst, nvec, blocks_per_cu);
   }
   launch_vec_u<T, NSRC, POL, UNROLL>(s, t, dst, nvec, blocks_per_cu);
 }
@@ -717,17 +720,17 @@ void launch_reduce(hipStream_t s, const ReduceSpec& spec, DType dt, ReduceImpl i
   }
   // Vec load/store policy and grid (bench/stream_variants.hip sweep):
   //   sources fit the Infinity Cache      -> plain loads, NT stores, 16 blocks/CU
-  //   big stream with a big output        -> NT loads + NT stores, unroll 2, 4 blocks/CU
+  //   big stream with a big output        -> NT loads + NT stores, unroll 2 (4 for one source), 2 blocks/CU
   //   otherwise (many sources, <=256 MiB) -> NT loads, plain stores, 4 blocks/CU
   int pol = kNtl, bpc = 4;
   if (impl == ReduceImpl::Vec) {
     if (rbytes <= (int64_t(256) << 20)) pol = kNts, bpc = 16;
-    else if (wbytes >= (int64_t(512) << 20)) pol = kBoth, bpc = 4;
+    else if (wbytes >= (int64_t(512) << 20)) pol = kBoth, bpc = 2;  // 1 GiB bf16: 5.56 vs 5.11 TB/s at 4 (profiles/r03/pass_u, pass_v)
     else pol = kNtl, bpc = 4;
   } else if (impl == ReduceImpl::VecNts) {
     pol = kNts, bpc = 16;
   } else if (impl == ReduceImpl::VecBoth) {
-    pol = kBoth, bpc = 4;
+    pol = kBoth, bpc = 2;
   } else if (impl == ReduceImpl::VecNtl) {
     pol = kNtl, bpc = 8;
   }
