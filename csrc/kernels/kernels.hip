@@ -396,7 +396,7 @@ __global__ __launch_bounds__(kBlock) void colsum_bf16_kernel(float* __restrict__
                                                              const unsigned short* __restrict__ in, int64_t M,
                                                              int64_t ncol, float* __restrict__ part,
                                                              uint32_t* __restrict__ tickets, int32_t vec) {
-  __shared__ float red[kBlock / 64][kCsCols];
+  __shared__ float red[kBlock / 64][kCsCols + kCsCols / 8];
   __shared__ uint32_t last;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t c0 = int64_t(blockIdx.x) * kCsCols + lane * 8;
@@ -423,16 +423,20 @@ __global__ __launch_bounds__(kBlock) void colsum_bf16_kernel(float* __restrict__
       for (int q = 0; q < 8; ++q)
         if (c0 + q < ncol) acc[q] += to_f(in[r * ncol + c0 + q]);
   }
-  // the workgroup's 4 waves -> one partial row (acc[q] is column c0 + q)
+  // the workgroup's 4 waves -> one partial row (acc[q] is column c0 + q),
+  // staged with one pad word per lane (slot lane * 9 + q): a wave's stores of
+  // one q are 9 words apart and the combine's reads of consecutive columns
+  // are consecutive but for the pads -- no bank conflicts either way
 #pragma unroll
-  for (int q = 0; q < 8; ++q) red[wave][lane * 8 + q] = acc[q];
+  for (int q = 0; q < 8; ++q) red[wave][lane * 9 + q] = acc[q];
   __syncthreads();
   float* prow = part + int64_t(blockIdx.y) * ncol;
   const auto prs = xgmi::sys_rsrc(part, int64_t(gridDim.y) * ncol * 4);
   for (int i = threadIdx.x; i < kCsCols; i += kBlock) {
     const int64_t c = int64_t(blockIdx.x) * kCsCols + i;
     if (c >= ncol) continue;
-    const float v = red[0][i] + red[1][i] + red[2][i] + red[3][i];
+    const int li = i + (i >> 3);  // column i of the tile = lane i / 8, element i % 8
+    const float v = red[0][li] + red[1][li] + red[2][li] + red[3][li];
     if constexpr (LITE)
       __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), prs, int((int64_t(blockIdx.y) * ncol + c) * 4), 0,
                                             xgmi::kSysAux);
