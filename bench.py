@@ -369,13 +369,24 @@ def apply_lane_choice(ar, name) -> None:
     ar.use_lane(name)
 
 
+def _shareable(ar):
+    """The headline engine if another exact-round engine can adopt its
+    transport (stream transport, N > 1), else None."""
+    if ar is None or getattr(ar, "transport", None) != "stream" or ar.world_size < 2 or ar.worker is None:
+        return None
+    return ar
+
+
 def run_extras(world: int, dev, barrier, which=("cfg1", "cfg3", "cfg4", "cfg5"), rank: int = 0,
                cfg4_size_mb: float = 64.0, cfg4_delay_ms: float = 50.0, cfg4_rounds: int = 64,
                cfg4_transport: str = "onesided",
-               lane: str | None = None, data_plane: str = "rccl") -> dict:
+               lane: str | None = None, data_plane: str = "rccl", share=None) -> dict:
     """BASELINE config 3 (8-rank bf16, 1 GB buffer, link-sized chunks),
     config 4 (threshold 0.75/0.75 + straggler, N>1 only) and config 5 (2-layer
-    MLP DP-SGD step/s) at this N, on synthetic data."""
+    MLP DP-SGD step/s) at this N, on synthetic data.  ``share``: the
+    headline's ThresholdAllreduce; configs 3 and 5 ride on its transport
+    (same device streams and communicator, its ipc windows where they fit)
+    instead of adding streams -- hardware queues -- to the process."""
     import torch
 
     from akka_allreduce_amd.parallel import ThresholdAllreduce
@@ -410,7 +421,7 @@ def run_extras(world: int, dev, barrier, which=("cfg1", "cfg3", "cfg4", "cfg5"),
         nbytes = 1 << 30
         S = nbytes // 2
         ar = ThresholdAllreduce(S, max_chunk_size=(8 << 20) // 2, dtype=torch.bfloat16, device=dev,
-                                data_plane=data_plane)
+                                data_plane=data_plane, share_transport_with=_shareable(share))
         keep.append(ar)
         apply_lane_choice(ar, lane)
         x = torch.randn(S, device=dev, dtype=torch.bfloat16)
@@ -422,7 +433,8 @@ def run_extras(world: int, dev, barrier, which=("cfg1", "cfg3", "cfg4", "cfg5"),
         res["cfg3_bf16_1GiB_chunk8MiB"] = {"algbw_GBps": round(nbytes / (dt / steps) / 1e9, 3),
                                            "ms_per_step": round(dt / steps * 1e3, 4), "lane": link.get("lane"),
                                            "ipc_mode": {k: ipc.get(k) for k in ("mode", "fused", "lite", "max_wgs",
-                                                                                "portions", "rounds")}
+                                                                                "portions", "rounds",
+                                                                                "shares_windows", "window_bytes")}
                                            if ipc else None}
         del x, out
     except _Skip:
@@ -440,7 +452,8 @@ def run_extras(world: int, dev, barrier, which=("cfg1", "cfg3", "cfg4", "cfg5"),
         d_in, hidden, classes, batch = 4096, 8192, 1000, 256
         model = MLP(d_in, hidden, classes).to(dev)
         bucket = GradientBucket(list(model.parameters()), flatten_params=True)
-        ar = ThresholdAllreduce(bucket.numel, max_chunk_size=(4 << 20) // 4, device=dev, data_plane=data_plane)
+        ar = ThresholdAllreduce(bucket.numel, max_chunk_size=(4 << 20) // 4, device=dev, data_plane=data_plane,
+                                share_transport_with=_shareable(share))
         keep.append(ar)
         apply_lane_choice(ar, lane)
         gen = torch.Generator(device=dev).manual_seed(1000 + (ar.rank or 0))
@@ -589,12 +602,23 @@ def main() -> int:
 
     from akka_allreduce_amd.parallel import ThresholdAllreduce
 
+    # The extras' exact-round engines ride on the headline engine's transport
+    # (run_extras(share=...)); its ipc windows are sized for config 3's 1 GiB
+    # so that engine reuses them too: a second window set mapped by every
+    # process slowed whole rounds by 4-20x when ranks share one card
+    # (profiles/r03/README.md), and costs mappings on a node.
+    will_cfg3 = (world > 1 and args.transport == "stream" and args.device == "cuda"
+                 and (args.extras == "on" or (args.extras == "auto" and args.size_mb == 256.0
+                                              and args.dtype == "float32"))
+                 and (not args.extras_only or "cfg3" in args.extras_only.split(",")))
+    ipc_cap = max(S, (1 << 30) // esize) if will_cfg3 else 0
+
     def rccl_init():
         env_phase_stall(rank, "rccl_init")
         return ThresholdAllreduce(S, max_chunk_size=C, dtype=dtype, th_reduce=args.th_reduce,
                                   th_complete=args.th_complete, max_lag=args.max_lag, broadcast_lag=args.bcast_lag,
                                   device=dev, transport=args.transport, lane=args.lane,
-                                  data_plane=args.data_plane)
+                                  data_plane=args.data_plane, ipc_capacity=ipc_cap)
 
     # RCCL failing on EVERY rank (agreed) does not cost the headline: the job
     # is rebuilt in this same process on the ipc data plane (one-sided xGMI,
@@ -610,7 +634,7 @@ def main() -> int:
             args.data_plane = "ipc"
             ar = guard.run("ipc_init", dl, lambda: ThresholdAllreduce(
                 S, max_chunk_size=C, dtype=dtype, max_lag=args.max_lag, broadcast_lag=args.bcast_lag, device=dev,
-                data_plane="ipc"))
+                data_plane="ipc", ipc_capacity=ipc_cap))
         else:
             guard.fail("rccl_init", "error", init_errors)
 
@@ -900,7 +924,7 @@ def main() -> int:
         line["extra_configs"] = run_extras(world, dev, barrier, which, rank, args.cfg4_size_mb,
                                            args.cfg4_delay_ms, args.cfg4_rounds, cfg4_transport=args.cfg4_transport,
                                            lane=chosen_lane,
-                                           data_plane=args.data_plane)
+                                           data_plane=args.data_plane, share=ar)
         if chosen_lane and world > 1:
             line["extra_configs"]["lane"] = chosen_lane
         guard.disarm()
