@@ -198,6 +198,9 @@ class GraphedDPStep:
             for _ in range(warmup):
                 fb()
         side.synchronize()
+        # kept alive: the per-stream workspaces baked into the graph are keyed
+        # by this stream's handle, which must not be handed to another stream
+        self._side = side
         self.graph = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.graph, stream=side):
             self.loss = fb().detach()
