@@ -673,13 +673,41 @@ def main() -> int:
     def preflight():
         # one exact full-size round before anything is timed: a hang or a wrong
         # sum shows up here, under its own deadline, with its own failure line
-        env_phase_stall(rank, "preflight")
+        env_phase_stall(rank, "preflight")  # fault injection (AKKA_FAULT_STALL_*): stall or raise here
         if not exact_round("preflight"):
             raise RuntimeError("preflight round is not exact (sum or counts differ on some rank)")
         return True
 
+    # A preflight that fails on EVERY rank (an error or a wrong sum, agreed) on
+    # the two-sided default lane does not cost the headline either: the job
+    # moves to the one-sided ipc lane (no RCCL kernel involved) and checks it
+    # with its own exact round; lane selection then only tries ipc lanes.  A
+    # failure on some ranks only, or a hang, still ends the job.
+    preflight_fallback = None
+    ipc_only = False
     if world > 1 or args.preflight == "on":
-        guard.run("preflight", args.preflight_deadline_s, preflight)
+        can_fall_back = (world > 1 and dev.type == "cuda" and ar.transport == "stream"
+                         and args.data_plane != "ipc" and args.ipc == "on")
+        if can_fall_back:
+            _, pf_errors = guard.try_run("preflight", args.preflight_deadline_s, preflight)
+            if pf_errors and len(pf_errors) == world:
+                preflight_fallback = {"errors": {str(k): v[:200] for k, v in pf_errors.items()},
+                                      "lane": "ipc_fused_lite"}
+
+                def preflight_ipc():
+                    if not ar.state().get("link", {}).get("ipc"):
+                        ar.enable_ipc()  # collective over torch.distributed (gloo)
+                    ar.use_lane("ipc_fused_lite")
+                    if not exact_round("preflight_ipc"):
+                        raise RuntimeError("ipc preflight round is not exact")
+                    return True
+
+                guard.run("preflight_ipc", args.preflight_deadline_s, preflight_ipc)
+                ipc_only = True
+            elif pf_errors:
+                guard.fail("preflight", "error", pf_errors)
+        else:
+            guard.run("preflight", args.preflight_deadline_s, preflight)
 
     g = torch.Generator(device=dev)
     g.manual_seed(1234 + rank)
@@ -707,6 +735,8 @@ def main() -> int:
 
     def lane_select():
         env_phase_stall(rank, "lane_select")
+        if ipc_only:  # the two-sided lane failed its preflight: ipc lanes only
+            return ar.tune(candidates=[k for k in ar.LANES if k.startswith("ipc")])
         return ar.tune(try_ipc=args.ipc == "on")
 
     lane_sel = None
@@ -761,6 +791,8 @@ def main() -> int:
     # Comparator (outside the timed region): RCCL's own all_reduce on the same
     # buffer, same N and step count, through a separate nccl (= RCCL) group.
     compare = (world > 1) if args.compare_rccl == "auto" else (args.compare_rccl == "on")
+    if ipc_only:
+        compare = False  # RCCL failed the preflight: no RCCL comparator after the headline
 
     def comparator():
         if not (compare and world > 1):
@@ -797,7 +829,7 @@ def main() -> int:
         used = chosen_lane or ("ipc" if args.data_plane == "ipc" else "collective" if coll > steps_p2p else "p2p")
         if world == 1:
             return "local", None
-        if args.data_plane == "ipc":
+        if args.data_plane == "ipc" or ipc_only:
             return used, None
         if ar.transport != "stream":
             return used, None
@@ -838,7 +870,8 @@ def main() -> int:
         "ms_per_step": round(ms, 4),
         "busbw_GBps": round(busbw, 3) if busbw is not None else None,
         "exact": ok,
-        "preflight": "passed" if "preflight" in guard.history else "skipped",
+        "preflight": ("passed" if "preflight" in guard.history else
+                      "passed on the ipc lane" if "preflight_ipc" in guard.history else "skipped"),
         "groups_per_round": round((link.get("groups", 0) - link0.get("groups", 0)) / rounds_done, 3),
         "host_us_per_round": round(host_s / args.steps * 1e6, 2),
         "p2p_kind": p2p0.get("kind"),
@@ -870,6 +903,8 @@ def main() -> int:
         line["rccl_compare_error"] = rccl_err
     if rccl_fallback:
         line["rccl_fallback"] = rccl_fallback
+    if preflight_fallback:
+        line["preflight_fallback"] = preflight_fallback
     if os.environ.get("AKKA_SHARE_GPU") == "1" and world > 1:
         line["data"] += "; N ranks sharing ONE GPU (rehearsal of the N-rank flow, not the metric)"
     if world == 1:

@@ -117,3 +117,31 @@ def test_bench_rccl_init_failure_falls_back_to_ipc():
     assert d["rccl_fallback"]["data_plane"] == "ipc" and set(d["rccl_fallback"]["rccl_init_errors"]) == {"0", "1"}
     assert d["config"]["data_plane"] == "ipc" and d["lane"].startswith("ipc") and d["lane_is_framework"] is True
     assert d["exact"] is True and d["value"] > 0
+
+
+def test_bench_preflight_failure_falls_back_to_ipc():
+    """The two-sided default lane failing its preflight on EVERY rank
+    (injected: phase preflight, mode raise; the mailbox p2p data plane stands
+    in for RCCL on a shared card) does not cost the headline: the job checks
+    and times the one-sided ipc lanes only, and the line says so."""
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, AKKA_SHARE_GPU="1", GPU_MAX_HW_QUEUES="8", AKKA_FAULT_STALL_RANK="all",
+               AKKA_FAULT_STALL_PHASE="preflight", AKKA_FAULT_STALL_MODE="raise")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+                        "--gpus", "2", "--steps", "3", "--warmup", "1", "--size-mb", "16", "--data-plane", "ipc_p2p",
+                        "--extras", "off", "--link-probe", "off"], capture_output=True, text=True, timeout=300,
+                       cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip().startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert set(d["preflight_fallback"]["errors"]) == {"0", "1"}, d
+    assert d["preflight"] == "passed on the ipc lane"
+    assert d["lane"].startswith("ipc") and d["lane_is_framework"] is True
+    assert all(k.startswith("ipc") for k in d["lane_select"] if k != "chosen"), d["lane_select"]
+    assert d["exact"] is True and d["value"] > 0 and d["rccl_allreduce_algbw_GBps"] is None
