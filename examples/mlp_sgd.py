@@ -40,6 +40,8 @@ def main() -> int:
                    help="GEMM dtype (bfloat16: autocast onto bf16 MFMA; weights/grads/allreduce stay fp32)")
     p.add_argument("--transport", choices=["stream", "reactive"], default="stream",
                    help="reactive: straggler-tolerant data path (pair with thresholds < 1)")
+    p.add_argument("--graph", action="store_true",
+                   help="replay forward + backward from one HIP graph (GraphedDPStep; GPU, stream transport)")
     p.add_argument("--straggler-ms", type=float, default=0.0,
                    help="the last rank sleeps this long before every step (BASELINE config 4)")
     a = p.parse_args()
@@ -57,7 +59,7 @@ def main() -> int:
     if world > 1:
         dist.init_process_group("gloo", rank=rank, world_size=world)
 
-    from akka_allreduce_amd.models.mlp import MLP, dp_sgd_step, synthetic_batch
+    from akka_allreduce_amd.models.mlp import MLP, GraphedDPStep, dp_sgd_step, synthetic_batch
     from akka_allreduce_amd.parallel import ThresholdAllreduce
     from akka_allreduce_amd.parallel.dp import GradientBucket
 
@@ -70,6 +72,17 @@ def main() -> int:
     gen = torch.Generator(device=dev).manual_seed(1000 + rank)
     x, y = synthetic_batch(a.batch, a.d_in, a.classes, device=dev, generator=gen)
     cdt = getattr(torch, a.compute_dtype)
+    if a.graph and not a.cpu:
+        # the batch lives in the graph's static buffers; a data loader would
+        # write each new batch there before the step
+        graphed = GraphedDPStep(model, bucket, x, y, compute_dtype=cdt)
+        x, y = graphed.static_inputs()
+
+        def step():
+            return graphed(x, y, a.lr, ar)
+    else:
+        def step():
+            return dp_sgd_step(model, x, y, a.lr, ar, bucket, sync_loss=False, compute_dtype=cdt)
 
     def sync():
         ar.drain()  # reactive: finish transfers slower peers still need before a blocking collective
@@ -80,13 +93,13 @@ def main() -> int:
 
     losses = []
     for _ in range(a.warmup):
-        losses.append(dp_sgd_step(model, x, y, a.lr, ar, bucket, sync_loss=False, compute_dtype=cdt))
+        losses.append(step().clone())
     sync()
     t0 = time.perf_counter()
     for _ in range(a.steps):
         if nap:
             time.sleep(nap)
-        losses.append(dp_sgd_step(model, x, y, a.lr, ar, bucket, sync_loss=False, compute_dtype=cdt))
+        losses.append(step().clone())
     if dev.type == "cuda":
         torch.cuda.synchronize()
     own = time.perf_counter() - t0  # this rank's own time (fast ranks vs the straggler)
@@ -109,6 +122,7 @@ def main() -> int:
             "loss_last": round(float(losses[-1]), 4),
             "fast_ranks_steps_per_s": round(a.steps / max(owns[:-1] if world > 1 else owns), 3),
             "transport": a.transport, "straggler_ms": a.straggler_ms, "compute_dtype": a.compute_dtype,
+            "graph": bool(a.graph and not a.cpu),
             "config": {"d_in": a.d_in, "hidden": a.hidden, "classes": a.classes, "batch_per_rank": a.batch},
         }), flush=True)
     if world > 1:
