@@ -68,6 +68,38 @@ class _LinearIntoBucket(torch.autograd.Function):
         return gx, None, None, None, None, None, None
 
 
+class _LinearReluIntoBucket(torch.autograd.Function):
+    """``relu(x @ w.T + b)`` under bf16 autocast on the GPU, gradients into the
+    bucket like ``_LinearIntoBucket``.  Forward: bias and ReLU in the GEMM's
+    epilogue (``torch._addmm_activation``: hipBLASLt's RELU_BIAS epilogue), no
+    separate activation kernel.  Backward: the ReLU mask, the masked dY and
+    the bias gradient in ONE pass (``colsum(relu_of=...)``, gfx950), then the
+    dW GEMM on the masked dY."""
+
+    @staticmethod
+    def forward(ctx, x, w, b, gw, gb, ws, bs):
+        dt = torch.get_autocast_dtype(x.device.type)
+        with torch.autocast(device_type=x.device.type, enabled=False):
+            xc = x.to(dt)
+            wc = ws if ws is not None else w.to(dt)
+            bc = bs if bs is not None else b.to(dt)
+            x2 = xc.reshape(-1, xc.shape[-1])
+            h = torch._addmm_activation(bc, x2, wc.t(), use_gelu=False)
+        ctx.save_for_backward(x2, wc, h)
+        ctx.gw, ctx.gb, ctx.xshape = gw, gb, xc.shape
+        return h.reshape(*xc.shape[:-1], wc.shape[0])
+
+    @staticmethod
+    def backward(ctx, go):
+        x2, wc, h = ctx.saved_tensors
+        go2 = go.reshape(-1, go.shape[-1]).to(wc.dtype).contiguous()
+        g = torch.empty_like(go2)
+        colsum(go2, out=ctx.gb.view(-1), relu_of=h, masked_out=g)  # ReLU backward + db fused
+        _mm_into(g.t(), x2, ctx.gw)
+        gx = (g @ wc).reshape(ctx.xshape) if ctx.needs_input_grad[0] else None
+        return gx, None, None, None, None, None, None
+
+
 class MLP(nn.Module):
     def __init__(self, d_in: int, d_hidden: int, d_out: int):
         super().__init__()
@@ -87,8 +119,18 @@ class MLP(nn.Module):
             return _LinearIntoBucket.apply(x, fc.weight, fc.bias, fc.weight.grad, fc.bias.grad, ws, bs)
         return fc(x)
 
+    def _linear_relu(self, fc: nn.Linear, x: torch.Tensor) -> torch.Tensor:
+        if (self.direct_grads and torch.is_grad_enabled() and x.is_cuda and torch.is_autocast_enabled("cuda")
+                and torch.get_autocast_dtype("cuda") == torch.bfloat16 and fc.bias is not None
+                and fc.bias.grad is not None and fc.bias.grad.is_contiguous()):
+            sb = self.shadow_bucket
+            ws = sb.shadow_of(fc.weight) if sb is not None else None
+            bs = sb.shadow_of(fc.bias) if sb is not None else None
+            return _LinearReluIntoBucket.apply(x, fc.weight, fc.bias, fc.weight.grad, fc.bias.grad, ws, bs)
+        return F.relu(self._linear(fc, x))
+
     def forward(self, x: torch.Tensor) -> torch.Tensor:
-        return self._linear(self.fc2, F.relu(self._linear(self.fc1, x)))
+        return self._linear(self.fc2, self._linear_relu(self.fc1, x))
 
 
 def dp_sgd_step(model: nn.Module, x: torch.Tensor, y: torch.Tensor, lr: float,

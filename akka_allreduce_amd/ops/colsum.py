@@ -24,11 +24,14 @@ _TILE = 512
 
 
 def colsum(x: torch.Tensor, out: Optional[torch.Tensor] = None, splits: Optional[int] = None,
-           lite: bool = True) -> torch.Tensor:
+           lite: bool = True, relu_of: Optional[torch.Tensor] = None,
+           masked_out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """``out[c] = sum_r x[r, c]`` for a 2-D bf16 ``x``, fp32 result.
     ``splits`` (1..16) overrides the row split per column tile; ``lite=False``
     hands the partial rows over with fences instead of write-through stores
-    (both are measurement knobs)."""
+    (both are measurement knobs).  With ``relu_of`` (the ReLU's output, same
+    shape) the ReLU backward is fused in: ``masked_out = x * (relu_of > 0)``
+    is written and ``out`` sums it."""
     if x.dim() != 2:
         raise ValueError("colsum expects a 2-D tensor")
     M, ncol = x.shape
@@ -36,12 +39,22 @@ def colsum(x: torch.Tensor, out: Optional[torch.Tensor] = None, splits: Optional
         out = torch.empty(ncol, dtype=torch.float32, device=x.device)
     if out.dtype != torch.float32 or out.numel() != ncol or not out.is_contiguous():
         raise ValueError("colsum: out must be a contiguous fp32 tensor of x.shape[1] elements")
+    if (relu_of is None) != (masked_out is None):
+        raise ValueError("colsum: relu_of and masked_out go together")
+    if relu_of is not None and (relu_of.shape != x.shape or masked_out.shape != x.shape
+                                or masked_out.dtype != x.dtype or not masked_out.is_contiguous()):
+        raise ValueError("colsum: relu_of / masked_out must match x (masked_out contiguous)")
     if x.device.type != "cuda" or x.dtype != torch.bfloat16:
+        if relu_of is not None:
+            torch.where(relu_of > 0, x, torch.zeros_like(x), out=masked_out)
+            x = masked_out
         torch.sum(x, 0, dtype=torch.float32, out=out)
         return out
     if M == 0:
         return out.zero_()
     x = x.contiguous()
+    if relu_of is not None:
+        relu_of = relu_of.contiguous()
     n = _load()
     splits = int(splits or n.colsum_row_splits(M, ncol))
     stream = torch.cuda.current_stream(x.device)
@@ -54,5 +67,6 @@ def colsum(x: torch.Tensor, out: Optional[torch.Tensor] = None, splits: Optional
               torch.zeros((ncol + _TILE - 1) // _TILE, dtype=torch.int32, device=x.device))
         _WS[key] = ws
     n.colsum_bf16(out.data_ptr(), x.data_ptr(), M, ncol, ws[0].data_ptr(), ws[1].data_ptr(), splits,
-                  stream.cuda_stream, bool(lite))
+                  stream.cuda_stream, bool(lite), relu_of.data_ptr() if relu_of is not None else 0,
+                  masked_out.data_ptr() if masked_out is not None else 0)
     return out

@@ -882,11 +882,12 @@ PYBIND11_MODULE(_native, m) {
      py::arg("kmax"), py::arg("dtype"), py::arg("stream"), py::arg("axpy") = false, py::arg("alpha") = 0.f,
      py::arg("shadow") = 0);
   m.def("colsum_bf16", [](uintptr_t out, uintptr_t in, int64_t M, int64_t ncol, uintptr_t part, uintptr_t tickets,
-                          int32_t splits, uintptr_t stream, bool lite) {
+                          int32_t splits, uintptr_t stream, bool lite, uintptr_t act, uintptr_t gout) {
     launch_colsum_bf16(as_stream(stream), reinterpret_cast<float*>(out), reinterpret_cast<const void*>(in), M, ncol,
-                       reinterpret_cast<float*>(part), reinterpret_cast<uint32_t*>(tickets), splits, lite);
+                       reinterpret_cast<float*>(part), reinterpret_cast<uint32_t*>(tickets), splits, lite,
+                       reinterpret_cast<const void*>(act), reinterpret_cast<void*>(gout));
   }, py::arg("out"), py::arg("in"), py::arg("M"), py::arg("ncol"), py::arg("part"), py::arg("tickets"),
-     py::arg("splits"), py::arg("stream"), py::arg("lite") = true);
+     py::arg("splits"), py::arg("stream"), py::arg("lite") = true, py::arg("act") = 0, py::arg("gout") = 0);
   m.def("colsum_row_splits", &colsum_row_splits);
   m.def("xent_fwd", [](uintptr_t x, uintptr_t y, int64_t B, int64_t C, uintptr_t lse, uintptr_t rowloss, uintptr_t out,
                        uintptr_t ticket, uintptr_t stream) {

@@ -31,8 +31,11 @@ void launch_count_mean(hipStream_t s, void* dst, const void* src, const int32_t*
 // out[c] = sum_r in[r, c] (bf16 [M, ncol] row-major, fp32 out): the bias
 // gradient.  part: fp32 [splits, ncol] workspace; tickets: uint32
 // [ceil(ncol / 512)] zeroed once (each launch leaves them zero again).
+// act / gout (both or neither, bf16 [M, ncol]): ReLU backward fused in --
+// gout = in where act > 0 else 0, and out sums gout.
 void launch_colsum_bf16(hipStream_t s, float* out, const void* in, int64_t M, int64_t ncol, float* part,
-                        uint32_t* tickets, int32_t splits, bool lite = true);
+                        uint32_t* tickets, int32_t splits, bool lite = true, const void* act = nullptr,
+                        void* gout = nullptr);
 int32_t colsum_row_splits(int64_t M, int64_t ncol);
 // Cross entropy over bf16 logits [B, C] with int64 labels (mean over the rows
 // whose label is in [0, C)).  Forward: lse [B] fp32, rowloss [2B] fp32

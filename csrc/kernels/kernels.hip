@@ -391,11 +391,28 @@ constexpr int kCsCols = 64 * 8;  // columns per workgroup (one wave's width)
 constexpr int kCsRows = 8;       // rows per lane in flight
 constexpr int kCsMaxSplits = 16;
 
-template <bool LITE>
+// RELU: the ReLU backward rides along -- the summed value is in[r, c] where
+// act[r, c] > 0, else 0, and it is also written to gout (bf16, same layout):
+// dY of the layer below the activation and its bias gradient in one pass.
+__device__ __forceinline__ v4u relu_mask_bf16x8(const v4u& g, const v4u& h) {
+  v4u o;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint32_t gw = g[k], hw = h[k];
+    // bf16 > 0: sign bit clear and not +0 (NaN passes through as > 0 is false for NaN in fp32 too)
+    const bool lo = __uint_as_float(hw << 16) > 0.f, hi = __uint_as_float(hw & 0xffff0000u) > 0.f;
+    o[k] = (lo ? (gw & 0xffffu) : 0u) | (hi ? (gw & 0xffff0000u) : 0u);
+  }
+  return o;
+}
+
+template <bool LITE, bool RELU>
 __global__ __launch_bounds__(kBlock) void colsum_bf16_kernel(float* __restrict__ out,
                                                              const unsigned short* __restrict__ in, int64_t M,
                                                              int64_t ncol, float* __restrict__ part,
-                                                             uint32_t* __restrict__ tickets, int32_t vec) {
+                                                             uint32_t* __restrict__ tickets, int32_t vec,
+                                                             const unsigned short* __restrict__ act,
+                                                             unsigned short* __restrict__ gout) {
   __shared__ float red[kBlock / 64][kCsCols + kCsCols / 8];
   __shared__ uint32_t last;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -413,15 +430,39 @@ __global__ __launch_bounds__(kBlock) void colsum_bf16_kernel(float* __restrict__
       v4u v[kCsRows];
 #pragma unroll
       for (int u = 0; u < kCsRows; ++u) v[u] = *reinterpret_cast<const v4u*>(in + (r + 4 * u) * ncol + c0);
+      if constexpr (RELU) {
+        v4u h[kCsRows];
+#pragma unroll
+        for (int u = 0; u < kCsRows; ++u) h[u] = *reinterpret_cast<const v4u*>(act + (r + 4 * u) * ncol + c0);
+#pragma unroll
+        for (int u = 0; u < kCsRows; ++u) {
+          v[u] = relu_mask_bf16x8(v[u], h[u]);
+          *reinterpret_cast<v4u*>(gout + (r + 4 * u) * ncol + c0) = v[u];
+        }
+      }
 #pragma unroll
       for (int u = 0; u < kCsRows; ++u) add_vec(acc, v[u], (unsigned short)0);
     }
-    for (; r < r1; r += 4) add_vec(acc, *reinterpret_cast<const v4u*>(in + r * ncol + c0), (unsigned short)0);
+    for (; r < r1; r += 4) {
+      v4u v = *reinterpret_cast<const v4u*>(in + r * ncol + c0);
+      if constexpr (RELU) {
+        v = relu_mask_bf16x8(v, *reinterpret_cast<const v4u*>(act + r * ncol + c0));
+        *reinterpret_cast<v4u*>(gout + r * ncol + c0) = v;
+      }
+      add_vec(acc, v, (unsigned short)0);
+    }
   } else {
     for (int64_t r = r0 + wave; r < r1; r += 4)
 #pragma unroll
       for (int q = 0; q < 8; ++q)
-        if (c0 + q < ncol) acc[q] += to_f(in[r * ncol + c0 + q]);
+        if (c0 + q < ncol) {
+          float g = to_f(in[r * ncol + c0 + q]);
+          if constexpr (RELU) {
+            if (!(to_f(act[r * ncol + c0 + q]) > 0.f)) g = 0.f;
+            gout[r * ncol + c0 + q] = from_f<unsigned short>(g);
+          }
+          acc[q] += g;
+        }
   }
   // the workgroup's 4 waves -> one partial row (acc[q] is column c0 + q),
   // staged with one pad word per lane (slot lane * 9 + q): a wave's stores of
@@ -821,20 +862,35 @@ int32_t colsum_row_splits(int64_t M, int64_t ncol) {
 }
 
 void launch_colsum_bf16(hipStream_t s, float* out, const void* in, int64_t M, int64_t ncol, float* part,
-                        uint32_t* tickets, int32_t splits, bool lite) {
+                        uint32_t* tickets, int32_t splits, bool lite, const void* act, void* gout) {
   if (ncol <= 0) return;
   AKKA_CHECK(M > 0 && splits >= 1 && splits <= kCsMaxSplits, "colsum: bad shape or row splits (1..16)");
   const int64_t tiles = (ncol + kCsCols - 1) / kCsCols;
   AKKA_CHECK(tiles < (int64_t(1) << 31), "colsum: too many columns");
   // the partial rows are addressed through one buffer resource (32-bit offsets)
   AKKA_CHECK(int64_t(splits) * ncol * 4 < (int64_t(1) << 31), "colsum: partial rows exceed 2 GiB");
-  const int vec = ((reinterpret_cast<uintptr_t>(in) & 15) == 0 && ncol % 8 == 0) ? 1 : 0;
-  if (lite)
-    hipLaunchKernelGGL(colsum_bf16_kernel<true>, dim3(uint32_t(tiles), uint32_t(splits)), dim3(kBlock), 0, s, out,
-                       static_cast<const unsigned short*>(in), M, ncol, part, tickets, vec);
-  else
-    hipLaunchKernelGGL(colsum_bf16_kernel<false>, dim3(uint32_t(tiles), uint32_t(splits)), dim3(kBlock), 0, s, out,
-                       static_cast<const unsigned short*>(in), M, ncol, part, tickets, vec);
+  AKKA_CHECK((act == nullptr) == (gout == nullptr), "colsum: the ReLU mask needs both act and gout");
+  const bool relu = act != nullptr;
+  const int vec = ((reinterpret_cast<uintptr_t>(in) | (relu ? reinterpret_cast<uintptr_t>(act) |
+                                                                   reinterpret_cast<uintptr_t>(gout)
+                                                             : uintptr_t(0))) &
+                   15) == 0 && ncol % 8 == 0
+                      ? 1
+                      : 0;
+  const auto* a16 = static_cast<const unsigned short*>(act);
+  auto* g16 = static_cast<unsigned short*>(gout);
+  const dim3 grid{uint32_t(tiles), uint32_t(splits), 1u};
+#define AKKA_CS(L, R)                                                                                         \
+  hipLaunchKernelGGL((colsum_bf16_kernel<L, R>), grid, dim3(kBlock), 0, s, out, static_cast<const unsigned short*>(in), \
+                     M, ncol, part, tickets, vec, a16, g16)
+  if (lite) {
+    if (relu) AKKA_CS(true, true);
+    else AKKA_CS(true, false);
+  } else {
+    if (relu) AKKA_CS(false, true);
+    else AKKA_CS(false, false);
+  }
+#undef AKKA_CS
   check_launch("colsum_bf16");
 }
 

@@ -1,0 +1,15 @@
+#!/bin/bash
+# Round-3 GPU pass AD: fc1 as linear + ReLU in one autograd node (bias + ReLU
+# in the GEMM epilogue, ReLU backward fused into the bias-gradient column sum):
+# tests, config-5 step A/B on one box, kernel stats.
+set -o pipefail
+mkdir -p gpurun_out/r03ad
+R=$(pwd)
+timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_fused_step_gpu.py \
+  tests/test_collective_gpu.py > gpurun_out/r03ad/pytest.log 2>&1 &&
+for i in 1 2; do
+  timeout -k 10 120 python -u bench/cfg5_step.py --dtype bf16 --graph --steps 500 --warmup 50 >> gpurun_out/r03ad/cfg5.jsonl 2>/dev/null || exit 1
+done
+(cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
+  -d $R/gpurun_out/r03ad/cfg5_trace -o run -- python3 $R/bench/cfg5_step.py --dtype bf16 --graph --steps 30 \
+  > $R/gpurun_out/r03ad/cfg5_trace.log 2>&1)

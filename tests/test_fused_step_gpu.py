@@ -150,3 +150,21 @@ def test_graphed_step_matches_eager(cdt):
         assert abs(a - b) <= 1e-5 * abs(a) + 1e-6, (runs[0][0], runs[1][0])
     for a, b in zip(runs[0][1], runs[1][1]):
         torch.testing.assert_close(a, b, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("M,ncol,off", [(256, 8192, 0), (37, 1003, 0), (64, 520, 3)])
+def test_colsum_fused_relu_backward_matches_torch(M, ncol, off):
+    """colsum(relu_of=h): the ReLU backward (dY where h > 0, else 0) written
+    bitwise like torch's threshold_backward, and its column sums."""
+    from akka_allreduce_amd.ops import colsum
+
+    g = torch.Generator(device="cuda").manual_seed(M + ncol)
+    base = torch.randn(M * ncol + off, device="cuda", generator=g).to(torch.bfloat16)
+    dy = base[off:].view(M, ncol)
+    h = torch.relu(torch.randn(M, ncol, device="cuda", generator=g)).to(torch.bfloat16)
+    masked = torch.empty(M, ncol, device="cuda", dtype=torch.bfloat16)
+    got = colsum(dy, relu_of=h, masked_out=masked)
+    want_masked = torch.ops.aten.threshold_backward(dy, h, 0)
+    torch.cuda.synchronize()
+    assert torch.equal(masked, want_masked)
+    torch.testing.assert_close(got, want_masked.float().sum(0), rtol=1e-5, atol=1e-4 * max(1.0, M ** 0.5))
