@@ -221,8 +221,13 @@ class GraphedDPStep:
         self.lowp = compute_dtype if (shadow_weights and compute_dtype is not None
                                       and compute_dtype != torch.float32) else None
         # the static batch: write the next batch into these (static_inputs())
-        # and the replay reads it in place, no copy
-        self.sx = x.detach().clone()
+        # and the replay reads it in place, no copy.  With bf16 GEMMs the
+        # input buffer is bf16 -- the first GEMM reads bf16(x) either way --
+        # so a batch is converted once as it is written (what a loader that
+        # emits bf16 does), not again inside every replay
+        lowx = compute_dtype if (compute_dtype is not None and compute_dtype != torch.float32
+                                 and x.is_floating_point() and x.dtype == torch.float32) else None
+        self.sx = x.detach().to(lowx) if lowx is not None else x.detach().clone()
         self.sy = y.detach().clone()
         self._seed = torch.ones((), dtype=torch.float32, device=x.device)
         self._ptrs = self._pointers()
