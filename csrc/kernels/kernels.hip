@@ -626,7 +626,7 @@ void launch_vec_pol(hipStream_t s, const SrcTable& t, v4u* dst, int64_t nvec, in
   // kBoth (big streams): 2 vectors per lane per source, but 4 for the
   // one-source pass (1 GiB bf16: 5.69 vs 5.53 TB/s at 2 blocks/CU, pass V)
   constexpr int UNROLL = POL == kBoth ? (NSRC == 1 ? 4 : (U0 < 2 ? U0 : 2)) : U0;
-  if constexpr ((NSRC == 8 && POL == kNts && std::is_same<T, float>::value) || (NSRC == 1 && POL == kBoth)) {
+  if constexpr ((NSRC == 8 && POL == kNts && std::is_same<T, float>::value) || (NSRC == 1 && POL != kNtl)) {
     // experiments (bench/reduce_kernel_bw.py, bench/n1_bigcopy.py sweeps): loads in flight per lane
     static const int u = [] {
       const char* v = std::getenv("AKKA_VEC_UNROLL");
@@ -764,12 +764,14 @@ void launch_reduce(hipStream_t s, const ReduceSpec& spec, DType dt, ReduceImpl i
     impl = (rbytes + wbytes <= (int64_t(96) << 20) && sp.nsrc <= 8) ? ReduceImpl::Lds : ReduceImpl::Vec;
   }
   // Vec load/store policy and grid (bench/stream_variants.hip sweep):
-  //   sources fit the Infinity Cache      -> plain loads, NT stores, 16 blocks/CU
+  //   sources fit the Infinity Cache      -> plain loads, NT stores, 16 blocks/CU (64 for one source)
   //   big stream with a big output        -> NT loads + NT stores, unroll 2 (4 for one source), 2 blocks/CU
   //   otherwise (many sources, <=256 MiB) -> NT loads, plain stores, 4 blocks/CU
   int pol = kNtl, bpc = 4;
   if (impl == ReduceImpl::Vec) {
-    if (rbytes <= (int64_t(256) << 20)) pol = kNts, bpc = 16;
+    // one source (the N=1 round): a grid that covers the whole stream in one
+    // pass, 76 vs 80-82 us per 256 MiB fp32 (profiles/r03/pass_ai)
+    if (rbytes <= (int64_t(256) << 20)) pol = kNts, bpc = sp.nsrc == 1 ? 64 : 16;
     else if (wbytes >= (int64_t(512) << 20)) pol = kBoth, bpc = 2;  // 1 GiB bf16: 5.56 vs 5.11 TB/s at 4 (profiles/r03/pass_u, pass_v)
     else pol = kNtl, bpc = 4;
   } else if (impl == ReduceImpl::VecNts) {
