@@ -920,8 +920,13 @@ void launch_count_mean(hipStream_t s, void* dst, const void* src, const int32_t*
   AKKA_CHECK(shadow == nullptr || (axpy && dt == DType::F32 && (reinterpret_cast<uintptr_t>(shadow) & 15) == 0),
              "count_mean: a bf16 shadow needs the fp32 SGD update and a 16-B aligned buffer");
   const int64_t regions = int64_t(N) * kmax;
-  int grid = int(regions < kMaxGrid ? regions : kMaxGrid);
-  int split = int(kMaxGrid / grid);
+  // workgroups over the whole pass (AKKA_CM_MAXGRID: measurement knob)
+  static const int64_t max_grid = [] {
+    const char* v = std::getenv("AKKA_CM_MAXGRID");
+    return v && std::atoll(v) > 0 ? int64_t(std::atoll(v)) : int64_t(kMaxGrid);
+  }();
+  int grid = int(regions < max_grid ? regions : max_grid);
+  int split = int(max_grid / grid);
   const int64_t per_region_vecs = (S / regions) / 4 + 1;
   const int64_t useful = (per_region_vecs + kBlock - 1) / kBlock;
   if (split > useful) split = int(useful);
