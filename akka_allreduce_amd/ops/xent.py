@@ -6,8 +6,11 @@ a downcast of the gradient: six small launches, ~40 µs per step on MI355X
 (``profiles/r03/pass_n/cfg5_bf16_kernel_stats.csv``).  ``xent_fwd_kernel``
 computes every row's log-sum-exp and loss in one launch (the mean over rows
 combined by the last workgroup), ``xent_bwd_kernel`` writes the bf16
-gradient ``(softmax - onehot) * go / n_valid`` in one more.  Labels outside
-``[0, C)`` are ignored like torch's ``ignore_index`` (mean over the rest).
+gradient ``(softmax - onehot) * go / n_valid`` in one more.  Label -100 is
+ignored like torch's default ``ignore_index`` (mean over the rest); any other
+label outside ``[0, C)`` -- an error in torch -- makes the loss NaN and is
+counted on the device (``last_bad_labels()``; ``AKKA_CHECK_LABELS=1`` raises
+at once, at the cost of a host synchronisation per call).
 
 CUDA bf16 inputs always go to the native kernels (a missing extension
 raises); anything else uses ``F.cross_entropy``, which is also the
@@ -15,6 +18,7 @@ numerics reference of the GPU test.
 """
 from __future__ import annotations
 
+import os
 from typing import Dict, Tuple
 
 import torch
@@ -23,6 +27,15 @@ import torch.nn.functional as F
 from .._native_loader import load as _load
 
 _TICKETS: Dict[Tuple[int, int], torch.Tensor] = {}
+_CHECK_LABELS = os.environ.get("AKKA_CHECK_LABELS") == "1"
+_LAST: Dict[int, torch.Tensor] = {}
+
+
+def last_bad_labels() -> int:
+    """Targets outside ``[0, C)`` (other than -100) in the last fused call
+    (synchronises); 0 before any fused call."""
+    out = _LAST.get(0)
+    return int(out[2].item()) if out is not None else 0
 
 
 def _ticket(dev: torch.device, stream: int) -> torch.Tensor:
@@ -43,10 +56,14 @@ class _FusedXent(torch.autograd.Function):
         stream = torch.cuda.current_stream(x.device).cuda_stream
         lse = torch.empty(B, dtype=torch.float32, device=x.device)
         rowloss = torch.empty(2 * B, dtype=torch.float32, device=x.device)
-        out = torch.empty(2, dtype=torch.float32, device=x.device)
+        out = torch.empty(3, dtype=torch.float32, device=x.device)  # [loss, n_valid, n_bad_labels]
         _load().xent_fwd(x.data_ptr(), y.data_ptr(), B, C, lse.data_ptr(), rowloss.data_ptr(), out.data_ptr(),
                          _ticket(x.device, stream).data_ptr(), stream)
         ctx.save_for_backward(x, y, lse, out)
+        if _CHECK_LABELS and float(out[2].item()) > 0:
+            raise ValueError(f"cross_entropy: {int(out[2].item())} target(s) outside [0, {C}) "
+                             "(only -100 is ignored)")
+        _LAST[0] = out  # last_bad_labels()
         return out[0]
 
     @staticmethod

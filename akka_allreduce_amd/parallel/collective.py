@@ -234,6 +234,9 @@ class ThresholdAllreduce:
             # ride on another engine's transport: one communicator (and one set
             # of device streams) for every engine of the job, e.g. one per DDP
             # bucket size (WorkerCore.adopt_transport)
+            if transport != "stream":
+                raise ValueError("share_transport_with: only the scheduled (stream) transport can be shared "
+                                 "(reactive links issue groups in a timing-dependent order)")
             if (share.transport != transport or share.device != self.device or share.world_size != self.world_size
                     or share.rank != self.rank or getattr(share, "data_plane", data_plane) != data_plane):
                 raise ValueError("share_transport_with: the engines differ in transport, device, rank or data plane")
@@ -260,7 +263,12 @@ class ThresholdAllreduce:
             if self.world_size == 1:
                 spec = ("local",)
             elif transport == "reactive":
-                post, test = make_async_fns()
+                # one gloo group per reactive engine: its pair transfers can
+                # outlive a call and gloo matches by (peer, tag), so another
+                # engine's transfers must never share the group (like one
+                # RCCL pair communicator set per engine on the GPU)
+                grp = dist.new_group(backend="gloo") if dist.is_initialized() else None
+                post, test = make_async_fns(grp)
                 spec = ("async_callback", post, test, self.rank, self.world_size)
             else:
                 spec = ("callback", make_group_fn(), self.rank, self.world_size)
@@ -431,9 +439,9 @@ class ThresholdAllreduce:
 
         Every candidate runs three exact rounds with different integer data (the
         last after `rounds` timed rounds of other data, so a stale read shows)
-        and the timed rounds.  Only rounds run inside a try -- no host-group
-        collective -- so a rank whose rounds raise still meets the others at the
-        one agreement per candidate (max over ranks of time and failure).  The
+        and the timed rounds.  Each step runs inside a try and is agreed on
+        (max over ranks of failure and time) before the next: a step that
+        fails on any rank ends the candidate on every rank.  The
         one-sided lanes join when every rank could map every other rank's
         window.  Leaves the object on the winner; returns every candidate's
         result and the choice.  Needs thresholds 1 (exact rounds)."""
@@ -482,29 +490,41 @@ class ThresholdAllreduce:
             want = float((salt + 1) * N * (N + 1) // 2)
             return bool(torch.all(o.data == want).item()) and bool(torch.all(o.count == N).item())
 
-        for name in cands:
-            ok, ms, err = False, 0.0, None
-            try:
-                self.use_lane(name)
-                # every rank runs the same rounds whatever its local verdicts:
-                # a rank that skipped rounds would leave its peers waiting
-                e1 = exact(1)
-                e2 = exact(2)
+        def timed_block() -> float:
+            o = self(x, async_op=cuda, out=buf)
+            o.wait()
+            sync()
+            t0 = time.perf_counter()
+            for _ in range(rounds):  # the ranks are coupled by the rounds themselves
                 o = self(x, async_op=cuda, out=buf)
-                o.wait()
-                sync()
-                t0 = time.perf_counter()
-                for _ in range(rounds):  # the ranks are coupled by the rounds themselves
-                    o = self(x, async_op=cuda, out=buf)
-                o.wait()
-                sync()
-                ms = (time.perf_counter() - t0) / rounds * 1e3
-                ok = e1 and e2 and exact(3)
-            except Exception as e:  # noqa: BLE001 - the candidate is rejected
-                ok, err = False, f"{type(e).__name__}: {e}"[:160]
-            bad, worst = self._agree_max([0.0 if ok else 1.0, ms])
-            good = bad == 0.0
-            res[name] = {"exact": good, "ms": round(worst, 4) if good else None}
+            o.wait()
+            sync()
+            return (time.perf_counter() - t0) / rounds * 1e3
+
+        for name in cands:
+            ok, ms, err = True, 0.0, None
+            # Every step is agreed on before the next one runs: a step that
+            # raised on one rank only ends the candidate on EVERY rank, so no
+            # rank issues rounds its peers will never match (p2p lanes).
+            steps = [("lane", lambda: (self.use_lane(name), True)[1]), ("exact1", lambda: exact(1)),
+                     ("exact2", lambda: exact(2)), ("timed", timed_block), ("exact3", lambda: exact(3))]
+            for tag, step in steps:
+                val = 0.0
+                try:
+                    v = step()
+                    if tag == "timed":
+                        val = float(v)
+                    elif not v:
+                        ok = False
+                except Exception as e:  # noqa: BLE001 - the candidate is rejected
+                    ok, err = False, f"{tag}: {type(e).__name__}: {e}"[:160]
+                bad, worst = self._agree_max([0.0 if ok else 1.0, val])
+                if tag == "timed":
+                    ms = worst
+                if bad != 0.0:
+                    ok = False
+                    break
+            res[name] = {"exact": ok, "ms": round(ms, 4) if ok else None}
             if err:
                 res[name]["error"] = err
         good = [n for n in cands if res[n]["exact"]]

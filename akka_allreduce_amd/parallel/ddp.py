@@ -36,13 +36,17 @@ class ThresholdHookState:
     lane once and keeps the fastest; later engines take the same lane
     (ThresholdAllreduce.tune).
 
-    One transport per hook: the engines of the different bucket sizes share
-    the first engine's device streams and communicator
+    One transport per hook (scheduled ``stream`` transport): the engines of
+    the different bucket sizes share the first engine's device streams and
+    communicator
     (``share_transport_with``), so a job holds ONE RCCL communicator however
     many bucket shapes DDP produces, and every bucket's round is ordered on the
     same streams in the bucket order every rank sees.  With the ipc data plane
     the engines also share the first engine's window memory when it is large
-    enough (``ipc_capacity``: the window is sized for ``bucket_cap_mb``)."""
+    enough (``ipc_capacity``: the window is sized for ``bucket_cap_mb``).
+    Reactive engines keep one transport each (their phase-2 groups are issued
+    in a timing-dependent order, which two engines must not interleave on one
+    pair communicator)."""
 
     def __init__(self, *, th_reduce: float = 1.0, th_complete: float = 1.0, max_lag: int = 2,
                  max_chunk_size: int = 1 << 20, transport: str = "stream", broadcast_lag: int = 2,
@@ -66,7 +70,11 @@ class ThresholdHookState:
         if ar is None:
             first = self.first.get((t.dtype, t.device))
             cap = max(t.numel(), self.bucket_cap_bytes // t.element_size())
-            ar = ThresholdAllreduce(t.numel(), dtype=t.dtype, device=t.device, share_transport_with=first,
+            # one transport per hook only for the scheduled link: reactive
+            # engines drive their pair communicators from per-peer streams in
+            # a timing-dependent order, so each keeps its own
+            share = first if self.kw["transport"] == "stream" else None
+            ar = ThresholdAllreduce(t.numel(), dtype=t.dtype, device=t.device, share_transport_with=share,
                                     ipc_capacity=cap, **self.kw)
             if first is None:
                 self.first[(t.dtype, t.device)] = ar

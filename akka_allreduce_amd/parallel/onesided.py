@@ -46,13 +46,13 @@ _DTYPES = {torch.float32: "float32", torch.bfloat16: "bfloat16"}
 class OneSidedOutput(AllReduceOutput):
     """AllReduceOutput whose ``iteration`` (the round served) and ``status``
     come from the lane's per-call record; on the GPU reading them waits for
-    the call's kernels."""
+    the call's kernels (``status_nowait`` reads the record without waiting)."""
 
-    __slots__ = ("_lane", "_slot", "_stream", "_status")
+    __slots__ = ("_lane", "_call", "_stream", "_status")
 
-    def __init__(self, data, *, lane, slot, stream, **kw):
+    def __init__(self, data, *, lane, call, stream, **kw):
         self._lane = lane
-        self._slot = slot
+        self._call = call
         self._stream = stream
         self._status = None
         super().__init__(data, **kw)
@@ -66,13 +66,29 @@ class OneSidedOutput(AllReduceOutput):
         pass
 
     @property
+    def call(self) -> int:
+        """The lane's id of the call that produced this output."""
+        return self._call
+
+    def status_nowait(self) -> dict:
+        """The call's record as it is now (host memory the final kernel
+        writes): ``round`` is -1 while the call runs.  Raises if the record
+        was reused (64 or more later calls)."""
+        if self._status is not None:
+            return self._status
+        st = self._lane.status(self._call)
+        if st["round"] >= 0:
+            self._status = st
+        return st
+
+    @property
     def status(self) -> dict:
         if self._status is None:
             if self._stream is not None:
                 self._stream.synchronize()
-            st = self._lane.status(self._slot)
+            st = self._lane.status(self._call)
             if st["round"] < 0:
-                raise RuntimeError("onesided call has not finished (or its status slot was reused)")
+                raise RuntimeError("onesided call has not finished")
             self._status = st
         return self._status
 
@@ -99,6 +115,7 @@ class OneSidedAllreduce:
         part_bytes: int = 256 << 10,
         timeout_s: float = 30.0,
         threads: int = 256,
+        role_wgs: int = 0,
         data_sink: Any = None,
     ):
         if dtype not in _DTYPES:
@@ -130,7 +147,8 @@ class OneSidedAllreduce:
         self.lane = n.OneSidedLane(dev_index, self.data_size, self.world_size, int(max_chunk_size), self.rank,
                                    _DTYPES[dtype], th_reduce=float(th_reduce), th_complete=float(th_complete),
                                    max_lag=int(max_lag), rows=int(rows), part_bytes=int(part_bytes),
-                                   timeout_ms=int(timeout_s * 1000), threads=int(threads))
+                                   timeout_ms=int(timeout_s * 1000), threads=int(threads),
+                                   role_wgs=int(role_wgs))
         self.th_reduce, self.th_complete, self.max_lag = float(th_reduce), float(th_complete), int(max_lag)
         iid = OneSidedAllreduce._instances
         OneSidedAllreduce._instances += 1
@@ -142,6 +160,7 @@ class OneSidedAllreduce:
         exchange_done(b"1")
         self.lane.unlink()
         self._kmax = self.geometry.kmax
+        self._counts: Optional[torch.Tensor] = None
         self.calls = 0
 
     def __call__(self, x: torch.Tensor, out: Optional[torch.Tensor] = None, async_op: bool = False) -> OneSidedOutput:
@@ -153,16 +172,24 @@ class OneSidedAllreduce:
         if x.dtype != self.dtype or x.device != self.device:
             x = x.to(device=self.device, dtype=self.dtype)
         x = x.reshape(-1).contiguous()
+        reuse = out is not None
         if out is None:
             out = torch.empty_like(x)
         elif out.numel() != self.data_size or out.dtype != self.dtype or not out.is_contiguous():
             raise ValueError("out must be a contiguous tensor of the buffer's size and dtype")
-        counts = torch.empty((self.world_size, self._kmax), dtype=torch.int32, device=self.device)
+        if reuse:
+            # the caller manages the output's lifetime (``out`` given): the
+            # counts table is reused with it, like the output buffer itself
+            if self._counts is None:
+                self._counts = torch.empty((self.world_size, self._kmax), dtype=torch.int32, device=self.device)
+            counts = self._counts
+        else:
+            counts = torch.empty((self.world_size, self._kmax), dtype=torch.int32, device=self.device)
         stream = torch.cuda.current_stream(self.device) if self.device.type == "cuda" else None
-        slot = self.lane.round(stream.cuda_stream if stream is not None else 0, x.data_ptr(), out.data_ptr(),
+        call = self.lane.round(stream.cuda_stream if stream is not None else 0, x.data_ptr(), out.data_ptr(),
                                counts.data_ptr(), self._kmax)
         self.calls += 1
-        o = OneSidedOutput(out.view(-1), lane=self.lane, slot=slot, stream=stream, counts_per_chunk=counts,
+        o = OneSidedOutput(out.view(-1), lane=self.lane, call=call, stream=stream, counts_per_chunk=counts,
                            geometry=self.geometry, expander=self._expand if stream is not None else None)
         if self.data_sink is not None:
             self.data_sink(o)

@@ -169,6 +169,7 @@ def run_cfg4(world: int, rank: int, dev, barrier, size_mb: float, delay_ms: floa
            "rounds_per_phase": rounds, "buffer_bytes": S * esize, "chunk_bytes": C * esize, "transport": "onesided",
            "lane": ar.state()["link"]["onesided"]}
     res["lane"].pop("stats", None)
+    res.update(cfg4_threshold_needs(world, S, C, 0.75, 0.75, straggler))
 
     def sync():
         if dev.type == "cuda":
@@ -178,7 +179,7 @@ def run_cfg4(world: int, rank: int, dev, barrier, size_mb: float, delay_ms: floa
     for pi, key in enumerate(("no_straggler", "with_straggler")):
         target = (pi + 1) * rounds - 1
         st0 = ar._os.stats()
-        ms, cnt, calls = [], [], 0
+        ms, outs, calls = [], [], 0
         while last < target:
             if key == "with_straggler" and rank == straggler:
                 time.sleep(delay_ms / 1e3)
@@ -186,9 +187,14 @@ def run_cfg4(world: int, rank: int, dev, barrier, size_mb: float, delay_ms: floa
             o = ar(x, out=out)
             sync()
             ms.append((time.perf_counter() - t0) * 1e3)
-            last = o.iteration
-            cnt.append(float(o.count.float().mean()))
+            # the call's record is host memory the final kernel wrote: read
+            # without another stream synchronisation; counts are resolved
+            # after the phase (one device copy per phase, not per call)
+            last = o.status_nowait()["round"]
+            outs.append(o.counts_per_chunk.sum())
             calls += 1
+        nch = float(sum(ar._os.geometry.num_chunks(p) for p in range(world)))
+        cnt = [float(v) / max(1.0, nch) for v in torch.stack(outs).cpu().tolist()]  # mean per-chunk count
         st1 = ar._os.stats()
         tail = sorted(ms[len(ms) // 2:])
         mine = {"median_ms": statistics.median(tail), "p90_ms": tail[min(len(tail) - 1, int(0.9 * len(tail)))],
@@ -221,6 +227,27 @@ def run_cfg4(world: int, rank: int, dev, barrier, size_mb: float, delay_ms: floa
     sync()
     barrier()
     return res
+
+
+def cfg4_threshold_needs(world: int, S: int, C: int, th_reduce: float, th_complete: float, straggler: int) -> dict:
+    """What config 4's thresholds demand at this N (float32 products, like
+    the reference, SB:9 / RB:13-17).  ``straggler_block_required``: the
+    completion threshold cannot be met by the other ranks' chunks alone, so
+    every round waits for (or is forced without) the straggler's block --
+    at N=2 with 16 chunks, floor(0.75*16) = 12 > 16 - 8."""
+    import numpy as np
+
+    from akka_allreduce_amd.data import Geometry
+
+    g = Geometry(S, world, C)
+    total = sum(g.num_chunks(p) for p in range(world))
+    need_c = int(np.floor(np.float32(th_complete) * np.float32(total)))
+    need_r = int(np.floor(np.float32(th_reduce) * np.float32(world)))
+    strag = g.num_chunks(straggler)
+    return {"total_chunks": total, "need_complete_chunks": need_c, "need_reduce_copies": need_r,
+            "straggler_chunks": strag,
+            "straggler_block_required": need_c > total - strag,
+            "straggler_copy_required": need_r > world - 1}
 
 
 def run_cfg4_reactive(world: int, rank: int, dev, barrier, size_mb: float, delay_ms: float, rounds: int,
@@ -363,8 +390,11 @@ def apply_lane_choice(ar, name) -> None:
             from akka_allreduce_amd.utils.phases import progress
 
             progress(f"rank {ar.rank}: ipc lane unavailable for this buffer ({type(e).__name__}: {str(e)[:120]}); "
-                     "collective lane instead")
-            ar.use_lane("collective")
+                     "the framework's p2p lane instead")
+            # the framework's chunk-pipelined p2p schedule (gfx950 reduce), never
+            # RCCL's own reduce-scatter + all-gather: that is the comparator
+            ar.use_lane("p2p")
+            ar.lane_fallback = f"{name} -> p2p ({type(e).__name__})"
             return
     ar.use_lane(name)
 
@@ -432,6 +462,8 @@ def run_extras(world: int, dev, barrier, which=("cfg1", "cfg3", "cfg4", "cfg5"),
         ipc = link.get("ipc") or {}
         res["cfg3_bf16_1GiB_chunk8MiB"] = {"algbw_GBps": round(nbytes / (dt / steps) / 1e9, 3),
                                            "ms_per_step": round(dt / steps * 1e3, 4), "lane": link.get("lane"),
+                                           "lane_fallback": getattr(ar, "lane_fallback", None),
+                                           "lane_is_framework": link.get("lane") != "collective",
                                            "ipc_mode": {k: ipc.get(k) for k in ("mode", "fused", "lite", "max_wgs",
                                                                                 "portions", "rounds",
                                                                                 "shares_windows", "window_bytes")}
@@ -685,6 +717,7 @@ def main() -> int:
     # failure on some ranks only, or a hang, still ends the job.
     preflight_fallback = None
     ipc_only = False
+    failed_engines: list = []
     if world > 1 or args.preflight == "on":
         can_fall_back = (world > 1 and dev.type == "cuda" and ar.transport == "stream"
                          and args.data_plane != "ipc" and args.ipc == "on")
@@ -695,8 +728,15 @@ def main() -> int:
                                       "lane": "ipc_fused_lite"}
 
                 def preflight_ipc():
-                    if not ar.state().get("link", {}).get("ipc"):
-                        ar.enable_ipc()  # collective over torch.distributed (gloo)
+                    nonlocal ar
+                    # a FRESH engine on the ipc data plane (no RCCL communicator):
+                    # the failed engine's comm stream may still hold failed or
+                    # queued RCCL work and its round state is suspect, so it is
+                    # kept alive (never torn down mid-failure) but not reused
+                    failed_engines.append(ar)
+                    ar = ThresholdAllreduce(S, max_chunk_size=C, dtype=dtype, max_lag=args.max_lag,
+                                            broadcast_lag=args.bcast_lag, device=dev, data_plane="ipc",
+                                            ipc_capacity=ipc_cap)
                     ar.use_lane("ipc_fused_lite")
                     if not exact_round("preflight_ipc"):
                         raise RuntimeError("ipc preflight round is not exact")
@@ -704,6 +744,7 @@ def main() -> int:
 
                 guard.run("preflight_ipc", args.preflight_deadline_s, preflight_ipc)
                 ipc_only = True
+                args.data_plane = "ipc"
             elif pf_errors:
                 guard.fail("preflight", "error", pf_errors)
         else:

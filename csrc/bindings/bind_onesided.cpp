@@ -2,6 +2,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include "../kernels/onesided_kernels.h"
 #include "../transport/onesided.h"
 
 namespace py = pybind11;
@@ -22,7 +23,7 @@ void bind_onesided(py::module_& m) {
   py::class_<OneSidedLane>(m, "OneSidedLane")
       .def(py::init([](int32_t device, int64_t S, int32_t N, int64_t C, int32_t me, const std::string& dtype,
                        float th_reduce, float th_complete, int32_t max_lag, int32_t rows, int64_t part_bytes,
-                       int64_t timeout_ms, int32_t threads) {
+                       int64_t timeout_ms, int32_t threads, int32_t role_wgs) {
              OneSidedParams p;
              p.th_reduce = th_reduce;
              p.th_complete = th_complete;
@@ -31,12 +32,14 @@ void bind_onesided(py::module_& m) {
              p.part_bytes = part_bytes;
              p.timeout_ms = timeout_ms;
              p.threads = threads;
+             p.role_wgs = role_wgs;
              const DType dt = (dtype == "bfloat16" || dtype == "bf16") ? DType::BF16 : DType::F32;
              return std::make_unique<OneSidedLane>(device, S, N, C, me, dt, p);
            }),
            py::arg("device"), py::arg("S"), py::arg("N"), py::arg("C"), py::arg("me"), py::arg("dtype") = "float32",
            py::arg("th_reduce") = 1.f, py::arg("th_complete") = 1.f, py::arg("max_lag") = 1, py::arg("rows") = 0,
-           py::arg("part_bytes") = int64_t(256) << 10, py::arg("timeout_ms") = 30000, py::arg("threads") = 256)
+           py::arg("part_bytes") = int64_t(256) << 10, py::arg("timeout_ms") = 30000, py::arg("threads") = 256,
+           py::arg("role_wgs") = 0)
       .def("handle", [](const OneSidedLane& l) { return py::bytes(l.handle()); })
       .def("open", [](OneSidedLane& l, std::vector<std::string> handles) {
         py::gil_scoped_release nogil;
@@ -50,9 +53,10 @@ void bind_onesided(py::module_& m) {
                             reinterpret_cast<int32_t*>(counts), kcols);
            })
       .def("status",
-           [](const OneSidedLane& l, int32_t slot) {
-             const os::CallStatus c = l.status(slot);
+           [](const OneSidedLane& l, int64_t call) {
+             const os::CallStatus c = l.status(call);
              py::dict d;
+             d["call"] = call;
              d["round"] = c.round;
              d["reason"] = c.round >= 0 && c.reason >= 0 && c.reason < 6 ? kReasons[c.reason] : "pending";
              d["landed_chunks"] = c.landed_chunks;
@@ -70,6 +74,32 @@ void bind_onesided(py::module_& m) {
              for (size_t i = 0; i < sizeof(kStatNames) / sizeof(kStatNames[0]); ++i) d[kStatNames[i]] = v[i];
              return d;
            })
+      .def("begin",
+           [](OneSidedLane& l, uintptr_t in, uintptr_t out, uintptr_t counts, int32_t kcols) {
+             return l.begin(reinterpret_cast<const void*>(in), reinterpret_cast<void*>(out),
+                            reinterpret_cast<int32_t*>(counts), kcols);
+           })
+      .def("progress", &OneSidedLane::progress)
+      .def("active", &OneSidedLane::active)
+      .def("set_hold", &OneSidedLane::set_hold)
+      .def("outbox",
+           [](const OneSidedLane& l) {
+             py::list out;
+             for (const auto& e : l.outbox()) {
+               py::dict d;
+               d["phase"] = e[0] == 0 ? "scatter" : "gather";
+               d["dst"] = e[1];
+               d["chunk"] = e[2];
+               d["part"] = e[3];
+               d["round"] = e[4];
+               d["count"] = e[5];
+               out.append(d);
+             }
+             return out;
+           })
+      .def("deliver", &OneSidedLane::deliver)
+      .def("drop", &OneSidedLane::drop)
+      .def("note_replays", &OneSidedLane::note_replays)
       .def("error", &OneSidedLane::error)
       .def("clear_error", &OneSidedLane::clear_error)
       .def("set_dead", &OneSidedLane::set_dead)
@@ -87,6 +117,12 @@ void bind_onesided(py::module_& m) {
         d["memory"] = l.memory_kind();
         d["calls"] = l.calls();
         d["total_chunks"] = l.geometry().total_chunks();
+        d["threads"] = l.threads();
+        d["ranks_on_this_gpu"] = l.shared_ranks();
+        d["pieces_per_part"] = l.pieces();
+        const auto g = l.role_grid();
+        d["role_wgs"] = py::dict(py::arg("push") = g[0], py::arg("reduce") = g[1], py::arg("copy") = g[2],
+                                 py::arg("finish") = g[3]);
         return d;
       });
   m.def("onesided_layout", [](int32_t N, int32_t D, int32_t Kmax, int32_t P) {
@@ -107,10 +143,18 @@ void bind_onesided(py::module_& m) {
       for (int32_t k = 0; k < Kmax; ++k) {
         exported.push_back(L.fired(d, k));
         exported.push_back(L.sread(d, k));
-        local.push_back(L.dec(d, k));
-        local.push_back(L.dec(d, k) + 1);
       }
       exported.push_back(L.gread(d));
+    }
+    for (int32_t k = 0; k < Kmax; ++k) {
+      local.push_back(L.dec(k));
+      local.push_back(L.dec(k) + 1);
+      local.push_back(L.kctr(k));
+      local.push_back(L.odone(k));
+      for (int32_t j = 0; j < P; ++j) {
+        local.push_back(L.okq(k, j));
+        local.push_back(L.pctr(k, j));
+      }
     }
     exported.push_back(L.done());
     for (int32_t s = 0; s < N; ++s) {
@@ -128,6 +172,17 @@ void bind_onesided(py::module_& m) {
     return r;
   });
   m.def("onesided_rules", [](uint32_t t, uint32_t r) { return os::tag_state(t, r); });
+  m.def("onesided_completion_verdict", &os::completion_verdict);
+  m.def(
+      "onesided_reduce_role_bench",
+      [](int32_t N, int64_t block, int64_t chunk, int64_t part, int32_t nsub, const std::string& dtype,
+         int32_t threads, int32_t grid, int32_t iters, int32_t device) {
+        py::gil_scoped_release nogil;
+        return os::onesided_reduce_role_bench(N, block, chunk, part, nsub, dtype == "float32" ? 0 : 1, threads, grid,
+                                              iters, device);
+      },
+      py::arg("N"), py::arg("block"), py::arg("chunk"), py::arg("part"), py::arg("nsub"), py::arg("dtype") = "float32",
+      py::arg("threads") = 1024, py::arg("grid") = 256, py::arg("iters") = 10, py::arg("device") = 0);
   m.def("onesided_evaluate", &os::evaluate);
   m.def("onesided_select_round", &os::select_round);
 }

@@ -228,6 +228,12 @@ class WorkerCore final : public EngineHost {
     AKKA_CHECK(other.dev_ && other.p2p_, "adopt_transport: the other engine has no connected transport");
     AKKA_CHECK(other.link_kind_ == link_kind_ && other.device_idx_ == device_idx_ && other.deferred_ == deferred_,
                "adopt_transport: the engines differ in link kind or device");
+    // Only the scheduled link orders every engine's groups on one comm stream
+    // in the call order all ranks share.  Reactive links issue their phase-2
+    // groups from per-peer streams when chunks become ready (timing-dependent,
+    // rank-dependent order): two of them on one pair communicator could match
+    // a send of one engine with a receive of the other.
+    AKKA_CHECK(link_kind_ == "stream", "adopt_transport: only the scheduled (stream) link can be shared");
     dev_ = other.dev_;
     adopted_p2p_ = other.p2p_;
   }

@@ -547,6 +547,8 @@ __device__ __forceinline__ float block_reduce(float v, float* red, bool is_max) 
   return r;
 }
 
+constexpr int64_t kIgnoreIndex = -100;  // torch's default ignore_index
+
 __global__ __launch_bounds__(kBlock) void xent_fwd_kernel(const unsigned short* __restrict__ x,
                                                           const int64_t* __restrict__ y, int64_t B, int64_t C,
                                                           float* __restrict__ lse, float* __restrict__ rowloss,
@@ -565,12 +567,14 @@ __global__ __launch_bounds__(kBlock) void xent_fwd_kernel(const unsigned short* 
     const float l = m + __logf(sum);
     const int64_t t = y[r];
     const bool valid = t >= 0 && t < C;
+    // torch ignores ignore_index (-100) only; any other label outside [0, C)
+    // is an error there: here the row is flagged (-1) and the loss is NaN
+    const float flag = valid ? 1.f : (t == kIgnoreIndex ? 0.f : -1.f);
     lse[r] = l;
-    // [loss, valid] per row, written through for the last arriver
+    // [loss, flag] per row, written through for the last arriver
     __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(valid ? l - to_f(row[t]) : 0.f), rs, int(r * 8), 0,
                                           xgmi::kSysAux);
-    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(valid ? 1.f : 0.f), rs, int(r * 8 + 4), 0,
-                                          xgmi::kSysAux);
+    __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(flag), rs, int(r * 8 + 4), 0, xgmi::kSysAux);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     red[kBlock / 64] =
         __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == uint32_t(B - 1) ? 1.f : 0.f;
@@ -579,16 +583,21 @@ __global__ __launch_bounds__(kBlock) void xent_fwd_kernel(const unsigned short* 
   if (red[kBlock / 64] == 0.f) return;
   // last workgroup: mean over the valid rows, in row order per thread, then
   // a fixed-order tree across threads (deterministic)
-  float ls = 0.f, nv = 0.f;
+  float ls = 0.f, nv = 0.f, nb = 0.f;
   for (int64_t i = threadIdx.x; i < B; i += kBlock) {
     ls += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, int(i * 8), 0, xgmi::kSysAux));
-    nv += __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, int(i * 8 + 4), 0, xgmi::kSysAux));
+    const float f = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(rs, int(i * 8 + 4), 0, xgmi::kSysAux));
+    nv += f > 0.f ? f : 0.f;
+    nb += f < 0.f ? 1.f : 0.f;
   }
   ls = block_reduce(ls, red, false);
   nv = block_reduce(nv, red, false);
+  nb = block_reduce(nb, red, false);
   if (threadIdx.x == 0) {
-    out[0] = nv > 0.f ? ls / nv : __uint_as_float(0x7fc00000u);  // torch: NaN when every row is ignored
+    // torch: NaN when every row is ignored; NaN (and the bad-label count) when a label is out of range
+    out[0] = (nv > 0.f && nb == 0.f) ? ls / nv : __uint_as_float(0x7fc00000u);
     out[1] = nv;
+    out[2] = nb;
     __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
@@ -602,7 +611,7 @@ __global__ __launch_bounds__(kBlock) void xent_bwd_kernel(const unsigned short* 
   const int64_t r = blockIdx.x;
   const int64_t t = y[r];
   const float nv = stat[1];
-  const float scale = (t >= 0 && t < C && nv > 0.f) ? go[0] / nv : 0.f;
+  const float scale = (t >= 0 && t < C && nv > 0.f && stat[2] == 0.f) ? go[0] / nv : 0.f;
   const float l = lse[r];
   const unsigned short* row = x + r * C;
   unsigned short* g = gx + r * C;

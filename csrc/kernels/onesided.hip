@@ -2,12 +2,24 @@
 //
 // The protocol decisions (tags, gates, verdicts, round selection) are the
 // functions of onesided_protocol.h, shared with the CPU backend; this file
-// only maps them onto workgroups and moves the bytes.  Hand-offs follow the
-// system-scope recipe of xgmi_device.h: data -> release -> "done" tag;
-// observe tag -> acquire -> system-coherent (sc0 sc1) loads of the data.
+// maps them onto the roles of one launch and moves the bytes.
+//
+// Hand-offs are fence-free ("lite", MI355X_MICROARCH.md handoff-flag /
+// publish-large): every byte a peer reads is stored write-through (sc0 sc1)
+// or read system-coherent (sc0 sc1 loads), each storing wave drains
+// (s_waitcnt vmcnt(0)) before its workgroup's flag store, and flag / local
+// words live in uncached memory, accessed with system-scope atomics -- so a
+// store followed by s_waitcnt vmcnt(0) is performed before any later load
+// issues (the announce -> look hand-shake).  No buffer_wbl2 / buffer_inv on
+// the aligned paths; unaligned spans (odd chunk sizes) fall back to plain
+// stores + a system release.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <type_traits>
 
 #include "onesided_kernels.h"
 #include "xgmi_device.h"
@@ -18,27 +30,37 @@ namespace {
 
 using namespace xgmi;
 
-constexpr int kWaitThreads = 256;  // decide / cdecide workgroups
 constexpr int kMaxThreads = 1024;
 
-// Memory policy of the protocol functions on the device: flag words are in
-// uncached fine-grained memory (own or a peer's, over xGMI) -> system scope.
+// Memory policy of the protocol functions on the device (flag words: own or a
+// peer's, over xGMI; both uncached, system-scope atomics).
 struct DevMem {
   __device__ static uint32_t ld(const uint32_t* p) { return sys_load(p); }
   __device__ static void st(uint32_t* p, uint32_t v) { sys_store(p, v); }
-  // announce, then look: the store must be performed before the load issues
+  // announce, then look: the store is performed before the next load issues
   __device__ static void st_sc(uint32_t* p, uint32_t v) {
-    __hip_atomic_store(p, v, __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
+    sys_store(p, v);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
-  __device__ static uint32_t ld_sc(const uint32_t* p) {
-    return __hip_atomic_load(const_cast<uint32_t*>(p), __ATOMIC_SEQ_CST, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
+  __device__ static uint32_t ld_sc(const uint32_t* p) { return sys_load(p); }
 };
+
+__device__ inline uint64_t ld64(const uint32_t* p) {
+  return __hip_atomic_load(reinterpret_cast<uint64_t*>(const_cast<uint32_t*>(p)), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ inline void st64(uint32_t* p, uint64_t v) {
+  __hip_atomic_store(reinterpret_cast<uint64_t*>(p), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ inline uint32_t add_loc(uint32_t* p, uint32_t v) {
+  return __hip_atomic_fetch_add(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 __device__ inline void stat_add(const Args& a, int32_t i, unsigned long long v) {
   if (v) atomicAdd(a.stats + i, v);
 }
+
+__device__ inline void set_err(const Args& a) { sys_store(a.err, 1u); }
 
 // Part j of chunk k of block p: element offset inside the block and length.
 __device__ inline int64_t part_len_of(const Args& a, int32_t p, int32_t k, int32_t j) {
@@ -49,38 +71,53 @@ __device__ inline int64_t part_off(const Args& a, int32_t k, int32_t j) {
   return int64_t(k) * a.C + int64_t(j) * a.part_len;
 }
 
-__device__ inline uint32_t cur_round(const Args& a) { return a.loc[a.L.state(kCur)]; }
-
-// ---- begin: round selection (catch-up) ----------------------------------------
-__global__ void os_begin_kernel(Args a) {
+// ---- begin (workgroup 0): round selection (catch-up), announcements --------------
+__device__ void begin_role(const Args& a) {
   if (threadIdx.x != 0) return;
   const Layout& L = a.L;
   uint32_t* fl = a.tab->fl[a.me];
   uint32_t* loc = a.loc;
-  const uint32_t next = loc[L.state(kNext)];
+  const uint32_t seq = sys_load(loc + L.state(kCallSeq));
+  const uint32_t next = sys_load(loc + L.state(kNext));
   const int64_t sm = seen_max<DevMem>(fl, L, a.me);
   const uint32_t r = select_round(next, sm, a.max_lag);
   stat_add(a, kSkippedRounds, r - next);
-  loc[L.state(kCur)] = r;
-  loc[L.state(kNext)] = r + 1u;
-  loc[L.state(kCtrReduce)] = 0;
-  loc[L.state(kCtrCopy)] = 0;
-  loc[L.state(kForcedChunks)] = 0;
+  sys_store(loc + L.state(kCur), r);
+  sys_store(loc + L.state(kNext), r + 1u);
+  sys_store(loc + L.state(kCtrFinish), 0u);
+  sys_store(loc + L.state(kForcedChunks), 0u);
   // rounds skipped by catch-up count as completed for the senders' outdated check
   if (DevMem::ld(fl + L.done()) < r) DevMem::st(fl + L.done(), r);
+  // from now on this call reads its gather row: announce before any copy
+  // workgroup looks at a tag (the overwrite hand-shake)
+  DevMem::st_sc(fl + L.gread(int32_t(r % uint32_t(L.D))), r + 1u);
+  sys_store(loc + L.state(kBegun), seq + 1u);
+}
+
+// Every other role: wait for begin, return the call's round.
+__device__ uint32_t wait_begun(const Args& a) {
+  __shared__ uint32_t r_s;
+  if (threadIdx.x == 0) {
+    const uint32_t seq = sys_load(a.loc + a.L.state(kCallSeq));
+    while (sys_load(a.loc + a.L.state(kBegun)) != seq + 1u) __builtin_amdgcn_s_sleep(1);
+    r_s = sys_load(a.loc + a.L.state(kCur));
+  }
+  __syncthreads();
+  return r_s;
 }
 
 // ---- push: phase 1, fire and forget -----------------------------------------------
 template <int ES>
-__global__ __launch_bounds__(kMaxThreads) void os_push_kernel(Args a) {
+__device__ void push_role(const Args& a, uint32_t r, int32_t w0, int32_t stride) {
   const Layout& L = a.L;
   const int32_t N = L.N, P = L.P;
   const int32_t items = (N - 1) * L.Kmax * P;
-  const uint32_t r = cur_round(a);
   const int32_t row = int32_t(r % uint32_t(L.D));
   __shared__ int32_t go;
-  for (int32_t w = blockIdx.x; w < items; w += gridDim.x) {
-    // part-major, peers rotated from me + 1: consecutive workgroups feed different links
+  for (int32_t w = w0; w < items; w += stride) {
+    // chunk-major, peers rotated from me + 1: a chunk lands everywhere early
+    // (its owner can reduce it while later chunks are still moving) and
+    // consecutive workgroups feed different links
     const int32_t i = w % (N - 1), kj = w / (N - 1);
     const int32_t k = kj / P, j = kj % P;
     const int32_t p = (a.me + 1 + i) % N;
@@ -100,28 +137,33 @@ __global__ __launch_bounds__(kMaxThreads) void os_push_kernel(Args a) {
     if (go == kGo) {
       const int64_t n = part_len_of(a, p, k, j);
       const int64_t off = part_off(a, k, j);
-      if (n > 0)
-        copy_bytes(a.tab->sd[row][p] + (int64_t(a.me) * a.slot + off) * ES, a.in + (a.tab->bstart[p] + off) * ES,
-                   n * ES);
-      release_wg();
+      char* dst = a.tab->sd[row][p] + (int64_t(a.me) * a.slot + off) * ES;
+      const char* src = a.in + (a.tab->bstart[p] + off) * ES;
+      const bool lite = ((uintptr_t(dst) | uintptr_t(src) | uintptr_t(n * ES)) & 15) == 0;
+      if (n > 0) {
+        if (lite) copy_out_sys(dst, src, n * ES);
+        else copy_bytes(dst, src, n * ES);
+      }
+      if (lite) drain_wg();
+      else release_wg();
       if (threadIdx.x == 0) DevMem::st(ofl + L.stag(row, a.me, k, j), tag_done(r));
     }
     __syncthreads();  // `go` is rewritten by the next item
   }
 }
 
-// ---- decide: reduce threshold of one chunk of my block --------------------------
-__global__ __launch_bounds__(kWaitThreads) void os_decide_kernel(Args a) {
+// ---- decide: reduce threshold of chunk k of my block, then the phase-2 gates ----
+__device__ void decide_role(const Args& a, uint32_t r, int32_t k) {
   const Layout& L = a.L;
   const int32_t N = L.N, P = L.P, me = a.me;
-  const int32_t k = blockIdx.x;
-  const uint32_t r = cur_round(a);
   const int32_t row = int32_t(r % uint32_t(L.D));
   uint32_t* fl = a.tab->fl[me];
   __shared__ int32_t dn[kMaxRanks], lost[kMaxRanks];
   __shared__ int32_t verdict;
   __shared__ uint32_t mask_s;
+  __shared__ uint32_t okq_s[kMaxParts];
   if (threadIdx.x == 0) DevMem::st_sc(fl + L.sread(row, k), r + 1u);  // announce before looking
+  if (threadIdx.x < kMaxParts) okq_s[threadIdx.x] = 0u;
   __syncthreads();
   const uint64_t deadline = wall_clock64() + a.timeout;
   while (true) {
@@ -160,33 +202,59 @@ __global__ __launch_bounds__(kWaitThreads) void os_decide_kernel(Args a) {
     if (verdict != kWait) break;
     __builtin_amdgcn_s_sleep(8);
   }
+  const uint32_t mask = mask_s;
   if (threadIdx.x == 0) {
-    a.loc[L.dec(row, k)] = r + 1u;
-    a.loc[L.dec(row, k) + 1] = mask_s;
     DevMem::st(fl + L.fired(row, k), r + 1u);  // late senders of round <= r now skip
     if (verdict == kThreshold) {
       stat_add(a, kReduceThreshold, 1);
     } else {
       stat_add(a, kReduceForced, 1);
-      atomicAdd(a.loc + L.state(kForcedChunks), 1u);
+      add_loc(a.loc + L.state(kForcedChunks), 1u);
     }
     if (verdict == kTimeout) {
       stat_add(a, kTimeouts, 1);
-      sys_store(a.err, 1u);
+      set_err(a);
     }
-    stat_add(a, kReduceContribs, __popc(mask_s));
+    stat_add(a, kReduceContribs, __popc(mask));
   }
+  // phase-2 gates of every (part, peer), one lane each: the remote round
+  // trips overlap instead of running per reduce piece
+  const uint32_t cnt = uint32_t(__popc(mask));
+  for (int32_t t = threadIdx.x; t < P * (N - 1); t += blockDim.x) {
+    const int32_t j = t / (N - 1), qi = t % (N - 1);
+    const int32_t q = (me + 1 + qi) % N;
+    if (sys_load(a.dead + q)) {
+      stat_add(a, kDeadSkips, 1);
+      continue;
+    }
+    uint32_t* qfl = a.tab->fl[q];
+    if (k == 0 && j == 0) DevMem::st(qfl + L.seen(me), r + 1u);
+    const int32_t g = gather_gate<DevMem>(qfl, L, row, me, k, j, r);
+    if (g == kGo) {
+      DevMem::st(qfl + L.gtag(row, me, k, j) + 1, cnt);  // count, performed before the "done" tag
+      atomicOr(&okq_s[j], 1u << q);
+      stat_add(a, kGatherPushed, 1);
+    } else {
+      stat_add(a, g == kOutdated ? kGatherOutdated : kGatherConflict, 1);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x < P) sys_store(a.loc + L.okq(k, threadIdx.x), okq_s[threadIdx.x]);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) st64(a.loc + L.dec(k), (uint64_t(mask) << 32) | uint64_t(r + 1u));
 }
 
-// ---- reduce: masked sum of the landed set, phase 2 pushes ------------------------
+// ---- reduce: masked sum of the landed set, phase-2 pushes ------------------------
 // Sources in ascending rank order (the exact lanes' order): my own input
 // (plain loads), peers' SD slots (system-coherent loads).  Destinations: my
-// output block (local) and GD[row][me] of every peer in `okq`.
-// Vector body with the rank count NS known at compile time: every thread
-// issues the loads of all landed sources (U = 16 / NS vectors each) before the
-// first add, as the exact lanes' reduce does; a source outside `mask` reads as
-// zeros without a load (the branch is uniform).  Same ascending-source order as
-// the runtime-N body, so the sums are bitwise identical.
+// output block (nontemporal: nobody reads it in this launch) and GD[row][me]
+// of every peer in `okq` (write-through).  Vector body with the rank count
+// NS known at compile time: every thread issues the loads of all landed
+// sources (U vectors each) before the first add; a source outside `mask`
+// reads as zeros without a load (the branch is uniform).  Same ascending-
+// source order as the runtime-N body, so the sums are bitwise identical.
 template <typename T, int NS>
 __device__ void masked_sum_n(const Args& a, const char* mine, const char* sd, char* o, int64_t goff, int32_t row,
                              uint32_t mask, uint32_t okq, int64_t off, int64_t n) {
@@ -229,19 +297,20 @@ __device__ void masked_sum_n(const Args& a, const char* mine, const char* sd, ch
         if ((mask >> s) & 1u) Elt<T>::add(acc, v[s][u]);
       if (i < nv) {
         const uint4 w = Elt<T>::pack(acc);
-        store_nt16(reinterpret_cast<uint4*>(o) + i, w);  // my output: not read again in this kernel
+        store_nt16(reinterpret_cast<uint4*>(o) + i, w);
 #pragma unroll
         for (int q = 0; q < NS; ++q)
-          if ((okq >> q) & 1u) reinterpret_cast<uint4*>(a.tab->gd[row][q] + goff)[i] = w;
+          if ((okq >> q) & 1u) store_sys16(sys_rsrc(a.tab->gd[row][q] + goff, nv * 16), i * 16, w);
       }
     }
   }
 }
 
-// NS > 0: instantiated for N == NS (one reduce kernel per node rank count);
-// NS == 0: any N.
+// NS > 0: instantiated for N == NS (one kernel per node rank count);
+// NS == 0: any N.  Returns whether the window stores need a release fence
+// before the tags (plain stores: runtime-N and unaligned bodies).
 template <typename T, int NS>
-__device__ void masked_sum(const Args& a, int32_t row, uint32_t mask, uint32_t okq, int64_t off, int64_t n) {
+__device__ bool masked_sum(const Args& a, int32_t row, uint32_t mask, uint32_t okq, int64_t off, int64_t n) {
   constexpr int ES = sizeof(T);
   constexpr int PV = Elt<T>::kPerVec;
   const int32_t N = a.L.N, me = a.me;
@@ -254,7 +323,7 @@ __device__ void masked_sum(const Args& a, int32_t row, uint32_t mask, uint32_t o
   if ((al & 15) == 0) {
     if constexpr (NS > 0) {
       masked_sum_n<T, NS>(a, mine, sd, o, goff, row, mask, okq, off, n);
-      return;
+      return false;
     }
     const int64_t nv = n / PV;
     for (int64_t i0 = threadIdx.x; i0 < nv; i0 += kUnroll * int(blockDim.x)) {
@@ -305,94 +374,97 @@ __device__ void masked_sum(const Args& a, int32_t row, uint32_t mask, uint32_t o
         if ((okq >> q) & 1u) Elt<T>::store1(a.tab->gd[row][q] + goff + i * ES, acc);
     }
   }
+  return true;
 }
 
-template <typename T, int NS, int LB>
-__global__ __launch_bounds__(LB) void os_reduce_kernel(Args a) {
+// Piece s of part j of my chunk k, once the chunk is decided.
+template <typename T, int NS>
+__device__ void reduce_piece(const Args& a, uint32_t r, int32_t k, int32_t j, int32_t s, bool wait_decision) {
   const Layout& L = a.L;
   const int32_t N = L.N, P = L.P, me = a.me;
-  const int32_t kme = a.tab->nch[me];
-  const int32_t items = kme * P;
-  const uint32_t r = cur_round(a);
   const int32_t row = int32_t(r % uint32_t(L.D));
-  __shared__ uint32_t okq_s, mask_s;
-  for (int32_t w = blockIdx.x; w < items; w += gridDim.x) {
-    const int32_t k = w / P, j = w % P;
-    if (threadIdx.x == 0) {
-      const uint32_t mask = a.loc[L.dec(row, k) + 1];  // decided by the previous kernel
-      const uint32_t cnt = uint32_t(__popc(mask));
-      uint32_t okq = 0;
-      for (int32_t i = 1; i < N; ++i) {
-        const int32_t q = (me + i) % N;
-        if (sys_load(a.dead + q)) {
-          stat_add(a, kDeadSkips, 1);
-          continue;
-        }
-        uint32_t* qfl = a.tab->fl[q];
-        if (k == 0 && j == 0) DevMem::st(qfl + L.seen(me), r + 1u);
-        const int32_t g = gather_gate<DevMem>(qfl, L, row, me, k, j, r);
-        if (g == kGo) {
-          okq |= 1u << q;
-          DevMem::st(qfl + L.gtag(row, me, k, j) + 1, cnt);  // count, ordered before the tag by the release
-          stat_add(a, kGatherPushed, 1);
-        } else {
-          stat_add(a, g == kOutdated ? kGatherOutdated : kGatherConflict, 1);
-        }
-      }
-      if (j == 0) a.counts[int64_t(me) * a.kcols + k] = int32_t(cnt);
-      okq_s = okq;
-      mask_s = mask;
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");  // the landed SD bytes (peers' tags seen by decide)
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
-    const int64_t n = part_len_of(a, me, k, j);
-    if (n > 0) masked_sum<T, NS>(a, row, mask_s, okq_s, part_off(a, k, j), n);
-    release_wg();
-    if (threadIdx.x == 0) {
-      for (int32_t q = 0; q < N; ++q)
-        if ((okq_s >> q) & 1u) DevMem::st(a.tab->fl[q] + L.gtag(row, me, k, j), tag_done(r));
-    }
-    __syncthreads();
-  }
-  // the last workgroup out withdraws the row's read announcements (every
-  // workgroup's SD loads completed before its increment: release_wg above)
+  __shared__ uint32_t mask_s, okq_s;
   if (threadIdx.x == 0) {
-    const uint32_t prev = __hip_atomic_fetch_add(a.loc + L.state(kCtrReduce), 1u, __ATOMIC_ACQ_REL,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
-    if (prev == gridDim.x - 1) {
-      for (int32_t k = 0; k < kme; ++k) DevMem::st(a.tab->fl[me] + L.sread(row, k), 0u);
+    uint64_t d = ld64(a.loc + L.dec(k));
+    if (wait_decision) {
+      // the decider is a lower workgroup id and ends every wait itself; the
+      // bound here only guards against a broken decider
+      const uint64_t deadline = wall_clock64() + 2 * a.timeout + 1;
+      while (uint32_t(d) != r + 1u) {
+        if (wall_clock64() > deadline) {
+          set_err(a);
+          d = (uint64_t(1u << me) << 32) | uint64_t(r + 1u);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+        d = ld64(a.loc + L.dec(k));
+      }
     }
+    mask_s = uint32_t(d >> 32);
+    okq_s = sys_load(a.loc + L.okq(k, j));
+  }
+  __syncthreads();
+  const int64_t n = part_len_of(a, me, k, j);
+  const int64_t per = ((n + a.nsub - 1) / a.nsub + 63) / 64 * 64;
+  const int64_t lo = min(n, int64_t(s) * per), hi = min(n, lo + per);
+  bool fenced = false;
+  if (hi > lo) fenced = masked_sum<T, NS>(a, row, mask_s, okq_s, part_off(a, k, j) + lo, hi - lo);
+  // (uniform: the alignment of a piece is the same for every thread)
+  if (fenced) release_wg();
+  else drain_wg();
+  if (threadIdx.x == 0) {
+    // the last piece of the part publishes it: every other piece's stores
+    // were performed before its increment, which this one observed
+    if ((add_loc(a.loc + L.pctr(k, j), 1u) + 1u) % uint32_t(a.nsub) == 0u) {
+      const uint32_t okq = okq_s;
+      for (int32_t q = 0; q < N; ++q)
+        if ((okq >> q) & 1u) DevMem::st(a.tab->fl[q] + L.gtag(row, me, k, j), tag_done(r));
+      if ((add_loc(a.loc + L.kctr(k), 1u) + 1u) % uint32_t(P) == 0u)
+        sys_store(a.loc + L.odone(k), r + 1u);  // chunk k reduced: it counts towards my completion
+    }
+  }
+  __syncthreads();  // mask_s / okq_s are rewritten by the next piece
+}
+
+template <typename T, int NS>
+__device__ void reduce_role(const Args& a, uint32_t r, int32_t w0, int32_t stride) {
+  const int32_t P = a.L.P, ns = a.nsub;
+  const int32_t items = a.kme * P * ns;
+  for (int32_t w = w0; w < items; w += stride) {
+    const int32_t k = w / (P * ns), j = (w / ns) % P, s = w % ns;
+    reduce_piece<T, NS>(a, r, k, j, s, true);
   }
 }
 
-// ---- cdecide: completion threshold -------------------------------------------------
-__global__ __launch_bounds__(kWaitThreads) void os_cdecide_kernel(Args a) {
+// ---- complete: the thComplete decision -------------------------------------------
+__device__ void complete_role(const Args& a, uint32_t r) {
   const Layout& L = a.L;
   const int32_t N = L.N, P = L.P, me = a.me, K = L.Kmax;
-  const uint32_t r = cur_round(a);
   const int32_t row = int32_t(r % uint32_t(L.D));
   uint32_t* fl = a.tab->fl[me];
-  __shared__ int32_t landed_s, pending_s, verdict;
+  __shared__ int32_t landed_s, pending_s, own_s, verdict;
   __shared__ int32_t past[kMaxRanks];
-  if (threadIdx.x == 0) DevMem::st_sc(fl + L.gread(row), r + 1u);  // announce before looking
-  __syncthreads();
   const uint64_t deadline = wall_clock64() + a.timeout;
-  int32_t landed = 0;
+  const uint64_t hard = deadline + a.timeout;  // own reduces are bounded by their own waits
   while (true) {
     if (threadIdx.x == 0) {
       landed_s = 0;
       pending_s = 0;
+      own_s = 0;
     }
     if (threadIdx.x < kMaxRanks) {
       const int32_t p = threadIdx.x;
       past[p] = p < N && p != me && source_past<DevMem>(fl, L, p, r) ? 1 : 0;  // before the tags
     }
     __syncthreads();
-    int32_t my_l = 0, my_p = 0;
+    int32_t my_l = 0, my_p = 0, my_o = 0;
     for (int32_t c = threadIdx.x; c < N * K; c += blockDim.x) {
       const int32_t p = c / K, k = c % K;
-      if (p == me || k >= a.tab->nch[p]) continue;
+      if (k >= a.tab->nch[p]) continue;
+      if (p == me) {
+        my_o += sys_load(a.loc + L.odone(k)) == r + 1u;
+        continue;
+      }
       int32_t st = kLanded;
       for (int32_t j = 0; j < P; ++j) {
         const int32_t s = tag_state(DevMem::ld(fl + L.gtag(row, p, k, j)), r);
@@ -403,87 +475,176 @@ __global__ __launch_bounds__(kWaitThreads) void os_cdecide_kernel(Args a) {
         if (s == kPending) st = kPending;
       }
       if (st == kPending && (past[p] || sys_load(a.dead + p))) st = kLost;
-      a.loc[L.cmask(p, k)] = st == kLanded ? 1u : 0u;
       my_l += st == kLanded;
       my_p += st == kPending;
     }
     if (my_l) atomicAdd(&landed_s, my_l);
     if (my_p) atomicAdd(&pending_s, my_p);
+    if (my_o) atomicAdd(&own_s, my_o);
     __syncthreads();
     if (threadIdx.x == 0) {
-      landed = landed_s + a.tab->nch[me];  // my own reduced chunks are delivered to myself
-      verdict = evaluate(landed, pending_s, a.need_c, r, seen_max<DevMem>(fl, L, me), a.max_lag, sys_load(a.force),
-                         wall_clock64() > deadline);
+      const uint64_t now = wall_clock64();
+      verdict = completion_verdict(landed_s, pending_s, own_s, a.kme, a.need_c, r, seen_max<DevMem>(fl, L, me),
+                                   a.max_lag, sys_load(a.force), now > deadline);
+      if (verdict == kWait && now > hard) verdict = kTimeout;
     }
     __syncthreads();
     if (verdict != kWait) break;
     __builtin_amdgcn_s_sleep(8);
   }
+  // The output set: every chunk whose parts all landed (peers) / that is
+  // reduced (mine) -- read once more now, so chunks that landed while the
+  // verdict was being reached are kept (they are final: "done r" tags under
+  // this call's gather-row announcement).
+  int32_t my_l = 0;
+  for (int32_t c = threadIdx.x; c < N * K; c += blockDim.x) {
+    const int32_t p = c / K, k = c % K;
+    if (k >= a.tab->nch[p]) continue;
+    bool in;
+    if (p == me) {
+      in = sys_load(a.loc + L.odone(k)) == r + 1u;
+    } else {
+      in = true;
+      for (int32_t j = 0; j < P && in; ++j) in = tag_state(DevMem::ld(fl + L.gtag(row, p, k, j)), r) == kLanded;
+    }
+    sys_store(a.loc + L.cmask(p, k), in ? 1u : 0u);
+    my_l += in;
+  }
+  if (threadIdx.x == 0) landed_s = 0;
+  __syncthreads();
+  if (my_l) atomicAdd(&landed_s, my_l);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
   if (threadIdx.x == 0) {
-    a.loc[L.state(kCompReason)] = uint32_t(verdict);
-    a.loc[L.state(kCompLanded)] = uint32_t(landed);
+    sys_store(a.loc + L.state(kCompReason), uint32_t(verdict));
+    sys_store(a.loc + L.state(kCompLanded), uint32_t(landed_s));
     stat_add(a, verdict == kThreshold ? kCompleteThreshold : kCompleteForced, 1);
     if (verdict == kTimeout) {
       stat_add(a, kTimeouts, 1);
-      sys_store(a.err, 1u);
+      set_err(a);
     }
+    DevMem::st(fl + L.done(), r + 1u);  // senders of round <= r now skip me
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    sys_store(a.loc + L.state(kComp), r + 1u);  // the copy workgroups may read cmask
   }
 }
 
-// ---- copy: landed chunks -> output, completion ------------------------------------
+// ---- copy: a peer's part -> my output as soon as it lands ------------------------
 template <int ES>
-__global__ __launch_bounds__(kMaxThreads) void os_copy_kernel(Args a) {
+__device__ void copy_role(const Args& a, uint32_t r, int32_t w0, int32_t stride) {
   const Layout& L = a.L;
   const int32_t N = L.N, P = L.P, me = a.me;
   const int32_t items = (N - 1) * L.Kmax * P;
-  const uint32_t r = cur_round(a);
   const int32_t row = int32_t(r % uint32_t(L.D));
   uint32_t* fl = a.tab->fl[me];
-  if (threadIdx.x == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-  for (int32_t w = blockIdx.x; w < items; w += gridDim.x) {
+  __shared__ int32_t act;
+  for (int32_t w = w0; w < items; w += stride) {
     const int32_t i = w % (N - 1), kj = w / (N - 1);
     const int32_t k = kj / P, j = kj % P;
     const int32_t p = (me + 1 + i) % N;
     if (k >= a.tab->nch[p]) continue;
-    const bool landed = a.loc[L.cmask(p, k)] != 0u;
-    const int64_t n = part_len_of(a, p, k, j);
-    const int64_t off = part_off(a, k, j);
-    char* o = a.out + (a.tab->bstart[p] + off) * ES;
-    if (n > 0) {
-      if (landed) copy_in(o, a.tab->gd[row][me] + (int64_t(p) * a.slot + off) * ES, n * ES);
-      else zero_bytes(o, n * ES);
+    if (threadIdx.x == 0) {
+      const uint64_t deadline = wall_clock64() + 3 * a.timeout + 1;
+      int32_t v = 0;
+      while (true) {
+        const int32_t st = tag_state(DevMem::ld(fl + L.gtag(row, p, k, j)), r);
+        if (st == kLanded) {
+          v = 1;
+          break;
+        }
+        if (st == kLost) break;
+        if (sys_load(a.loc + L.state(kComp)) == r + 1u) {
+          v = sys_load(a.loc + L.cmask(p, k)) != 0u ? 1 : 0;
+          break;
+        }
+        if (wall_clock64() > deadline) {
+          set_err(a);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(4);
+      }
+      act = v;
     }
-    if (j == 0 && threadIdx.x == 0)
-      a.counts[int64_t(p) * a.kcols + k] = landed ? int32_t(DevMem::ld(fl + L.gtag(row, p, k, 0) + 1)) : 0;
+    __syncthreads();
+    const int64_t n = part_len_of(a, p, k, j);
+    if (act && n > 0) {
+      const int64_t off = part_off(a, k, j);
+      copy_in(a.out + (a.tab->bstart[p] + off) * ES, a.tab->gd[row][me] + (int64_t(p) * a.slot + off) * ES, n * ES);
+    }
+    __syncthreads();  // `act` is rewritten by the next item
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // my GD reads are done before the row is released
+}
+
+// ---- the round launch -------------------------------------------------------------
+template <typename T, int NS, int LB>
+__global__ __launch_bounds__(LB) void os_round_kernel(Args a) {
+  constexpr int ES = sizeof(T);
+  int32_t b = int32_t(blockIdx.x);
+  if (b == 0) {
+    begin_role(a);
+    return;
+  }
+  const uint32_t r = wait_begun(a);
+  b -= 1;
+  if (b < a.gp) return push_role<ES>(a, r, b, a.gp);
+  b -= a.gp;
+  if (b < a.kme) return decide_role(a, r, b);
+  b -= a.kme;
+  if (b < a.gr) return reduce_role<T, NS>(a, r, b, a.gr);
+  b -= a.gr;
+  if (b == 0) return complete_role(a, r);
+  b -= 1;
+  copy_role<ES>(a, r, b, a.gq);
+}
+
+// ---- finish: chunks outside the output set -> 0 / count 0, status -----------------
+template <int ES>
+__global__ __launch_bounds__(kMaxThreads) void os_finish_kernel(Args a) {
+  const Layout& L = a.L;
+  const int32_t N = L.N, K = L.Kmax, me = a.me;
+  const uint32_t r = sys_load(a.loc + L.state(kCur));
+  const int32_t row = int32_t(r % uint32_t(L.D));
+  uint32_t* fl = a.tab->fl[me];
+  for (int32_t c = blockIdx.x; c < N * K; c += gridDim.x) {
+    const int32_t p = c / K, k = c % K;
+    if (k >= a.tab->nch[p]) continue;
+    const bool in = sys_load(a.loc + L.cmask(p, k)) != 0u;
+    if (!in) {
+      const int64_t clen = min(a.C, a.tab->blen[p] - int64_t(k) * a.C);
+      zero_bytes(a.out + (a.tab->bstart[p] + int64_t(k) * a.C) * ES, clen * ES);
+    }
+    if (threadIdx.x == 0) {
+      int32_t cnt = 0;
+      if (in) cnt = p == me ? __popc(uint32_t(ld64(a.loc + L.dec(k)) >> 32))
+                            : int32_t(DevMem::ld(fl + L.gtag(row, p, k, 0) + 1));
+      a.counts[int64_t(p) * a.kcols + k] = cnt;
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    const uint32_t prev = __hip_atomic_fetch_add(a.loc + L.state(kCtrCopy), 1u, __ATOMIC_ACQ_REL,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t prev = add_loc(a.loc + L.state(kCtrFinish), 1u);
     if (prev == gridDim.x - 1) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      DevMem::st(fl + L.done(), r + 1u);  // senders of round <= r now skip me
+      // the last workgroup out: this call no longer reads its rows
+      for (int32_t k = 0; k < a.kme; ++k) DevMem::st(fl + L.sread(row, k), 0u);
       DevMem::st(fl + L.gread(row), 0u);
-      const uint32_t landed = a.loc[L.state(kCompLanded)];
+      const uint32_t landed = sys_load(a.loc + L.state(kCompLanded));
       int64_t total = 0;
       for (int32_t p = 0; p < N; ++p) total += a.tab->nch[p];
       stat_add(a, kRounds, 1);
       stat_add(a, kLandedChunks, landed);
       stat_add(a, kMissingChunks, uint64_t(total - int64_t(landed)));
-      CallStatus* cs = a.status + a.call_slot;
-      __hip_atomic_store(&cs->reason, int64_t(a.loc[L.state(kCompReason)]), __ATOMIC_RELAXED,
+      const uint32_t seq = sys_load(a.loc + L.state(kCallSeq));
+      CallStatus* cs = a.status + (seq % uint32_t(kStatusSlots));
+      __hip_atomic_store(&cs->call, int64_t(seq), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(&cs->reason, int64_t(sys_load(a.loc + L.state(kCompReason))), __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_SYSTEM);
       __hip_atomic_store(&cs->landed_chunks, int64_t(landed), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(&cs->forced_chunks, int64_t(a.loc[L.state(kForcedChunks)]), __ATOMIC_RELAXED,
+      __hip_atomic_store(&cs->forced_chunks, int64_t(sys_load(a.loc + L.state(kForcedChunks))), __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_SYSTEM);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __hip_atomic_store(&cs->round, int64_t(r), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      sys_store(a.loc + L.state(kCallSeq), seq + 1u);
     }
   }
 }
@@ -492,47 +653,44 @@ __global__ __launch_bounds__(kMaxThreads) void os_copy_kernel(Args a) {
 __global__ void os_retire_kernel(Args a) {
   const int32_t q = threadIdx.x;
   if (q >= a.L.N || q == a.me) return;
-  DevMem::st(a.tab->fl[q] + a.L.fin(a.me), a.loc[a.L.state(kNext)] + 1u);
+  DevMem::st(a.tab->fl[q] + a.L.fin(a.me), sys_load(a.loc + a.L.state(kNext)) + 1u);
 }
 
-int32_t grid_for(int64_t items, int32_t cap) { return int32_t(std::max<int64_t>(1, std::min<int64_t>(items, cap))); }
-
-// The reduce kernel for this call's rank count (2..8, 16; else runtime N) and
-// workgroup size (a 256-thread launch bound leaves the body all its VGPRs).
-template <typename T, int NS>
-void launch_reduce_ns(hipStream_t s, const Args& a, unsigned grid, unsigned nt) {
-  if (nt <= 256u) hipLaunchKernelGGL((os_reduce_kernel<T, NS, 256>), dim3(grid), dim3(nt), 0, s, a);
-  else hipLaunchKernelGGL((os_reduce_kernel<T, NS, kMaxThreads>), dim3(grid), dim3(nt), 0, s, a);
+// Reduce role alone (microbenchmark): every piece of my block, decisions pre-set.
+template <typename T, int NS, int LB>
+__global__ __launch_bounds__(LB) void os_reduce_bench_kernel(Args a, uint32_t r) {
+  const int32_t P = a.L.P, ns = a.nsub;
+  const int32_t items = a.kme * P * ns;
+  for (int32_t w = blockIdx.x; w < items; w += gridDim.x)
+    reduce_piece<T, NS>(a, r, w / (P * ns), (w / ns) % P, w % ns, false);
 }
 
-template <typename T>
-void launch_reduce(hipStream_t s, const Args& a, unsigned grid, unsigned nt) {
-  switch (a.L.N) {
-    case 2: return launch_reduce_ns<T, 2>(s, a, grid, nt);
-    case 3: return launch_reduce_ns<T, 3>(s, a, grid, nt);
-    case 4: return launch_reduce_ns<T, 4>(s, a, grid, nt);
-    case 5: return launch_reduce_ns<T, 5>(s, a, grid, nt);
-    case 6: return launch_reduce_ns<T, 6>(s, a, grid, nt);
-    case 7: return launch_reduce_ns<T, 7>(s, a, grid, nt);
-    case 8: return launch_reduce_ns<T, 8>(s, a, grid, nt);
-    case 16: return launch_reduce_ns<T, 16>(s, a, grid, nt);
-    default: return launch_reduce_ns<T, 0>(s, a, grid, nt);
+template <typename F>
+void with_ns(int32_t N, F&& f) {
+  switch (N) {
+    case 2: return f(std::integral_constant<int, 2>{});
+    case 3: return f(std::integral_constant<int, 3>{});
+    case 4: return f(std::integral_constant<int, 4>{});
+    case 5: return f(std::integral_constant<int, 5>{});
+    case 6: return f(std::integral_constant<int, 6>{});
+    case 7: return f(std::integral_constant<int, 7>{});
+    case 8: return f(std::integral_constant<int, 8>{});
+    case 16: return f(std::integral_constant<int, 16>{});
+    default: return f(std::integral_constant<int, 0>{});
   }
 }
 
 template <typename T>
 void launch_call(hipStream_t s, const Args& a) {
   constexpr int ES = sizeof(T);
-  const int32_t nt = (a.threads == 512 || a.threads == 1024) ? a.threads : 256;
-  const int64_t peer_items = int64_t(a.L.N - 1) * a.L.Kmax * a.L.P;
-  hipLaunchKernelGGL(os_begin_kernel, dim3(1), dim3(64), 0, s, a);
-  hipLaunchKernelGGL(os_push_kernel<ES>, dim3(unsigned(grid_for(peer_items, 8192))), dim3(unsigned(nt)), 0, s, a);
-  if (a.kme > 0) {
-    hipLaunchKernelGGL(os_decide_kernel, dim3(unsigned(a.kme)), dim3(kWaitThreads), 0, s, a);
-    launch_reduce<T>(s, a, unsigned(grid_for(int64_t(a.kme) * a.L.P, 8192)), unsigned(nt));
-  }
-  hipLaunchKernelGGL(os_cdecide_kernel, dim3(1), dim3(kWaitThreads), 0, s, a);
-  hipLaunchKernelGGL(os_copy_kernel<ES>, dim3(unsigned(grid_for(peer_items, 8192))), dim3(unsigned(nt)), 0, s, a);
+  const unsigned nt = a.threads <= 256 ? 256u : 1024u;
+  const unsigned grid = unsigned(onesided_grid(a));
+  with_ns(a.L.N, [&](auto ns) {
+    constexpr int NS = decltype(ns)::value;
+    if (nt == 256u) hipLaunchKernelGGL((os_round_kernel<T, NS, 256>), dim3(grid), dim3(nt), 0, s, a);
+    else hipLaunchKernelGGL((os_round_kernel<T, NS, kMaxThreads>), dim3(grid), dim3(nt), 0, s, a);
+  });
+  hipLaunchKernelGGL(os_finish_kernel<ES>, dim3(unsigned(std::max(1, a.gf))), dim3(256), 0, s, a);
 }
 
 }  // namespace
@@ -544,6 +702,105 @@ void launch_onesided_retire(hipStream_t s, const Args& a) {
 void launch_onesided_call(hipStream_t s, const Args& a, int32_t dtype) {
   if (dtype == 0) launch_call<float>(s, a);
   else launch_call<uint16_t>(s, a);
+}
+
+double onesided_reduce_role_bench(int32_t N, int64_t block, int64_t chunk, int64_t part, int32_t nsub, int32_t dtype,
+                                  int32_t threads, int32_t grid, int32_t iters, int32_t device) {
+  auto ok = [](hipError_t e, const char* w) {
+    if (e != hipSuccess) throw std::runtime_error(std::string("akka onesided bench: ") + w + ": " + hipGetErrorString(e));
+  };
+  ok(hipSetDevice(device), "set device");
+  const int64_t es = dtype == 0 ? 4 : 2;
+  const int64_t slot = (block + 63) / 64 * 64;
+  const int32_t K = int32_t((block + chunk - 1) / chunk);
+  const int32_t P = int32_t((chunk + part - 1) / part);
+  Layout L;
+  L.init(N, 2, K, P);
+  char *sd = nullptr, *gd = nullptr, *in = nullptr, *out = nullptr;
+  uint32_t *fl = nullptr, *loc = nullptr;
+  unsigned long long* stats = nullptr;
+  Tables* tab = nullptr;
+  ok(hipExtMallocWithFlags(reinterpret_cast<void**>(&sd), size_t(N * slot * es), hipDeviceMallocFinegrained), "sd");
+  ok(hipExtMallocWithFlags(reinterpret_cast<void**>(&gd), size_t(N * slot * es), hipDeviceMallocFinegrained), "gd");
+  ok(hipMalloc(&in, size_t(N * block * es)), "in");
+  ok(hipMalloc(&out, size_t(N * block * es)), "out");
+  ok(hipExtMallocWithFlags(reinterpret_cast<void**>(&fl), size_t(L.flag_words) * 4, hipDeviceMallocUncached), "fl");
+  ok(hipExtMallocWithFlags(reinterpret_cast<void**>(&loc), size_t(L.local_words) * 4, hipDeviceMallocUncached),
+     "loc");
+  ok(hipMalloc(reinterpret_cast<void**>(&stats), kNumStats * 8), "stats");
+  ok(hipMalloc(reinterpret_cast<void**>(&tab), sizeof(Tables)), "tab");
+  ok(hipMemset(sd, 0x3c, size_t(N * slot * es)), "fill");
+  ok(hipMemset(in, 0x3c, size_t(N * block * es)), "fill");
+  ok(hipMemset(fl, 0, size_t(L.flag_words) * 4), "fl");
+  ok(hipMemset(loc, 0, size_t(L.local_words) * 4), "loc");
+  Tables t;
+  std::memset(&t, 0, sizeof(t));
+  for (int32_t q = 0; q < N; ++q) {
+    t.fl[q] = fl;
+    t.bstart[q] = int64_t(q) * block;
+    t.blen[q] = block;
+    t.nch[q] = K;
+    for (int32_t d = 0; d < 2; ++d) {
+      t.sd[d][q] = sd;
+      t.gd[d][q] = gd;
+    }
+  }
+  ok(hipMemcpy(tab, &t, sizeof(t), hipMemcpyHostToDevice), "tab");
+  // every chunk decided with all N sources, every peer gated (bcast to N-1 rows)
+  std::vector<uint32_t> hl(size_t(L.local_words), 0u);
+  const uint32_t r = 0;
+  for (int32_t k = 0; k < K; ++k) {
+    const uint64_t d = (uint64_t((N >= 32 ? 0xffffffffu : ((1u << N) - 1u))) << 32) | uint64_t(r + 1u);
+    std::memcpy(&hl[size_t(L.dec(k))], &d, 8);
+    for (int32_t j = 0; j < P; ++j) hl[size_t(L.okq(k, j))] = ((1u << N) - 1u) & ~1u;  // me = 0
+  }
+  ok(hipMemcpy(loc, hl.data(), hl.size() * 4, hipMemcpyHostToDevice), "loc");
+  Args a;
+  a.tab = tab;
+  a.loc = loc;
+  a.stats = stats;
+  a.L = L;
+  a.C = chunk;
+  a.slot = slot;
+  a.part_len = part;
+  a.me = 0;
+  a.kme = K;
+  a.nsub = std::max(1, nsub);
+  a.threads = threads;
+  a.timeout = uint64_t(1) << 40;
+  a.in = in;
+  a.out = out;
+  const unsigned nt = threads <= 256 ? 256u : 1024u;
+  const unsigned g = unsigned(std::max(1, grid));
+  auto launch = [&]() {
+    auto go = [&](auto tt) {
+      using T = decltype(tt);
+      with_ns(N, [&](auto ns) {
+        constexpr int NS = decltype(ns)::value;
+        if (nt == 256u) hipLaunchKernelGGL((os_reduce_bench_kernel<T, NS, 256>), dim3(g), dim3(nt), 0, nullptr, a, r);
+        else hipLaunchKernelGGL((os_reduce_bench_kernel<T, NS, kMaxThreads>), dim3(g), dim3(nt), 0, nullptr, a, r);
+      });
+    };
+    if (dtype == 0) go(float{});
+    else go(uint16_t{});
+  };
+  hipEvent_t e0, e1;
+  ok(hipEventCreate(&e0), "event");
+  ok(hipEventCreate(&e1), "event");
+  for (int i = 0; i < 3; ++i) launch();
+  ok(hipEventRecord(e0, nullptr), "record");
+  for (int i = 0; i < iters; ++i) launch();
+  ok(hipEventRecord(e1, nullptr), "record");
+  ok(hipEventSynchronize(e1), "sync");
+  float ms = 0.f;
+  ok(hipEventElapsedTime(&ms, e0, e1), "elapsed");
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  for (void* p : {static_cast<void*>(sd), static_cast<void*>(gd), static_cast<void*>(in), static_cast<void*>(out),
+                  static_cast<void*>(fl), static_cast<void*>(loc), static_cast<void*>(stats),
+                  static_cast<void*>(tab)})
+    (void)hipFree(p);
+  return double(ms) / std::max(1, iters);
 }
 
 }  // namespace os

@@ -1,19 +1,22 @@
 // gfx950 kernels of the one-sided threshold lane (onesided.hip); protocol in
 // onesided_protocol.h, host side in transport/onesided.{h,cpp}.
 //
-// One call (one round of this rank) is six launches on the caller's stream:
-//   begin    1 workgroup   pick the round (catch-up over what peers announced)
-//   push     (N-1)*K*P     phase 1: my input's block p -> rank p's SD[row][me]
-//   decide   K_me          per chunk of my block: wait (bounded) until
-//                          floor(thReduce*N) copies landed or the round is
-//                          forced; record the landed mask
-//   reduce   K_me*P        masked sum -> my output block and every peer's
-//                          GD[row][me] (phase 2, remote stores)
-//   cdecide  1             wait until floor(thComplete*total) reduced chunks
-//                          landed in my GD[row] or the round is forced
-//   copy     (N-1)*K*P     landed chunks GD -> output, the rest 0 / count 0
-// Only decide and cdecide wait, and their grids are tiny, so no workgroup
-// ever waits on a workgroup that might not be resident.  Senders never wait.
+// One call (one round of this rank) is two launches on the caller's stream:
+//   round   one grid, roles by workgroup id (onesided_protocol.h, "One call"):
+//             [0]                  begin: round selection, announcements
+//             [1, 1+gp)            push: (N-1)*K*P parts, fire and forget
+//             [.., +kme)           decide: one workgroup per chunk of my block
+//             [.., +gr)            reduce: kme*P*nsub pieces, each starts when
+//                                  its chunk is decided
+//             [.., +1)             complete: the thComplete decision
+//             [.., +gq)            copy: (N-1)*K*P landed parts -> output
+//   finish  chunks outside the completion set -> 0, counts, status.
+// Deadlock-free without co-residency: workgroups are dispatched in id order,
+// every role waits only on roles with lower ids (or on peers' pushers, which
+// never wait), and every wait is bounded by the lane's timeout.
+// The call id and the round live in device memory (kCallSeq, kCur): the
+// launches' arguments are the same every call, so a call can be captured in
+// a HIP graph and replayed.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -37,13 +40,15 @@ struct Tables {
 
 struct Args {
   const Tables* tab = nullptr;
-  uint32_t* loc = nullptr;                 // local state (Layout local words)
+  uint32_t* loc = nullptr;                 // local state (Layout local words), uncached device memory
   unsigned long long* stats = nullptr;     // kNumStats counters
   Layout L;
   int64_t C = 1, slot = 0, part_len = 64;  // elements
   int32_t me = 0, kme = 0, need_r = 1, need_c = 1, max_lag = 0;  // kme: chunks of my block
   int32_t kcols = 1;                       // columns of the counts table [N][kcols]
-  int32_t call_slot = 0, threads = 256;
+  int32_t threads = 1024;
+  int32_t gp = 1, gr = 1, gq = 1, gf = 1;  // push / reduce / copy / finish workgroups
+  int32_t nsub = 1;                        // reduce pieces per part
   uint64_t timeout = 0;                    // per wait, wall-clock ticks
   const char* in = nullptr;                // round input [S]
   char* out = nullptr;                     // round output [S]
@@ -58,6 +63,14 @@ struct Args {
 void launch_onesided_call(hipStream_t s, const Args& a, int32_t dtype);
 // Announce to every peer that this rank serves no further round (fin words).
 void launch_onesided_retire(hipStream_t s, const Args& a);
+// Workgroups of the round launch for these role sizes.
+inline int32_t onesided_grid(const Args& a) { return 1 + a.gp + a.kme + a.gr + 1 + a.gq; }
+
+// Microbenchmark of the reduce role alone (one process, local windows, every
+// decision pre-set, no peer gated): N sources of `block` elements, `parts`
+// (elements) per part, `nsub` pieces each.  Returns ms per launch.
+double onesided_reduce_role_bench(int32_t N, int64_t block, int64_t chunk, int64_t part, int32_t nsub, int32_t dtype,
+                                  int32_t threads, int32_t grid, int32_t iters, int32_t device);
 
 }  // namespace os
 }  // namespace akka

@@ -50,7 +50,25 @@
 //           "writing x": never mistaken for data).
 // Either the writer sees the reader's announcement and drops, or the reader
 // sees "writing x" and excludes that source -- never a torn read.  Readers
-// clear the announcement as soon as their kernel finished reading the row.
+// clear the announcement once the call stopped reading the row.  (Flag words
+// live in uncached memory: "store -> s_waitcnt vmcnt(0) -> load" is the
+// full fence on the GPU, no cache write-back or invalidate involved.)
+//
+// One call, as roles (GPU: workgroups of one launch; CPU: a progress loop):
+//   begin    pick the round (catch-up), announce the gather row
+//   push     phase 1: my input's block p -> rank p's SD[row][me], gated
+//   decide   per chunk k of my block: wait until floor(thReduce*N) copies
+//            landed (or the round is forced), then gate the phase-2 pushes
+//   reduce   per piece of chunk k, as soon as k is decided: masked sum ->
+//            my output block + every gated peer's GD[row][me]; the last
+//            piece of a part stores its "done" tags, the last part marks k
+//            reduced (it then counts towards my completion)
+//   complete wait until floor(thComplete*total) reduced chunks landed (mine
+//            counted once reduced) or the round is forced; publish the set
+//   copy     per part of a peer's block: copied to the output as soon as it
+//            lands (the reference's per-chunk fire, W:177-181), or skipped
+//   finish   chunks outside the completion set -> 0 / count 0, counts,
+//            withdraw the announcements, publish the call's status
 #pragma once
 
 #include <cstdint>
@@ -83,8 +101,8 @@ struct Layout {
   int32_t N = 0, D = 0, Kmax = 0, P = 0;
   // exported (peers read or write these over the link)
   int64_t stag0 = 0, gtag0 = 0, fired0 = 0, sread0 = 0, gread0 = 0, done0 = 0, seen0 = 0, fin0 = 0, flag_words = 0;
-  // local only
-  int64_t dec0 = 0, cmask0 = 0, state0 = 0, local_words = 0;
+  // local only (this rank's kernels / progress thread)
+  int64_t dec0 = 0, okq0 = 0, pctr0 = 0, kctr0 = 0, odone0 = 0, cmask0 = 0, state0 = 0, local_words = 0;
 
   OS_HD void init(int32_t N_, int32_t D_, int32_t Kmax_, int32_t P_) {
     N = N_;
@@ -101,8 +119,12 @@ struct Layout {
     seen0 = done0 + 16;  // its own 64-B line
     fin0 = seen0 + N;
     flag_words = (fin0 + N + 15) / 16 * 16;
-    dec0 = 0;
-    cmask0 = dec0 + 2 * int64_t(D) * Kmax;
+    dec0 = 0;  // 64-bit words: even offsets
+    okq0 = dec0 + 2 * int64_t(Kmax);
+    pctr0 = okq0 + int64_t(Kmax) * P;
+    kctr0 = pctr0 + int64_t(Kmax) * P;
+    odone0 = kctr0 + Kmax;
+    cmask0 = odone0 + Kmax;
     state0 = (cmask0 + int64_t(N) * Kmax + 15) / 16 * 16;
     local_words = state0 + kStateWords;
   }
@@ -120,23 +142,35 @@ struct Layout {
   OS_HD int64_t seen(int32_t src) const { return seen0 + src; }
   // src retired: it serves no round >= fin - 1 (0: active)
   OS_HD int64_t fin(int32_t src) const { return fin0 + src; }
-  // local: decision of my chunk k in row (round+1, mask), landed chunk map
-  OS_HD int64_t dec(int32_t row, int32_t k) const { return dec0 + 2 * (int64_t(row) * Kmax + k); }
+  // local: decision of my chunk k, one 64-bit word (landed mask << 32 | round + 1)
+  OS_HD int64_t dec(int32_t k) const { return dec0 + 2 * int64_t(k); }
+  // local: peers whose gather row takes part j of my chunk k this round (bit q)
+  OS_HD int64_t okq(int32_t k, int32_t j) const { return okq0 + int64_t(k) * P + j; }
+  // local: finished reduce pieces of part (k, j) / parts of chunk k (counted modulo, never reset)
+  OS_HD int64_t pctr(int32_t k, int32_t j) const { return pctr0 + int64_t(k) * P + j; }
+  OS_HD int64_t kctr(int32_t k) const { return kctr0 + k; }
+  // local: round + 1 once my chunk k is reduced (self-delivery of its ReduceBlock, W:260-261)
+  OS_HD int64_t odone(int32_t k) const { return odone0 + k; }
+  // local: chunk (blk, k) is part of this round's output (completion decision)
   OS_HD int64_t cmask(int32_t blk, int32_t k) const { return cmask0 + int64_t(blk) * Kmax + k; }
   OS_HD int64_t state(int32_t i) const { return state0 + i; }
 
   static constexpr int32_t kStateWords = 16;
 };
 
+constexpr int32_t kMaxParts = 64;
+
 // local state words (Layout::state(i))
 enum StateWord : int32_t {
-  kNext = 0,        // next round this rank may serve
-  kCur = 1,         // round of the call in progress
-  kCtrReduce = 2,   // reduce workgroups finished (last one clears the row's announcements)
-  kCtrCopy = 3,     // copy workgroups finished (last one publishes completion)
-  kCompReason = 4,  // how the completion decision was reached (Verdict)
-  kCompLanded = 5,  // chunks landed at the completion decision (mine included)
-  kForcedChunks = 6,
+  kNext = 0,         // next round this rank may serve
+  kCur = 1,          // round of the call in progress
+  kCallSeq = 2,      // calls finished on this lane (the next call's id; device-resident)
+  kBegun = 3,        // call id + 1 once the call's round is selected
+  kCtrFinish = 4,    // finish workgroups done (the last one publishes the call)
+  kCompReason = 5,   // how the completion decision was reached (Verdict)
+  kCompLanded = 6,   // chunks landed at the completion decision (mine included)
+  kForcedChunks = 7,
+  kComp = 8,         // round + 1 once the completion decision (cmask) is published
 };
 
 // stats counters (uint64, local device memory / host memory on the CPU)
@@ -179,6 +213,20 @@ OS_HD inline int32_t evaluate(int32_t landed, int32_t pending, int32_t need, uin
   if (force_through > r) return kHostForce;
   if (timed_out) return kTimeout;
   return kWait;
+}
+
+// Completion decision (RB:60-66, plus the lane's liveness rules).  My own
+// chunks count once reduced (the self-delivered ReduceBlock, W:260-261); a
+// FORCED completion (catch-up, unreachable, host force, timeout) first waits
+// for every one of them, as the reference force-reduces its own chunks before
+// it completes a round (W:101-105) -- they are bounded by their own waits.
+OS_HD inline int32_t completion_verdict(int32_t landed_peers, int32_t pending_peers, int32_t own_done, int32_t kme,
+                                        int32_t need, uint32_t r, int64_t seen_max, int32_t max_lag,
+                                        uint32_t force_through, bool timed_out) {
+  const int32_t v = evaluate(landed_peers + own_done, pending_peers + (kme - own_done), need, r, seen_max, max_lag,
+                             force_through, timed_out);
+  if (v != kWait && v != kThreshold && own_done < kme) return kWait;
+  return v;
 }
 
 // Round a call serves: the next one, unless a peer already pushed rounds so
@@ -240,12 +288,16 @@ OS_HD inline int32_t gather_gate(uint32_t* q_fl, const Layout& L, int32_t row, i
 }
 
 // Host-visible per-call status record (host memory, written by the last
-// workgroup of the call's final kernel).
+// workgroup of the call's final kernel).  Slot = call id % kStatusSlots; the
+// record names its call, so a reader holding an older call's slot sees that
+// the slot was reused instead of another call's round.
 struct CallStatus {
+  int64_t call;           // call id (lane's call sequence number)
   int64_t round;          // round served (-1 until the call finished)
   int64_t reason;         // completion Verdict
   int64_t landed_chunks;  // reduced chunks landed at completion (mine included)
   int64_t forced_chunks;  // my chunks whose reduce was forced
+  int64_t pad[3];
 };
 constexpr int kStatusSlots = 64;
 

@@ -70,6 +70,25 @@ int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
 }  // namespace
 
+// Role sizes of the round launch.  Defaults: 256 workgroups per data role
+// (256 threads each) -- the whole grid (~3 per CU) is resident at once on a
+// GPU of its own, so the copies of landed chunks run while later chunks are
+// still crossing the links.  Fixed once open() ran (the reduce pieces'
+// counters count modulo nsub_).
+void OneSidedLane::size_roles(int64_t wgs) {
+  const int32_t N = g_.N;
+  wgs = std::max<int64_t>(1, wgs);
+  const int64_t push_items = int64_t(N - 1) * Kmax_ * P_;
+  const int64_t red_parts = int64_t(g_.num_chunks(me_)) * P_;
+  gp_ = int32_t(std::clamp<int64_t>(push_items, 1, wgs));
+  gq_ = gp_;
+  // pieces of >= 4096 elements, enough of them to give every data CU a reducer
+  const int64_t max_sub = std::max<int64_t>(1, part_len_ / 4096);
+  nsub_ = red_parts > 0 ? int32_t(std::clamp<int64_t>((wgs + red_parts - 1) / red_parts, 1, max_sub)) : 1;
+  gr_ = red_parts > 0 ? int32_t(std::clamp<int64_t>(red_parts * nsub_, 1, wgs)) : 0;
+  gf_ = int32_t(std::clamp<int64_t>(int64_t(N) * Kmax_, 1, 64));
+}
+
 OneSidedLane::OneSidedLane(int32_t device, int64_t S, int32_t N, int64_t C, int32_t me, DType dt,
                            const OneSidedParams& p)
     : device_(device), g_(S, N, C), me_(me), dt_(dt), es_(dtype_size(dt)), p_(p) {
@@ -92,10 +111,13 @@ OneSidedLane::OneSidedLane(int32_t device, int64_t S, int32_t N, int64_t C, int3
   need_r_ = std::clamp(float_threshold(p.th_reduce, N), 1, N);
   const int64_t total = g_.total_chunks();
   need_c_ = int32_t(std::clamp<int64_t>(float_threshold(p.th_complete, total), 1, std::max<int64_t>(total, 1)));
+  AKKA_CHECK(P_ <= kMaxParts, "onesided lane: too many parts per chunk");
   AKKA_CHECK(int64_t(D_) * N * Kmax_ * P_ <= (int64_t(1) << 22),
              "onesided lane: " + std::to_string(int64_t(D_) * N * Kmax_ * P_) +
                  " chunk parts per ring -- use a larger max_chunk_size");
   L_.init(N, D_, Kmax_, P_);
+  nt_ = p.threads <= 256 ? 256 : 1024;
+  size_roles(p.role_wgs > 0 ? p.role_wgs : kDefaultRoleWgs);
   flag_bytes_ = size_t(L_.flag_words) * sizeof(uint32_t);
   row_bytes_ = size_t(N) * size_t(slot_) * es_;
   win_bytes_ = flag_bytes_ + 2 * size_t(D_) * row_bytes_;
@@ -112,6 +134,9 @@ OneSidedLane::OneSidedLane(int32_t device, int64_t S, int32_t N, int64_t C, int3
                    std::to_string(kIpcMaxWindowBytes >> 20) +
                    " MiB an IPC mapping opens (allocations of 2 GiB or more hang in hipIpcOpenMemHandle)");
     AKKA_OS_HIP(hipSetDevice(device_));
+    char bus[32] = {0};
+    AKKA_OS_HIP(hipDeviceGetPCIBusId(bus, int(sizeof(bus)) - 1, device_));
+    my_bus_ = bus;
     if (hipExtMallocWithFlags(reinterpret_cast<void**>(&flags_), flag_bytes_, hipDeviceMallocUncached) != hipSuccess) {
       (void)hipGetLastError();
       AKKA_OS_HIP(hipMalloc(reinterpret_cast<void**>(&flags_), flag_bytes_));
@@ -121,7 +146,12 @@ OneSidedLane::OneSidedLane(int32_t device, int64_t S, int32_t N, int64_t C, int3
       sd_[size_t(d)] = static_cast<char*>(ipc_alloc_window(row_bytes_, d == 0 ? &mem_kind_ : nullptr));
       gd_[size_t(d)] = static_cast<char*>(ipc_alloc_window(row_bytes_, nullptr));
     }
-    AKKA_OS_HIP(hipMalloc(reinterpret_cast<void**>(&loc_), size_t(L_.local_words) * sizeof(uint32_t)));
+    // local words: uncached, like the flag area (system-scope atomics across XCDs, no cache maintenance)
+    if (hipExtMallocWithFlags(reinterpret_cast<void**>(&loc_), size_t(L_.local_words) * sizeof(uint32_t),
+                              hipDeviceMallocUncached) != hipSuccess) {
+      (void)hipGetLastError();
+      AKKA_OS_HIP(hipMalloc(reinterpret_cast<void**>(&loc_), size_t(L_.local_words) * sizeof(uint32_t)));
+    }
     AKKA_OS_HIP(hipMemset(loc_, 0, size_t(L_.local_words) * sizeof(uint32_t)));
     AKKA_OS_HIP(hipMalloc(reinterpret_cast<void**>(&stats_dev_), kNumStats * sizeof(unsigned long long)));
     AKKA_OS_HIP(hipMemset(stats_dev_, 0, kNumStats * sizeof(unsigned long long)));
@@ -129,6 +159,7 @@ OneSidedLane::OneSidedLane(int32_t device, int64_t S, int32_t N, int64_t C, int3
     AKKA_OS_HIP(hipHostMalloc(reinterpret_cast<void**>(&hw_), sizeof(HostWords),
                               hipHostMallocMapped | hipHostMallocCoherent));
     std::memset(hw_, 0, sizeof(HostWords));
+    for (auto& c : hw_->status) c.call = -1;
     AKKA_OS_HIP(hipHostGetDevicePointer(reinterpret_cast<void**>(&hw_dev_), hw_, 0));
     AKKA_OS_HIP(hipDeviceSynchronize());
     int khz = 0;
@@ -168,6 +199,7 @@ OneSidedLane::OneSidedLane(int32_t device, int64_t S, int32_t N, int64_t C, int3
     stats_host_.assign(kNumStats, 0ull);
     hw_ = new HostWords();
     std::memset(hw_, 0, sizeof(HostWords));
+    for (auto& c : hw_->status) c.call = -1;
     timeout_ticks_ = uint64_t(std::max<int64_t>(1, p.timeout_ms));  // milliseconds on the host
   }
   pfl_[size_t(me_)] = flags_;
@@ -216,7 +248,7 @@ std::string OneSidedLane::handle() const {
   b.part_len = part_len_;
   b.shm_bytes = int64_t(shm_bytes_);
   if (device_ >= 0) {
-    AKKA_OS_HIP(hipDeviceGetPCIBusId(b.bus, int(sizeof(b.bus)) - 1, device_));
+    std::memcpy(b.bus, my_bus_.c_str(), std::min(sizeof(b.bus) - 1, my_bus_.size()));
     AKKA_OS_HIP(hipIpcGetMemHandle(&b.h[0], flags_));
     for (int32_t d = 0; d < D_; ++d) {
       AKKA_OS_HIP(hipIpcGetMemHandle(&b.h[1 + d], sd_[size_t(d)]));
@@ -275,6 +307,26 @@ void OneSidedLane::open(const std::vector<std::string>& handles) {
       }
     }
   }
+  if (device_ >= 0 && p_.role_wgs <= 0) {
+    // Ranks sharing this GPU (tests / rehearsals on a 1-GPU box): every
+    // rank's round launch must fit on the card at once, or one rank's
+    // waiting workgroups could hold the slots another rank's pushers need.
+    // Budget: 1024 resident 256-thread workgroups, half of it for the lane.
+    int32_t share = 0;
+    for (int32_t q = 0; q < g_.N; ++q) {
+      Blob b;
+      std::memcpy(&b, handles[size_t(q)].data(), sizeof(b));
+      share += std::strncmp(b.bus, my_bus_.c_str(), sizeof(b.bus)) == 0;
+    }
+    shared_ranks_ = share;
+    if (share > 1) {
+      nt_ = 256;
+      const char* bv = std::getenv("AKKA_OS_SHARED_BUDGET");  // measurement knob (resident 256-thread WGs)
+      const int64_t total = bv ? std::max(16, std::atoi(bv)) : 512;
+      const int64_t budget = total / share - 2 - g_.num_chunks(me_);
+      size_roles(std::max<int64_t>(2, budget / 3));
+    }
+  }
   if (device_ >= 0) {
     Tables t;
     std::memset(&t, 0, sizeof(t));
@@ -300,19 +352,25 @@ void OneSidedLane::unlink() {
   }
 }
 
-int32_t OneSidedLane::round(uintptr_t stream, const void* in, void* out, int32_t* counts, int32_t kcols) {
+
+int64_t OneSidedLane::round(uintptr_t stream, const void* in, void* out, int32_t* counts, int32_t kcols) {
   AKKA_CHECK(ready_, "onesided lane: open() the peer windows first");
   AKKA_CHECK(kcols >= Kmax_, "onesided lane: counts table has too few columns");
-  const int32_t slot = int32_t(calls_ % kStatusSlots);
-  ++calls_;
-  hw_->status[slot] = CallStatus{-1, 0, 0, 0};
-  if (device_ >= 0) gpu_call(stream, static_cast<const char*>(in), static_cast<char*>(out), counts, kcols, slot);
-  else cpu_call(static_cast<const char*>(in), static_cast<char*>(out), counts, kcols, slot);
-  return slot;
+  if (device_ >= 0) {
+    const int64_t call = calls_++;
+    gpu_call(stream, static_cast<const char*>(in), static_cast<char*>(out), counts, kcols);
+    return call;
+  }
+  const int64_t call = begin(in, out, counts, kcols);
+  int us = 20;
+  while (!progress()) {
+    std::this_thread::sleep_for(std::chrono::microseconds(us));
+    us = std::min(us * 2, 1000);
+  }
+  return call;
 }
 
-void OneSidedLane::gpu_call(uintptr_t stream, const char* in, char* out, int32_t* counts, int32_t kcols,
-                            int32_t slot) {
+void OneSidedLane::gpu_call(uintptr_t stream, const char* in, char* out, int32_t* counts, int32_t kcols) {
   Args a;
   a.tab = static_cast<const Tables*>(tab_dev_);
   a.loc = loc_;
@@ -327,8 +385,12 @@ void OneSidedLane::gpu_call(uintptr_t stream, const char* in, char* out, int32_t
   a.need_c = need_c_;
   a.max_lag = p_.max_lag;
   a.kcols = kcols;
-  a.call_slot = slot;
-  a.threads = p_.threads;
+  a.threads = nt_;
+  a.gp = gp_;
+  a.gr = gr_;
+  a.gq = gq_;
+  a.gf = gf_;
+  a.nsub = nsub_;
   a.timeout = timeout_ticks_;
   a.in = in;
   a.out = out;
@@ -342,249 +404,307 @@ void OneSidedLane::gpu_call(uintptr_t stream, const char* in, char* out, int32_t
   AKKA_OS_HIP(hipGetLastError());
 }
 
-void OneSidedLane::cpu_call(const char* in, char* out, int32_t* counts, int32_t kcols, int32_t slot) {
-  using clock = std::chrono::steady_clock;
+// ---- CPU backend: the kernel's roles as a progress loop -------------------------
+
+int64_t OneSidedLane::begin(const void* in, void* out, int32_t* counts, int32_t kcols) {
+  AKKA_CHECK(ready_, "onesided lane: open() the peer windows first");
+  AKKA_CHECK(device_ < 0, "onesided lane: begin/progress drive the CPU backend");
+  AKKA_CHECK(!cr_.active, "onesided lane: a round is already in progress");
+  AKKA_CHECK(kcols >= Kmax_, "onesided lane: counts table has too few columns");
   const int32_t N = g_.N, me = me_, P = P_;
-  const size_t es = es_;
   uint32_t* fl = pfl_[size_t(me)];
   uint32_t* loc = loc_;
-  auto stat = [&](int32_t i, uint64_t v) { stats_host_[size_t(i)] += v; };
-  auto dead = [&](int32_t q) { return __atomic_load_n(&hw_->dead[q], __ATOMIC_ACQUIRE) != 0u; };
-  auto plen = [&](int32_t p, int32_t k, int32_t j) {
-    const int64_t clen = std::min(g_.C, g_.block_len(p) - int64_t(k) * g_.C);
-    return std::max<int64_t>(0, std::min(part_len_, clen - int64_t(j) * part_len_));
-  };
-  auto poff = [&](int32_t k, int32_t j) { return int64_t(k) * g_.C + int64_t(j) * part_len_; };
-  auto nap = [](int& us) {
-    std::this_thread::sleep_for(std::chrono::microseconds(us));
-    us = std::min(us * 2, 1000);
-  };
-  const auto deadline_of = [&]() { return clock::now() + std::chrono::milliseconds(int64_t(timeout_ticks_)); };
-
-  // begin: round selection
+  // begin: round selection (catch-up), the gather row announcement
   const uint32_t next = loc[L_.state(kNext)];
   const uint32_t r = select_round(next, seen_max<HostMem>(fl, L_, me), p_.max_lag);
-  stat(kSkippedRounds, r - next);
+  stats_host_[kSkippedRounds] += r - next;
   loc[L_.state(kCur)] = r;
   loc[L_.state(kNext)] = r + 1u;
   loc[L_.state(kForcedChunks)] = 0;
   if (HostMem::ld(fl + L_.done()) < r) HostMem::st(fl + L_.done(), r);
   const int32_t row = int32_t(r % uint32_t(D_));
-
-
-  auto dump = [&](const char* role, int32_t k) {
-    if (!std::getenv("AKKA_OS_DEBUG")) return;
-    std::fprintf(stderr, "[onesided r%d] %s timeout: round %u chunk %d next %u seen/fin:", me, role, r, k,
-                 loc[L_.state(kNext)]);
-    for (int32_t s = 0; s < N; ++s) std::fprintf(stderr, " %u/%u", HostMem::ld(fl + L_.seen(s)), HostMem::ld(fl + L_.fin(s)));
-    std::fprintf(stderr, " done %u | tags:", HostMem::ld(fl + L_.done()));
-    for (int32_t s = 0; s < N; ++s) {
-      if (s == me) continue;
-      if (k >= 0) std::fprintf(stderr, " s%d=%u", s, HostMem::ld(fl + L_.stag(row, s, k, 0)));
-      else
-        for (int32_t kk = 0; kk < g_.num_chunks(s); ++kk) std::fprintf(stderr, " b%dk%d=%u", s, kk, HostMem::ld(fl + L_.gtag(row, s, kk, 0)));
-    }
-    std::fprintf(stderr, "\n");
-  };
-
-  // push: phase 1, fire and forget (the kernel's item order)
+  HostMem::st_sc(fl + L_.gread(row), r + 1u);
+  cr_ = CpuRound();
+  cr_.active = true;
+  cr_.r = r;
+  cr_.row = row;
+  cr_.call = calls_++;
+  cr_.in = static_cast<const char*>(in);
+  cr_.out = static_cast<char*>(out);
+  cr_.counts = counts;
+  cr_.kcols = kcols;
+  cr_.decided.assign(size_t(g_.num_chunks(me)), 0);
+  cr_.deadline_ms = std::chrono::duration_cast<std::chrono::milliseconds>(
+                        std::chrono::steady_clock::now().time_since_epoch()).count() + int64_t(timeout_ticks_);
+  // decide announces (before any look at the scatter tags)
+  for (int32_t k = 0; k < g_.num_chunks(me); ++k) HostMem::st_sc(fl + L_.sread(row, k), r + 1u);
+  // push: phase 1 in the kernel's item order (chunk-major, peers from me + 1)
   const int64_t items = int64_t(N - 1) * Kmax_ * P;
   for (int64_t w = 0; w < items; ++w) {
     const int32_t i = int32_t(w % (N - 1)), kj = int32_t(w / (N - 1));
     const int32_t k = kj / P, j = kj % P;
     const int32_t p = (me + 1 + i) % N;
     if (k >= g_.num_chunks(p)) continue;
-    if (dead(p)) {
-      stat(kDeadSkips, 1);
-      continue;
-    }
-    uint32_t* ofl = pfl_[size_t(p)];
-    if (k == 0 && j == 0) HostMem::st(ofl + L_.seen(me), r + 1u);
-    const int32_t g = scatter_gate<HostMem>(ofl, L_, row, me, k, j, r);
-    stat(g == kGo ? kScatterPushed : g == kOutdated ? kScatterOutdated : kScatterConflict, 1);
-    if (g != kGo) continue;
-    const int64_t n = plen(p, k, j), off = poff(k, j);
-    if (n > 0)
-      std::memcpy(psd_[size_t(row)][size_t(p)] + (int64_t(me) * slot_ + off) * int64_t(es),
-                  in + (g_.block_start(p) + off) * int64_t(es), size_t(n) * es);
-    HostMem::st(ofl + L_.stag(row, me, k, j), tag_done(r));  // release: the bytes are visible first
+    push(0, p, k, j, r, 0, cr_.in + (g_.block_start(p) + int64_t(k) * g_.C + int64_t(j) * part_len_) * int64_t(es_));
   }
+  return cr_.call;
+}
 
-  // decide: reduce threshold per chunk of my block
-  const int32_t kme = g_.num_chunks(me);
-  for (int32_t k = 0; k < kme; ++k) {
-    HostMem::st_sc(fl + L_.sread(row, k), r + 1u);
-    const auto deadline = deadline_of();
-    int us = 20;
-    int32_t verdict = kWait;
-    uint32_t mask = 0;
-    while (true) {
-      int32_t landed = 1, pending = 0;
-      mask = 1u << me;
-      for (int32_t s = 0; s < N; ++s) {
-        if (s == me) continue;
-        int32_t dn = 0;
-        bool lost = source_past<HostMem>(fl, L_, s, r);  // before the tags
-        for (int32_t j = 0; j < P; ++j) {
-          const int32_t st = tag_state(HostMem::ld(fl + L_.stag(row, s, k, j)), r);
-          dn += st == kLanded;
-          lost |= st == kLost;
-        }
-        if (dn == P) {
-          ++landed;
-          mask |= 1u << s;
-        } else if (!lost && !dead(s)) {
-          ++pending;
-        }
-      }
-      verdict = evaluate(landed, pending, need_r_, r, seen_max<HostMem>(fl, L_, me), p_.max_lag,
-                         __atomic_load_n(&hw_->force, __ATOMIC_ACQUIRE), clock::now() > deadline);
-      if (verdict != kWait) break;
-      nap(us);
-    }
-    loc[L_.dec(row, k)] = r + 1u;
-    loc[L_.dec(row, k) + 1] = mask;
-    HostMem::st(fl + L_.fired(row, k), r + 1u);
-    if (verdict == kThreshold) {
-      stat(kReduceThreshold, 1);
-    } else {
-      stat(kReduceForced, 1);
-      ++loc[L_.state(kForcedChunks)];
-    }
-    if (verdict == kTimeout) {
-      stat(kTimeouts, 1);
-      __atomic_store_n(&hw_->err, 1u, __ATOMIC_RELEASE);
-      dump("decide", k);
-    }
-    stat(kReduceContribs, uint64_t(__builtin_popcount(mask)));
+// A push: performed at once, or (held) queued with a copy of its bytes.
+void OneSidedLane::push(int32_t phase, int32_t dst, int32_t k, int32_t j, uint32_t r, uint32_t cnt,
+                        const char* src) {
+  Msg m{phase, dst, k, j, r, cnt, {}};
+  if (!hold_) {
+    exec(m, src);
+    return;
   }
+  const int64_t clen = std::min(g_.C, g_.block_len(phase == 0 ? dst : me_) - int64_t(k) * g_.C);
+  const int64_t n = std::max<int64_t>(0, std::min(part_len_, clen - int64_t(j) * part_len_));
+  m.bytes.assign(src, src + n * int64_t(es_));
+  outbox_.push_back(std::move(m));
+}
 
-  // reduce: masked sum (ascending source order, fp32 accumulation), phase 2
-  std::vector<float> acc;
-  std::vector<char> part;
-  for (int32_t k = 0; k < kme; ++k) {
-    const uint32_t mask = loc[L_.dec(row, k) + 1];
-    const uint32_t cnt = uint32_t(__builtin_popcount(mask));
+void OneSidedLane::exec(const Msg& m, const char* src) {
+  const int32_t me = me_, q = m.dst, k = m.k, j = m.j;
+  const uint32_t r = m.r;
+  const int32_t row = int32_t(r % uint32_t(D_));
+  if (__atomic_load_n(&hw_->dead[q], __ATOMIC_ACQUIRE) != 0u) {
+    stats_host_[kDeadSkips] += 1;
+    return;
+  }
+  uint32_t* qfl = pfl_[size_t(q)];
+  if (k == 0 && j == 0) HostMem::st(qfl + L_.seen(me), r + 1u);  // implicit start at the receiver
+  const int64_t tag = m.phase == 0 ? L_.stag(row, me, k, j) : L_.gtag(row, me, k, j);
+  // A held message older than what this sender already wrote to that slot
+  // (a later round, delivered first) is outdated: the single writer of a slot
+  // moves forward only (the reference drops it on arrival, W:155-156).
+  if (HostMem::ld(qfl + tag) >= tag_writing(r + 1u)) {
+    stats_host_[m.phase == 0 ? kScatterOutdated : kGatherOutdated] += 1;
+    return;
+  }
+  const int32_t g = m.phase == 0 ? scatter_gate<HostMem>(qfl, L_, row, me, k, j, r)
+                                 : gather_gate<HostMem>(qfl, L_, row, me, k, j, r);
+  if (m.phase == 0) stats_host_[g == kGo ? kScatterPushed : g == kOutdated ? kScatterOutdated : kScatterConflict] += 1;
+  else stats_host_[g == kGo ? kGatherPushed : g == kOutdated ? kGatherOutdated : kGatherConflict] += 1;
+  if (g != kGo) return;
+  const int32_t blk = m.phase == 0 ? q : me;
+  const int64_t clen = std::min(g_.C, g_.block_len(blk) - int64_t(k) * g_.C);
+  const int64_t n = std::max<int64_t>(0, std::min(part_len_, clen - int64_t(j) * part_len_));
+  const int64_t off = int64_t(k) * g_.C + int64_t(j) * part_len_;
+  if (m.phase == 1) HostMem::st(qfl + tag + 1, m.cnt);  // count before the "done" tag
+  char* dst = (m.phase == 0 ? psd_ : pgd_)[size_t(row)][size_t(q)] + (int64_t(me) * slot_ + off) * int64_t(es_);
+  if (n > 0) std::memcpy(dst, src ? src : m.bytes.data(), size_t(n) * es_);
+  HostMem::st(qfl + tag, tag_done(r));  // release: the bytes are visible first
+}
+
+void OneSidedLane::flush() {
+  if (hold_) return;
+  while (!outbox_.empty()) {
+    Msg m = std::move(outbox_.front());
+    outbox_.pop_front();
+    exec(m, nullptr);
+  }
+}
+
+std::vector<std::array<int64_t, 6>> OneSidedLane::outbox() const {
+  std::vector<std::array<int64_t, 6>> v;
+  for (const Msg& m : outbox_) v.push_back({m.phase, m.dst, m.k, m.j, int64_t(m.r), int64_t(m.cnt)});
+  return v;
+}
+
+void OneSidedLane::deliver(int64_t i) {
+  AKKA_CHECK(i >= 0 && i < int64_t(outbox_.size()), "onesided lane: no such outbox entry");
+  Msg m = std::move(outbox_[size_t(i)]);
+  outbox_.erase(outbox_.begin() + i);
+  exec(m, nullptr);
+}
+
+void OneSidedLane::drop(int64_t i) {
+  AKKA_CHECK(i >= 0 && i < int64_t(outbox_.size()), "onesided lane: no such outbox entry");
+  outbox_.erase(outbox_.begin() + i);
+}
+
+// decide (+ reduce + phase-2 pushes) of my chunk k, if its wait is over.
+bool OneSidedLane::try_decide(int32_t k, bool timed_out) {
+  const int32_t N = g_.N, me = me_, P = P_;
+  const uint32_t r = cr_.r;
+  const int32_t row = cr_.row;
+  uint32_t* fl = pfl_[size_t(me)];
+  int32_t landed = 1, pending = 0;  // my own copy is always there (W:228-232)
+  uint32_t mask = 1u << me;
+  for (int32_t s = 0; s < N; ++s) {
+    if (s == me) continue;
+    int32_t dn = 0;
+    bool lost = source_past<HostMem>(fl, L_, s, r);  // before the tags
     for (int32_t j = 0; j < P; ++j) {
-      uint32_t okq = 0;
-      for (int32_t i = 1; i < N; ++i) {
-        const int32_t q = (me + i) % N;
-        if (dead(q)) {
-          stat(kDeadSkips, 1);
-          continue;
-        }
-        uint32_t* qfl = pfl_[size_t(q)];
-        if (k == 0 && j == 0) HostMem::st(qfl + L_.seen(me), r + 1u);
-        const int32_t g = gather_gate<HostMem>(qfl, L_, row, me, k, j, r);
-        if (g == kGo) {
-          okq |= 1u << q;
-          HostMem::st(qfl + L_.gtag(row, me, k, j) + 1, cnt);
-          stat(kGatherPushed, 1);
-        } else {
-          stat(g == kOutdated ? kGatherOutdated : kGatherConflict, 1);
-        }
-      }
-      if (j == 0) counts[int64_t(me) * kcols + k] = int32_t(cnt);
-      const int64_t n = plen(me, k, j), off = poff(k, j);
-      if (n > 0) {
-        acc.assign(size_t(n), 0.f);
-        for (int32_t s = 0; s < N; ++s) {
-          if (!((mask >> s) & 1u)) continue;
-          const char* src = s == me ? in + (g_.block_start(me) + off) * int64_t(es)
-                                    : sd_[size_t(row)] + (int64_t(s) * slot_ + off) * int64_t(es);
-          if (dt_ == DType::F32) {
-            const float* f = reinterpret_cast<const float*>(src);
-            for (int64_t e = 0; e < n; ++e) acc[size_t(e)] += f[e];
-          } else {
-            const uint16_t* h = reinterpret_cast<const uint16_t*>(src);
-            for (int64_t e = 0; e < n; ++e) acc[size_t(e)] += bf16_f32(h[e]);
-          }
-        }
-        part.resize(size_t(n) * es);
-        if (dt_ == DType::F32) {
-          std::memcpy(part.data(), acc.data(), size_t(n) * 4);
-        } else {
-          uint16_t* h = reinterpret_cast<uint16_t*>(part.data());
-          for (int64_t e = 0; e < n; ++e) h[e] = f32_bf16(acc[size_t(e)]);
-        }
-        std::memcpy(out + (g_.block_start(me) + off) * int64_t(es), part.data(), part.size());
-        for (int32_t q = 0; q < N; ++q)
-          if ((okq >> q) & 1u)
-            std::memcpy(pgd_[size_t(row)][size_t(q)] + (int64_t(me) * slot_ + off) * int64_t(es), part.data(),
-                        part.size());
-      }
-      for (int32_t q = 0; q < N; ++q)
-        if ((okq >> q) & 1u) HostMem::st(pfl_[size_t(q)] + L_.gtag(row, me, k, j), tag_done(r));
+      const int32_t st = tag_state(HostMem::ld(fl + L_.stag(row, s, k, j)), r);
+      dn += st == kLanded;
+      lost |= st == kLost;
+    }
+    if (dn == P) {
+      ++landed;
+      mask |= 1u << s;
+    } else if (!lost && __atomic_load_n(&hw_->dead[s], __ATOMIC_ACQUIRE) == 0u) {
+      ++pending;
     }
   }
-  for (int32_t k = 0; k < kme; ++k) HostMem::st(fl + L_.sread(row, k), 0u);
-
-  // cdecide: completion threshold
-  HostMem::st_sc(fl + L_.gread(row), r + 1u);
-  int32_t verdict = kWait, landed = 0;
-  {
-    const auto deadline = deadline_of();
-    int us = 20;
-    while (true) {
-      int32_t l = 0, pending = 0;
-      for (int32_t p = 0; p < N; ++p) {
-        if (p == me) continue;
-        const bool past = source_past<HostMem>(fl, L_, p, r);  // before the tags
-        for (int32_t k = 0; k < g_.num_chunks(p); ++k) {
-          int32_t st = kLanded;
-          for (int32_t j = 0; j < P; ++j) {
-            const int32_t s = tag_state(HostMem::ld(fl + L_.gtag(row, p, k, j)), r);
-            if (s == kLost) {
-              st = kLost;
-              break;
-            }
-            if (s == kPending) st = kPending;
-          }
-          if (st == kPending && (past || dead(p))) st = kLost;
-          loc[L_.cmask(p, k)] = st == kLanded ? 1u : 0u;
-          l += st == kLanded;
-          pending += st == kPending;
-        }
-      }
-      landed = l + kme;
-      verdict = evaluate(landed, pending, need_c_, r, seen_max<HostMem>(fl, L_, me), p_.max_lag,
-                         __atomic_load_n(&hw_->force, __ATOMIC_ACQUIRE), clock::now() > deadline);
-      if (verdict != kWait) break;
-      nap(us);
-    }
+  const int32_t verdict = evaluate(landed, pending, need_r_, r, seen_max<HostMem>(fl, L_, me), p_.max_lag,
+                                   __atomic_load_n(&hw_->force, __ATOMIC_ACQUIRE), timed_out);
+  if (verdict == kWait) return false;
+  uint32_t* loc = loc_;
+  const uint64_t d = (uint64_t(mask) << 32) | uint64_t(r + 1u);
+  std::memcpy(&loc[L_.dec(k)], &d, 8);
+  HostMem::st(fl + L_.fired(row, k), r + 1u);  // late senders of round <= r now skip
+  if (verdict == kThreshold) {
+    stats_host_[kReduceThreshold] += 1;
+  } else {
+    stats_host_[kReduceForced] += 1;
+    ++loc[L_.state(kForcedChunks)];
   }
-  stat(verdict == kThreshold ? kCompleteThreshold : kCompleteForced, 1);
   if (verdict == kTimeout) {
-    stat(kTimeouts, 1);
+    stats_host_[kTimeouts] += 1;
     __atomic_store_n(&hw_->err, 1u, __ATOMIC_RELEASE);
-    dump("cdecide", -1);
+    dump("decide", k);
   }
+  const uint32_t cnt = uint32_t(__builtin_popcount(mask));
+  stats_host_[kReduceContribs] += cnt;
+  // reduce: masked sum, ascending source order, fp32 accumulation -> my output block
+  const size_t es = es_;
+  for (int32_t j = 0; j < P; ++j) {
+    const int64_t clen = std::min(g_.C, g_.block_len(me) - int64_t(k) * g_.C);
+    const int64_t n = std::max<int64_t>(0, std::min(part_len_, clen - int64_t(j) * part_len_));
+    const int64_t off = int64_t(k) * g_.C + int64_t(j) * part_len_;
+    char* o = cr_.out + (g_.block_start(me) + off) * int64_t(es);
+    if (n > 0) {
+      acc_.assign(size_t(n), 0.f);
+      for (int32_t s = 0; s < N; ++s) {
+        if (!((mask >> s) & 1u)) continue;
+        const char* src = s == me ? cr_.in + (g_.block_start(me) + off) * int64_t(es)
+                                  : sd_[size_t(row)] + (int64_t(s) * slot_ + off) * int64_t(es);
+        if (dt_ == DType::F32) {
+          const float* f = reinterpret_cast<const float*>(src);
+          for (int64_t e = 0; e < n; ++e) acc_[size_t(e)] += f[e];
+        } else {
+          const uint16_t* h = reinterpret_cast<const uint16_t*>(src);
+          for (int64_t e = 0; e < n; ++e) acc_[size_t(e)] += bf16_f32(h[e]);
+        }
+      }
+      if (dt_ == DType::F32) {
+        std::memcpy(o, acc_.data(), size_t(n) * 4);
+      } else {
+        uint16_t* h = reinterpret_cast<uint16_t*>(o);
+        for (int64_t e = 0; e < n; ++e) h[e] = f32_bf16(acc_[size_t(e)]);
+      }
+    }
+    // phase 2: broadcast to every peer, rotated from me + 1 (W:254-255)
+    for (int32_t i = 1; i < N; ++i) push(1, (me + i) % N, k, j, r, cnt, o);
+  }
+  loc[L_.odone(k)] = r + 1u;  // reduced: counts towards my completion (self-delivery, W:260-261)
+  return true;
+}
 
-  // copy: landed chunks -> output, the rest 0 / count 0
+// complete (+ copy + finish), if its wait is over.
+bool OneSidedLane::try_complete(bool timed_out) {
+  const int32_t N = g_.N, me = me_, P = P_;
+  const uint32_t r = cr_.r;
+  const int32_t row = cr_.row;
+  uint32_t* fl = pfl_[size_t(me)];
+  uint32_t* loc = loc_;
+  const int32_t kme = g_.num_chunks(me);
+  int32_t lp = 0, pending = 0, own = 0;
+  for (int32_t k = 0; k < kme; ++k) own += loc[L_.odone(k)] == r + 1u;
   for (int32_t p = 0; p < N; ++p) {
     if (p == me) continue;
+    const bool past = source_past<HostMem>(fl, L_, p, r);  // before the tags
     for (int32_t k = 0; k < g_.num_chunks(p); ++k) {
-      const bool ok = loc[L_.cmask(p, k)] != 0u;
+      int32_t st = kLanded;
       for (int32_t j = 0; j < P; ++j) {
-        const int64_t n = plen(p, k, j), off = poff(k, j);
-        if (n <= 0) continue;
-        char* o = out + (g_.block_start(p) + off) * int64_t(es);
-        if (ok) std::memcpy(o, gd_[size_t(row)] + (int64_t(p) * slot_ + off) * int64_t(es), size_t(n) * es);
-        else std::memset(o, 0, size_t(n) * es);
+        const int32_t s = tag_state(HostMem::ld(fl + L_.gtag(row, p, k, j)), r);
+        if (s == kLost) {
+          st = kLost;
+          break;
+        }
+        if (s == kPending) st = kPending;
       }
-      counts[int64_t(p) * kcols + k] = ok ? int32_t(HostMem::ld(fl + L_.gtag(row, p, k, 0) + 1)) : 0;
+      if (st == kPending && (past || __atomic_load_n(&hw_->dead[p], __ATOMIC_ACQUIRE) != 0u)) st = kLost;
+      lp += st == kLanded;
+      pending += st == kPending;
     }
   }
-  HostMem::st(fl + L_.done(), r + 1u);
+  const int32_t verdict = completion_verdict(lp, pending, own, kme, need_c_, r, seen_max<HostMem>(fl, L_, me),
+                                             p_.max_lag, __atomic_load_n(&hw_->force, __ATOMIC_ACQUIRE), timed_out);
+  if (verdict == kWait) return false;
+  // the output set, copies, the rest 0 / count 0 (copy + finish roles)
+  int32_t landed = 0;
+  for (int32_t p = 0; p < N; ++p) {
+    for (int32_t k = 0; k < g_.num_chunks(p); ++k) {
+      bool in = true;
+      if (p == me) in = loc[L_.odone(k)] == r + 1u;
+      else
+        for (int32_t j = 0; j < P && in; ++j) in = tag_state(HostMem::ld(fl + L_.gtag(row, p, k, j)), r) == kLanded;
+      loc[L_.cmask(p, k)] = in ? 1u : 0u;
+      landed += in;
+      const int64_t clen = g_.chunk_len(p, k);
+      char* o = cr_.out + g_.chunk_offset(p, k) * int64_t(es_);
+      if (in && p != me) std::memcpy(o, gd_[size_t(row)] + (int64_t(p) * slot_ + int64_t(k) * g_.C) * int64_t(es_),
+                                     size_t(clen) * es_);
+      if (!in) std::memset(o, 0, size_t(clen) * es_);
+      uint64_t d = 0;
+      if (p == me) std::memcpy(&d, &loc[L_.dec(k)], 8);
+      cr_.counts[int64_t(p) * cr_.kcols + k] =
+          !in ? 0 : p == me ? __builtin_popcount(uint32_t(d >> 32)) : int32_t(HostMem::ld(fl + L_.gtag(row, p, k, 0) + 1));
+    }
+  }
+  stats_host_[verdict == kThreshold ? kCompleteThreshold : kCompleteForced] += 1;
+  if (verdict == kTimeout) {
+    stats_host_[kTimeouts] += 1;
+    __atomic_store_n(&hw_->err, 1u, __ATOMIC_RELEASE);
+    dump("complete", -1);
+  }
+  HostMem::st(fl + L_.done(), r + 1u);  // senders of round <= r now skip me
+  for (int32_t k = 0; k < kme; ++k) HostMem::st(fl + L_.sread(row, k), 0u);
   HostMem::st(fl + L_.gread(row), 0u);
-  stat(kRounds, 1);
-  stat(kLandedChunks, uint64_t(landed));
-  stat(kMissingChunks, uint64_t(g_.total_chunks() - landed));
-  CallStatus& cs = hw_->status[slot];
+  stats_host_[kRounds] += 1;
+  stats_host_[kLandedChunks] += uint64_t(landed);
+  stats_host_[kMissingChunks] += uint64_t(g_.total_chunks() - landed);
+  CallStatus& cs = hw_->status[cr_.call % kStatusSlots];
+  cs.round = r;
   cs.reason = verdict;
   cs.landed_chunks = landed;
   cs.forced_chunks = loc[L_.state(kForcedChunks)];
-  __atomic_store_n(&cs.round, int64_t(r), __ATOMIC_RELEASE);
+  __atomic_store_n(&cs.call, cr_.call, __ATOMIC_RELEASE);  // the record names its call last
+  cr_.active = false;
+  return true;
+}
+
+bool OneSidedLane::progress() {
+  flush();
+  if (!cr_.active) return false;
+  const int64_t now = std::chrono::duration_cast<std::chrono::milliseconds>(
+                          std::chrono::steady_clock::now().time_since_epoch()).count();
+  const bool timed_out = now > cr_.deadline_ms;
+  for (int32_t k = 0; k < int32_t(cr_.decided.size()); ++k)
+    if (!cr_.decided[size_t(k)] && try_decide(k, timed_out)) cr_.decided[size_t(k)] = 1;
+  return try_complete(timed_out);
+}
+
+void OneSidedLane::dump(const char* role, int32_t k) const {
+  if (!std::getenv("AKKA_OS_DEBUG")) return;
+  const int32_t N = g_.N, me = me_;
+  const uint32_t* fl = pfl_[size_t(me)];
+  std::fprintf(stderr, "[onesided r%d] %s timeout: round %u chunk %d next %u seen/fin:", me, role, cr_.r, k,
+               loc_[L_.state(kNext)]);
+  for (int32_t s = 0; s < N; ++s)
+    std::fprintf(stderr, " %u/%u", HostMem::ld(fl + L_.seen(s)), HostMem::ld(fl + L_.fin(s)));
+  std::fprintf(stderr, " done %u | tags:", HostMem::ld(fl + L_.done()));
+  for (int32_t s = 0; s < N; ++s) {
+    if (s == me) continue;
+    if (k >= 0) std::fprintf(stderr, " s%d=%u", s, HostMem::ld(fl + L_.stag(cr_.row, s, k, 0)));
+    else
+      for (int32_t kk = 0; kk < g_.num_chunks(s); ++kk)
+        std::fprintf(stderr, " b%dk%d=%u", s, kk, HostMem::ld(fl + L_.gtag(cr_.row, s, kk, 0)));
+  }
+  std::fprintf(stderr, "\n");
 }
 
 void OneSidedLane::retire(uintptr_t stream) {
@@ -599,18 +719,24 @@ void OneSidedLane::retire(uintptr_t stream) {
     launch_onesided_retire(reinterpret_cast<hipStream_t>(stream), a);
     AKKA_OS_HIP(hipGetLastError());
   } else {
+    flush();
     for (int32_t q = 0; q < g_.N; ++q)
       if (q != me_) HostMem::st(pfl_[size_t(q)] + L_.fin(me_), loc_[L_.state(kNext)] + 1u);
   }
 }
 
-CallStatus OneSidedLane::status(int32_t slot) const {
-  AKKA_CHECK(slot >= 0 && slot < kStatusSlots, "onesided lane: bad status slot");
+CallStatus OneSidedLane::status(int64_t call) const {
+  AKKA_CHECK(call >= 0 && call < calls_, "onesided lane: no such call");
+  const CallStatus& rec = hw_->status[call % kStatusSlots];
   CallStatus c;
-  c.round = __atomic_load_n(&hw_->status[slot].round, __ATOMIC_ACQUIRE);
-  c.reason = hw_->status[slot].reason;
-  c.landed_chunks = hw_->status[slot].landed_chunks;
-  c.forced_chunks = hw_->status[slot].forced_chunks;
+  c.call = __atomic_load_n(&rec.call, __ATOMIC_ACQUIRE);
+  if (c.call > call)
+    throw AkkaError("onesided lane: the status record of call " + std::to_string(call) + " was reused by call " +
+                    std::to_string(c.call) + " (read an output's status within 64 calls)");
+  c.round = c.call == call ? rec.round : -1;
+  c.reason = rec.reason;
+  c.landed_chunks = rec.landed_chunks;
+  c.forced_chunks = rec.forced_chunks;
   return c;
 }
 

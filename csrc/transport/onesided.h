@@ -12,16 +12,25 @@
 //
 // Two backends run the same protocol functions:
 //  * GPU (device >= 0): windows are fine-grained HBM exported with IPC
-//    handles, the round is six kernels on the caller's stream;
-//  * CPU (device < 0): windows are POSIX shared memory, the round runs in the
-//    calling thread -- the multi-process CPU tests of the same semantics.
+//    handles, the round is one role-partitioned launch + a finish launch on
+//    the caller's stream (onesided_kernels.h): each chunk of my block is
+//    reduced and pushed the moment its threshold is met, each peer chunk is
+//    copied out the moment it lands;
+//  * CPU (device < 0): windows are POSIX shared memory, the round is a
+//    progress loop over the same roles in the calling thread -- the
+//    multi-process CPU tests of the same semantics.  Its pushes can be HELD
+//    (an outbox of messages with their bytes, delivered or dropped one by
+//    one): a harness then replays the reference spec's arrival orders
+//    (AllreduceSpec.scala) against the lane, deterministically.
 //
 // Setup is collective, like the exact ipc lane: handle() on every rank, the
 // handles go to every rank out of band, open(all handles); then unlink()
 // (CPU) once every rank opened (a killed rank then leaves nothing behind).
 #pragma once
 
+#include <array>
 #include <cstdint>
+#include <deque>
 #include <string>
 #include <vector>
 
@@ -37,7 +46,8 @@ struct OneSidedParams {
   int32_t rows = 0;                      // ring depth D (0: max(3, maxLag + 2))
   int64_t part_bytes = int64_t(256) << 10;
   int64_t timeout_ms = 30000;            // bound of every wait (then forced + error)
-  int32_t threads = 256;                 // workgroup size of the data kernels
+  int32_t threads = 256;                 // workgroup size of the round launch (256 or 1024)
+  int32_t role_wgs = 0;                  // workgroups per data role (push / reduce / copy); 0: automatic
 };
 
 class OneSidedLane {
@@ -55,10 +65,11 @@ class OneSidedLane {
 
   // One call = one round of this rank: in[S] -> out[S], counts[N][kcols]
   // (per chunk).  GPU: enqueued on `stream`; CPU: runs to completion.
-  // Returns the status slot of the call (status()).
-  int32_t round(uintptr_t stream, const void* in, void* out, int32_t* counts, int32_t kcols);
-  // The call's record; round = -1 until it finished (host memory: no sync).
-  os::CallStatus status(int32_t slot) const;
+  // Returns the call id (status()).
+  int64_t round(uintptr_t stream, const void* in, void* out, int32_t* counts, int32_t kcols);
+  // The call's record (host memory, no sync): round = -1 while it runs;
+  // throws if the record was already reused by a call 64 or more later.
+  os::CallStatus status(int64_t call) const;
   std::vector<uint64_t> stats();  // GPU: synchronises the device first
   uint32_t error() const;
   void clear_error();
@@ -69,6 +80,24 @@ class OneSidedLane {
   // This rank serves no further round: peers stop waiting for its copies of
   // rounds >= its next one (the end of a job; GPU: enqueued on `stream`).
   void retire(uintptr_t stream);
+  // Calls a captured (graphed) call ran in addition to round()'s own: keeps
+  // the host's call ids in step with the device's sequence.
+  void note_replays(int64_t n) { calls_ += n; }
+
+  // ---- CPU backend, step by step (the deterministic replay harness) ----------
+  // begin(): start a round (non-blocking), returns its call id; progress():
+  // one pass over every role, true once the round completed.
+  int64_t begin(const void* in, void* out, int32_t* counts, int32_t kcols);
+  bool progress();
+  bool active() const { return cr_.active; }
+  // Held pushes stay in the outbox (with their bytes) until delivered.
+  void set_hold(bool hold) { hold_ = hold; }
+  // outbox entries: (phase 0 scatter / 1 gather, dst, chunk, part, round, count)
+  std::vector<std::array<int64_t, 6>> outbox() const;
+  // Perform / discard outbox entry i (gates evaluated at delivery, as the
+  // reference's receiver checks a message when it arrives).
+  void deliver(int64_t i);
+  void drop(int64_t i);
 
   bool on_gpu() const { return device_ >= 0; }
   int32_t rows() const { return D_; }
@@ -76,6 +105,10 @@ class OneSidedLane {
   int64_t part_elems() const { return part_len_; }
   int32_t need_reduce() const { return need_r_; }
   int32_t need_complete() const { return need_c_; }
+  int32_t pieces() const { return nsub_; }
+  int32_t threads() const { return nt_; }
+  int32_t shared_ranks() const { return shared_ranks_; }
+  std::array<int32_t, 4> role_grid() const { return {gp_, gr_, gq_, gf_}; }
   size_t window_bytes() const { return win_bytes_; }
   const std::string& memory_kind() const { return mem_kind_; }
   const Geometry& geometry() const { return g_; }
@@ -89,8 +122,33 @@ class OneSidedLane {
     uint32_t pad[14];
     os::CallStatus status[os::kStatusSlots];
   };
-  void cpu_call(const char* in, char* out, int32_t* counts, int32_t kcols, int32_t slot);
-  void gpu_call(uintptr_t stream, const char* in, char* out, int32_t* counts, int32_t kcols, int32_t slot);
+  struct Msg {
+    int32_t phase, dst, k, j;
+    uint32_t r, cnt;
+    std::vector<char> bytes;
+  };
+  struct CpuRound {
+    bool active = false;
+    uint32_t r = 0;
+    int32_t row = 0;
+    int64_t call = 0;
+    const char* in = nullptr;
+    char* out = nullptr;
+    int32_t* counts = nullptr;
+    int32_t kcols = 0;
+    std::vector<uint8_t> decided;
+    int64_t deadline_ms = 0;
+  };
+  static constexpr int64_t kDefaultRoleWgs = 256;
+  void size_roles(int64_t wgs);
+  void gpu_call(uintptr_t stream, const char* in, char* out, int32_t* counts, int32_t kcols);
+  // CPU roles
+  void push(int32_t phase, int32_t dst, int32_t k, int32_t j, uint32_t r, uint32_t cnt, const char* src);
+  void exec(const Msg& m, const char* src);
+  bool try_decide(int32_t k, bool timed_out);
+  bool try_complete(bool timed_out);
+  void flush();
+  void dump(const char* role, int32_t k) const;
 
   int32_t device_;
   Geometry g_;
@@ -100,6 +158,8 @@ class OneSidedLane {
   OneSidedParams p_;
   os::Layout L_;
   int32_t D_ = 0, P_ = 1, Kmax_ = 0, need_r_ = 1, need_c_ = 1;
+  int32_t nsub_ = 1, nt_ = 256, gp_ = 1, gr_ = 0, gq_ = 1, gf_ = 1, shared_ranks_ = 1;
+  std::string my_bus_;
   int64_t slot_ = 0, part_len_ = 64;
   size_t flag_bytes_ = 0, row_bytes_ = 0, win_bytes_ = 0;
   std::string mem_kind_;
@@ -116,13 +176,20 @@ class OneSidedLane {
   std::vector<void*> opened_;             // GPU: IPC mappings to close
 
   // local state
-  uint32_t* loc_ = nullptr;             // GPU: device memory; CPU: loc_host_
+  uint32_t* loc_ = nullptr;             // GPU: uncached device memory; CPU: loc_host_
   unsigned long long* stats_dev_ = nullptr;
   void* tab_dev_ = nullptr;             // GPU: os::Tables
   HostWords* hw_ = nullptr;             // host
   HostWords* hw_dev_ = nullptr;         // device view of hw_ (GPU)
   std::vector<uint32_t> loc_host_;
   std::vector<unsigned long long> stats_host_;
+
+  // CPU progress state
+  CpuRound cr_;
+  std::deque<Msg> outbox_;
+  bool hold_ = false;
+  std::vector<float> acc_;
+  std::vector<char> part_;
 
   // CPU shared memory
   std::string shm_name_;

@@ -86,3 +86,27 @@ def test_ddp_hook_onesided_matches_stock_ddp():
     for rank, ok, rounds, engines, _ in _run({"transport": "onesided"}):
         assert ok, (rank, rounds)
         assert rounds >= 3 and engines >= 3
+
+
+def test_ddp_hook_reactive_keeps_one_transport_per_engine():
+    """Reactive engines issue their phase-2 groups from per-peer streams in a
+    timing-dependent order, so the hook never lets two of them share a
+    transport: each bucket size gets its own, and training still
+    matches stock DDP at thresholds 1 over several bucket sizes."""
+    for rank, ok, rounds, engines, transports in _run({"transport": "reactive"}):
+        assert ok, (rank, rounds)
+        assert rounds >= 3 and engines >= 3
+        assert transports == engines
+
+
+def test_share_transport_refuses_reactive():
+    import pytest
+
+    from akka_allreduce_amd.parallel import ThresholdAllreduce
+
+    class _Fake:
+        transport = "reactive"
+
+    with pytest.raises(ValueError, match="only the scheduled"):
+        ThresholdAllreduce(16, transport="reactive", rank=0, world_size=2, device=torch.device("cpu"),
+                           share_transport_with=_Fake())

@@ -100,6 +100,28 @@ def test_fused_cross_entropy_matches_torch(B, C):
         torch.testing.assert_close(a.grad.float(), r.grad, rtol=1e-2, atol=2e-3 * float(r.grad.abs().max()) + 1e-6)
 
 
+def test_fused_cross_entropy_flags_invalid_labels():
+    """torch ignores only -100 and raises on other out-of-range labels: the
+    fused kernel makes the loss NaN, counts the bad rows on the device, and
+    AKKA_CHECK_LABELS raises."""
+    from akka_allreduce_amd.ops import xent
+
+    logits = torch.randn(8, 5, device="cuda").to(torch.bfloat16)
+    y = torch.tensor([0, 1, -100, 4, 7, 2, -3, 1], device="cuda")
+    loss = xent.cross_entropy(logits, y)
+    assert torch.isnan(loss).item()
+    assert xent.last_bad_labels() == 2
+    y_ok = torch.tensor([0, 1, -100, 4, 3, 2, 0, 1], device="cuda")
+    assert torch.isfinite(xent.cross_entropy(logits, y_ok)).item() and xent.last_bad_labels() == 0
+    old = xent._CHECK_LABELS
+    xent._CHECK_LABELS = True
+    try:
+        with pytest.raises(ValueError, match="outside"):
+            xent.cross_entropy(logits, y)
+    finally:
+        xent._CHECK_LABELS = old
+
+
 def test_mlp_bf16_fused_loss_tracks_torch_loss():
     from akka_allreduce_amd.models.mlp import MLP, dp_sgd_step, synthetic_batch
     from akka_allreduce_amd.parallel import ThresholdAllreduce
