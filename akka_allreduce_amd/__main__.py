@@ -131,9 +131,10 @@ def main(argv=None) -> int:
     m.add_argument("--th-allreduce", type=float)
     m.add_argument("--th-reduce", type=float)
     m.add_argument("--th-complete", type=float)
-    m.add_argument("--transport", choices=["auto", "rccl", "tcp", "ipc_p2p"],
-                   help="GPU data plane the master hands out: RCCL (auto/rccl), or ipc_p2p = mailboxes in mapped "
-                        "peer memory (no RCCL; several workers may share one GPU)")
+    m.add_argument("--transport", choices=["auto", "rccl", "tcp", "ipc_p2p", "onesided"],
+                   help="GPU data plane the master hands out: RCCL (auto/rccl), ipc_p2p = mailboxes in mapped "
+                        "peer memory (no RCCL; several workers may share one GPU), or onesided = threshold rounds "
+                        "as stores into mapped peer windows (workers --transport onesided; GPU or CPU)")
     m.set_defaults(fn=_master)
 
     w = sub.add_parser("worker", help="run one AllreduceWorker (one per GPU)")
@@ -148,9 +149,10 @@ def main(argv=None) -> int:
     w.add_argument("--assert-multiple", type=int, default=0)
     w.add_argument("--device", help="cpu | cuda | cuda:N | auto")
     w.add_argument("--dtype", default="float32")
-    w.add_argument("--transport", choices=["auto", "stream", "reactive", "outbox"], default="auto",
+    w.add_argument("--transport", choices=["auto", "stream", "reactive", "outbox", "onesided"], default="auto",
                    help="GPU data path: stream (scheduled RCCL steps) or reactive (per-peer streams, straggler-"
-                        "tolerant); outbox = messages through the control plane (CPU)")
+                        "tolerant); outbox = messages through the control plane (CPU); onesided = stores into "
+                        "mapped peer windows, fast workers never wait (master --transport onesided)")
     w.set_defaults(fn=_worker)
 
     d = sub.add_parser("demo", help="master + N CPU workers on localhost")

@@ -96,9 +96,9 @@ class MasterProcess:
         self.node = Node(host, port, name="master")
         self.transport = transport
         self._store = None
-        if transport == "ipc_p2p":
-            # the workers' rendezvous for their mailbox window handles: a
-            # key-value store hosted by the master (no RCCL id to mint)
+        if transport in ("ipc_p2p", "onesided"):
+            # the workers' rendezvous for their window handles: a key-value
+            # store hosted by the master (no RCCL id to mint)
             from torch.distributed import TCPStore
 
             self._store = TCPStore(host, 0, is_master=True, wait_for_workers=False)
@@ -129,7 +129,8 @@ class MasterProcess:
             # the dead peer (ReactiveLink / IpcP2P.abort_peer), not a new epoch
             if getattr(self, "_ipc_key", None) is None:
                 self._ipc_key = f"akka/cluster/{int(time.time() * 1e6)}"
-            return {"kind": "ipc_p2p", "store": [self.node.host, int(self._store.port)], "key": self._ipc_key}
+            kind = "onesided" if self.transport == "onesided" else "ipc_p2p"
+            return {"kind": kind, "store": [self.node.host, int(self._store.port)], "key": self._ipc_key}
         refs = list(self.master.workers.values())
         all_gpu = bool(refs) and all(self._gpu_workers.get(getattr(r, "address", ""), False) for r in refs)
         want_rccl = self.transport == "rccl" or (self.transport == "auto" and all_gpu)
@@ -219,8 +220,17 @@ class WorkerProcess:
             transport = "stream" if dev.type == "cuda" else "outbox"
         if transport in ("stream", "reactive") and dev.type != "cuda":
             raise ValueError(f"{transport} transport needs a GPU worker")
-        self.worker = AllreduceWorker(data_source, data_sink, device=dev, dtype=dtype, transport=transport,
-                                      name=f"worker@{self.node.address}")
+        if transport == "onesided":
+            # threshold rounds over mapped peer windows (GPU) or shared memory
+            # (CPU): fast workers never wait for a straggler; master pacing
+            # with thAllreduce on top (parallel/onesided_worker.py)
+            from .onesided_worker import OneSidedWorker
+
+            self.worker = OneSidedWorker(data_source, data_sink, device=dev, dtype=dtype,
+                                         name=f"worker@{self.node.address}")
+        else:
+            self.worker = AllreduceWorker(data_source, data_sink, device=dev, dtype=dtype, transport=transport,
+                                          name=f"worker@{self.node.address}")
         self.stopped = threading.Event()
         self.node.aliases.append(self.worker)
         if transport == "reactive":
@@ -242,13 +252,15 @@ class WorkerProcess:
     def receive(self, msg: Any) -> None:
         if isinstance(msg, Shutdown):
             log.info("%s: shutdown (%s)", self.worker.name, msg.reason)
+            if hasattr(self.worker, "close"):
+                self.worker.close()
             self.stopped.set()
             self.node.stop()
             return
         self.worker.receive(msg)
 
     def _poll(self) -> Optional[bool]:
-        core = self.worker._core
+        core = getattr(self.worker, "_core", None)
         if core is None or not self.worker.initialized or core.in_flight() == 0:
             return None
         return self.worker.poll()

@@ -24,7 +24,8 @@ framework's lanes).  Rounds with thresholds < 1 always take the p2p schedule
 ``th_allreduce`` adds the reference's third straggler knob, the master's
 round pacing (M:54-63): a rank starts round r only once ``thAllreduce * N``
 ranks completed round r-1 (counters in the job's TCPStore, no master
-process).  ``None`` (default): each rank paces itself.
+process); on the onesided transport a call also reports the rounds it skipped
+by catch-up as completed.  ``None`` (default): each rank paces itself.
 
 ``transport="onesided"`` is the straggler-tolerant path of choice
 (parallel/onesided.py, csrc/transport/onesided.h): every send is a store into
@@ -189,8 +190,6 @@ class ThresholdAllreduce:
         if transport == "onesided":
             # thresholds over mapped peer windows: no send ever waits for a
             # peer (parallel/onesided.py, csrc/transport/onesided.h)
-            if th_allreduce is not None:
-                raise ValueError("the onesided transport paces rounds by catch-up (maxLag), not thAllreduce")
             from ..utils.faults import env_straggler_delay
             from .onesided import OneSidedAllreduce
 
@@ -201,6 +200,20 @@ class ThresholdAllreduce:
             self.transport, self.worker, self.pacer, self.store = "onesided", None, None, store
             self.data_size, self._round = int(data_size), 0
             self.fault_delay_s = env_straggler_delay(self.rank)
+            self._max_lag = int(max_lag)
+            if th_allreduce is not None and self.world_size > 1:
+                # the master's pacing (M:54-63) on top of the lane's catch-up:
+                # round r starts once thAllreduce * N ranks completed r - 1
+                pstore = store
+                if pstore is None:
+                    import torch.distributed as dist
+
+                    if not dist.is_initialized():
+                        raise RuntimeError("thAllreduce pacing needs torch.distributed initialised or a store")
+                    pstore = dist.distributed_c10d._get_default_store()
+                ThresholdAllreduce._instances += 1
+                self.pacer = RoundPacer(pstore, f"akka/pace/os/{ThresholdAllreduce._instances}", self.world_size,
+                                        float(th_allreduce))
             return
         if transport not in ("stream", "reactive"):
             raise ValueError("transport must be 'stream', 'reactive' or 'onesided'")
@@ -319,8 +332,20 @@ class ThresholdAllreduce:
             time.sleep(self.fault_delay_s)
         r = self._round
         if self.transport == "onesided":
-            self._round += 1
-            return self._os(x, out=out)
+            if self.pacer is None:
+                self._round += 1
+                return self._os(x, out=out)
+            # paced: wait for round r, call, then report every round this call
+            # completed -- the served one and any it skipped by catch-up (the
+            # reference force-completes those, W:100-106) -- like
+            # CompleteAllreduce to the master (W:276)
+            self.pacer.wait_start(r)
+            o = self._os(x, out=out)
+            served = o.iteration  # waits for the call
+            for rr in range(r, served + 1):
+                self.pacer.completed(rr)
+            self._round = served + 1
+            return o
         if self.pacer is not None:
             self.pacer.wait_start(r, self.worker.poll if self.transport == "reactive" else None)
         out = self.worker.allreduce(x, async_op=async_op, out=out)

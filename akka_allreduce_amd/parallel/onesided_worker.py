@@ -1,0 +1,204 @@
+"""OneSidedWorker: the reference's worker actor on the one-sided threshold lane.
+
+The reference's straggler tolerance lives in its actors (AllreduceWorker.scala
+with AllreduceMaster.scala): workers pull rounds from a ``dataSource`` and hand
+``(sum, count, round)`` to a ``dataSink`` (W:7-8, W:197-210), every send is
+fire-and-forget (W:227-232, W:259-264), and the master starts round r+1 once
+``thAllreduce * N`` workers completed round r (M:54-63).  This actor keeps that
+API -- ``InitWorkers`` / ``StartAllreduce`` in, ``CompleteAllreduce`` out --
+with the data plane on ``OneSidedAllreduce`` (csrc/transport/onesided.h):
+stores into mapped peer windows, device-side thresholds, no send ever waits.
+
+  * ``InitWorkers`` (carrying the master's rendezvous store in
+    ``transport = {"kind": "onesided", ...}``) maps every worker's window;
+  * ``StartAllreduce(r)`` raises ``maxRound`` (W:99); a round thread serves
+    the worker's next rounds up to it: fetch (W:197-204), one lane call, the
+    sink, ``CompleteAllreduce`` (W:270-277).  The master's start of round R
+    also forces every wait of a round < R - maxLag (catch-up, W:100-106);
+  * rounds the lane skipped by catch-up (its peers were more than maxLag
+    ahead) are force-completed like the reference's: the sink gets zeros with
+    count 0 and the master a ``CompleteAllreduce`` for each (W:100-106);
+  * ``WorkerTerminated`` marks the peer dead: it is never waited for again;
+  * ``close`` (the master's Shutdown at maxRound) retires this rank, so peers
+    stop waiting for its copies of later rounds.
+Every handler swallows and records errors like the reference's ``tryCatch``
+(W:287-299)."""
+from __future__ import annotations
+
+import logging
+import threading
+from typing import Any, List, Optional
+
+import torch
+
+from ..data import AllReduceInput, AllReduceInputRequest, AllReduceOutput, Geometry
+from ..messages import CompleteAllreduce, InitWorkers, StartAllreduce, WorkerTerminated
+
+log = logging.getLogger("akka_allreduce_amd.onesided_worker")
+
+
+class OneSidedWorker:
+    def __init__(self, dataSource, dataSink, *, device: Any = "cpu", dtype: torch.dtype = torch.float32,
+                 name: str = "onesided-worker", timeout_s: float = 30.0):
+        self.dataSource = dataSource
+        self.dataSink = dataSink
+        self.device = torch.device(device)
+        self.dtype = dtype
+        self.name = name
+        self.timeout_s = timeout_s
+        self.id = -1
+        self.master: Any = None
+        self.geometry: Optional[Geometry] = None
+        self.ar = None
+        self.max_round = -1
+        self.next_round = 0      # the next round this worker serves
+        self.rounds_done = 0
+        self.forced_rounds = 0   # skipped by catch-up, force-completed with zeros
+        self.errors: List[BaseException] = []
+        self._cv = threading.Condition()
+        self._stop = False
+        self._thread: Optional[threading.Thread] = None
+        self._store = None
+        self._max_lag = 0
+
+    # ---- actor API ---------------------------------------------------------------
+    @property
+    def initialized(self) -> bool:
+        return self.id >= 0
+
+    @property
+    def round(self) -> int:
+        return self.next_round
+
+    def tell(self, msg: Any, sender: Any = None) -> None:
+        self.receive(msg)
+
+    def receive(self, msg: Any) -> None:
+        try:
+            if isinstance(msg, InitWorkers):
+                self._on_init(msg)
+            elif isinstance(msg, StartAllreduce):
+                self._on_start(int(msg.round))
+            elif isinstance(msg, WorkerTerminated):
+                if self.ar is not None and int(msg.workerId) != self.id:
+                    self.ar.mark_dead(int(msg.workerId))
+            else:
+                raise TypeError(f"onesided worker: unhandled message {type(msg).__name__}")
+        except Exception as e:  # tryCatch (W:287-299)
+            self.errors.append(e)
+            log.error("%s: error handling %s: %s", self.name, type(msg).__name__, e)
+
+    def _on_init(self, m: InitWorkers) -> None:
+        if self.initialized:
+            return  # fixed membership per window set: a death is handled by mark_dead
+        tinfo = getattr(m, "transport", None) or {}
+        if tinfo.get("kind") != "onesided":
+            raise RuntimeError("onesided worker: InitWorkers carries no onesided rendezvous (master --transport "
+                               "onesided)")
+        from torch.distributed import TCPStore
+
+        from .onesided import OneSidedAllreduce
+
+        host, port = tinfo["store"]
+        self._store = TCPStore(host, int(port), is_master=False)
+        self.id = int(m.destId)
+        self.master = m.master
+        self._max_lag = int(m.maxLag)
+        self.geometry = Geometry(int(m.dataSize), int(m.workerNum), int(m.maxChunkSize))
+        # collective over the master's store: every worker gets InitWorkers
+        self.ar = OneSidedAllreduce(int(m.dataSize), max_chunk_size=int(m.maxChunkSize), dtype=self.dtype,
+                                    th_reduce=float(m.thReduce), th_complete=float(m.thComplete),
+                                    max_lag=int(m.maxLag), rank=self.id, world_size=int(m.workerNum),
+                                    device=self.device, store=_PrefixStore(self._store, tinfo["key"]),
+                                    timeout_s=self.timeout_s)
+        log.info("%s: id=%d onesided lane %s", self.name, self.id, self.ar.info())
+        self._thread = threading.Thread(target=self._run, name=f"{self.name}-rounds", daemon=True)
+        self._thread.start()
+
+    def _on_start(self, r: int) -> None:
+        with self._cv:
+            self.max_round = max(self.max_round, r)  # W:99
+            self._cv.notify_all()
+        if self.ar is not None and r - self._max_lag > 0:
+            # the master started round r: rounds older than r - maxLag end with
+            # what landed (the reference's catch-up, W:100-106)
+            self.ar.force_below(r - self._max_lag)
+
+    # ---- the round thread ----------------------------------------------------------
+    def _run(self) -> None:
+        if self.device.type == "cuda":
+            torch.cuda.set_device(self.device)
+        while True:
+            with self._cv:
+                while not self._stop and self.next_round > self.max_round:
+                    self._cv.wait(0.5)
+                if self._stop:
+                    return
+                want = self.next_round
+            try:
+                inp = self.dataSource(AllReduceInputRequest(want))  # W:197-204
+                x = inp.data if isinstance(inp, AllReduceInput) else inp
+                x = torch.as_tensor(x).to(device=self.device, dtype=self.dtype).reshape(-1)
+                # a fresh output per round: the sink may keep it (the
+                # reference's flush builds new arrays, RB:26-53)
+                o = self.ar(x)
+                served = o.iteration  # waits for the call (GPU)
+                for skipped in range(want, served):
+                    self._force_complete(skipped)
+                self.next_round = served + 1
+                self.rounds_done += 1
+                self.dataSink(o)
+                self._complete(served)
+            except Exception as e:  # tryCatch (W:287-299); the thread keeps serving
+                self.errors.append(e)
+                log.error("%s: round %d failed: %s", self.name, want, e)
+                with self._cv:
+                    if self._stop:
+                        return
+                    self._cv.wait(0.1)
+
+    def _force_complete(self, r: int) -> None:
+        """A round the lane skipped by catch-up: zeros, count 0 (W:100-106)."""
+        g = self.geometry
+        self.forced_rounds += 1
+        z = torch.zeros(g.dataSize, dtype=self.dtype, device=self.device)
+        self.dataSink(AllReduceOutput(z, torch.zeros(g.dataSize, dtype=torch.int32, device=self.device), r))
+        self._complete(r)
+
+    def _complete(self, r: int) -> None:
+        if self.master is not None:
+            self.master.tell(CompleteAllreduce(self.id, r))  # W:276
+
+    # ---- lifecycle -----------------------------------------------------------------
+    def close(self) -> None:
+        with self._cv:
+            self._stop = True
+            self._cv.notify_all()
+        if self.ar is not None:
+            # peers stop waiting for this rank's copies of later rounds; a
+            # call in flight ends at its own bounded waits (or forced)
+            self.ar.force_below(1 << 31)
+        if self._thread is not None and self._thread is not threading.current_thread():
+            self._thread.join(self.timeout_s + 5)
+        if self.ar is not None:
+            try:
+                self.ar.retire()
+                self.ar.synchronize()
+            except Exception as e:  # noqa: BLE001 - teardown
+                self.errors.append(e)
+
+    def __repr__(self) -> str:
+        return f"OneSidedWorker({self.name}, id={self.id}, next={self.next_round})"
+
+
+class _PrefixStore:
+    """Keys of one job's window exchange under the master's job key."""
+
+    def __init__(self, store, prefix: str):
+        self.store, self.prefix = store, prefix
+
+    def set(self, k, v):
+        self.store.set(f"{self.prefix}/{k}", v)
+
+    def get(self, k):
+        return self.store.get(f"{self.prefix}/{k}")

@@ -14,9 +14,9 @@ const char* kStatNames[] = {
     "rounds",           "skipped_rounds",     "scatter_pushed",  "scatter_outdated", "scatter_conflict",
     "gather_pushed",    "gather_outdated",    "gather_conflict", "reduce_threshold", "reduce_forced",
     "complete_threshold", "complete_forced",  "timeouts",        "landed_chunks",    "missing_chunks",
-    "dead_skips",       "reduce_contribs",
+    "dead_skips",       "reduce_contribs",    "reduce_abandoned",
 };
-const char* kReasons[] = {"wait", "threshold", "unreachable", "catch_up", "host_force", "timeout"};
+const char* kReasons[] = {"wait", "threshold", "unreachable", "catch_up", "host_force", "timeout", "abandoned"};
 }  // namespace
 
 void bind_onesided(py::module_& m) {
@@ -58,7 +58,7 @@ void bind_onesided(py::module_& m) {
              py::dict d;
              d["call"] = call;
              d["round"] = c.round;
-             d["reason"] = c.round >= 0 && c.reason >= 0 && c.reason < 6 ? kReasons[c.reason] : "pending";
+             d["reason"] = c.round >= 0 && c.reason >= 0 && c.reason < 7 ? kReasons[c.reason] : "pending";
              d["landed_chunks"] = c.landed_chunks;
              d["forced_chunks"] = c.forced_chunks;
              return d;
@@ -98,6 +98,12 @@ void bind_onesided(py::module_& m) {
              return out;
            })
       .def("deliver", &OneSidedLane::deliver)
+      .def("outbox_bytes", [](const OneSidedLane& l, int64_t i) { return py::bytes(l.outbox_bytes(i)); })
+      .def("inject",
+           [](OneSidedLane& l, int32_t phase, int32_t dst, int32_t k, int32_t j, uint32_t r, uint32_t cnt,
+              py::bytes data) { l.inject(phase, dst, k, j, r, cnt, std::string(data)); },
+           py::arg("phase"), py::arg("dst"), py::arg("chunk"), py::arg("part"), py::arg("round"),
+           py::arg("count") = 0, py::arg("data") = py::bytes(""))
       .def("drop", &OneSidedLane::drop)
       .def("note_replays", &OneSidedLane::note_replays)
       .def("error", &OneSidedLane::error)

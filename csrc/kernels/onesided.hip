@@ -196,13 +196,27 @@ __device__ void decide_role(const Args& a, uint32_t r, int32_t k) {
       }
       verdict = evaluate(landed, pending, a.need_r, r, seen_max<DevMem>(fl, L, me), a.max_lag, sys_load(a.force),
                          wall_clock64() > deadline);
-      mask_s = mask;
+      // the round completed without this chunk: like the reference, which
+      // drops scatters of a completed round (W:155-156), it is never reduced
+      if (verdict == kWait && sys_load(a.loc + L.state(kComp)) == r + 1u) verdict = kAbandoned;
+      mask_s = verdict == kAbandoned ? 0u : mask;
     }
     __syncthreads();
     if (verdict != kWait) break;
     __builtin_amdgcn_s_sleep(8);
   }
   const uint32_t mask = mask_s;
+  if (verdict == kAbandoned) {
+    if (threadIdx.x == 0) {
+      DevMem::st(fl + L.fired(row, k), r + 1u);
+      stat_add(a, kReduceAbandoned, 1);
+    }
+    if (threadIdx.x < P) sys_store(a.loc + L.okq(k, threadIdx.x), 0u);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) st64(a.loc + L.dec(k), uint64_t(r + 1u));  // empty mask: the pieces skip
+    return;
+  }
   if (threadIdx.x == 0) {
     DevMem::st(fl + L.fired(row, k), r + 1u);  // late senders of round <= r now skip
     if (verdict == kThreshold) {
@@ -408,7 +422,7 @@ __device__ void reduce_piece(const Args& a, uint32_t r, int32_t k, int32_t j, in
   const int64_t per = ((n + a.nsub - 1) / a.nsub + 63) / 64 * 64;
   const int64_t lo = min(n, int64_t(s) * per), hi = min(n, lo + per);
   bool fenced = false;
-  if (hi > lo) fenced = masked_sum<T, NS>(a, row, mask_s, okq_s, part_off(a, k, j) + lo, hi - lo);
+  if (hi > lo && mask_s != 0u) fenced = masked_sum<T, NS>(a, row, mask_s, okq_s, part_off(a, k, j) + lo, hi - lo);
   // (uniform: the alignment of a piece is the same for every thread)
   if (fenced) release_wg();
   else drain_wg();
@@ -419,7 +433,7 @@ __device__ void reduce_piece(const Args& a, uint32_t r, int32_t k, int32_t j, in
       const uint32_t okq = okq_s;
       for (int32_t q = 0; q < N; ++q)
         if ((okq >> q) & 1u) DevMem::st(a.tab->fl[q] + L.gtag(row, me, k, j), tag_done(r));
-      if ((add_loc(a.loc + L.kctr(k), 1u) + 1u) % uint32_t(P) == 0u)
+      if ((add_loc(a.loc + L.kctr(k), 1u) + 1u) % uint32_t(P) == 0u && mask_s != 0u)
         sys_store(a.loc + L.odone(k), r + 1u);  // chunk k reduced: it counts towards my completion
     }
   }

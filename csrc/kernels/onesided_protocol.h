@@ -192,6 +192,7 @@ enum Stat : int32_t {
   kMissingChunks,
   kDeadSkips,            // pushes not made because the peer is marked dead
   kReduceContribs,       // sum of reduce counts (popcount of the masks)
+  kReduceAbandoned,      // my chunks never reduced: the round completed first (W:155-156 drops their scatters)
   kNumStats = 20,
 };
 
@@ -203,6 +204,7 @@ enum Verdict : int32_t {
   kCatchUp = 3,      // a peer pushed a round beyond r + maxLag (W:100-106)
   kHostForce = 4,    // the host forced the round (close / dead peers)
   kTimeout = 5,      // bounded wait expired: forced, and the lane reports an error
+  kAbandoned = 6,    // (a chunk's wait only) the round completed first: the chunk is not reduced
 };
 
 OS_HD inline int32_t evaluate(int32_t landed, int32_t pending, int32_t need, uint32_t r, int64_t seen_max,

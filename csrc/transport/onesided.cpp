@@ -519,6 +519,26 @@ void OneSidedLane::deliver(int64_t i) {
   exec(m, nullptr);
 }
 
+std::string OneSidedLane::outbox_bytes(int64_t i) const {
+  AKKA_CHECK(i >= 0 && i < int64_t(outbox_.size()), "onesided lane: no such outbox entry");
+  const Msg& m = outbox_[size_t(i)];
+  return std::string(m.bytes.begin(), m.bytes.end());
+}
+
+void OneSidedLane::inject(int32_t phase, int32_t dst, int32_t k, int32_t j, uint32_t r, uint32_t cnt,
+                          const std::string& bytes) {
+  AKKA_CHECK(ready_ && device_ < 0, "onesided lane: inject drives the CPU backend");
+  AKKA_CHECK(phase == 0 || phase == 1, "onesided lane: phase 0 (scatter) or 1 (gather)");
+  AKKA_CHECK(dst >= 0 && dst < g_.N && dst != me_, "onesided lane: bad destination");
+  const int32_t blk = phase == 0 ? dst : me_;
+  AKKA_CHECK(k >= 0 && k < g_.num_chunks(blk) && j >= 0 && j < P_, "onesided lane: no such chunk part");
+  const int64_t clen = std::min(g_.C, g_.block_len(blk) - int64_t(k) * g_.C);
+  const int64_t n = std::max<int64_t>(0, std::min(part_len_, clen - int64_t(j) * part_len_));
+  AKKA_CHECK(int64_t(bytes.size()) == n * int64_t(es_), "onesided lane: injected part has the wrong size");
+  Msg m{phase, dst, k, j, r, cnt, std::vector<char>(bytes.begin(), bytes.end())};
+  exec(m, nullptr);
+}
+
 void OneSidedLane::drop(int64_t i) {
   AKKA_CHECK(i >= 0 && i < int64_t(outbox_.size()), "onesided lane: no such outbox entry");
   outbox_.erase(outbox_.begin() + i);
@@ -662,6 +682,14 @@ bool OneSidedLane::try_complete(bool timed_out) {
     dump("complete", -1);
   }
   HostMem::st(fl + L_.done(), r + 1u);  // senders of round <= r now skip me
+  // my chunks still waiting are never reduced: the round completed first
+  // (the reference drops scatters of a completed round, W:155-156)
+  for (int32_t k = 0; k < kme; ++k)
+    if (!cr_.decided[size_t(k)]) {
+      cr_.decided[size_t(k)] = 1;
+      HostMem::st(fl + L_.fired(row, k), r + 1u);
+      stats_host_[kReduceAbandoned] += 1;
+    }
   for (int32_t k = 0; k < kme; ++k) HostMem::st(fl + L_.sread(row, k), 0u);
   HostMem::st(fl + L_.gread(row), 0u);
   stats_host_[kRounds] += 1;

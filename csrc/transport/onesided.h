@@ -98,6 +98,10 @@ class OneSidedLane {
   // reference's receiver checks a message when it arrives).
   void deliver(int64_t i);
   void drop(int64_t i);
+  std::string outbox_bytes(int64_t i) const;
+  // Play this rank as a TestKit-style peer (AllreduceSpec.scala:812-818): a
+  // push of arbitrary bytes from this rank, through the same gates.
+  void inject(int32_t phase, int32_t dst, int32_t k, int32_t j, uint32_t r, uint32_t cnt, const std::string& bytes);
 
   bool on_gpu() const { return device_ >= 0; }
   int32_t rows() const { return D_; }

@@ -1,0 +1,108 @@
+"""The reference's actor API on the one-sided threshold lane, with master
+pacing (AllreduceMaster.scala:54-63 + AllreduceWorker.scala:7-8, 197-210):
+a master process and 4 worker processes (``--transport onesided``),
+thAllreduce = thReduce = thComplete = 0.75, maxLag 1, one worker's data
+source sleeping 50 ms per round.  The fast workers keep their pace: their
+median round stays within 2x of the same job without the straggler, the
+straggler catches up by skipping rounds (force-completed, W:100-106), and
+every sink sees chunks whose value encodes a contributor set of the size of
+its count.  CPU processes here (shared-memory windows, the GPU kernels'
+protocol functions); tests/test_cluster_onesided_gpu.py runs the same job
+with every worker on the box's GPU."""
+import glob
+import json
+import os
+import socket
+import statistics
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def run_job(device="cpu", delay_ms=0.0, rounds=64, size=1 << 14, chunk=1 << 10, workers=4, timeout=240):
+    port = _port()
+    base = [sys.executable, "-m", "akka_allreduce_amd", "--log-level", "WARNING"]
+    with tempfile.TemporaryDirectory() as out:
+        master = subprocess.Popen(base + ["master", "--port", str(port), "--workers", str(workers), "--data-size",
+                                          str(size), "--max-chunk-size", str(chunk), "--max-round", str(rounds - 1),
+                                          "--max-lag", "1", "--th-allreduce", "0.75", "--th-reduce", "0.75",
+                                          "--th-complete", "0.75", "--transport", "onesided"],
+                                  cwd=ROOT, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
+        t_end = time.time() + 60
+        while time.time() < t_end:
+            try:
+                socket.create_connection(("127.0.0.1", port), timeout=0.5).close()
+                break
+            except OSError:
+                time.sleep(0.1)
+        procs = []
+        for i in range(workers):
+            d = delay_ms if i == workers - 1 else 0.0
+            procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "cluster_onesided_ranks.py"),
+                                           "--master", f"127.0.0.1:{port}", "--size", str(size), "--device", device,
+                                           "--delay-ms", str(d), "--out-dir", out, "--timeout-s", str(timeout - 30)],
+                                          cwd=ROOT, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True))
+            if i < workers - 1:
+                time.sleep(0.3)  # join order = ids: the straggler joins last (id 3)
+        errs = []
+        try:
+            for p in procs:
+                p.wait(timeout=timeout)
+                errs.append(p.stderr.read()[-2000:])
+            master.wait(timeout=30)
+        finally:
+            for p in procs + [master]:
+                if p.poll() is None:
+                    p.kill()
+                    p.wait()
+        rows = [json.load(open(f)) for f in glob.glob(os.path.join(out, "worker*.json"))]
+    return rows, errs
+
+
+def fast_median_ms(rows):
+    meds = []
+    for r in rows:
+        if r["straggler"]:
+            continue
+        t = [x["t"] for x in r["records"]]
+        gaps = [(b - a) * 1e3 for a, b in zip(t, t[1:])]
+        tail = gaps[len(gaps) // 2:]
+        meds.append(statistics.median(tail))
+    return max(meds)
+
+
+def check_job(device, rounds=64, slack_ms=2.0, **kw):
+    base, e0 = run_job(device, 0.0, rounds, **kw)
+    assert len(base) == 4, e0
+    strag, e1 = run_job(device, 50.0, rounds, **kw)
+    assert len(strag) == 4, e1
+    for rows in (base, strag):
+        for r in rows:
+            assert r["finished"] and not r["errors"], r["errors"]
+            assert all(x["bad"] == 0 for x in r["records"]), r["id"]
+            rs = [x["round"] for x in r["records"]]
+            assert rs == sorted(rs) and len(set(rs)) == len(rs), rs[:20]
+    for r in base:
+        assert [x["round"] for x in r["records"]] == list(range(rounds))
+    b, s = fast_median_ms(base), fast_median_ms(strag)
+    assert s <= 2 * b + slack_ms, (b, s)
+    st = [r for r in strag if r["straggler"]][0]
+    assert st["forced_rounds"] > 0 and len(st["records"]) < rounds + st["forced_rounds"] + 1
+    fast = [r for r in strag if not r["straggler"]]
+    for r in fast:
+        assert r["records"][-1]["round"] == rounds - 1
+        assert min(x["mean_count"] for x in r["records"]) >= 2.0  # 3 of 4 contributors at least on most chunks
+    return b, s
+
+
+def test_cluster_onesided_master_pacing_cpu():
+    check_job("cpu")

@@ -1,0 +1,17 @@
+"""GPU twin of tests/test_cluster_onesided.py: a master process and 4 worker
+processes on the box's one MI355X (``--transport onesided``: windows in HBM
+mapped through IPC handles, rounds on the gfx950 kernels), thAllreduce =
+thReduce = thComplete = 0.75, maxLag 1, one worker's data source sleeping
+50 ms per round, 64 rounds: the fast workers' median round stays within 2x
+of the straggler-free job, sinks see consistent contributor sets, the
+straggler catches up by skipping rounds."""
+import pytest
+
+from test_cluster_onesided import check_job
+
+pytestmark = pytest.mark.gpu
+
+
+def test_cluster_onesided_master_pacing_gpu():
+    b, s = check_job("cuda", slack_ms=1.0, size=1 << 20, chunk=1 << 16)
+    print(f"fast workers' median ms per round: {b:.3f} without, {s:.3f} with the straggler")

@@ -126,7 +126,9 @@ def test_onesided_shallow_ring_with_lagging_rank():
     for d in rows:
         for ph in ("no_straggler", "straggler"):
             assert d[ph]["bad_chunks"] == 0, (d["rank"], ph)
-    assert sum(d["stats"]["scatter_conflict"] + d["stats"]["gather_conflict"] for d in rows) >= 0
+    # whether a conflict happens here depends on timing; the hand-shake itself
+    # is forced deterministically in tests/test_onesided_spec.py
+    # (test_overwrite_handshake_drops_writes_into_a_row_being_read)
 
 
 def test_onesided_layout_disjoint():

@@ -44,7 +44,7 @@ def test_onesided_gpu_straggler_steady_state():
             assert d[ph]["bad_chunks"] == 0 and d[ph]["own_block_has_me"], (d["rank"], ph)
     for d in rows[:3]:
         base, strag = _median_tail(d["no_straggler"]["ms"]), _median_tail(d["straggler"]["ms"])
-        assert strag <= 2 * base + 1.0, (d["rank"], base, strag)
+        assert strag <= 2 * base + 0.2, (d["rank"], base, strag)
     s = rows[3]["stats"]
     assert s["skipped_rounds"] > 0 and s["scatter_outdated"] + s["gather_outdated"] > 0, s
 
