@@ -199,8 +199,10 @@ class GraphedDPStep:
     """``dp_sgd_step`` with the forward + backward captured once in a HIP
     graph (``torch.cuda.CUDAGraph``): a step is two input copies, one graph
     replay, then the gradient allreduce and the fused average + SGD pass,
-    eagerly -- the allreduce keeps its own per-round host protocol (round
-    ids, peer flags), so it stays outside the graph.  The ~30 launches of
+    eagerly -- an allreduce with a per-round host protocol (the engine's
+    lanes) stays outside the graph.  ``allreduce=`` a capturable one (the
+    one-sided lane, ``OneSidedAllreduce``) and ``lr=`` capture the WHOLE
+    step: forward, backward, allreduce and update in one replay.  The ~30 launches of
     the forward/backward cost one replay instead of ~10 µs of host time each
     (the step is otherwise host-bound at this size).
 
@@ -211,7 +213,8 @@ class GraphedDPStep:
     fine (they refresh the shadow before the replay)."""
 
     def __init__(self, model: "MLP", bucket: GradientBucket, x: torch.Tensor, y: torch.Tensor,
-                 compute_dtype: Optional[torch.dtype] = None, shadow_weights: bool = True, warmup: int = 3):
+                 compute_dtype: Optional[torch.dtype] = None, shadow_weights: bool = True, warmup: int = 3,
+                 allreduce: Optional[AllreduceFn] = None, lr: Optional[float] = None):
         if not (x.is_cuda and isinstance(model, MLP)):
             raise ValueError("GraphedDPStep: an MLP on a GPU")
         if bucket.pflat is None or not bucket.bound() or not bucket.params_bound():
@@ -232,15 +235,35 @@ class GraphedDPStep:
         self._seed = torch.ones((), dtype=torch.float32, device=x.device)
         self._ptrs = self._pointers()
 
+        # Whole-step capture: an allreduce whose rounds keep their protocol
+        # state on the device (``capturable``: the one-sided lane's call id,
+        # round and decisions live in device memory, its launch arguments are
+        # the same every call) is captured too, with the fused average + SGD
+        # update behind it -- a step is then ONE graph replay.
+        self.allreduce = allreduce if (allreduce is not None and getattr(allreduce, "capturable", False)) else None
+        if allreduce is not None and self.allreduce is None:
+            raise ValueError("GraphedDPStep: this allreduce keeps host-side round state; pass it at call time")
+        if self.allreduce is not None and lr is None:
+            raise ValueError("GraphedDPStep: a captured update needs its learning rate")
+        self.lr = lr
+        self._out = torch.empty_like(bucket.flat) if self.allreduce is not None else None
+        self.replays = 0
+
         def fb():
-            return _forward_backward(model, self.sx, self.sy, bucket, compute_dtype, True, shadow_weights, True,
+            loss = _forward_backward(model, self.sx, self.sy, bucket, compute_dtype, True, shadow_weights, True,
                                      grad_seed=self._seed)
+            if self.allreduce is not None:
+                bucket.sgd_from(self.allreduce, float(lr), out_buf=self._out)
+            return loss
 
         # warm up and capture on ONE stream: the kernels' per-stream workspaces
         # (colsum / cross-entropy tickets) are created, and zeroed, by the
         # warmup, so the graph holds no fill for them
         side = torch.cuda.Stream(device=x.device)
         side.wait_stream(torch.cuda.current_stream(x.device))
+        # a captured update changes the parameters in the warmup steps: they
+        # are put back afterwards (the warmup's rounds still ran on every rank)
+        snap = bucket.pflat.clone() if self.allreduce is not None else None
         with torch.cuda.stream(side):
             for _ in range(warmup):
                 fb()
@@ -252,6 +275,11 @@ class GraphedDPStep:
         with torch.cuda.graph(self.graph, stream=side):
             self.loss = fb().detach()
         torch.cuda.current_stream(x.device).wait_stream(side)
+        if snap is not None:
+            bucket.pflat.copy_(snap)
+            if bucket.sflat is not None:
+                bucket.sflat.copy_(bucket.pflat)
+            bucket._shadow_versions = [p._version for p in bucket.params]
         self._ptrs = self._pointers()  # the shadow exists now
 
     def static_inputs(self):
@@ -275,8 +303,19 @@ class GraphedDPStep:
             self.sx.copy_(x)
         if y.data_ptr() != self.sy.data_ptr():
             self.sy.copy_(y)
-        self.graph.replay()
-        b.sgd_from(allreduce, lr)
+        if self.allreduce is not None:
+            if allreduce is not None and allreduce is not self.allreduce:
+                raise RuntimeError("GraphedDPStep: the step captured another allreduce")
+            if lr != self.lr:
+                raise RuntimeError(f"GraphedDPStep: the update was captured with lr={self.lr}")
+            self.graph.replay()  # forward + backward + allreduce + fused update
+            self.replays += 1
+            self.allreduce.note_replays(1)
+            if b._shadow_on:
+                b._shadow_versions = [p._version for p in b.params]
+        else:
+            self.graph.replay()
+            b.sgd_from(allreduce, lr)
         return float(self.loss) if sync_loss else self.loss
 
 

@@ -187,6 +187,7 @@ class ThresholdAllreduce:
         share_transport_with: Optional["ThresholdAllreduce"] = None,
         ipc_capacity: int = 0,
     ):
+        self._lane_os = False  # exact rounds on the one-sided lane (use_lane("onesided"))
         if transport == "onesided":
             # thresholds over mapped peer windows: no send ever waits for a
             # peer (parallel/onesided.py, csrc/transport/onesided.h)
@@ -299,6 +300,8 @@ class ThresholdAllreduce:
         self._ipc_capacity = int(ipc_capacity)
         self._iid = ThresholdAllreduce._instances
         self._ipc_epoch = 0
+        self._exact_os = None  # the one-sided lane at thresholds 1 (lane "onesided")
+        self._th_exact = th_reduce >= 1.0 and th_complete >= 1.0
         if data_plane == "ipc" and self.world_size > 1:
             self.enable_ipc()
             lane = "ipc"
@@ -348,7 +351,12 @@ class ThresholdAllreduce:
             return o
         if self.pacer is not None:
             self.pacer.wait_start(r, self.worker.poll if self.transport == "reactive" else None)
-        out = self.worker.allreduce(x, async_op=async_op, out=out)
+        if self._lane_os:
+            # exact rounds on the one-sided lane (tune candidate "onesided"):
+            # valid in the caller's stream order, like an async round
+            out = self._exact_os(x, out=out)
+        else:
+            out = self.worker.allreduce(x, async_op=async_op, out=out)
         if out is None:
             raise RuntimeError("round did not complete (thresholds need every rank in the scheduled transport)")
         self._round += 1
@@ -361,6 +369,7 @@ class ThresholdAllreduce:
         csrc/transport/stream_link.h) -- every rank must switch at the same round."""
         if self.transport != "stream":
             raise ValueError("lanes belong to the scheduled (stream) transport")
+        self._lane_os = False
         self.worker.set_lane(lane)
 
     def enable_ipc(self) -> None:
@@ -447,11 +456,39 @@ class ThresholdAllreduce:
         # store can beat a remote read, which the shared-card rehearsals cannot
         # show (both stay inside one card's HBM there)
         "ipc_fused_bcast_lite": ("ipc", -1, "bcast", True, 1024, True),
+        # the one-sided threshold lane at thresholds 1 (enable_onesided): one
+        # role-partitioned launch, each chunk reduced and pushed as soon as
+        # its copies landed, peer chunks copied out as they land
+        "onesided": ("onesided", -1, None, False, 0, False),
     }
+
+    def enable_onesided(self) -> None:
+        """Map the one-sided threshold lane (parallel/onesided.py) for this
+        buffer at thresholds 1: exact rounds as the lane's role-partitioned
+        launch (per-chunk reduce + push the moment a chunk's copies landed).
+        Collective, like enable_ipc."""
+        if self._exact_os is not None:
+            return
+        if self.device.type != "cuda" or self.world_size < 2:
+            raise ValueError("the onesided lane needs GPUs and N > 1")
+        if not self._th_exact:
+            raise ValueError("lane 'onesided' of this engine runs exact rounds (thresholds 1); use "
+                             "transport='onesided' for threshold rounds")
+        from .onesided import OneSidedAllreduce
+
+        g = self.worker.geometry
+        self._exact_os = OneSidedAllreduce(self.data_size, max_chunk_size=int(g.maxChunkSize), dtype=self.worker.dtype,
+                                           th_reduce=1.0, th_complete=1.0, max_lag=1, rank=self.rank,
+                                           world_size=self.world_size, device=self.device, store=self.store)
 
     def use_lane(self, name: str) -> None:
         """Switch to a named lane candidate (see LANES); every rank must do the
         same at the same round."""
+        if name == "onesided":
+            self.enable_onesided()
+            self._lane_os = True
+            return
+        self._lane_os = False
         ln, unit, mode, fused, threads, lite = self.LANES[name]
         self.set_lane(ln)
         if ln == "ipc":
@@ -499,6 +536,17 @@ class ThresholdAllreduce:
                 if ipc_open:
                     cands += ["ipc", "ipc_bcast", "ipc_fused", "ipc_fused_bcast", "ipc_wide", "ipc_bcast_wide",
                               "ipc_lite", "ipc_bcast_lite", "ipc_fused_lite", "ipc_fused_bcast_lite"]
+                if self._th_exact:
+                    err = None
+                    try:
+                        self.enable_onesided()
+                    except Exception as e:  # noqa: BLE001 - the candidate is skipped on every rank
+                        err = f"{type(e).__name__}: {e}"[:200]
+                    if self._agree_max([1.0 if err else 0.0])[0] == 0.0:
+                        cands.append("onesided")
+                    else:
+                        res["onesided"] = {"exact": None, "ms": None,
+                                           "error": err or "another rank could not map its one-sided windows"}
         S, N, r = self.data_size, self.world_size, self.rank
         dtype = self.worker.dtype
         x = torch.randn(S, device=self.device).to(dtype)
@@ -586,6 +634,12 @@ class ThresholdAllreduce:
         return [float(v) for v in t.cpu().tolist()]
 
     def state(self) -> dict:
+        if self._lane_os:
+            st = self.worker.state()
+            link = dict(st.get("link", {}))
+            link["lane"] = "onesided"
+            link["onesided"] = {**self._exact_os.info(), "stats": self._exact_os.stats()}
+            return {**st, "link": link}
         if self.transport == "onesided":
             return {"link": {"lane": "onesided", "onesided": {**self._os.info(), "stats": self._os.stats()}},
                     "stats": {"rounds_forced": self._os.stats()["complete_forced"]}}

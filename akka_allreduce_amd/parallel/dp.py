@@ -156,14 +156,16 @@ class GradientBucket:
         return out
 
 
-    def sgd_from(self, allreduce: Optional[AllreduceFn], lr: float) -> Optional[AllReduceOutput]:
+    def sgd_from(self, allreduce: Optional[AllreduceFn], lr: float,
+                 out_buf: Optional[torch.Tensor] = None) -> Optional[AllReduceOutput]:
         """Average the gradients over the contributors and apply SGD.  With
         flattened parameters this is one fused pass over the allreduce output
-        (no averaged-gradient tensor is written)."""
+        (no averaged-gradient tensor is written).  ``out_buf``: the round's
+        output buffer (reused; a captured step needs fixed buffers)."""
         if allreduce is None:
             sgd_step(self.params, lr)
             return None
-        out = allreduce(self.flat)
+        out = allreduce(self.flat) if out_buf is None else allreduce(self.flat, out=out_buf)
         if self.pflat is not None and out.data.dtype == self.pflat.dtype:
             out.axpy_mean_(self.pflat, -lr, shadow=self.sflat if self._shadow_on else None)
         else:

@@ -144,16 +144,29 @@ class OneSidedAllreduce:
         dev_index = self.device.index if self.device.type == "cuda" else -1
         if dev_index is None:
             dev_index = torch.cuda.current_device()
-        self.lane = n.OneSidedLane(dev_index, self.data_size, self.world_size, int(max_chunk_size), self.rank,
-                                   _DTYPES[dtype], th_reduce=float(th_reduce), th_complete=float(th_complete),
-                                   max_lag=int(max_lag), rows=int(rows), part_bytes=int(part_bytes),
-                                   timeout_ms=int(timeout_s * 1000), threads=int(threads),
-                                   role_wgs=int(role_wgs))
         self.th_reduce, self.th_complete, self.max_lag = float(th_reduce), float(th_complete), int(max_lag)
         iid = OneSidedAllreduce._instances
         OneSidedAllreduce._instances += 1
         exchange = _handle_exchange(self.rank, self.world_size, store, f"akka/onesided/{iid}")
-        handles = exchange(self.lane.handle())
+        # every rank takes part in the exchange even if its own window failed
+        # (an empty handle): a local failure raises on EVERY rank, none is
+        # left blocked in the collective
+        err = None
+        try:
+            self.lane = n.OneSidedLane(dev_index, self.data_size, self.world_size, int(max_chunk_size), self.rank,
+                                       _DTYPES[dtype], th_reduce=float(th_reduce), th_complete=float(th_complete),
+                                       max_lag=int(max_lag), rows=int(rows), part_bytes=int(part_bytes),
+                                       timeout_ms=int(timeout_s * 1000), threads=int(threads),
+                                       role_wgs=int(role_wgs))
+            mine = self.lane.handle()
+        except Exception as e:  # noqa: BLE001 - re-raised after the exchange
+            mine, err = b"", e
+        handles = exchange(mine)
+        if err is not None:
+            raise err
+        missing = [i for i, h in enumerate(handles) if not h]
+        if missing:
+            raise RuntimeError(f"onesided lane: ranks {missing} could not create their windows")
         self.lane.open(handles)
         # every rank mapped every window: names may go (a killed rank leaves no shm behind)
         exchange_done = _handle_exchange(self.rank, self.world_size, store, f"akka/onesided/{iid}/opened")
@@ -194,6 +207,18 @@ class OneSidedAllreduce:
         if self.data_sink is not None:
             self.data_sink(o)
         return o
+
+    @property
+    def capturable(self) -> bool:
+        """A call can be captured in a HIP graph (GPU): its launches take the
+        same arguments every call (with ``out`` given) and the lane's round /
+        call sequence lives in device memory.  After each replay of a captured
+        call, ``note_replays(1)`` keeps the host's call ids in step."""
+        return self.device.type == "cuda" and self.data_sink is None
+
+    def note_replays(self, n: int) -> None:
+        self.lane.note_replays(int(n))
+        self.calls += int(n)
 
     def _expand(self, per_chunk: torch.Tensor) -> torch.Tensor:
         g = self.geometry

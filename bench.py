@@ -383,6 +383,17 @@ def apply_lane_choice(ar, name) -> None:
     chose (ThresholdAllreduce.LANES); None: leave auto."""
     if not name or ar.world_size < 2 or ar.transport != "stream":
         return
+    if name == "onesided":
+        try:
+            ar.enable_onesided()  # collective; a failure on any rank raises on every rank
+        except Exception as e:  # noqa: BLE001 - keep the job on the framework's p2p lane
+            from akka_allreduce_amd.utils.phases import progress
+
+            progress(f"rank {ar.rank}: onesided lane unavailable for this buffer ({type(e).__name__}: "
+                     f"{str(e)[:120]}); the framework's p2p lane instead")
+            ar.use_lane("p2p")
+            ar.lane_fallback = f"onesided -> p2p ({type(e).__name__})"
+            return
     if name.startswith("ipc") and not ar.state().get("link", {}).get("ipc"):
         try:
             ar.enable_ipc()  # collective; fails alike on every rank (e.g. a window too large for one mapping)
@@ -932,6 +943,7 @@ def main() -> int:
     line["config"] = dict(base["config"])
     line["config"].update({
         "transport": ("xgmi-ipc" if str(lane_used).startswith("ipc") else
+                      "xgmi-onesided" if lane_used == "onesided" else
                       "xgmi-mailbox-p2p" if args.data_plane == "ipc_p2p" else
                       "rccl-pair-reactive" if ar.transport == "reactive" else "rccl-p2p-xgmi")
         if world > 1 and dev.type == "cuda" else ("gloo-p2p" if world > 1 else "local"),

@@ -107,34 +107,55 @@ __device__ uint32_t wait_begun(const Args& a) {
 }
 
 // ---- push: phase 1, fire and forget -----------------------------------------------
+// The gates of a workgroup's items run first, one lane per item, so their
+// remote round trips (owner's fired word, the writing marker, its read
+// announcement: ~µs each over xGMI) overlap instead of preceding every copy;
+// then the workgroup copies its items one by one.
+constexpr int kGateBatch = 256;
+
 template <int ES>
 __device__ void push_role(const Args& a, uint32_t r, int32_t w0, int32_t stride) {
   const Layout& L = a.L;
   const int32_t N = L.N, P = L.P;
   const int32_t items = (N - 1) * L.Kmax * P;
   const int32_t row = int32_t(r % uint32_t(L.D));
-  __shared__ int32_t go;
-  for (int32_t w = w0; w < items; w += stride) {
-    // chunk-major, peers rotated from me + 1: a chunk lands everywhere early
-    // (its owner can reduce it while later chunks are still moving) and
-    // consecutive workgroups feed different links
+  __shared__ int8_t go_s[kGateBatch];
+  // chunk-major, peers rotated from me + 1: a chunk lands everywhere early
+  // (its owner can reduce it while later chunks are still moving) and
+  // consecutive workgroups feed different links
+  auto item = [&](int32_t w, int32_t& p, int32_t& k, int32_t& j) {
     const int32_t i = w % (N - 1), kj = w / (N - 1);
-    const int32_t k = kj / P, j = kj % P;
-    const int32_t p = (a.me + 1 + i) % N;
-    if (k >= a.tab->nch[p]) continue;  // uniform over the workgroup
-    uint32_t* ofl = a.tab->fl[p];
-    if (threadIdx.x == 0) {
-      int32_t g = kDead;
-      if (!sys_load(a.dead + p)) {
-        if (k == 0 && j == 0) DevMem::st(ofl + L.seen(a.me), r + 1u);  // implicit start at the owner
-        g = scatter_gate<DevMem>(ofl, L, row, a.me, k, j, r);
+    k = kj / P;
+    j = kj % P;
+    p = (a.me + 1 + i) % N;
+  };
+  for (int32_t base = w0; base < items; base += stride * kGateBatch) {
+    for (int32_t t = threadIdx.x; t < kGateBatch; t += blockDim.x) {
+      const int32_t w = base + t * stride;
+      int32_t g = -1;  // no such item / no such chunk
+      if (w < items) {
+        int32_t p, k, j;
+        item(w, p, k, j);
+        if (k < a.tab->nch[p]) {
+          g = kDead;
+          if (!sys_load(a.dead + p)) {
+            uint32_t* ofl = a.tab->fl[p];
+            if (k == 0 && j == 0) DevMem::st(ofl + L.seen(a.me), r + 1u);  // implicit start at the owner
+            g = scatter_gate<DevMem>(ofl, L, row, a.me, k, j, r);
+          }
+          stat_add(a, g == kGo ? kScatterPushed : g == kOutdated ? kScatterOutdated
+                                                  : g == kConflict ? kScatterConflict : kDeadSkips, 1);
+        }
       }
-      go = g;
-      stat_add(a, g == kGo ? kScatterPushed : g == kOutdated ? kScatterOutdated : g == kConflict ? kScatterConflict
-                                                                                               : kDeadSkips, 1);
+      go_s[t] = int8_t(g);
     }
     __syncthreads();
-    if (go == kGo) {
+    for (int32_t t = 0; t < kGateBatch; ++t) {
+      const int32_t w = base + t * stride;
+      if (w >= items) break;
+      if (go_s[t] != kGo) continue;  // uniform over the workgroup
+      int32_t p, k, j;
+      item(w, p, k, j);
       const int64_t n = part_len_of(a, p, k, j);
       const int64_t off = part_off(a, k, j);
       char* dst = a.tab->sd[row][p] + (int64_t(a.me) * a.slot + off) * ES;
@@ -146,9 +167,9 @@ __device__ void push_role(const Args& a, uint32_t r, int32_t w0, int32_t stride)
       }
       if (lite) drain_wg();
       else release_wg();
-      if (threadIdx.x == 0) DevMem::st(ofl + L.stag(row, a.me, k, j), tag_done(r));
+      if (threadIdx.x == 0) DevMem::st(a.tab->fl[p] + L.stag(row, a.me, k, j), tag_done(r));
     }
-    __syncthreads();  // `go` is rewritten by the next item
+    __syncthreads();  // go_s is rewritten by the next batch
   }
 }
 
@@ -400,14 +421,17 @@ __device__ void reduce_piece(const Args& a, uint32_t r, int32_t k, int32_t j, in
   __shared__ uint32_t mask_s, okq_s;
   if (threadIdx.x == 0) {
     uint64_t d = ld64(a.loc + L.dec(k));
+    bool gated = true;
     if (wait_decision) {
       // the decider is a lower workgroup id and ends every wait itself; the
-      // bound here only guards against a broken decider
+      // bound here only guards against a broken decider: then nothing is
+      // reduced or pushed (no gate ran for this round)
       const uint64_t deadline = wall_clock64() + 2 * a.timeout + 1;
       while (uint32_t(d) != r + 1u) {
         if (wall_clock64() > deadline) {
           set_err(a);
-          d = (uint64_t(1u << me) << 32) | uint64_t(r + 1u);
+          d = uint64_t(r + 1u);
+          gated = false;
           break;
         }
         __builtin_amdgcn_s_sleep(2);
@@ -415,7 +439,7 @@ __device__ void reduce_piece(const Args& a, uint32_t r, int32_t k, int32_t j, in
       }
     }
     mask_s = uint32_t(d >> 32);
-    okq_s = sys_load(a.loc + L.okq(k, j));
+    okq_s = gated ? sys_load(a.loc + L.okq(k, j)) : 0u;
   }
   __syncthreads();
   const int64_t n = part_len_of(a, me, k, j);

@@ -9,7 +9,7 @@ export TMPDIR=/tmp
 O=gpurun_out/r04b
 mkdir -p $O/base $O/trace
 timeout -k 10 700 python -u -m pytest -x -v -s --timeout 200 --timeout-method thread tests/test_onesided_gpu.py \
-  tests/test_cluster_onesided_gpu.py \
+  tests/test_cluster_onesided_gpu.py tests/test_graph_step_gpu.py \
   > $O/pytest.log 2>&1 || { echo "pytest rc=$?"; tail -40 $O/pytest.log; exit 1; }
 tail -3 $O/pytest.log
 timeout -k 10 300 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node=4 --master-addr 127.0.0.1 \

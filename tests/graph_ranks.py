@@ -1,0 +1,73 @@
+"""Rank program for tests/test_graph_step_gpu.py: the 2-layer MLP's DP-SGD
+step with the WHOLE step (forward, backward, the one-sided allreduce and the
+fused average + SGD update) captured in one HIP graph, against the eager step
+on the same batches (every rank on the box's one GPU).  Writes rank<i>.pt."""
+import argparse
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out-dir", required=True)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--dtype", default="bf16")
+    a = ap.parse_args()
+    rank = int(os.environ["RANK"])
+    dist.init_process_group("gloo")
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    from akka_allreduce_amd.models.mlp import MLP, GraphedDPStep, dp_sgd_step, synthetic_batch
+    from akka_allreduce_amd.parallel.dp import GradientBucket
+    from akka_allreduce_amd.parallel.onesided import OneSidedAllreduce
+
+    cdt = torch.bfloat16 if a.dtype == "bf16" else None
+    lr = 0.05
+
+    def batches():
+        for s in range(a.steps):
+            g = torch.Generator(device=dev).manual_seed(1000 * s + rank)
+            yield synthetic_batch(64, 256, 10, device=dev, generator=g)
+
+    def fresh():
+        torch.manual_seed(0)
+        m = MLP(256, 512, 10).to(dev)
+        return m, GradientBucket(list(m.parameters()), flatten_params=True)
+
+    m1, b1 = fresh()
+    ar = OneSidedAllreduce(b1.numel, max_chunk_size=1 << 14, device=dev)
+    eager_losses = []
+    for x, y in batches():
+        eager_losses.append(dp_sgd_step(m1, x, y, lr, ar, b1, sync_loss=False, compute_dtype=cdt))
+    eager = b1.pflat.clone()
+
+    m2, b2 = fresh()
+    x0, y0 = next(batches())
+    gs = GraphedDPStep(m2, b2, x0, y0, compute_dtype=cdt, allreduce=ar, lr=lr)
+    sx, sy = gs.static_inputs()
+    graph_losses = []
+    calls0 = ar.calls
+    for x, y in batches():
+        sx.copy_(x)
+        sy.copy_(y)
+        graph_losses.append(gs(sx, sy, lr, None).clone())
+    torch.cuda.synchronize()
+    graphed = b2.pflat.clone()
+    st = ar.stats()
+    torch.save({"eager": eager.cpu(), "graphed": graphed.cpu(), "eager_losses": torch.stack(eager_losses).cpu(),
+                "graph_losses": torch.stack(graph_losses).cpu(), "replays": gs.replays, "calls": ar.calls - calls0,
+                "error": ar.error(), "rounds": st["rounds"], "forced": st["complete_forced"]},
+               os.path.join(a.out_dir, f"rank{rank}.pt"))
+    ar.retire()
+    torch.cuda.synchronize()
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
