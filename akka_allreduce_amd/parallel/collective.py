@@ -188,6 +188,7 @@ class ThresholdAllreduce:
         ipc_capacity: int = 0,
     ):
         self._lane_os = False  # exact rounds on the one-sided lane (use_lane("onesided"))
+        self._direct = None    # an open CapturableExact view
         if transport == "onesided":
             # thresholds over mapped peer windows: no send ever waits for a
             # peer (parallel/onesided.py, csrc/transport/onesided.h)
@@ -351,6 +352,8 @@ class ThresholdAllreduce:
             return o
         if self.pacer is not None:
             self.pacer.wait_start(r, self.worker.poll if self.transport == "reactive" else None)
+        if self._direct is not None:
+            raise RuntimeError("this engine's rounds run through its capturable view now (close() it first)")
         if self._lane_os:
             # exact rounds on the one-sided lane (tune candidate "onesided"):
             # valid in the caller's stream order, like an async round
@@ -462,6 +465,16 @@ class ThresholdAllreduce:
         "onesided": ("onesided", -1, None, False, 0, False),
     }
 
+    def capturable(self) -> "CapturableExact":
+        """A graph-capturable view of this engine's exact rounds (GPU, N > 1):
+        the one-sided lane (lane ``"onesided"``) or the ipc lane with its
+        round id moved to device memory.  Its calls launch the lane's kernels
+        straight on the caller's stream with fixed arguments (give ``out``),
+        so ``GraphedDPStep(allreduce=..., lr=...)`` can capture a whole
+        training step.  Collective (every rank, same round); while it is open
+        the engine's own calls are refused (``close()`` returns to them)."""
+        return CapturableExact(self)
+
     def enable_onesided(self) -> None:
         """Map the one-sided threshold lane (parallel/onesided.py) for this
         buffer at thresholds 1: exact rounds as the lane's role-partitioned
@@ -477,9 +490,13 @@ class ThresholdAllreduce:
         from .onesided import OneSidedAllreduce
 
         g = self.worker.geometry
+        # exact rounds take milliseconds: a 10 s bound ends a misbehaving
+        # lane's waits (forced, error flagged -> rejected by tune) well inside
+        # a job's phase deadlines
         self._exact_os = OneSidedAllreduce(self.data_size, max_chunk_size=int(g.maxChunkSize), dtype=self.worker.dtype,
                                            th_reduce=1.0, th_complete=1.0, max_lag=1, rank=self.rank,
-                                           world_size=self.world_size, device=self.device, store=self.store)
+                                           world_size=self.world_size, device=self.device, store=self.store,
+                                           timeout_s=10.0)
 
     def use_lane(self, name: str) -> None:
         """Switch to a named lane candidate (see LANES); every rank must do the
@@ -589,6 +606,8 @@ class ThresholdAllreduce:
                         val = float(v)
                     elif not v:
                         ok = False
+                    if name == "onesided" and self._exact_os is not None and self._exact_os.error():
+                        ok, err = False, f"{tag}: a bounded wait of the onesided lane expired"
                 except Exception as e:  # noqa: BLE001 - the candidate is rejected
                     ok, err = False, f"{tag}: {type(e).__name__}: {e}"[:160]
                 bad, worst = self._agree_max([0.0 if ok else 1.0, val])
@@ -679,3 +698,59 @@ class ThresholdAllreduce:
                 time.sleep(1e-4)
             if time.monotonic() - t0 > timeout:
                 raise TimeoutError(f"rank {self.rank}: {core.in_flight()} transfers still in flight")
+
+
+class CapturableExact:
+    """Exact rounds of a ``ThresholdAllreduce`` as a capturable callable
+    (``ThresholdAllreduce.capturable()``).  Two lanes:
+
+    * ``onesided``: the engine's one-sided lane (its call id, round and
+      decisions are device-resident by design);
+    * ``ipc``: the engine's ipc lane with DEVICE rounds -- a bump launch
+      advances a device round word in front of every round and the round's
+      kernels read their id there (csrc/kernels/ipc_kernels.h ``round_dev``),
+      so a captured round replays with a fresh id on every rank.
+    The counts of an exact round are N everywhere (a fixed table)."""
+
+    def __init__(self, ar: "ThresholdAllreduce"):
+        if ar.transport != "stream" or ar.world_size < 2 or ar.device.type != "cuda":
+            raise ValueError("capturable rounds need the stream transport on GPUs with N > 1")
+        if not ar._th_exact:
+            raise ValueError("capturable rounds are exact (thresholds 1)")
+        self.ar = ar
+        g = ar.worker.geometry
+        self.geometry = g
+        if ar._lane_os:
+            self.lane = "onesided"
+        elif ar.state().get("link", {}).get("ipc"):
+            self.lane = "ipc"
+            ar.worker._core.ipc_device_rounds(True)  # collective in effect: same round on every rank
+            self.counts = torch.full((g.workerNum, g.kmax), g.workerNum, dtype=torch.int32, device=ar.device)
+        else:
+            raise ValueError("capturable rounds run on the ipc or onesided lane: use_lane() one of them first")
+        ar._direct = self
+
+    @property
+    def capturable(self) -> bool:
+        return True
+
+    def note_replays(self, n: int) -> None:
+        if self.lane == "onesided":
+            self.ar._exact_os.note_replays(n)
+
+    def __call__(self, x: torch.Tensor, out: Optional[torch.Tensor] = None) -> AllReduceOutput:
+        if self.lane == "onesided":
+            return self.ar._exact_os(x, out=out)
+        g = self.geometry
+        if out is None:
+            out = torch.empty_like(x)
+        stream = torch.cuda.current_stream(self.ar.device)
+        self.ar.worker._core.ipc_round_direct(x.data_ptr(), out.data_ptr(), stream.cuda_stream)
+        return AllReduceOutput(out, iteration=-1, counts_per_chunk=self.counts, geometry=g,
+                               expander=self.ar.worker._expand_counts)
+
+    def close(self) -> None:
+        """Back to the engine's own calls (every rank, same round)."""
+        if self.lane == "ipc":
+            self.ar.worker._core.ipc_device_rounds(False)
+        self.ar._direct = None

@@ -281,6 +281,25 @@ class WorkerCore final : public EngineHost {
     if (threads) stream_link_->ipc()->set_threads(threads);
     if (lite >= 0) stream_link_->ipc()->set_lite(lite != 0);
   }
+  // Exact ipc round straight on `stream`, none of the engine's round
+  // bookkeeping (exact rounds: every count is N) -- the graph-capturable
+  // path, with device-resident round ids (ipc_device_rounds(true)).
+  void ipc_round_direct(uintptr_t in, uintptr_t out, uintptr_t stream) {
+    AKKA_CHECK(stream_link_ && stream_link_->ipc(), "ipc_round_direct: the ipc lane is not open");
+    AKKA_CHECK(stream_link_->ipc()->device_rounds(), "ipc_round_direct: switch device rounds on first");
+    stream_link_->ipc()->round(reinterpret_cast<StreamH>(stream), reinterpret_cast<const void*>(in),
+                               reinterpret_cast<void*>(out));
+  }
+  void ipc_device_rounds(bool on) {
+    AKKA_CHECK(stream_link_ && stream_link_->ipc(), "ipc_device_rounds: the ipc lane is not open");
+    py::gil_scoped_release nogil;
+    stream_link_->ipc()->set_device_rounds(on);
+  }
+  uint32_t ipc_current_round() {
+    AKKA_CHECK(stream_link_ && stream_link_->ipc(), "ipc_current_round: the ipc lane is not open");
+    py::gil_scoped_release nogil;
+    return stream_link_->ipc()->current_round();
+  }
   void ipc_close() {
     ipc_pending_.reset();
     if (stream_link_) stream_link_->set_ipc(nullptr);
@@ -727,6 +746,9 @@ PYBIND11_MODULE(_native, m) {
       .def("ipc_open", &WorkerCore::ipc_open)
       .def("ipc_error", &WorkerCore::ipc_error)
       .def("ipc_close", &WorkerCore::ipc_close)
+      .def("ipc_round_direct", &WorkerCore::ipc_round_direct)
+      .def("ipc_device_rounds", &WorkerCore::ipc_device_rounds)
+      .def("ipc_current_round", &WorkerCore::ipc_current_round)
       .def("ipc_set_mode", &WorkerCore::ipc_set_mode, py::arg("mode"), py::arg("fused") = false,
            py::arg("threads") = 0, py::arg("lite") = -1)
       .def("scatter_count", &WorkerCore::scatter_count)

@@ -69,6 +69,10 @@ __device__ bool wait_flag(const IpcArgs& a, uint32_t* f, uint32_t want, uint64_t
   }
 }
 
+// This round's id: a kernel argument, or (graph-capturable rounds) the
+// device word the bump launch in front of the round advanced.
+__device__ inline uint32_t round_of(const IpcArgs& a) { return a.round_dev ? sys_load(a.round_dev) : a.round; }
+
 __device__ inline void signal(uint32_t* f, uint32_t v) {  // lane 0, after release_wg
   __hip_atomic_store(f, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
@@ -234,7 +238,7 @@ __device__ void push_item(const IpcArgs& a, int32_t j, int32_t p) {
   }
   if (lite) drain_wg();
   else release_wg();
-  if (threadIdx.x == 0) signal(a.flags[p] + ipc_flag_push(a.me, j, a.nportions), a.round);
+  if (threadIdx.x == 0) signal(a.flags[p] + ipc_flag_push(a.me, j, a.nportions), round_of(a));
   __syncthreads();
 }
 
@@ -267,7 +271,7 @@ __device__ void reduce_item(const IpcArgs& a, int32_t j, int32_t part) {
   {
     // every peer's push flag polled by a lane of its own: the waits overlap
     const int32_t s = int32_t(threadIdx.x);
-    if (s < N && s != me) ok = wait_flag(a, fl + ipc_flag_push(s, j, np), a.round, wall_clock64() + a.timeout);
+    if (s < N && s != me) ok = wait_flag(a, fl + ipc_flag_push(s, j, np), round_of(a), wall_clock64() + a.timeout);
   }
   ok = settle_waits(a, ok);
   const int64_t e0 = int64_t(j) * a.portion;
@@ -285,9 +289,9 @@ __device__ void reduce_item(const IpcArgs& a, int32_t j, int32_t part) {
   if (threadIdx.x == 0) {
     if (a.bcast) {
       for (int32_t p = 0; p < N; ++p)
-        if (p != me) signal(a.flags[p] + ipc_flag_gather(me, j, part, N, np), a.round);
+        if (p != me) signal(a.flags[p] + ipc_flag_gather(me, j, part, N, np), round_of(a));
     } else {
-      signal(fl + ipc_flag_reduced(j, part, N, np), a.round);
+      signal(fl + ipc_flag_reduced(j, part, N, np), round_of(a));
     }
   }
   __syncthreads();  // `ok` is rewritten by the next item
@@ -305,7 +309,7 @@ __device__ void phase2_item(const IpcArgs& a, int32_t j, int32_t p) {
     if (part < kReduceSplit)
       ok = wait_flag(a, a.bcast ? a.flags[me] + ipc_flag_gather(p, j, part, N, np)
                                 : a.flags[p] + ipc_flag_reduced(j, part, N, np),
-                     a.round, wall_clock64() + a.timeout);
+                     round_of(a), wall_clock64() + a.timeout);
   }
   ok = settle_waits(a, ok);
   const int64_t e0 = int64_t(j) * a.portion;
@@ -507,6 +511,14 @@ int32_t ipc_p2p_resident_wgs(int32_t device) {
   if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&bpm, ipc_p2p_kernel, kThreads, 0) != hipSuccess) bpm = 4;
   if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) cus = 256;
   return std::max(1, bpm) * std::max(1, cus);
+}
+
+__global__ void ipc_round_bump_kernel(uint32_t* p) {
+  if (threadIdx.x == 0) sys_store(p, sys_load(p) + 1u);
+}
+
+void launch_ipc_round_bump(hipStream_t s, uint32_t* round_dev) {
+  hipLaunchKernelGGL(ipc_round_bump_kernel, dim3(1), dim3(64), 0, s, round_dev);
 }
 
 void launch_ipc_round(hipStream_t s, const IpcArgs& a, DType dt) {

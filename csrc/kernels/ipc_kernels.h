@@ -51,6 +51,10 @@ struct IpcArgs {
   int32_t plain_slots = 0;  // measurement only: plain slot loads behind the acquire instead of sc0 sc1 loads
   int32_t lite = 0;         // fence-free hand-offs: write-through window stores + drained flags (xgmi_device.h)
   uint32_t round = 0;       // this round's id (1, 2, ... identical on every rank)
+  // device-resident round id (graph-capturable rounds): when set, the round's
+  // kernels read the id here instead of `round`; a bump launch in front of
+  // the round advances it, so a captured round replays with a fresh id
+  const uint32_t* round_dev = nullptr;
   uint64_t timeout = 0;     // per wait, in wall-clock ticks (100 MHz)
   const char* in = nullptr;  // round input [S]
   char* out = nullptr;       // round output [S]
@@ -143,5 +147,7 @@ double ipc_reduce_role_bench(int32_t N, int64_t block, int64_t portion_bytes, DT
 // bcast = 1, the reducer writes its rows into every peer's gather slot and a
 // local gather copies them out.
 void launch_ipc_round(hipStream_t s, const IpcArgs& a, DType dt);
+// round_dev += 1 (one thread), in stream order before a device-round round.
+void launch_ipc_round_bump(hipStream_t s, uint32_t* round_dev);
 
 }  // namespace akka

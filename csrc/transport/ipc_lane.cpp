@@ -146,6 +146,7 @@ IpcLane::~IpcLane() {
   for (void* m : opened_flags_) hipIpcCloseMemHandle(m);
   if (flags_) hipFree(flags_);
   if (err_host_) hipHostFree(err_host_);
+  if (round_dev_) hipFree(round_dev_);
   // win_: freed by its last owner (IpcWindows::~IpcWindows)
 }
 
@@ -234,6 +235,10 @@ void IpcLane::round(StreamH s, const void* in, void* out) {
   a.N = g_.N;
   a.me = me_;
   a.round = ++round_;
+  if (round_dev_on_) {
+    a.round_dev = round_dev_;
+    launch_ipc_round_bump(static_cast<hipStream_t>(s), round_dev_);
+  }
   a.timeout = timeout_ticks_;
   a.in = static_cast<const char*>(in);
   a.out = static_cast<char*>(out);
@@ -244,6 +249,34 @@ void IpcLane::round(StreamH s, const void* in, void* out) {
   if (bcast_) ++stats_.bcast_rounds;
   stats_.bytes_pushed += (g_.S - g_.block_len(me_)) * int64_t(es_);
   stats_.bytes_pulled += (g_.S - g_.block_len(me_)) * int64_t(es_);
+}
+
+void IpcLane::set_device_rounds(bool on) {
+  AKKA_CHECK(ready_, "ipc lane: open() the peer windows first");
+  if (on == round_dev_on_) return;
+  AKKA_IPC_HIP(hipSetDevice(dev_->device_index()));
+  if (!round_dev_) {
+    if (hipExtMallocWithFlags(reinterpret_cast<void**>(&round_dev_), 64, hipDeviceMallocUncached) != hipSuccess) {
+      (void)hipGetLastError();
+      AKKA_IPC_HIP(hipMalloc(reinterpret_cast<void**>(&round_dev_), 64));
+    }
+  }
+  AKKA_IPC_HIP(hipDeviceSynchronize());  // every round enqueued so far has its id
+  if (on) {
+    AKKA_IPC_HIP(hipMemcpy(round_dev_, &round_, sizeof(uint32_t), hipMemcpyHostToDevice));
+  } else {
+    AKKA_IPC_HIP(hipMemcpy(&round_, round_dev_, sizeof(uint32_t), hipMemcpyDeviceToHost));
+  }
+  round_dev_on_ = on;
+}
+
+uint32_t IpcLane::current_round() {
+  if (!round_dev_on_) return round_;
+  AKKA_IPC_HIP(hipSetDevice(dev_->device_index()));
+  AKKA_IPC_HIP(hipDeviceSynchronize());
+  uint32_t v = 0;
+  AKKA_IPC_HIP(hipMemcpy(&v, round_dev_, sizeof(uint32_t), hipMemcpyDeviceToHost));
+  return v;
 }
 
 uint32_t IpcLane::error() {

@@ -111,6 +111,13 @@ class IpcLane {
   bool lite() const { return lite_; }
   // Enqueue one exact round on `s`: in[S] from every rank summed into out[S].
   void round(StreamH s, const void* in, void* out);
+  // Device-resident round ids (graph capture): on, the round id lives in a
+  // device word that a bump launch in front of every round advances -- a
+  // captured round replays with a fresh id.  Switching copies the id across
+  // (off: synchronises to read it back).  Every rank switches at the same round.
+  void set_device_rounds(bool on);
+  bool device_rounds() const { return round_dev_on_; }
+  uint32_t current_round();  // host view (off) / device word (on: synchronises)
   // The error word (a wait timed out): error() after draining the device,
   // error_now() as far as the kernels got (no synchronisation).
   uint32_t error();
@@ -145,6 +152,8 @@ class IpcLane {
   std::vector<uint32_t*> peer_flags_; // [N]
   std::vector<void*> opened_flags_;
   uint32_t round_ = 0;
+  uint32_t* round_dev_ = nullptr;  // uncached device word (device rounds)
+  bool round_dev_on_ = false;
   int32_t max_wgs_ = 1024, sharers_ = 1;
   int32_t threads_ = 256;  // workgroup size of the round kernels (AKKA_IPC_THREADS)
   uint64_t timeout_ticks_ = 0;

@@ -1,0 +1,14 @@
+#!/bin/bash
+# Round-4 pass D: the whole GPU suite, smoke(), bench.py N=1.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+export TMPDIR=/tmp
+O=gpurun_out/r04d
+mkdir -p $O
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread \
+  > $O/pytest_gpu.log 2>&1 || { echo "pytest rc=$?"; tail -40 $O/pytest_gpu.log; exit 1; }
+tail -3 $O/pytest_gpu.log
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { echo "smoke rc=$?"; tail -20 $O/smoke.log; exit 1; }
+tail -1 $O/smoke.log
+timeout -k 10 600 python bench.py > $O/bench_n1.json 2> $O/bench_n1.err || { echo "bench rc=$?"; tail -20 $O/bench_n1.err; exit 1; }
+cat $O/bench_n1.json

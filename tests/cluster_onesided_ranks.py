@@ -24,6 +24,11 @@ def main():
     ap.add_argument("--out-dir", required=True)
     ap.add_argument("--timeout-s", type=float, default=240.0)
     a = ap.parse_args()
+    import faulthandler
+    import logging
+
+    logging.basicConfig(level=logging.INFO, format="%(asctime)s %(levelname)s %(name)s: %(message)s")
+    faulthandler.dump_traceback_later(max(10.0, a.timeout_s - 5), exit=False)  # stacks into the log on a hang
     from akka_allreduce_amd.parallel.cluster import start_worker
 
     holder = {}

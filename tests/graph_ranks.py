@@ -17,6 +17,7 @@ def main():
     ap.add_argument("--out-dir", required=True)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--dtype", default="bf16")
+    ap.add_argument("--lane", default="onesided", choices=["onesided", "ipc"])
     a = ap.parse_args()
     rank = int(os.environ["RANK"])
     dist.init_process_group("gloo")
@@ -40,7 +41,16 @@ def main():
         return m, GradientBucket(list(m.parameters()), flatten_params=True)
 
     m1, b1 = fresh()
-    ar = OneSidedAllreduce(b1.numel, max_chunk_size=1 << 14, device=dev)
+    if a.lane == "onesided":
+        ar = OneSidedAllreduce(b1.numel, max_chunk_size=1 << 14, device=dev)
+        cap = ar
+    else:
+        # the engine's ipc lane: eager steps through the engine, graphed
+        # steps through its capturable view (device round ids)
+        from akka_allreduce_amd.parallel import ThresholdAllreduce
+
+        ar = ThresholdAllreduce(b1.numel, max_chunk_size=1 << 14, device=dev, data_plane="ipc")
+        ar.use_lane("ipc_fused_lite")
     eager_losses = []
     for x, y in batches():
         eager_losses.append(dp_sgd_step(m1, x, y, lr, ar, b1, sync_loss=False, compute_dtype=cdt))
@@ -48,20 +58,28 @@ def main():
 
     m2, b2 = fresh()
     x0, y0 = next(batches())
-    gs = GraphedDPStep(m2, b2, x0, y0, compute_dtype=cdt, allreduce=ar, lr=lr)
+    if a.lane == "ipc":
+        torch.cuda.synchronize()
+        cap = ar.capturable()
+    gs = GraphedDPStep(m2, b2, x0, y0, compute_dtype=cdt, allreduce=cap, lr=lr)
     sx, sy = gs.static_inputs()
     graph_losses = []
-    calls0 = ar.calls
+    calls0 = ar.calls if a.lane == "onesided" else 0
     for x, y in batches():
         sx.copy_(x)
         sy.copy_(y)
         graph_losses.append(gs(sx, sy, lr, None).clone())
     torch.cuda.synchronize()
     graphed = b2.pflat.clone()
-    st = ar.stats()
+    if a.lane == "onesided":
+        st = ar.stats()
+        extra = {"calls": ar.calls - calls0, "error": ar.error(), "forced": st["complete_forced"]}
+    else:
+        r_after = ar.worker._core.ipc_current_round()
+        cap.close()
+        extra = {"calls": 20, "error": ar.ipc_error(), "forced": 0, "device_round": r_after}
     torch.save({"eager": eager.cpu(), "graphed": graphed.cpu(), "eager_losses": torch.stack(eager_losses).cpu(),
-                "graph_losses": torch.stack(graph_losses).cpu(), "replays": gs.replays, "calls": ar.calls - calls0,
-                "error": ar.error(), "rounds": st["rounds"], "forced": st["complete_forced"]},
+                "graph_losses": torch.stack(graph_losses).cpu(), "replays": gs.replays, **extra},
                os.path.join(a.out_dir, f"rank{rank}.pt"))
     ar.retire()
     torch.cuda.synchronize()

@@ -28,15 +28,21 @@ def _port() -> int:
         return s.getsockname()[1]
 
 
-def run_job(device="cpu", delay_ms=0.0, rounds=64, size=1 << 14, chunk=1 << 10, workers=4, timeout=240):
+def run_job(device="cpu", delay_ms=0.0, rounds=64, size=1 << 14, chunk=1 << 10, workers=4, timeout=240,
+            log_dir=None):
     port = _port()
     base = [sys.executable, "-m", "akka_allreduce_amd", "--log-level", "WARNING"]
     with tempfile.TemporaryDirectory() as out:
+        logs = log_dir or out
+        os.makedirs(logs, exist_ok=True)
+        # stderr into files, never a pipe nobody reads while waiting (a full
+        # pipe would block a chatty process)
+        mlog = open(os.path.join(logs, f"master_d{int(delay_ms)}.log"), "w")
         master = subprocess.Popen(base + ["master", "--port", str(port), "--workers", str(workers), "--data-size",
                                           str(size), "--max-chunk-size", str(chunk), "--max-round", str(rounds - 1),
                                           "--max-lag", "1", "--th-allreduce", "0.75", "--th-reduce", "0.75",
                                           "--th-complete", "0.75", "--transport", "onesided"],
-                                  cwd=ROOT, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
+                                  cwd=ROOT, stdout=subprocess.DEVNULL, stderr=mlog)
         t_end = time.time() + 60
         while time.time() < t_end:
             try:
@@ -44,26 +50,30 @@ def run_job(device="cpu", delay_ms=0.0, rounds=64, size=1 << 14, chunk=1 << 10, 
                 break
             except OSError:
                 time.sleep(0.1)
-        procs = []
+        procs, wlogs = [], []
         for i in range(workers):
             d = delay_ms if i == workers - 1 else 0.0
+            wlogs.append(os.path.join(logs, f"worker{i}_d{int(delay_ms)}.log"))
             procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "cluster_onesided_ranks.py"),
                                            "--master", f"127.0.0.1:{port}", "--size", str(size), "--device", device,
                                            "--delay-ms", str(d), "--out-dir", out, "--timeout-s", str(timeout - 30)],
-                                          cwd=ROOT, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True))
+                                          cwd=ROOT, stdout=subprocess.DEVNULL, stderr=open(wlogs[-1], "w")))
             if i < workers - 1:
                 time.sleep(0.3)  # join order = ids: the straggler joins last (id 3)
         errs = []
         try:
-            for p in procs:
-                p.wait(timeout=timeout)
-                errs.append(p.stderr.read()[-2000:])
+            for p, lg in zip(procs, wlogs):
+                try:
+                    p.wait(timeout=timeout)
+                finally:
+                    errs.append(open(lg).read()[-2000:])
             master.wait(timeout=30)
         finally:
             for p in procs + [master]:
                 if p.poll() is None:
                     p.kill()
                     p.wait()
+            mlog.close()
         rows = [json.load(open(f)) for f in glob.glob(os.path.join(out, "worker*.json"))]
     return rows, errs
 
@@ -81,6 +91,9 @@ def fast_median_ms(rows):
 
 
 def check_job(device, rounds=64, slack_ms=2.0, **kw):
+    import os as _os
+
+    kw.setdefault("log_dir", _os.environ.get("AKKA_TEST_LOGS") or None)
     base, e0 = run_job(device, 0.0, rounds, **kw)
     assert len(base) == 4, e0
     strag, e1 = run_job(device, 50.0, rounds, **kw)
