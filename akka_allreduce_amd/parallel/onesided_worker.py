@@ -43,6 +43,8 @@ class OneSidedWorker:
         self.dataSource = dataSource
         self.dataSink = dataSink
         self.device = torch.device(device)
+        if self.device.type == "cuda" and self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
         self.dtype = dtype
         self.name = name
         self.timeout_s = timeout_s
@@ -126,8 +128,12 @@ class OneSidedWorker:
 
     # ---- the round thread ----------------------------------------------------------
     def _run(self) -> None:
-        if self.device.type == "cuda":
-            torch.cuda.set_device(self.device)
+        try:
+            if self.device.type == "cuda":
+                torch.cuda.set_device(self.device)
+        except Exception as e:  # noqa: BLE001 - recorded; the rounds below report their own errors
+            self.errors.append(e)
+            log.error("%s: cannot select %s: %s", self.name, self.device, e)
         while True:
             with self._cv:
                 while not self._stop and self.next_round > self.max_round:

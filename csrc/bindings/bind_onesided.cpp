@@ -160,6 +160,7 @@ void bind_onesided(py::module_& m) {
       for (int32_t j = 0; j < P; ++j) {
         local.push_back(L.okq(k, j));
         local.push_back(L.pctr(k, j));
+        local.push_back(L.pdone(k, j));
       }
     }
     exported.push_back(L.done());

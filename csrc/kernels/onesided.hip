@@ -62,6 +62,11 @@ __device__ inline void stat_add(const Args& a, int32_t i, unsigned long long v) 
 
 __device__ inline void set_err(const Args& a) { sys_store(a.err, 1u); }
 
+// A work item: part j of chunk k of block p.
+struct Item {
+  int32_t p, k, j;
+};
+
 // Part j of chunk k of block p: element offset inside the block and length.
 __device__ inline int64_t part_len_of(const Args& a, int32_t p, int32_t k, int32_t j) {
   const int64_t clen = min(a.C, a.tab->blen[p] - int64_t(k) * a.C);
@@ -123,19 +128,16 @@ __device__ void push_role(const Args& a, uint32_t r, int32_t w0, int32_t stride)
   // chunk-major, peers rotated from me + 1: a chunk lands everywhere early
   // (its owner can reduce it while later chunks are still moving) and
   // consecutive workgroups feed different links
-  auto item = [&](int32_t w, int32_t& p, int32_t& k, int32_t& j) {
+  auto item = [&](int32_t w) {
     const int32_t i = w % (N - 1), kj = w / (N - 1);
-    k = kj / P;
-    j = kj % P;
-    p = (a.me + 1 + i) % N;
+    return Item{(a.me + 1 + i) % N, kj / P, kj % P};
   };
   for (int32_t base = w0; base < items; base += stride * kGateBatch) {
     for (int32_t t = threadIdx.x; t < kGateBatch; t += blockDim.x) {
       const int32_t w = base + t * stride;
       int32_t g = -1;  // no such item / no such chunk
       if (w < items) {
-        int32_t p, k, j;
-        item(w, p, k, j);
+        const auto [p, k, j] = item(w);
         if (k < a.tab->nch[p]) {
           g = kDead;
           if (!sys_load(a.dead + p)) {
@@ -154,8 +156,7 @@ __device__ void push_role(const Args& a, uint32_t r, int32_t w0, int32_t stride)
       const int32_t w = base + t * stride;
       if (w >= items) break;
       if (go_s[t] != kGo) continue;  // uniform over the workgroup
-      int32_t p, k, j;
-      item(w, p, k, j);
+      const auto [p, k, j] = item(w);
       const int64_t n = part_len_of(a, p, k, j);
       const int64_t off = part_off(a, k, j);
       char* dst = a.tab->sd[row][p] + (int64_t(a.me) * a.slot + off) * ES;
@@ -457,6 +458,7 @@ __device__ void reduce_piece(const Args& a, uint32_t r, int32_t k, int32_t j, in
       const uint32_t okq = okq_s;
       for (int32_t q = 0; q < N; ++q)
         if ((okq >> q) & 1u) DevMem::st(a.tab->fl[q] + L.gtag(row, me, k, j), tag_done(r));
+      sys_store(a.loc + L.pdone(k, j), r + 1u);  // my output span of this part is final
       if ((add_loc(a.loc + L.kctr(k), 1u) + 1u) % uint32_t(P) == 0u && mask_s != 0u)
         sys_store(a.loc + L.odone(k), r + 1u);  // chunk k reduced: it counts towards my completion
     }
@@ -546,6 +548,11 @@ __device__ void complete_role(const Args& a, uint32_t r) {
       for (int32_t j = 0; j < P && in; ++j) in = tag_state(DevMem::ld(fl + L.gtag(row, p, k, j)), r) == kLanded;
     }
     sys_store(a.loc + L.cmask(p, k), in ? 1u : 0u);
+    // the output's per-chunk contributor counts (0 outside the output set)
+    int32_t cnt = 0;
+    if (in) cnt = p == me ? __popc(uint32_t(ld64(a.loc + L.dec(k)) >> 32))
+                          : int32_t(DevMem::ld(fl + L.gtag(row, p, k, 0) + 1));
+    a.counts[int64_t(p) * a.kcols + k] = cnt;
     my_l += in;
   }
   if (threadIdx.x == 0) landed_s = 0;
@@ -568,18 +575,29 @@ __device__ void complete_role(const Args& a, uint32_t r) {
 }
 
 // ---- copy: a peer's part -> my output as soon as it lands ------------------------
+// Then, once the output set is published, every part of this workgroup's
+// items (peer parts and, past them, my own block's parts) that is outside it
+// is zeroed -- a part copied early of a chunk that did not complete, a part
+// that never landed, my own chunk reduced too late -- so the zeroing is
+// spread over the copy workgroups instead of a pass of its own.
 template <int ES>
 __device__ void copy_role(const Args& a, uint32_t r, int32_t w0, int32_t stride) {
   const Layout& L = a.L;
   const int32_t N = L.N, P = L.P, me = a.me;
-  const int32_t items = (N - 1) * L.Kmax * P;
+  const int32_t peer_items = (N - 1) * L.Kmax * P;
+  const int32_t items = peer_items + a.kme * P;
   const int32_t row = int32_t(r % uint32_t(L.D));
   uint32_t* fl = a.tab->fl[me];
   __shared__ int32_t act;
-  for (int32_t w = w0; w < items; w += stride) {
-    const int32_t i = w % (N - 1), kj = w / (N - 1);
-    const int32_t k = kj / P, j = kj % P;
-    const int32_t p = (me + 1 + i) % N;
+  auto item = [&](int32_t w) {
+    if (w < peer_items) {
+      const int32_t i = w % (N - 1), kj = w / (N - 1);
+      return Item{(me + 1 + i) % N, kj / P, kj % P};
+    }
+    return Item{me, (w - peer_items) / P, (w - peer_items) % P};
+  };
+  for (int32_t w = w0; w < peer_items; w += stride) {
+    const auto [p, k, j] = item(w);
     if (k >= a.tab->nch[p]) continue;
     if (threadIdx.x == 0) {
       const uint64_t deadline = wall_clock64() + 3 * a.timeout + 1;
@@ -611,6 +629,83 @@ __device__ void copy_role(const Args& a, uint32_t r, int32_t w0, int32_t stride)
     }
     __syncthreads();  // `act` is rewritten by the next item
   }
+  // the output set (the complete role is a lower workgroup id)
+  if (threadIdx.x == 0) {
+    const uint64_t deadline = wall_clock64() + 3 * a.timeout + 1;
+    int32_t v = 1;
+    while (sys_load(a.loc + L.state(kComp)) != r + 1u) {
+      if (wall_clock64() > deadline) {
+        set_err(a);
+        v = 0;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(4);
+    }
+    act = v;
+  }
+  __syncthreads();
+  if (!act) return;
+  for (int32_t w = w0; w < items; w += stride) {
+    const auto [p, k, j] = item(w);
+    if (k >= a.tab->nch[p]) continue;
+    if (threadIdx.x == 0) {
+      int32_t z = sys_load(a.loc + L.cmask(p, k)) == 0u ? 1 : 0;
+      if (z && p == me) {
+        // my own part: its reduce pieces may still be writing it (a chunk
+        // reduced after the decision) -- zero it once they are done
+        const uint64_t deadline = wall_clock64() + 3 * a.timeout + 1;
+        while (sys_load(a.loc + L.pdone(k, j)) != r + 1u) {
+          if (wall_clock64() > deadline) {
+            set_err(a);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(4);
+        }
+      }
+      act = z;
+    }
+    __syncthreads();
+    const int64_t n = part_len_of(a, p, k, j);
+    if (act && n > 0) zero_bytes(a.out + (a.tab->bstart[p] + part_off(a, k, j)) * ES, n * ES);
+    __syncthreads();  // `act` is rewritten by the next item
+  }
+}
+
+// ---- finish: the last workgroup out of the launch --------------------------------
+// Every workgroup's reads of the rows and writes of the output are done
+// (each drained before its increment): withdraw the read announcements,
+// count the round, publish the call's status, advance the call sequence.
+__device__ void finish_if_last(const Args& a) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  const Layout& L = a.L;
+  const uint32_t prev = add_loc(a.loc + L.state(kCtrFinish), 1u);
+  if (prev != gridDim.x - 1) return;
+  const int32_t N = L.N, me = a.me;
+  const uint32_t r = sys_load(a.loc + L.state(kCur));
+  const int32_t row = int32_t(r % uint32_t(L.D));
+  uint32_t* fl = a.tab->fl[me];
+  for (int32_t k = 0; k < a.kme; ++k) DevMem::st(fl + L.sread(row, k), 0u);
+  DevMem::st(fl + L.gread(row), 0u);
+  const uint32_t landed = sys_load(a.loc + L.state(kCompLanded));
+  int64_t total = 0;
+  for (int32_t p = 0; p < N; ++p) total += a.tab->nch[p];
+  stat_add(a, kRounds, 1);
+  stat_add(a, kLandedChunks, landed);
+  stat_add(a, kMissingChunks, uint64_t(total - int64_t(landed)));
+  const uint32_t seq = sys_load(a.loc + L.state(kCallSeq));
+  CallStatus* cs = a.status + (seq % uint32_t(kStatusSlots));
+  __hip_atomic_store(&cs->round, int64_t(r), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(&cs->reason, int64_t(sys_load(a.loc + L.state(kCompReason))), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(&cs->landed_chunks, int64_t(landed), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(&cs->forced_chunks, int64_t(sys_load(a.loc + L.state(kForcedChunks))), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_SYSTEM);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  // the record names its call last: a reader that sees this id sees the fields above
+  __hip_atomic_store(&cs->call, int64_t(seq), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  sys_store(a.loc + L.state(kCallSeq), seq + 1u);
 }
 
 // ---- the round launch -------------------------------------------------------------
@@ -620,71 +715,22 @@ __global__ __launch_bounds__(LB) void os_round_kernel(Args a) {
   int32_t b = int32_t(blockIdx.x);
   if (b == 0) {
     begin_role(a);
-    return;
-  }
-  const uint32_t r = wait_begun(a);
-  b -= 1;
-  if (b < a.gp) return push_role<ES>(a, r, b, a.gp);
-  b -= a.gp;
-  if (b < a.kme) return decide_role(a, r, b);
-  b -= a.kme;
-  if (b < a.gr) return reduce_role<T, NS>(a, r, b, a.gr);
-  b -= a.gr;
-  if (b == 0) return complete_role(a, r);
-  b -= 1;
-  copy_role<ES>(a, r, b, a.gq);
-}
-
-// ---- finish: chunks outside the output set -> 0 / count 0, status -----------------
-template <int ES>
-__global__ __launch_bounds__(kMaxThreads) void os_finish_kernel(Args a) {
-  const Layout& L = a.L;
-  const int32_t N = L.N, K = L.Kmax, me = a.me;
-  const uint32_t r = sys_load(a.loc + L.state(kCur));
-  const int32_t row = int32_t(r % uint32_t(L.D));
-  uint32_t* fl = a.tab->fl[me];
-  for (int32_t c = blockIdx.x; c < N * K; c += gridDim.x) {
-    const int32_t p = c / K, k = c % K;
-    if (k >= a.tab->nch[p]) continue;
-    const bool in = sys_load(a.loc + L.cmask(p, k)) != 0u;
-    if (!in) {
-      const int64_t clen = min(a.C, a.tab->blen[p] - int64_t(k) * a.C);
-      zero_bytes(a.out + (a.tab->bstart[p] + int64_t(k) * a.C) * ES, clen * ES);
-    }
-    if (threadIdx.x == 0) {
-      int32_t cnt = 0;
-      if (in) cnt = p == me ? __popc(uint32_t(ld64(a.loc + L.dec(k)) >> 32))
-                            : int32_t(DevMem::ld(fl + L.gtag(row, p, k, 0) + 1));
-      a.counts[int64_t(p) * a.kcols + k] = cnt;
+  } else {
+    const uint32_t r = wait_begun(a);
+    b -= 1;
+    if (b < a.gp) {
+      push_role<ES>(a, r, b, a.gp);
+    } else if ((b -= a.gp) < a.kme) {
+      decide_role(a, r, b);
+    } else if ((b -= a.kme) < a.gr) {
+      reduce_role<T, NS>(a, r, b, a.gr);
+    } else if ((b -= a.gr) == 0) {
+      complete_role(a, r);
+    } else {
+      copy_role<ES>(a, r, b - 1, a.gq);
     }
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const uint32_t prev = add_loc(a.loc + L.state(kCtrFinish), 1u);
-    if (prev == gridDim.x - 1) {
-      // the last workgroup out: this call no longer reads its rows
-      for (int32_t k = 0; k < a.kme; ++k) DevMem::st(fl + L.sread(row, k), 0u);
-      DevMem::st(fl + L.gread(row), 0u);
-      const uint32_t landed = sys_load(a.loc + L.state(kCompLanded));
-      int64_t total = 0;
-      for (int32_t p = 0; p < N; ++p) total += a.tab->nch[p];
-      stat_add(a, kRounds, 1);
-      stat_add(a, kLandedChunks, landed);
-      stat_add(a, kMissingChunks, uint64_t(total - int64_t(landed)));
-      const uint32_t seq = sys_load(a.loc + L.state(kCallSeq));
-      CallStatus* cs = a.status + (seq % uint32_t(kStatusSlots));
-      __hip_atomic_store(&cs->call, int64_t(seq), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(&cs->reason, int64_t(sys_load(a.loc + L.state(kCompReason))), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(&cs->landed_chunks, int64_t(landed), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(&cs->forced_chunks, int64_t(sys_load(a.loc + L.state(kForcedChunks))), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_SYSTEM);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __hip_atomic_store(&cs->round, int64_t(r), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      sys_store(a.loc + L.state(kCallSeq), seq + 1u);
-    }
-  }
+  finish_if_last(a);
 }
 
 // retire: tell every peer that this rank serves no round >= its next one
@@ -728,7 +774,6 @@ void launch_call(hipStream_t s, const Args& a) {
     if (nt == 256u) hipLaunchKernelGGL((os_round_kernel<T, NS, 256>), dim3(grid), dim3(nt), 0, s, a);
     else hipLaunchKernelGGL((os_round_kernel<T, NS, kMaxThreads>), dim3(grid), dim3(nt), 0, s, a);
   });
-  hipLaunchKernelGGL(os_finish_kernel<ES>, dim3(unsigned(std::max(1, a.gf))), dim3(256), 0, s, a);
 }
 
 }  // namespace

@@ -102,7 +102,7 @@ struct Layout {
   // exported (peers read or write these over the link)
   int64_t stag0 = 0, gtag0 = 0, fired0 = 0, sread0 = 0, gread0 = 0, done0 = 0, seen0 = 0, fin0 = 0, flag_words = 0;
   // local only (this rank's kernels / progress thread)
-  int64_t dec0 = 0, okq0 = 0, pctr0 = 0, kctr0 = 0, odone0 = 0, cmask0 = 0, state0 = 0, local_words = 0;
+  int64_t dec0 = 0, okq0 = 0, pctr0 = 0, pdone0 = 0, kctr0 = 0, odone0 = 0, cmask0 = 0, state0 = 0, local_words = 0;
 
   OS_HD void init(int32_t N_, int32_t D_, int32_t Kmax_, int32_t P_) {
     N = N_;
@@ -122,7 +122,8 @@ struct Layout {
     dec0 = 0;  // 64-bit words: even offsets
     okq0 = dec0 + 2 * int64_t(Kmax);
     pctr0 = okq0 + int64_t(Kmax) * P;
-    kctr0 = pctr0 + int64_t(Kmax) * P;
+    pdone0 = pctr0 + int64_t(Kmax) * P;
+    kctr0 = pdone0 + int64_t(Kmax) * P;
     odone0 = kctr0 + Kmax;
     cmask0 = odone0 + Kmax;
     state0 = (cmask0 + int64_t(N) * Kmax + 15) / 16 * 16;
@@ -148,6 +149,8 @@ struct Layout {
   OS_HD int64_t okq(int32_t k, int32_t j) const { return okq0 + int64_t(k) * P + j; }
   // local: finished reduce pieces of part (k, j) / parts of chunk k (counted modulo, never reset)
   OS_HD int64_t pctr(int32_t k, int32_t j) const { return pctr0 + int64_t(k) * P + j; }
+  // local: round + 1 once every reduce piece of part (k, j) finished (its output span is final)
+  OS_HD int64_t pdone(int32_t k, int32_t j) const { return pdone0 + int64_t(k) * P + j; }
   OS_HD int64_t kctr(int32_t k) const { return kctr0 + k; }
   // local: round + 1 once my chunk k is reduced (self-delivery of its ReduceBlock, W:260-261)
   OS_HD int64_t odone(int32_t k) const { return odone0 + k; }

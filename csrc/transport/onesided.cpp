@@ -86,7 +86,12 @@ void OneSidedLane::size_roles(int64_t wgs) {
   const int64_t max_sub = std::max<int64_t>(1, part_len_ / 4096);
   nsub_ = red_parts > 0 ? int32_t(std::clamp<int64_t>((wgs + red_parts - 1) / red_parts, 1, max_sub)) : 1;
   gr_ = red_parts > 0 ? int32_t(std::clamp<int64_t>(red_parts * nsub_, 1, wgs)) : 0;
-  gf_ = int32_t(std::clamp<int64_t>(int64_t(N) * Kmax_, 1, 64));
+  gf_ = 0;  // the finish is the last workgroup out of the round launch
+  if (const char* v = std::getenv("AKKA_OS_REDUCE_WGS")) {  // measurement knob
+    const int64_t rw = std::max<int64_t>(1, std::atoll(v));
+    nsub_ = red_parts > 0 ? int32_t(std::clamp<int64_t>((rw + red_parts - 1) / red_parts, 1, max_sub)) : 1;
+    gr_ = red_parts > 0 ? int32_t(std::clamp<int64_t>(red_parts * nsub_, 1, rw)) : 0;
+  }
 }
 
 OneSidedLane::OneSidedLane(int32_t device, int64_t S, int32_t N, int64_t C, int32_t me, DType dt,
@@ -117,7 +122,10 @@ OneSidedLane::OneSidedLane(int32_t device, int64_t S, int32_t N, int64_t C, int3
                  " chunk parts per ring -- use a larger max_chunk_size");
   L_.init(N, D_, Kmax_, P_);
   nt_ = p.threads <= 256 ? 256 : 1024;
-  size_roles(p.role_wgs > 0 ? p.role_wgs : kDefaultRoleWgs);
+  if (const char* v = std::getenv("AKKA_OS_THREADS")) nt_ = std::atoi(v) >= 1024 ? 1024 : 256;  // measurement knob
+  int64_t wgs = p.role_wgs > 0 ? p.role_wgs : kDefaultRoleWgs;
+  if (const char* v = std::getenv("AKKA_OS_ROLE_WGS")) wgs = std::max<int64_t>(1, std::atoll(v));
+  size_roles(wgs);
   flag_bytes_ = size_t(L_.flag_words) * sizeof(uint32_t);
   row_bytes_ = size_t(N) * size_t(slot_) * es_;
   win_bytes_ = flag_bytes_ + 2 * size_t(D_) * row_bytes_;
@@ -307,7 +315,7 @@ void OneSidedLane::open(const std::vector<std::string>& handles) {
       }
     }
   }
-  if (device_ >= 0 && p_.role_wgs <= 0) {
+  if (device_ >= 0 && p_.role_wgs <= 0 && !std::getenv("AKKA_OS_ROLE_WGS")) {
     // Ranks sharing this GPU (tests / rehearsals on a 1-GPU box): every
     // rank's round launch must fit on the card at once, or one rank's
     // waiting workgroups could hold the slots another rank's pushers need.
