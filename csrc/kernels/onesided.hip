@@ -603,12 +603,14 @@ __device__ void copy_role(const Args& a, uint32_t r, int32_t w0, int32_t stride)
       const uint64_t deadline = wall_clock64() + 3 * a.timeout + 1;
       int32_t v = 0;
       while (true) {
-        const int32_t st = tag_state(DevMem::ld(fl + L.gtag(row, p, k, j)), r);
-        if (st == kLanded) {
+        // landed: copy now.  Anything else waits for the output set: a tag a
+        // later round's writer marked after a conflict says "lost" although
+        // this round's bytes are intact, and the complete role may already
+        // have counted them in
+        if (tag_state(DevMem::ld(fl + L.gtag(row, p, k, j)), r) == kLanded) {
           v = 1;
           break;
         }
-        if (st == kLost) break;
         if (sys_load(a.loc + L.state(kComp)) == r + 1u) {
           v = sys_load(a.loc + L.cmask(p, k)) != 0u ? 1 : 0;
           break;

@@ -70,10 +70,10 @@ int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 
 }  // namespace
 
-// Role sizes of the round launch.  Defaults: 256 workgroups per data role
-// (256 threads each) -- the whole grid (~3 per CU) is resident at once on a
-// GPU of its own, so the copies of landed chunks run while later chunks are
-// still crossing the links.  Fixed once open() ran (the reduce pieces'
+// Role sizes of the round launch.  Defaults: 256 workgroups for push and
+// copy, 512 for reduce (256 threads each) -- the whole grid (~4 per CU) is
+// resident at once on a GPU of its own, so the copies of landed chunks run
+// while later chunks are still crossing the links.  Fixed once open() ran (the reduce pieces'
 // counters count modulo nsub_).
 void OneSidedLane::size_roles(int64_t wgs) {
   const int32_t N = g_.N;
@@ -82,10 +82,13 @@ void OneSidedLane::size_roles(int64_t wgs) {
   const int64_t red_parts = int64_t(g_.num_chunks(me_)) * P_;
   gp_ = int32_t(std::clamp<int64_t>(push_items, 1, wgs));
   gq_ = gp_;
-  // pieces of >= 4096 elements, enough of them to give every data CU a reducer
+  // pieces of >= 4096 elements; twice the workgroups of the other roles:
+  // the reduce reads N sources per element (bench/onesided_role.py: 512
+  // 256-thread workgroups reach 5.0 TB/s at N=8 where 256 reach 3.7)
+  const int64_t rwgs = 2 * wgs;
   const int64_t max_sub = std::max<int64_t>(1, part_len_ / 4096);
-  nsub_ = red_parts > 0 ? int32_t(std::clamp<int64_t>((wgs + red_parts - 1) / red_parts, 1, max_sub)) : 1;
-  gr_ = red_parts > 0 ? int32_t(std::clamp<int64_t>(red_parts * nsub_, 1, wgs)) : 0;
+  nsub_ = red_parts > 0 ? int32_t(std::clamp<int64_t>((rwgs + red_parts - 1) / red_parts, 1, max_sub)) : 1;
+  gr_ = red_parts > 0 ? int32_t(std::clamp<int64_t>(red_parts * nsub_, 1, rwgs)) : 0;
   gf_ = 0;  // the finish is the last workgroup out of the round launch
   if (const char* v = std::getenv("AKKA_OS_REDUCE_WGS")) {  // measurement knob
     const int64_t rw = std::max<int64_t>(1, std::atoll(v));
@@ -332,7 +335,7 @@ void OneSidedLane::open(const std::vector<std::string>& handles) {
       const char* bv = std::getenv("AKKA_OS_SHARED_BUDGET");  // measurement knob (resident 256-thread WGs)
       const int64_t total = bv ? std::max(16, std::atoi(bv)) : 512;
       const int64_t budget = total / share - 2 - g_.num_chunks(me_);
-      size_roles(std::max<int64_t>(2, budget / 3));
+      size_roles(std::max<int64_t>(2, budget / 4));  // push, copy: 1 share each; reduce: 2
     }
   }
   if (device_ >= 0) {
