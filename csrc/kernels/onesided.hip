@@ -333,7 +333,8 @@ __device__ void masked_sum_n(const Args& a, const char* mine, const char* sd, ch
         if ((mask >> s) & 1u) Elt<T>::add(acc, v[s][u]);
       if (i < nv) {
         const uint4 w = Elt<T>::pack(acc);
-        store_nt16(reinterpret_cast<uint4*>(o) + i, w);
+        if (a.own_wt) store_sys16(sys_rsrc(o, nv * 16), i * 16, w);
+        else store_nt16(reinterpret_cast<uint4*>(o) + i, w);
 #pragma unroll
         for (int q = 0; q < NS; ++q)
           if ((okq >> q) & 1u) store_sys16(sys_rsrc(a.tab->gd[row][q] + goff, nv * 16), i * 16, w);
@@ -668,7 +669,17 @@ __device__ void copy_role(const Args& a, uint32_t r, int32_t w0, int32_t stride)
     }
     __syncthreads();
     const int64_t n = part_len_of(a, p, k, j);
-    if (act && n > 0) zero_bytes(a.out + (a.tab->bstart[p] + part_off(a, k, j)) * ES, n * ES);
+    if (act && n > 0) {
+      char* o = a.out + (a.tab->bstart[p] + part_off(a, k, j)) * ES;
+      if (p == me && a.own_wt && ((uintptr_t(o) | uintptr_t(n * ES)) & 15) == 0) {
+        // my own part: written through, after the reduce pieces' own
+        // write-through stores (another XCD's): memory ends with the zeros
+        const auto rs = sys_rsrc(o, n * ES);
+        for (int64_t i = threadIdx.x; i < (n * ES) >> 4; i += blockDim.x) store_sys16(rs, i * 16, make_uint4(0, 0, 0, 0));
+      } else {
+        zero_bytes(o, n * ES);
+      }
+    }
     __syncthreads();  // `act` is rewritten by the next item
   }
 }

@@ -49,6 +49,11 @@ struct Args {
   int32_t threads = 1024;
   int32_t gp = 1, gr = 1, gq = 1, gf = 1;  // push / reduce / copy / finish workgroups
   int32_t nsub = 1;                        // reduce pieces per part
+  // my own output block is written through (sc0 sc1) instead of streamed:
+  // when a round can complete without my chunk (thComplete < 1), a copy
+  // workgroup on another XCD zeroes it after its reduce pieces -- two XCDs'
+  // L2s holding the same dirty lines would write back in any order
+  int32_t own_wt = 0;
   uint64_t timeout = 0;                    // per wait, wall-clock ticks
   const char* in = nullptr;                // round input [S]
   char* out = nullptr;                     // round output [S]

@@ -402,6 +402,7 @@ void OneSidedLane::gpu_call(uintptr_t stream, const char* in, char* out, int32_t
   a.gq = gq_;
   a.gf = gf_;
   a.nsub = nsub_;
+  a.own_wt = need_c_ < g_.total_chunks() ? 1 : 0;
   a.timeout = timeout_ticks_;
   a.in = in;
   a.out = out;

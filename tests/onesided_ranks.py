@@ -25,13 +25,21 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 
-def check_sets(o, world, me, dtype):
-    """Every chunk: value encodes a contributor set whose size is the count."""
+def check_sets(o, world, me, dtype, detail=None):
+    """Every chunk: value encodes a contributor set whose size is the count.
+    `detail` (a list) collects the first few bad chunks, for the report."""
     g = o.geometry
     data = o.data.float().cpu()
     counts = o.counts_per_chunk.cpu()
     bad = 0
     own_has_me = True
+
+    def note(p, k, seg, c):
+        if detail is not None and len(detail) < 8:
+            vals = torch.unique(seg)
+            detail.append({"round": o.iteration, "block": p, "chunk": k, "count": c, "values": vals[:6].tolist(),
+                           "n_values": int(vals.numel()), "first_bad": int((seg != seg[0]).nonzero()[0]) if
+                           vals.numel() > 1 else -1, "len": int(seg.numel()), "reason": o.status["reason"]})
     for p in range(world):
         for k in range(g.num_chunks(p)):
             s, e = g.chunk_range(p, k)
@@ -39,13 +47,15 @@ def check_sets(o, world, me, dtype):
                 continue
             seg = data[s:e]
             v = float(seg[0])
+            c = int(counts[p, k])
             if not bool((seg == v).all()):
                 bad += 1
+                note(p, k, seg, c)
                 continue
-            c = int(counts[p, k])
             iv = int(v)
             if float(iv) != v or iv < 0 or iv >= (1 << world) or bin(iv).count("1") != c:
                 bad += 1
+                note(p, k, seg, c)
             # my own chunk, when it is part of my output (it may be left out:
             # the round can complete before it is reduced, like the reference's
             # completion before the self-delivered ReduceBlock), includes my copy
@@ -114,7 +124,7 @@ def main():
         # catch-up, so call counts differ between ranks (the reference's
         # master ends the job at maxRound the same way, M:58-63).
         for pi, phase in enumerate(("no_straggler", "straggler")):
-            times, rounds, bad, own_ok, reasons = [], [], 0, True, []
+            times, rounds, bad, own_ok, reasons, detail = [], [], 0, True, [], []
             target, last, c = (pi + 1) * a.rounds - 1, -1 if pi == 0 else res["no_straggler"]["rounds"][-1], 0
             while last < target:
                 c += 1
@@ -132,14 +142,14 @@ def main():
                 o = ar(x, out=out)
                 sync()
                 times.append((time.perf_counter() - t0) * 1e3)
-                b, mine = check_sets(o, world, rank, dtype)
+                b, mine = check_sets(o, world, rank, dtype, detail)
                 bad += b
                 own_ok &= mine
                 last = o.iteration
                 rounds.append(last)
                 reasons.append(o.status["reason"])
             res[phase] = {"ms": times, "rounds": rounds, "bad_chunks": bad, "own_block_has_me": own_ok,
-                          "reasons": reasons, "stats": ar.stats()}
+                          "reasons": reasons, "stats": ar.stats(), "bad_detail": detail}
         ar.retire()
         sync()
     res["error"] = ar.error()

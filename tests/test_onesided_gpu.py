@@ -41,7 +41,7 @@ def test_onesided_gpu_straggler_steady_state():
     for d in rows:
         assert d["error"] == 0, d["stats"]
         for ph in ("no_straggler", "straggler"):
-            assert d[ph]["bad_chunks"] == 0 and d[ph]["own_block_has_me"], (d["rank"], ph)
+            assert d[ph]["bad_chunks"] == 0 and d[ph]["own_block_has_me"], (d["rank"], ph, d[ph]["bad_detail"], d[ph]["stats"])
     for d in rows[:3]:
         base, strag = _median_tail(d["no_straggler"]["ms"]), _median_tail(d["straggler"]["ms"])
         assert strag <= 2 * base + 0.2, (d["rank"], base, strag)
