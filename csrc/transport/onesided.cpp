@@ -322,7 +322,10 @@ void OneSidedLane::open(const std::vector<std::string>& handles) {
     // Ranks sharing this GPU (tests / rehearsals on a 1-GPU box): every
     // rank's round launch must fit on the card at once, or one rank's
     // waiting workgroups could hold the slots another rank's pushers need.
-    // Budget: 1024 resident 256-thread workgroups, half of it for the lane.
+    // Budget: 768 of the card's ~1024 resident 256-thread workgroups (103
+    // VGPRs: 4 per CU) for all sharing ranks' grids together (pass F sweep,
+    // profiles/r04/README.md: 512 / 768 / 1024 -> 1.26 / 1.15 / 1.44 ms at
+    // 256 MiB, 4 ranks).
     int32_t share = 0;
     for (int32_t q = 0; q < g_.N; ++q) {
       Blob b;
@@ -333,7 +336,7 @@ void OneSidedLane::open(const std::vector<std::string>& handles) {
     if (share > 1) {
       nt_ = 256;
       const char* bv = std::getenv("AKKA_OS_SHARED_BUDGET");  // measurement knob (resident 256-thread WGs)
-      const int64_t total = bv ? std::max(16, std::atoi(bv)) : 512;
+      const int64_t total = bv ? std::max(16, std::atoi(bv)) : 768;
       const int64_t budget = total / share - 2 - g_.num_chunks(me_);
       size_roles(std::max<int64_t>(2, budget / 4));  // push, copy: 1 share each; reduce: 2
     }
