@@ -26,7 +26,8 @@ def main():
     for (k, grid), cs in sorted(rows.items()):
         parts = []
         for c, v in sorted(cs.items()):
-            parts.append(f"{c}={sum(v) / len(v):.4g}")
+            med = sorted(v)[len(v) // 2]
+            parts.append(f"{c}={sum(v) / len(v):.4g} (median {med:.4g}, n={len(v)})")
         print(f"{k} grid={grid}: " + " ".join(parts))
 
 
