@@ -91,8 +91,9 @@ def test_bench_multirank_on_one_card(plane):
         assert c4["transport"] == "onesided" and w["timeouts"] == 0, c4
         assert w["fast_rank_median_ms_per_round"] < 40 / 4 and w["catch_up_skipped_rounds"] > 0, c4
     else:
+        # the ipc lane's variants and the one-sided lane (exact rounds)
         assert set(cands) == {"ipc", "ipc_bcast", "ipc_fused", "ipc_fused_bcast", "ipc_wide", "ipc_bcast_wide",
-                              "ipc_lite", "ipc_bcast_lite", "ipc_fused_lite", "ipc_fused_bcast_lite"}
+                              "ipc_lite", "ipc_bcast_lite", "ipc_fused_lite", "ipc_fused_bcast_lite", "onesided"}
 
 
 def test_bench_rccl_init_failure_falls_back_to_ipc():
