@@ -116,7 +116,8 @@ def test_bench_rccl_init_failure_falls_back_to_ipc():
     assert len(lines) == 1, r.stdout
     d = json.loads(lines[0])
     assert d["rccl_fallback"]["data_plane"] == "ipc" and set(d["rccl_fallback"]["rccl_init_errors"]) == {"0", "1"}
-    assert d["config"]["data_plane"] == "ipc" and d["lane"].startswith("ipc") and d["lane_is_framework"] is True
+    assert d["config"]["data_plane"] == "ipc" and (d["lane"].startswith("ipc") or d["lane"] == "onesided") \
+        and d["lane_is_framework"] is True
     assert d["exact"] is True and d["value"] > 0
 
 
@@ -143,6 +144,7 @@ def test_bench_preflight_failure_falls_back_to_ipc():
     d = json.loads(lines[0])
     assert set(d["preflight_fallback"]["errors"]) == {"0", "1"}, d
     assert d["preflight"] == "passed on the ipc lane"
-    assert d["lane"].startswith("ipc") and d["lane_is_framework"] is True
-    assert all(k.startswith("ipc") for k in d["lane_select"] if k != "chosen"), d["lane_select"]
+    assert (d["lane"].startswith("ipc") or d["lane"] == "onesided") \
+        and d["lane_is_framework"] is True
+    assert all(k.startswith("ipc") or k == "onesided" for k in d["lane_select"] if k != "chosen"), d["lane_select"]
     assert d["exact"] is True and d["value"] > 0 and d["rccl_allreduce_algbw_GBps"] is None
