@@ -367,6 +367,12 @@ class ThresholdAllreduce:
             self.pacer.completed(r)  # CompleteAllreduce(id, r) to the "master" (W:276)
         return out
 
+    def runs_async(self) -> bool:
+        """Whether ``async_op=True`` rounds run on the engine's own streams.
+        The one-sided lane always runs on the caller's stream: its output is
+        valid in the caller's stream order, not behind the engine's streams."""
+        return self.transport == "stream" and not self._lane_os
+
     def set_lane(self, lane: str) -> None:
         """Switch the exact-round lane (``auto`` / ``p2p`` / ``collective``,
         csrc/transport/stream_link.h) -- every rank must switch at the same round."""

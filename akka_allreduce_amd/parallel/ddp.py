@@ -103,7 +103,8 @@ def threshold_allreduce_hook(state: ThresholdHookState, bucket: dist.GradBucket)
         work = flat
     ar = state.engine(work)
     cuda = work.is_cuda
-    async_op = bool(state.async_op and cuda and ar.transport == "stream")
+    # (a tuned one-sided lane runs on the caller's stream: no async round)
+    async_op = bool(state.async_op and cuda and ar.runs_async())
     out = ar(work.contiguous(), async_op=async_op)
     state.rounds += 1
     state.async_rounds += int(async_op)
