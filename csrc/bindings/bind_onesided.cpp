@@ -127,8 +127,7 @@ void bind_onesided(py::module_& m) {
         d["ranks_on_this_gpu"] = l.shared_ranks();
         d["pieces_per_part"] = l.pieces();
         const auto g = l.role_grid();
-        d["role_wgs"] = py::dict(py::arg("push") = g[0], py::arg("reduce") = g[1], py::arg("copy") = g[2],
-                                 py::arg("finish") = g[3]);
+        d["role_wgs"] = py::dict(py::arg("push") = g[0], py::arg("reduce") = g[1], py::arg("copy") = g[2]);
         return d;
       });
   m.def("onesided_layout", [](int32_t N, int32_t D, int32_t Kmax, int32_t P) {

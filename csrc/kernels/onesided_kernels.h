@@ -1,16 +1,18 @@
 // gfx950 kernels of the one-sided threshold lane (onesided.hip); protocol in
 // onesided_protocol.h, host side in transport/onesided.{h,cpp}.
 //
-// One call (one round of this rank) is two launches on the caller's stream:
-//   round   one grid, roles by workgroup id (onesided_protocol.h, "One call"):
-//             [0]                  begin: round selection, announcements
-//             [1, 1+gp)            push: (N-1)*K*P parts, fire and forget
-//             [.., +kme)           decide: one workgroup per chunk of my block
-//             [.., +gr)            reduce: kme*P*nsub pieces, each starts when
-//                                  its chunk is decided
-//             [.., +1)             complete: the thComplete decision
-//             [.., +gq)            copy: (N-1)*K*P landed parts -> output
-//   finish  chunks outside the completion set -> 0, counts, status.
+// One call (one round of this rank) is ONE launch on the caller's stream,
+// roles by workgroup id (onesided_protocol.h, "One call"):
+//   [0]                  begin: round selection, announcements
+//   [1, 1+gp)            push: (N-1)*K*P parts, fire and forget
+//   [.., +kme)           decide: one workgroup per chunk of my block
+//   [.., +gr)            reduce: kme*P*nsub pieces, each starts when its chunk
+//                        is decided
+//   [.., +1)             complete: the thComplete decision, counts
+//   [.., +gq)            copy: landed peer parts -> output; parts outside the
+//                        completion set -> 0
+// The last workgroup out finishes the call (announcements withdrawn, stats,
+// status record, call id + 1).
 // Deadlock-free without co-residency: workgroups are dispatched in id order,
 // every role waits only on roles with lower ids (or on peers' pushers, which
 // never wait), and every wait is bounded by the lane's timeout.
@@ -47,7 +49,7 @@ struct Args {
   int32_t me = 0, kme = 0, need_r = 1, need_c = 1, max_lag = 0;  // kme: chunks of my block
   int32_t kcols = 1;                       // columns of the counts table [N][kcols]
   int32_t threads = 1024;
-  int32_t gp = 1, gr = 1, gq = 1, gf = 1;  // push / reduce / copy / finish workgroups
+  int32_t gp = 1, gr = 1, gq = 1;          // push / reduce / copy workgroups
   int32_t nsub = 1;                        // reduce pieces per part
   // my own output block is written through (sc0 sc1) instead of streamed:
   // when a round can complete without my chunk (thComplete < 1), a copy

@@ -89,7 +89,6 @@ void OneSidedLane::size_roles(int64_t wgs) {
   const int64_t max_sub = std::max<int64_t>(1, part_len_ / 4096);
   nsub_ = red_parts > 0 ? int32_t(std::clamp<int64_t>((rwgs + red_parts - 1) / red_parts, 1, max_sub)) : 1;
   gr_ = red_parts > 0 ? int32_t(std::clamp<int64_t>(red_parts * nsub_, 1, rwgs)) : 0;
-  gf_ = 0;  // the finish is the last workgroup out of the round launch
   if (const char* v = std::getenv("AKKA_OS_REDUCE_WGS")) {  // measurement knob
     const int64_t rw = std::max<int64_t>(1, std::atoll(v));
     nsub_ = red_parts > 0 ? int32_t(std::clamp<int64_t>((rw + red_parts - 1) / red_parts, 1, max_sub)) : 1;
@@ -403,7 +402,6 @@ void OneSidedLane::gpu_call(uintptr_t stream, const char* in, char* out, int32_t
   a.gp = gp_;
   a.gr = gr_;
   a.gq = gq_;
-  a.gf = gf_;
   a.nsub = nsub_;
   a.own_wt = need_c_ < g_.total_chunks() ? 1 : 0;
   a.timeout = timeout_ticks_;

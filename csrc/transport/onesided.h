@@ -12,8 +12,8 @@
 //
 // Two backends run the same protocol functions:
 //  * GPU (device >= 0): windows are fine-grained HBM exported with IPC
-//    handles, the round is one role-partitioned launch + a finish launch on
-//    the caller's stream (onesided_kernels.h): each chunk of my block is
+//    handles, the round is one role-partitioned launch on the caller's
+//    stream (its last workgroup out finishes the call) (onesided_kernels.h): each chunk of my block is
 //    reduced and pushed the moment its threshold is met, each peer chunk is
 //    copied out the moment it lands;
 //  * CPU (device < 0): windows are POSIX shared memory, the round is a
@@ -112,7 +112,7 @@ class OneSidedLane {
   int32_t pieces() const { return nsub_; }
   int32_t threads() const { return nt_; }
   int32_t shared_ranks() const { return shared_ranks_; }
-  std::array<int32_t, 4> role_grid() const { return {gp_, gr_, gq_, gf_}; }
+  std::array<int32_t, 3> role_grid() const { return {gp_, gr_, gq_}; }
   size_t window_bytes() const { return win_bytes_; }
   const std::string& memory_kind() const { return mem_kind_; }
   const Geometry& geometry() const { return g_; }
@@ -162,7 +162,7 @@ class OneSidedLane {
   OneSidedParams p_;
   os::Layout L_;
   int32_t D_ = 0, P_ = 1, Kmax_ = 0, need_r_ = 1, need_c_ = 1;
-  int32_t nsub_ = 1, nt_ = 256, gp_ = 1, gr_ = 0, gq_ = 1, gf_ = 1, shared_ranks_ = 1;
+  int32_t nsub_ = 1, nt_ = 256, gp_ = 1, gr_ = 0, gq_ = 1, shared_ranks_ = 1;
   std::string my_bus_;
   int64_t slot_ = 0, part_len_ = 64;
   size_t flag_bytes_ = 0, row_bytes_ = 0, win_bytes_ = 0;
