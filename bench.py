@@ -147,7 +147,13 @@ def run_cfg4(world: int, rank: int, dev, barrier, size_mb: float, delay_ms: floa
     differ): without the straggler, then with rank N-1 sleeping `delay_ms`
     before each call.  Per phase: the fast ranks' median and p90 ms per call
     over the second half (worst fast rank), their mean contributor count, the
-    straggler's calls and catch-up skips, drops and forced reduces."""
+    straggler's calls and catch-up skips, drops and forced reduces.
+
+    Then an untimed validation phase (`validation`, straggler still late):
+    every rank contributes the constant 2^rank, so every output chunk must be
+    one integer whose set bits are its contributors, as many as its count --
+    a torn, stale or mixed chunk shows (on a node: the cross-device hand-offs
+    of the one-sided lane, checked on the job itself)."""
     import statistics
 
     import torch
@@ -223,10 +229,57 @@ def run_cfg4(world: int, rank: int, dev, barrier, size_mb: float, delay_ms: floa
     a, b = res["no_straggler"], res["with_straggler"]
     res["fast_rank_slowdown"] = round(b["fast_rank_median_ms_per_round"] / max(1e-9, a["fast_rank_median_ms_per_round"]),
                                       3)
+    res["validation"] = cfg4_validate(ar, world, rank, straggler, delay_ms, last, max(8, rounds // 4), dev)
     ar.retire()  # the job's end: nobody waits for this rank's later rounds
     sync()
     barrier()
     return res
+
+
+def cfg4_validate(ar, world: int, rank: int, straggler: int, delay_ms: float, last: int, rounds: int, dev) -> dict:
+    """Config 4's untimed validation rounds (run_cfg4): inputs 2^rank, every
+    chunk of every output checked against its contributor count."""
+    import torch
+    import torch.distributed as dist
+
+    os_ = ar._os
+    g = os_.geometry
+    S = ar.data_size
+    x = torch.full((S,), float(1 << rank), device=dev)
+    out = torch.empty_like(x)
+    bad, chunks, calls, first_bad = 0, 0, 0, None
+    lasts = [None] * world
+    dist.all_gather_object(lasts, last)
+    target = max(lasts) + rounds  # a common round, like the timed phases
+    while last < target:
+        if rank == straggler:
+            time.sleep(delay_ms / 1e3)
+        o = ar(x, out=out)
+        data = o.data.float().cpu()
+        counts = o.counts_per_chunk.cpu()
+        last = o.status_nowait()["round"]
+        calls += 1
+        for p in range(world):
+            for k in range(g.num_chunks(p)):
+                s0, e0 = g.chunk_range(p, k)
+                if e0 <= s0:
+                    continue
+                chunks += 1
+                seg = data[s0:e0]
+                v, c = float(seg[0]), int(counts[p, k])
+                iv = int(v)
+                ok = bool((seg == v).all()) and float(iv) == v and 0 <= iv < (1 << world) and bin(iv).count("1") == c
+                if not ok:
+                    bad += 1
+                    if first_bad is None:
+                        first_bad = {"round": last, "block": p, "chunk": k, "count": c, "value": v}
+    mine = {"bad": bad, "chunks": chunks, "calls": calls, "first_bad": first_bad}
+    allv = [None] * world
+    dist.all_gather_object(allv, mine)
+    return {"rounds": rounds, "calls": [v["calls"] for v in allv], "chunks_checked": sum(v["chunks"] for v in allv),
+            "bad_chunks": sum(v["bad"] for v in allv),
+            "first_bad": next((dict(v["first_bad"], rank=i) for i, v in enumerate(allv) if v["first_bad"]), None),
+            "contributor_sets_consistent": all(v["bad"] == 0 for v in allv)}
 
 
 def cfg4_threshold_needs(world: int, S: int, C: int, th_reduce: float, th_complete: float, straggler: int) -> dict:

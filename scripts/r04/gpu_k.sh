@@ -1,0 +1,12 @@
+#!/bin/bash
+# Round-4 pass K: small-buffer latency of the one-sided round vs the ipc lane
+# (4 processes on the card, exact rounds), 64 KiB .. 16 MiB.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
+export TMPDIR=/tmp
+O=gpurun_out/r04k
+mkdir -p $O/lat
+timeout -k 10 300 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node=4 --master-addr 127.0.0.1 \
+  --master-port 29700 bench/onesided_round.py --sizes-mb 0.0625,1,4,16 --chunk-mb 1 --lanes onesided,ipc \
+  --steps 50 --warmup 10 --out-dir $O/lat > $O/lat.log 2>&1 || { echo "lat rc=$?"; tail -20 $O/lat.log; exit 1; }
+python scripts/r04/summarize_round.py $O/lat 4 | tee $O/lat.jsonl | cut -c1-330

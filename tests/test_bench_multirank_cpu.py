@@ -159,6 +159,9 @@ def test_bench_cfg4_threshold_straggler():
     # at N=4 the three fast blocks alone meet floor(0.75 * 4) = 3 (one chunk per block here)
     assert c["straggler_block_required"] is False and c["need_complete_chunks"] == 3
     assert c["total_chunks"] == 4 and c["straggler_chunks"] == 1 and c["straggler_copy_required"] is False
+    # the untimed validation rounds: 2^rank inputs, every chunk's set matches its count
+    v = c["validation"]
+    assert v["contributor_sets_consistent"] is True and v["bad_chunks"] == 0 and v["chunks_checked"] >= 4 * 12, v
 
 
 def test_bench_cfg4_n2_labels_the_straggler_block_as_required():
