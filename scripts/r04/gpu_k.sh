@@ -10,3 +10,6 @@ timeout -k 10 300 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node
   --master-port 29700 bench/onesided_round.py --sizes-mb 0.0625,1,4,16 --chunk-mb 1 --lanes onesided,ipc \
   --steps 50 --warmup 10 --out-dir $O/lat > $O/lat.log 2>&1 || { echo "lat rc=$?"; tail -20 $O/lat.log; exit 1; }
 python scripts/r04/summarize_round.py $O/lat 4 | tee $O/lat.jsonl | cut -c1-330
+timeout -k 10 600 python -u -m pytest -x -v --timeout 250 --timeout-method thread tests/test_onesided_gpu.py -k chaos \
+  > $O/pytest_chaos.log 2>&1 || { echo "chaos rc=$?"; tail -30 $O/pytest_chaos.log; exit 1; }
+grep -E "PASSED|FAILED|passed|failed" $O/pytest_chaos.log

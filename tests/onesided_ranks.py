@@ -66,7 +66,8 @@ def check_sets(o, world, me, dtype, detail=None):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--mode", default="exact", choices=["exact", "straggler"])
+    ap.add_argument("--mode", default="exact", choices=["exact", "straggler", "chaos"])
+    ap.add_argument("--jitter-ms", type=float, default=2.0, help="chaos: every call waits U(0, jitter) first")
     ap.add_argument("--device", default="cpu")
     ap.add_argument("--size", type=int, default=1 << 16)
     ap.add_argument("--chunk", type=int, default=1 << 12)
@@ -116,6 +117,29 @@ def main():
             ok = torch.equal(o.data.cpu(), want.to(dtype)) and bool((o.count.cpu() == world).all())
             res["exact"].append(bool(ok))
             res["rounds"].append(o.iteration)
+    elif a.mode == "chaos":
+        # every rank waits a random time before each call (its own seeded
+        # stream): arrival orders, lags, catch-ups and overwrite conflicts
+        # all vary from round to round; every output chunk is checked
+        import random
+
+        rng = random.Random(1234 + rank)
+        x = torch.full((a.size,), float(1 << rank), dtype=dtype, device=dev)
+        out = torch.empty_like(x)
+        bad, detail, rounds, reasons, last = 0, [], [], [], -1
+        while last < a.rounds - 1:
+            time.sleep(rng.uniform(0.0, a.jitter_ms) / 1e3)
+            o = ar(x, out=out)
+            sync()
+            b, _ = check_sets(o, world, rank, dtype, detail)
+            bad += b
+            last = o.iteration
+            rounds.append(last)
+            reasons.append(o.status["reason"])
+        res["chaos"] = {"rounds": rounds, "bad_chunks": bad, "bad_detail": detail, "reasons": reasons,
+                        "stats": ar.stats()}
+        ar.retire()
+        sync()
     else:
         x = torch.full((a.size,), float(1 << rank), dtype=dtype, device=dev)
         out = torch.empty_like(x)

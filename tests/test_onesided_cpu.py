@@ -163,3 +163,19 @@ def test_onesided_rules():
     assert ev(2, 1, 3, 7, 7, 1, 0, True) == 5       # timeout
     sel = n.onesided_select_round  # (next, seen_max, max_lag)
     assert sel(5, 3, 1) == 5 and sel(5, 9, 1) == 8 and sel(5, 9, 0) == 9 and sel(0, -1, 2) == 0
+
+
+@pytest.mark.parametrize("n,th,max_lag", [(4, 0.75, 1), (3, 0.5, 2)])
+def test_onesided_chaos_jitter(n, th, max_lag):
+    """Every rank waits a random 0-3 ms before each call, 60 rounds: arrival
+    orders, lags and catch-ups vary from round to round.  Every output
+    chunk of every call is one contributor set matching its count; no wait
+    times out."""
+    r, rows = run_ranks(n, "--mode", "chaos", "--th", str(th), "--max-lag", str(max_lag), "--rounds", "60",
+                        "--jitter-ms", "3", "--size", str(1 << 14), "--chunk", str(1 << 10), "--timeout-s", "20")
+    assert r.returncode == 0, r.stderr[-3000:]
+    for d in rows:
+        c = d["chaos"]
+        assert c["bad_chunks"] == 0, (d["rank"], c["bad_detail"])
+        assert d["error"] == 0 and c["stats"]["timeouts"] == 0, c["stats"]
+        assert c["rounds"][-1] >= 59 and c["rounds"] == sorted(c["rounds"]), c["rounds"]

@@ -62,3 +62,21 @@ def test_onesided_gpu_straggler_killed_mid_run():
     for d in rows[:3]:
         assert d["error"] == 0 and d["straggler"]["bad_chunks"] == 0, d["stats"]
         assert d["straggler"]["rounds"][-1] >= 95 and d["stats"]["timeouts"] == 0
+
+
+@pytest.mark.parametrize("n,th,max_lag,dtype", [(4, 0.75, 1, "float32"), (8, 0.5, 2, "bfloat16"),
+                                                (3, 0.67, 1, "float32")])
+def test_onesided_gpu_chaos_jitter(n, th, max_lag, dtype):
+    """Every rank waits a random 0-2 ms before each call, 200 rounds, 16 MiB
+    (fp32) with 1 MiB chunks: arrival orders, lags, catch-ups and overwrite
+    conflicts vary from round to round across the card's XCDs.  Every output
+    chunk of every call is one contributor set matching its count."""
+    r, rows = run_ranks(n, "--mode", "chaos", "--th", str(th), "--max-lag", str(max_lag), "--rounds", "200",
+                        "--jitter-ms", "2", "--size", str(1 << 22), "--chunk", str(1 << 18), "--dtype", dtype,
+                        "--timeout-s", "10", device="cuda", timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    for d in rows:
+        c = d["chaos"]
+        assert c["bad_chunks"] == 0, (d["rank"], c["bad_detail"], c["stats"])
+        assert d["error"] == 0 and c["stats"]["timeouts"] == 0, c["stats"]
+        assert c["rounds"][-1] >= 199, c["rounds"][-5:]
