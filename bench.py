@@ -579,6 +579,26 @@ def run_extras(world: int, dev, barrier, which=("cfg1", "cfg3", "cfg4", "cfg5"),
                                              "samples_per_s": round(steps * batch * world / dt, 1),
                                              "compute_dtype": "bf16 autocast, fp32 master weights/grads; "
                                                               "forward+backward as one HIP graph replay"}
+        # N > 1 on a window lane (ipc* / onesided): the WHOLE step -- forward,
+        # backward, the allreduce and the fused average + SGD update -- as one
+        # replay (device-resident round ids, ThresholdAllreduce.capturable())
+        chosen = (ar.state().get("link", {}) or {}).get("lane") if world > 1 else None
+        if world > 1 and chosen is not None and (str(chosen).startswith("ipc") or chosen == "onesided"):
+            _sync()
+            barrier()
+            cap = ar.capturable()
+            try:
+                wstep = GraphedDPStep(model, bucket, xb, yb, compute_dtype=torch.bfloat16, allreduce=cap, lr=0.05)
+                wx, wy = wstep.static_inputs()
+                dt = timed(lambda: wstep(wx, wy, 0.05, None), steps, 5, world, barrier)
+                res["cfg5_mlp_dp_sgd_bf16_whole_graph"] = {
+                    "steps_per_s": round(steps / dt, 3), "samples_per_s": round(steps * batch * world / dt, 1),
+                    "lane": chosen, "compute_dtype": "bf16 autocast, fp32 master weights/grads; forward, backward, "
+                                                     "allreduce and update as one HIP graph replay"}
+            finally:
+                _sync()
+                barrier()
+                cap.close()
     except _Skip:
         pass
     except Exception as e:
