@@ -14,4 +14,5 @@ export UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1"
 export LD_PRELOAD="$ASAN_LIB:$UBSAN_LIB${LD_PRELOAD:+:$LD_PRELOAD}"
 python -m pytest -q -p no:cacheprovider tests/test_spec_worker.py tests/test_buffers.py tests/test_sim_schedule.py \
   tests/test_local_cluster.py tests/test_reactive_sim.py tests/test_faults.py tests/test_ipc_layout.py \
-  tests/test_membership_epochs.py tests/test_racecheck.py -m "not gpu" "$@"
+  tests/test_membership_epochs.py tests/test_racecheck.py tests/test_onesided_cpu.py tests/test_onesided_spec.py \
+  -m "not gpu" "$@"
