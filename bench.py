@@ -555,6 +555,7 @@ def run_extras(world: int, dev, barrier, which=("cfg1", "cfg3", "cfg4", "cfg5"),
         gen = torch.Generator(device=dev).manual_seed(1000 + (ar.rank or 0))
         xb, yb = synthetic_batch(batch, d_in, classes, device=dev, generator=gen)
         steps = 20
+        progress(f"rank {rank}: cfg5 eager fp32 (lane {(ar.state().get('link', {}) or {}).get('lane')})")
         dt = timed(lambda: dp_sgd_step(model, xb, yb, 0.05, ar, bucket, sync_loss=False), steps, 5, world, barrier)
         res["cfg5_mlp_dp_sgd"] = {"steps_per_s": round(steps / dt, 3),
                                   "samples_per_s": round(steps * batch * world / dt, 1),
@@ -563,6 +564,7 @@ def run_extras(world: int, dev, barrier, which=("cfg1", "cfg3", "cfg4", "cfg5"),
                                   "compute_dtype": "fp32"}
         # same model/step with bf16 MFMA GEMMs (autocast); fp32 weights, grads,
         # allreduce and update
+        progress(f"rank {rank}: cfg5 eager bf16")
         dt = timed(lambda: dp_sgd_step(model, xb, yb, 0.05, ar, bucket, sync_loss=False,
                                        compute_dtype=torch.bfloat16), steps, 5, world, barrier)
         res["cfg5_mlp_dp_sgd_bf16"] = {"steps_per_s": round(steps / dt, 3),
@@ -572,6 +574,7 @@ def run_extras(world: int, dev, barrier, which=("cfg1", "cfg3", "cfg4", "cfg5"),
         # allreduce and the fused update stay eager: GraphedDPStep)
         from akka_allreduce_amd.models.mlp import GraphedDPStep
 
+        progress(f"rank {rank}: cfg5 graphed forward+backward")
         gstep = GraphedDPStep(model, bucket, xb, yb, compute_dtype=torch.bfloat16)
         gx, gy = gstep.static_inputs()  # the synthetic batch lives in the graph's buffers
         dt = timed(lambda: gstep(gx, gy, 0.05, ar), steps, 5, world, barrier)
@@ -586,6 +589,7 @@ def run_extras(world: int, dev, barrier, which=("cfg1", "cfg3", "cfg4", "cfg5"),
         if world > 1 and chosen is not None and (str(chosen).startswith("ipc") or chosen == "onesided"):
             _sync()
             barrier()
+            progress(f"rank {rank}: cfg5 whole step graphed ({chosen})")
             cap = ar.capturable()
             try:
                 wstep = GraphedDPStep(model, bucket, xb, yb, compute_dtype=torch.bfloat16, allreduce=cap, lr=0.05)

@@ -125,6 +125,7 @@ void bind_onesided(py::module_& m) {
         d["total_chunks"] = l.geometry().total_chunks();
         d["threads"] = l.threads();
         d["ranks_on_this_gpu"] = l.shared_ranks();
+        d["lane_cus"] = l.lane_cus();
         d["pieces_per_part"] = l.pieces();
         const auto g = l.role_grid();
         d["role_wgs"] = py::dict(py::arg("push") = g[0], py::arg("reduce") = g[1], py::arg("copy") = g[2]);

@@ -224,6 +224,9 @@ OneSidedLane::~OneSidedLane() {
     hipSetDevice(device_);
     hipDeviceSynchronize();  // none of our kernels may still touch a window
     for (void* m : opened_) hipIpcCloseMemHandle(m);
+    if (cu_stream_) hipStreamDestroy(static_cast<hipStream_t>(cu_stream_));
+    if (ev_in_) hipEventDestroy(static_cast<hipEvent_t>(ev_in_));
+    if (ev_out_) hipEventDestroy(static_cast<hipEvent_t>(ev_out_));
     for (char* p : sd_)
       if (p) hipFree(p);
     for (char* p : gd_)
@@ -334,8 +337,32 @@ void OneSidedLane::open(const std::vector<std::string>& handles) {
     shared_ranks_ = share;
     if (share > 1) {
       nt_ = 256;
+      const char* cm = std::getenv("AKKA_OS_CU_MASK");  // "0": no mask (measurement knob)
+      int64_t total_default = 768;
+      if (!(cm && std::strcmp(cm, "0") == 0)) {
+        hipDeviceProp_t prop;
+        AKKA_OS_HIP(hipGetDeviceProperties(&prop, device_));
+        const int32_t ncu = std::max(1, prop.multiProcessorCount);
+        std::vector<uint32_t> mask(size_t((ncu + 31) / 32), 0u);
+        int32_t on = 0;
+        for (int32_t cu = 0; cu < ncu; ++cu)
+          if (cu % 4 != 3) {  // spread over every XCD / SE, a quarter of each left free
+            mask[size_t(cu / 32)] |= 1u << (cu % 32);
+            ++on;
+          }
+        hipStream_t s = nullptr;
+        AKKA_OS_HIP(hipExtStreamCreateWithCUMask(&s, uint32_t(mask.size()), mask.data()));
+        cu_stream_ = s;
+        hipEvent_t e0 = nullptr, e1 = nullptr;
+        AKKA_OS_HIP(hipEventCreateWithFlags(&e0, hipEventDisableTiming));
+        AKKA_OS_HIP(hipEventCreateWithFlags(&e1, hipEventDisableTiming));
+        ev_in_ = e0;
+        ev_out_ = e1;
+        lane_cus_ = on;
+        total_default = 768 * int64_t(on) / ncu;  // the same density on the masked CUs
+      }
       const char* bv = std::getenv("AKKA_OS_SHARED_BUDGET");  // measurement knob (resident 256-thread WGs)
-      const int64_t total = bv ? std::max(16, std::atoi(bv)) : 768;
+      const int64_t total = bv ? std::max(16, std::atoi(bv)) : total_default;
       const int64_t budget = total / share - 2 - g_.num_chunks(me_);
       size_roles(std::max<int64_t>(2, budget / 4));  // push, copy: 1 share each; reduce: 2
     }
@@ -413,7 +440,19 @@ void OneSidedLane::gpu_call(uintptr_t stream, const char* in, char* out, int32_t
   a.force = &hw_dev_->force;
   a.status = hw_dev_->status;
   AKKA_OS_HIP(hipSetDevice(device_));
-  launch_onesided_call(reinterpret_cast<hipStream_t>(stream), a, dt_ == DType::F32 ? 0 : 1);
+  hipStream_t caller = reinterpret_cast<hipStream_t>(stream);
+  if (cu_stream_) {
+    // fork/join through events (graph capture follows the same edges)
+    hipStream_t ls = static_cast<hipStream_t>(cu_stream_);
+    AKKA_OS_HIP(hipEventRecord(static_cast<hipEvent_t>(ev_in_), caller));
+    AKKA_OS_HIP(hipStreamWaitEvent(ls, static_cast<hipEvent_t>(ev_in_), 0));
+    launch_onesided_call(ls, a, dt_ == DType::F32 ? 0 : 1);
+    AKKA_OS_HIP(hipGetLastError());
+    AKKA_OS_HIP(hipEventRecord(static_cast<hipEvent_t>(ev_out_), ls));
+    AKKA_OS_HIP(hipStreamWaitEvent(caller, static_cast<hipEvent_t>(ev_out_), 0));
+    return;
+  }
+  launch_onesided_call(caller, a, dt_ == DType::F32 ? 0 : 1);
   AKKA_OS_HIP(hipGetLastError());
 }
 

@@ -112,6 +112,8 @@ class OneSidedLane {
   int32_t pieces() const { return nsub_; }
   int32_t threads() const { return nt_; }
   int32_t shared_ranks() const { return shared_ranks_; }
+  // CUs the round launch may use when ranks share this GPU (0: all)
+  int32_t lane_cus() const { return lane_cus_; }
   std::array<int32_t, 3> role_grid() const { return {gp_, gr_, gq_}; }
   size_t window_bytes() const { return win_bytes_; }
   const std::string& memory_kind() const { return mem_kind_; }
@@ -163,6 +165,16 @@ class OneSidedLane {
   os::Layout L_;
   int32_t D_ = 0, P_ = 1, Kmax_ = 0, need_r_ = 1, need_c_ = 1;
   int32_t nsub_ = 1, nt_ = 256, gp_ = 1, gr_ = 0, gq_ = 1, shared_ranks_ = 1;
+  // Ranks sharing one GPU: the round launch goes to a CU-masked stream (3 of
+  // every 4 CUs), joined to the caller's stream by events.  A rank's round
+  // waits on its peers; without the mask its waiting workgroups could sit on
+  // every SIMD of the card and keep a PEER process's compute kernels (those
+  // that need a whole SIMD's registers, e.g. fp32 MFMA GEMMs) from starting
+  // until the wait times out.
+  void* cu_stream_ = nullptr;  // hipStream_t
+  void* ev_in_ = nullptr;      // hipEvent_t
+  void* ev_out_ = nullptr;     // hipEvent_t
+  int32_t lane_cus_ = 0;
   std::string my_bus_;
   int64_t slot_ = 0, part_len_ = 64;
   size_t flag_bytes_ = 0, row_bytes_ = 0, win_bytes_ = 0;
