@@ -502,7 +502,8 @@ class ThresholdAllreduce:
         self._exact_os = OneSidedAllreduce(self.data_size, max_chunk_size=int(g.maxChunkSize), dtype=self.worker.dtype,
                                            th_reduce=1.0, th_complete=1.0, max_lag=1, rank=self.rank,
                                            world_size=self.world_size, device=self.device, store=self.store,
-                                           timeout_s=float(getattr(self, "onesided_timeout_s", 10.0)))
+                                           timeout_s=float(getattr(self, "onesided_timeout_s", 10.0)),
+                                           cu_keep=int(getattr(self, "onesided_cu_keep", 0)))
 
     def use_lane(self, name: str) -> None:
         """Switch to a named lane candidate (see LANES); every rank must do the

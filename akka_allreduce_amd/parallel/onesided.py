@@ -24,6 +24,11 @@ completions, catch-up skips.  GPU ranks (one per MI355X) map each other's
 windows through IPC handles; CPU ranks use POSIX shared memory -- the same
 protocol code, so multi-process CPU tests cover the GPU's decisions.
 
+Ranks sharing one GPU (tests, rehearsals) that also run compute between
+calls should pass ``cu_keep=6``: the round then runs on 6 of every 8 CUs, so
+a round waiting on its peers cannot hold every SIMD while a peer's GEMM
+needs one (csrc/transport/onesided.h, ``OneSidedParams::cu_keep``).
+
 Usage::
 
     ar = OneSidedAllreduce(n, max_chunk_size=1 << 20, th_reduce=0.75, th_complete=0.75, max_lag=1)
@@ -116,6 +121,7 @@ class OneSidedAllreduce:
         timeout_s: float = 30.0,
         threads: int = 256,
         role_wgs: int = 0,
+        cu_keep: int = 0,
         data_sink: Any = None,
     ):
         if dtype not in _DTYPES:
@@ -157,7 +163,7 @@ class OneSidedAllreduce:
                                        _DTYPES[dtype], th_reduce=float(th_reduce), th_complete=float(th_complete),
                                        max_lag=int(max_lag), rows=int(rows), part_bytes=int(part_bytes),
                                        timeout_ms=int(timeout_s * 1000), threads=int(threads),
-                                       role_wgs=int(role_wgs))
+                                       role_wgs=int(role_wgs), cu_keep=int(cu_keep))
             mine = self.lane.handle()
         except Exception as e:  # noqa: BLE001 - re-raised after the exchange
             mine, err = b"", e

@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--which", default="direct,engine")
     ap.add_argument("--dp-steps", type=int, default=0, help="then: config 5's MLP DP-SGD step on the lane")
     ap.add_argument("--blocks", default="5,20", help="then: DP steps in blocks without a sync inside")
+    ap.add_argument("--cu-keep", type=int, default=6, help="DP lane: CUs kept of every 8 (0: no mask)")
     ap.add_argument("--keep", action="store_true", help="keep the earlier lanes alive (no teardown before the DP lane)")
     ap.add_argument("--gemm", type=int, default=0, help="rank r runs r*GEMM 256x4096x8192 bf16 before each call")
     a = ap.parse_args()
@@ -76,6 +77,7 @@ def main():
         bucket = GradientBucket(list(model.parameters()), flatten_params=True)
         ar = ThresholdAllreduce(bucket.numel, max_chunk_size=a.chunk, device=dev, data_plane="ipc")
         ar.onesided_timeout_s = a.timeout_s
+        ar.onesided_cu_keep = a.cu_keep
         ar.use_lane("onesided")
         ar._exact_os.lane  # noqa: B018 - mapped
         gen = torch.Generator(device=dev).manual_seed(1000 + rank)

@@ -337,16 +337,17 @@ void OneSidedLane::open(const std::vector<std::string>& handles) {
     shared_ranks_ = share;
     if (share > 1) {
       nt_ = 256;
-      const char* cm = std::getenv("AKKA_OS_CU_MASK");  // "0": no mask (measurement knob)
+      const char* kv = std::getenv("AKKA_OS_CU_KEEP");  // CUs kept of every 8 (measurement knob)
+      const int32_t keep = kv ? std::clamp(std::atoi(kv), 0, 8) : std::clamp(p_.cu_keep, 0, 8);
       int64_t total_default = 768;
-      if (!(cm && std::strcmp(cm, "0") == 0)) {
+      if (keep > 0 && keep < 8) {
         hipDeviceProp_t prop;
         AKKA_OS_HIP(hipGetDeviceProperties(&prop, device_));
         const int32_t ncu = std::max(1, prop.multiProcessorCount);
         std::vector<uint32_t> mask(size_t((ncu + 31) / 32), 0u);
         int32_t on = 0;
         for (int32_t cu = 0; cu < ncu; ++cu)
-          if (cu % 4 != 3) {  // spread over every XCD / SE, a quarter of each left free
+          if (cu % 8 < keep) {  // spread over every XCD / SE, the rest of each group left free
             mask[size_t(cu / 32)] |= 1u << (cu % 32);
             ++on;
           }

@@ -48,6 +48,13 @@ struct OneSidedParams {
   int64_t timeout_ms = 30000;            // bound of every wait (then forced + error)
   int32_t threads = 256;                 // workgroup size of the round launch (256 or 1024)
   int32_t role_wgs = 0;                  // workgroups per data role (push / reduce / copy); 0: automatic
+  // Ranks sharing one GPU that also run compute kernels (a DP step): keep the
+  // round launch on `cu_keep` of every 8 CUs (a CU-masked stream), so a round
+  // waiting on its peers cannot hold every SIMD while a PEER's kernels that
+  // need a whole SIMD's registers (fp32 MFMA GEMMs) wait for one.  0: no mask
+  // (a rank on a GPU of its own never needs one; the mask costs the
+  // shared-card round ~0.25 ms at 64 MiB, profiles/r04/README.md)
+  int32_t cu_keep = 0;
 };
 
 class OneSidedLane {
@@ -165,12 +172,8 @@ class OneSidedLane {
   os::Layout L_;
   int32_t D_ = 0, P_ = 1, Kmax_ = 0, need_r_ = 1, need_c_ = 1;
   int32_t nsub_ = 1, nt_ = 256, gp_ = 1, gr_ = 0, gq_ = 1, shared_ranks_ = 1;
-  // Ranks sharing one GPU: the round launch goes to a CU-masked stream (3 of
-  // every 4 CUs), joined to the caller's stream by events.  A rank's round
-  // waits on its peers; without the mask its waiting workgroups could sit on
-  // every SIMD of the card and keep a PEER process's compute kernels (those
-  // that need a whole SIMD's registers, e.g. fp32 MFMA GEMMs) from starting
-  // until the wait times out.
+  // OneSidedParams::cu_keep on a shared GPU: the round launch goes to a
+  // CU-masked stream, joined to the caller's stream by events
   void* cu_stream_ = nullptr;  // hipStream_t
   void* ev_in_ = nullptr;      // hipEvent_t
   void* ev_out_ = nullptr;     // hipEvent_t
