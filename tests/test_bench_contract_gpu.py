@@ -148,3 +148,33 @@ def test_bench_preflight_failure_falls_back_to_ipc():
         and d["lane_is_framework"] is True
     assert all(k.startswith("ipc") or k == "onesided" for k in d["lane_select"] if k != "chosen"), d["lane_select"]
     assert d["exact"] is True and d["value"] > 0 and d["rccl_allreduce_algbw_GBps"] is None
+
+
+def test_bench_cfg5_two_ranks_on_one_card():
+    """BASELINE config 5 (MLP DP-SGD) in bench.py's N-rank flow, 2 processes
+    on the card, ipc data plane: the eager, graphed and -- on a window lane --
+    whole-step graphed variants all run (a one-sided round waiting on its
+    peer must not hold the peer's GEMMs off the card: cu_keep on a shared
+    GPU, profiles/r04/README.md)."""
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, AKKA_SHARE_GPU="1", GPU_MAX_HW_QUEUES="8")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+                        "--gpus", "2", "--steps", "3", "--warmup", "1", "--size-mb", "16", "--data-plane", "ipc",
+                        "--extras", "on", "--extras-only", "cfg5", "--link-probe", "off", "--compare-rccl", "off",
+                        "--extras-deadline-s", "150"], capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip().startswith("{")]
+    d = json.loads(lines[-1])
+    assert "extras_error" not in d, d.get("extras_error")
+    ex = d["extra_configs"]
+    assert "cfg5_error" not in ex, ex.get("cfg5_error")
+    for k in ("cfg5_mlp_dp_sgd", "cfg5_mlp_dp_sgd_bf16", "cfg5_mlp_dp_sgd_bf16_graph"):
+        assert ex[k]["steps_per_s"] > 50, ex
+    if d["lane"] == "onesided" or d["lane"].startswith("ipc"):
+        w = ex["cfg5_mlp_dp_sgd_bf16_whole_graph"]
+        assert w["lane"] == d["lane"] and w["steps_per_s"] > 50, ex
