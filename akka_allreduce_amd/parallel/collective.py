@@ -338,7 +338,7 @@ class ThresholdAllreduce:
         if self.transport == "onesided":
             if self.pacer is None:
                 self._round += 1
-                return self._os(x, out=out)
+                return self._os(x, out=out, async_op=async_op)
             # paced: wait for round r, call, then report every round this call
             # completed -- the served one and any it skipped by catch-up (the
             # reference force-completes those, W:100-106) -- like
@@ -357,7 +357,7 @@ class ThresholdAllreduce:
         if self._lane_os:
             # exact rounds on the one-sided lane (tune candidate "onesided"):
             # valid in the caller's stream order, like an async round
-            out = self._exact_os(x, out=out)
+            out = self._exact_os(x, out=out, async_op=async_op)
         else:
             out = self.worker.allreduce(x, async_op=async_op, out=out)
         if out is None:
@@ -368,10 +368,20 @@ class ThresholdAllreduce:
         return out
 
     def runs_async(self) -> bool:
-        """Whether ``async_op=True`` rounds run on the engine's own streams.
-        The one-sided lane always runs on the caller's stream: its output is
-        valid in the caller's stream order, not behind the engine's streams."""
-        return self.transport == "stream" and not self._lane_os
+        """Whether ``async_op=True`` rounds run off the caller's stream (then
+        ``async_stream()`` is where their results complete).  Paced one-sided
+        rounds wait for their call on the host and stay synchronous."""
+        if self.transport == "onesided":
+            return self.pacer is None and self.device.type == "cuda"
+        return self.transport == "stream"
+
+    def async_stream(self):
+        """The stream an async round's result completes on (see runs_async)."""
+        if self.transport == "onesided":
+            return self._os._side_stream()
+        if self._lane_os:
+            return self._exact_os._side_stream()
+        return self.worker._internal_streams()[1]
 
     def set_lane(self, lane: str) -> None:
         """Switch the exact-round lane (``auto`` / ``p2p`` / ``collective``,

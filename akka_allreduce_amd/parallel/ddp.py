@@ -103,7 +103,6 @@ def threshold_allreduce_hook(state: ThresholdHookState, bucket: dist.GradBucket)
         work = flat
     ar = state.engine(work)
     cuda = work.is_cuda
-    # (a tuned one-sided lane runs on the caller's stream: no async round)
     async_op = bool(state.async_op and cuda and ar.runs_async())
     out = ar(work.contiguous(), async_op=async_op)
     state.rounds += 1
@@ -117,7 +116,7 @@ def threshold_allreduce_hook(state: ThresholdHookState, bucket: dist.GradBucket)
     # record_streams the result).  Async: the count-mean runs on the engine's
     # compute stream behind the round, so the caller's stream -- the rest of
     # the backward pass -- only waits where DDP consumes the bucket.
-    side = ar.worker._internal_streams()[1] if async_op else torch.cuda.current_stream(work.device)
+    side = ar.async_stream() if async_op else torch.cuda.current_stream(work.device)
     with torch.cuda.stream(side):
         mean = out.mean().to(t.dtype).view_as(t)
         fut = torch.futures.Future(devices=[work.device])

@@ -180,11 +180,17 @@ class OneSidedAllreduce:
         self.lane.unlink()
         self._kmax = self.geometry.kmax
         self._counts: Optional[torch.Tensor] = None
+        self._side: Optional[torch.cuda.Stream] = None  # async_op rounds
         self.calls = 0
 
     def __call__(self, x: torch.Tensor, out: Optional[torch.Tensor] = None, async_op: bool = False) -> OneSidedOutput:
         """One round of this rank.  GPU: enqueued on the current stream (the
-        output is valid in its order; ``async_op`` is accepted for API parity).
+        output is valid in its order).  ``async_op=True`` (GPU): the round runs
+        on the lane's side stream, behind everything enqueued so far on the
+        current one, so later work on the current stream (the rest of a
+        backward pass) overlaps it; ``wait()`` -- or ``mean()`` / ``count`` /
+        ``axpy_mean_()``, which call it -- joins the result into the then
+        current stream (torch.distributed's ``async_op`` convention).
         CPU: returns after the round completed."""
         if x.numel() != self.data_size:
             raise ValueError(f"expected {self.data_size} elements, got {x.numel()}")
@@ -205,14 +211,30 @@ class OneSidedAllreduce:
         else:
             counts = torch.empty((self.world_size, self._kmax), dtype=torch.int32, device=self.device)
         stream = torch.cuda.current_stream(self.device) if self.device.type == "cuda" else None
+        event = None
+        if async_op and stream is not None:
+            side = self._side_stream()
+            side.wait_stream(stream)
+            for t in (x, out, counts):  # the caching allocator: in use on the side stream too
+                t.record_stream(side)
+            stream = side
         call = self.lane.round(stream.cuda_stream if stream is not None else 0, x.data_ptr(), out.data_ptr(),
                                counts.data_ptr(), self._kmax)
+        if async_op and stream is not None:
+            event = torch.cuda.Event()
+            event.record(stream)
         self.calls += 1
         o = OneSidedOutput(out.view(-1), lane=self.lane, call=call, stream=stream, counts_per_chunk=counts,
-                           geometry=self.geometry, expander=self._expand if stream is not None else None)
+                           geometry=self.geometry, expander=self._expand if stream is not None else None,
+                           event=event)
         if self.data_sink is not None:
             self.data_sink(o)
         return o
+
+    def _side_stream(self) -> "torch.cuda.Stream":
+        if self._side is None:
+            self._side = torch.cuda.Stream(self.device)
+        return self._side
 
     @property
     def capturable(self) -> bool:

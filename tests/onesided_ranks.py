@@ -67,6 +67,7 @@ def check_sets(o, world, me, dtype, detail=None):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--mode", default="exact", choices=["exact", "straggler", "chaos"])
+    ap.add_argument("--async-op", action="store_true", help="exact: async rounds (side stream), wait() then read")
     ap.add_argument("--jitter-ms", type=float, default=2.0, help="chaos: every call waits U(0, jitter) first")
     ap.add_argument("--device", default="cpu")
     ap.add_argument("--size", type=int, default=1 << 16)
@@ -108,7 +109,11 @@ def main():
         res["exact"], res["rounds"] = [], []
         for r in range(a.rounds):
             x = torch.randn(a.size, generator=torch.Generator().manual_seed(1000 * rank + r)).to(dtype)
-            o = ar(x.to(dev))
+            xd = x.to(dev)
+            o = ar(xd, async_op=a.async_op)
+            if a.async_op:
+                xd.mul_(0)  # the round read its input behind the fork: later work on this stream cannot change it
+                o.wait()
             sync()
             want = None
             for s in range(world):

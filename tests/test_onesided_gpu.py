@@ -30,6 +30,17 @@ def test_onesided_gpu_exact_rounds(n, size, chunk, dtype):
         assert d["error"] == 0 and d["stats"]["missing_chunks"] == 0, d["stats"]
 
 
+def test_onesided_gpu_exact_rounds_async():
+    """async_op=True: the round runs on the lane's side stream behind the
+    caller's stream; the input is overwritten on the caller's stream right
+    after the call (the round already read it in order), wait() joins."""
+    r, rows = run_ranks(4, "--mode", "exact", "--size", str(1 << 22), "--chunk", str(1 << 18), "--rounds", "4",
+                        "--async-op", "--timeout-s", "10", device="cuda", timeout=180)
+    assert r.returncode == 0, r.stderr[-3000:]
+    for d in rows:
+        assert d["exact"] == [True] * 4 and d["error"] == 0, d
+
+
 def test_onesided_gpu_straggler_steady_state():
     """N=4 on the card, 0.75 / 0.75, maxLag 1, rank 3 sleeps 50 ms per call,
     64 rounds: fast ranks' median round within 2x of the straggler-free phase,
