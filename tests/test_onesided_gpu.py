@@ -32,8 +32,7 @@ def test_onesided_gpu_exact_rounds(n, size, chunk, dtype):
 
 def test_onesided_gpu_exact_rounds_async():
     """async_op=True: the round runs on the lane's side stream behind the
-    caller's stream; the input is overwritten on the caller's stream right
-    after the call (the round already read it in order), wait() joins."""
+    caller's stream (the input's host-to-device copy); wait() joins it."""
     r, rows = run_ranks(4, "--mode", "exact", "--size", str(1 << 22), "--chunk", str(1 << 18), "--rounds", "4",
                         "--async-op", "--timeout-s", "10", device="cuda", timeout=180)
     assert r.returncode == 0, r.stderr[-3000:]
