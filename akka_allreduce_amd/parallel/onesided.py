@@ -42,6 +42,7 @@ from typing import Any, Optional
 import torch
 
 from .._native_loader import load as _load
+from ..utils import tracing as _tracing
 from ..data import AllReduceOutput, Geometry
 from .collective import _handle_exchange, env_rank_world
 
@@ -218,8 +219,10 @@ class OneSidedAllreduce:
             for t in (x, out, counts):  # the caching allocator: in use on the side stream too
                 t.record_stream(side)
             stream = side
-        call = self.lane.round(stream.cuda_stream if stream is not None else 0, x.data_ptr(), out.data_ptr(),
-                               counts.data_ptr(), self._kmax)
+        # roctx range around the enqueue (AKKA_TRACE=1; rocprofv3 --marker-trace)
+        with _tracing.range_(f"akka.onesided call {self.calls}"):
+            call = self.lane.round(stream.cuda_stream if stream is not None else 0, x.data_ptr(), out.data_ptr(),
+                                   counts.data_ptr(), self._kmax)
         if async_op and stream is not None:
             event = torch.cuda.Event()
             event.record(stream)
