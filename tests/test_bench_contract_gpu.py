@@ -90,6 +90,9 @@ def test_bench_multirank_on_one_card(plane):
         w = c4["with_straggler"]
         assert c4["transport"] == "onesided" and w["timeouts"] == 0, c4
         assert w["fast_rank_median_ms_per_round"] < 40 / 4 and w["catch_up_skipped_rounds"] > 0, c4
+        # the untimed validation rounds (2^rank inputs): every chunk's set matches its count
+        v = c4["validation"]
+        assert v["contributor_sets_consistent"] is True and v["bad_chunks"] == 0, v
     else:
         # the ipc lane's variants and the one-sided lane (exact rounds)
         assert set(cands) == {"ipc", "ipc_bcast", "ipc_fused", "ipc_fused_bcast", "ipc_wide", "ipc_bcast_wide",
