@@ -186,7 +186,11 @@ class ThresholdAllreduce:
         data_plane: str = "rccl",
         share_transport_with: Optional["ThresholdAllreduce"] = None,
         ipc_capacity: int = 0,
+        onesided_options: Optional[dict] = None,
     ):
+        # extra OneSidedAllreduce arguments for the one-sided lane (transport
+        # "onesided" or lane "onesided"), e.g. {"cu_keep": 6} on a shared GPU
+        self.onesided_options = dict(onesided_options or {})
         self._lane_os = False  # exact rounds on the one-sided lane (use_lane("onesided"))
         self._direct = None    # an open CapturableExact view
         if transport == "onesided":
@@ -197,7 +201,7 @@ class ThresholdAllreduce:
 
             self._os = OneSidedAllreduce(data_size, max_chunk_size=max_chunk_size, dtype=dtype, th_reduce=th_reduce,
                                          th_complete=th_complete, max_lag=max_lag, rank=rank, world_size=world_size,
-                                         device=device, store=store, data_sink=data_sink)
+                                         device=device, store=store, data_sink=data_sink, **self.onesided_options)
             self.rank, self.world_size, self.device = self._os.rank, self._os.world_size, self._os.device
             self.transport, self.worker, self.pacer, self.store = "onesided", None, None, store
             self.data_size, self._round = int(data_size), 0
@@ -512,8 +516,7 @@ class ThresholdAllreduce:
         self._exact_os = OneSidedAllreduce(self.data_size, max_chunk_size=int(g.maxChunkSize), dtype=self.worker.dtype,
                                            th_reduce=1.0, th_complete=1.0, max_lag=1, rank=self.rank,
                                            world_size=self.world_size, device=self.device, store=self.store,
-                                           timeout_s=float(getattr(self, "onesided_timeout_s", 10.0)),
-                                           cu_keep=int(getattr(self, "onesided_cu_keep", 0)))
+                                           **{"timeout_s": 10.0, **self.onesided_options})
 
     def use_lane(self, name: str) -> None:
         """Switch to a named lane candidate (see LANES); every rank must do the

@@ -16,7 +16,7 @@ windows, parallel/onesided.py; one window set per bucket size, since each
 lane's round tags are its own); ``transport="reactive"`` is the RCCL
 alternative, bounded by its send-slot pool.
 """
-from typing import Dict, Tuple
+from typing import Dict, Optional, Tuple
 
 import torch
 import torch.distributed as dist
@@ -51,10 +51,10 @@ class ThresholdHookState:
     def __init__(self, *, th_reduce: float = 1.0, th_complete: float = 1.0, max_lag: int = 2,
                  max_chunk_size: int = 1 << 20, transport: str = "stream", broadcast_lag: int = 2,
                  async_op: bool = True, th_allreduce=None, data_plane: str = "rccl", tune: bool = False,
-                 bucket_cap_mb: float = 25.0):
+                 bucket_cap_mb: float = 25.0, onesided_options: Optional[dict] = None):
         self.kw = dict(th_reduce=th_reduce, th_complete=th_complete, max_lag=max_lag, max_chunk_size=max_chunk_size,
                        transport=transport, broadcast_lag=broadcast_lag, th_allreduce=th_allreduce,
-                       data_plane=data_plane)
+                       data_plane=data_plane, onesided_options=onesided_options)
         self.engines: Dict[Tuple[int, torch.dtype, torch.device], ThresholdAllreduce] = {}
         self.rounds = 0
         self.async_op = async_op

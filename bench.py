@@ -548,13 +548,12 @@ def run_extras(world: int, dev, barrier, which=("cfg1", "cfg3", "cfg4", "cfg5"),
         d_in, hidden, classes, batch = 4096, 8192, 1000, 256
         model = MLP(d_in, hidden, classes).to(dev)
         bucket = GradientBucket(list(model.parameters()), flatten_params=True)
+        # ranks on ONE card: a one-sided round waiting on its peers must leave
+        # SIMDs free for the peers' GEMMs (OneSidedParams::cu_keep)
         ar = ThresholdAllreduce(bucket.numel, max_chunk_size=(4 << 20) // 4, device=dev, data_plane=data_plane,
-                                share_transport_with=_shareable(share))
+                                share_transport_with=_shareable(share),
+                                onesided_options={"cu_keep": 6} if os.environ.get("AKKA_SHARE_GPU") == "1" else None)
         keep.append(ar)
-        if os.environ.get("AKKA_SHARE_GPU") == "1":
-            # ranks on ONE card: a one-sided round waiting on its peers must
-            # leave SIMDs free for the peers' GEMMs (OneSidedParams::cu_keep)
-            ar.onesided_cu_keep = 6
         apply_lane_choice(ar, lane)
         gen = torch.Generator(device=dev).manual_seed(1000 + (ar.rank or 0))
         xb, yb = synthetic_batch(batch, d_in, classes, device=dev, generator=gen)

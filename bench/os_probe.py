@@ -75,9 +75,8 @@ def main():
         torch.manual_seed(0)
         model = MLP(4096, 8192, 1000).to(dev)
         bucket = GradientBucket(list(model.parameters()), flatten_params=True)
-        ar = ThresholdAllreduce(bucket.numel, max_chunk_size=a.chunk, device=dev, data_plane="ipc")
-        ar.onesided_timeout_s = a.timeout_s
-        ar.onesided_cu_keep = a.cu_keep
+        ar = ThresholdAllreduce(bucket.numel, max_chunk_size=a.chunk, device=dev, data_plane="ipc",
+                                onesided_options={"timeout_s": a.timeout_s, "cu_keep": a.cu_keep})
         ar.use_lane("onesided")
         ar._exact_os.lane  # noqa: B018 - mapped
         gen = torch.Generator(device=dev).manual_seed(1000 + rank)
