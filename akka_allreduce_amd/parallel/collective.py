@@ -372,11 +372,16 @@ class ThresholdAllreduce:
         return out
 
     def runs_async(self) -> bool:
-        """Whether ``async_op=True`` rounds run off the caller's stream (then
-        ``async_stream()`` is where their results complete).  Paced one-sided
-        rounds wait for their call on the host and stay synchronous."""
-        if self.transport == "onesided":
-            return self.pacer is None and self.device.type == "cuda"
+        """Whether the DDP hook should issue ``async_op=True`` rounds (then
+        ``async_stream()`` is where their results complete).  Not on the
+        one-sided lane: its round keeps a wave on every SIMD while it waits
+        for peers, so the backward kernels an async round would overlap wait
+        for it anyway, and the side-stream hand-offs cost more than they save
+        (bench/ddp_overlap.py, 2 ranks: 3.11 ms per DDP step sync vs 4.57
+        async; profiles/r04/README.md).  ``OneSidedAllreduce(async_op=True)``
+        stays available."""
+        if self.transport == "onesided" or self._lane_os:
+            return False
         return self.transport == "stream"
 
     def async_stream(self):
