@@ -181,6 +181,11 @@ def run_cfg4(world: int, rank: int, dev, barrier, size_mb: float, delay_ms: floa
         if dev.type == "cuda":
             torch.cuda.current_stream(dev).synchronize()
 
+    # every rank's setup kernels done before any round starts: on a shared
+    # card a peer's waiting round could otherwise hold the SIMDs a late
+    # rank's setup kernels need (docs/DESIGN.md §4c, cu_keep)
+    sync()
+    barrier()
     last = -1
     for pi, key in enumerate(("no_straggler", "with_straggler")):
         target = (pi + 1) * rounds - 1
@@ -248,6 +253,8 @@ def cfg4_validate(ar, world: int, rank: int, straggler: int, delay_ms: float, la
     x = torch.full((S,), float(1 << rank), device=dev)
     out = torch.empty_like(x)
     bad, chunks, calls, first_bad = 0, 0, 0, None
+    if dev.type == "cuda":
+        torch.cuda.synchronize(dev)  # x is written before any peer's round can wait on this rank
     lasts = [None] * world
     dist.all_gather_object(lasts, last)
     target = max(lasts) + rounds  # a common round, like the timed phases
