@@ -66,9 +66,11 @@
 //   complete wait until floor(thComplete*total) reduced chunks landed (mine
 //            counted once reduced) or the round is forced; publish the set
 //   copy     per part of a peer's block: copied to the output as soon as it
-//            lands (the reference's per-chunk fire, W:177-181), or skipped
-//   finish   chunks outside the completion set -> 0 / count 0, counts,
-//            withdraw the announcements, publish the call's status
+//            lands (the reference's per-chunk fire, W:177-181); once the set
+//            is published, parts outside it -> 0 (own parts after their
+//            reduce pieces); the complete role writes the counts
+//   finish   the last workgroup out: withdraw the announcements, publish the
+//            call's status, call id + 1
 #pragma once
 
 #include <cstdint>
@@ -169,7 +171,7 @@ enum StateWord : int32_t {
   kCur = 1,          // round of the call in progress
   kCallSeq = 2,      // calls finished on this lane (the next call's id; device-resident)
   kBegun = 3,        // call id + 1 once the call's round is selected
-  kCtrFinish = 4,    // finish workgroups done (the last one publishes the call)
+  kCtrFinish = 4,    // workgroups done with the call (the last one out finishes it)
   kCompReason = 5,   // how the completion decision was reached (Verdict)
   kCompLanded = 6,   // chunks landed at the completion decision (mine included)
   kForcedChunks = 7,
