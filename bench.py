@@ -1104,6 +1104,20 @@ def main() -> int:
             line["extra_configs"]["lane"] = chosen_lane
         guard.disarm()
 
+    if world > 1:
+        # the job's own correctness checks in one place (on a node: the
+        # cross-device hand-offs of the window lanes)
+        sel = line.get("lane_select") or {}
+        v4 = ((line.get("extra_configs") or {}).get("cfg4_threshold_straggler") or {}).get("validation") or {}
+        line["checks"] = {
+            "headline_exact": line.get("exact"),
+            "preflight": line.get("preflight"),
+            "lane_candidates_exact": sorted(k for k, v in sel.items() if isinstance(v, dict) and v.get("exact")),
+            "lane_candidates_rejected": sorted(k for k, v in sel.items() if isinstance(v, dict) and not v.get("exact")),
+            "cfg4_contributor_sets_consistent": v4.get("contributor_sets_consistent"),
+            "cfg4_chunks_checked": v4.get("chunks_checked"),
+        }
+
     if rank == 0:
         print(json.dumps(line), file=json_out, flush=True)
     if world > 1 and dist.is_initialized():

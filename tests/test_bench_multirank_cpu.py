@@ -162,6 +162,8 @@ def test_bench_cfg4_threshold_straggler():
     # the untimed validation rounds: 2^rank inputs, every chunk's set matches its count
     v = c["validation"]
     assert v["contributor_sets_consistent"] is True and v["bad_chunks"] == 0 and v["chunks_checked"] >= 4 * 12, v
+    ck = d["checks"]  # the line's summary of the job's own checks
+    assert ck["cfg4_contributor_sets_consistent"] is True and ck["cfg4_chunks_checked"] == v["chunks_checked"], ck
 
 
 def test_bench_cfg4_n2_labels_the_straggler_block_as_required():
