@@ -375,14 +375,16 @@ def run_cfg4_reactive(world: int, rank: int, dev, barrier, size_mb: float, delay
     return res
 
 
-def run_cfg1(rounds: int = 300) -> dict:
+def run_cfg1(rounds: int = 300, gpu: bool = False) -> dict:
     """BASELINE config 1, the reference's README demo: a master and 2 worker
     PROCESSES (the CLI, as `sbt runMain ...` in the reference) over loopback
     TCP, dataSize 10, maxChunkSize 2, maxLag 1, CPU data plane.  Run twice:
     the demo's thresholds (1 / 1 / 0.8, M:98-107) and exact thresholds with
     the sink's assertMultiple check (W:337-340).  Reports rounds per second
     and the sink's own MB/s figure (W:329-342) over the last checkpoint
-    interval of each worker."""
+    interval of each worker.  ``gpu``: a third run with the workers on this
+    GPU and their data plane on the one-sided lane (master hosts the window
+    rendezvous, paces with thAllreduce), exact thresholds + assertMultiple."""
     import re
     import socket
     import subprocess
@@ -392,7 +394,10 @@ def run_cfg1(rounds: int = 300) -> dict:
     cp = max(1, rounds // 3)
     res = {"workers": 2, "data_size": 10, "max_chunk_size": 2, "max_lag": 1, "rounds": rounds,
            "transport": "tcp, one process per worker (cpu)"}
-    for tag, thc, mult in (("demo_thresholds", 0.8, 0), ("exact_assert", 1.0, 2)):
+    runs = [("demo_thresholds", 0.8, 0, "tcp", "cpu", None), ("exact_assert", 1.0, 2, "tcp", "cpu", None)]
+    if gpu:
+        runs.append(("gpu_onesided_exact_assert", 1.0, 2, "onesided", "cuda", "onesided"))
+    for tag, thc, mult, mtransport, wdev, wtransport in runs:
         with socket.socket() as sk:
             sk.bind(("127.0.0.1", 0))
             port = sk.getsockname()[1]
@@ -400,7 +405,8 @@ def run_cfg1(rounds: int = 300) -> dict:
             logs = [open(os.path.join(td, f"p{i}.log"), "w+") for i in range(3)]
             procs = [subprocess.Popen(base + ["master", "--port", str(port), "--workers", "2", "--data-size", "10",
                                               "--max-chunk-size", "2", "--max-round", str(rounds), "--max-lag", "1",
-                                              "--th-reduce", "1.0", "--th-complete", str(thc), "--transport", "tcp"],
+                                              "--th-reduce", "1.0", "--th-complete", str(thc), "--transport",
+                                              mtransport],
                                       stdout=logs[0], stderr=subprocess.STDOUT, cwd=os.path.dirname(__file__) or ".")]
             t_end = time.time() + 20
             while time.time() < t_end:  # master listening?
@@ -409,9 +415,10 @@ def run_cfg1(rounds: int = 300) -> dict:
                     break
                 except OSError:
                     time.sleep(0.1)
+            wextra = ["--transport", wtransport] if wtransport else []
             procs += [subprocess.Popen(base + ["worker", "--master", f"127.0.0.1:{port}", "--data-size", "10",
                                                "--checkpoint", str(cp), "--assert-multiple", str(mult), "--device",
-                                               "cpu"], stdout=logs[i], stderr=subprocess.STDOUT,
+                                               wdev, *wextra], stdout=logs[i], stderr=subprocess.STDOUT,
                                        cwd=os.path.dirname(__file__) or ".") for i in (1, 2)]
             rcs = []
             try:
@@ -422,7 +429,8 @@ def run_cfg1(rounds: int = 300) -> dict:
                     if p.poll() is None:
                         p.kill()
                         p.wait()
-            entry = {"rcs": rcs, "rounds_per_s": [], "sink_MBps": [], "failures": []}
+            entry = {"rcs": rcs, "rounds_per_s": [], "sink_MBps": [], "failures": [], "workers_on": wdev,
+                     "data_plane": "one-sided lane (GPU windows)" if wtransport == "onesided" else "tcp"}
             for f in logs[1:]:
                 f.seek(0)
                 txt = f.read()
@@ -498,7 +506,7 @@ def run_extras(world: int, dev, barrier, which=("cfg1", "cfg3", "cfg4", "cfg5"),
     progress(f"rank {rank}: extras {','.join(which)}")
     if "cfg1" in which and rank == 0:
         try:
-            res["cfg1_readme_demo_cluster"] = run_cfg1()
+            res["cfg1_readme_demo_cluster"] = run_cfg1(gpu=dev.type == "cuda")
         except Exception as e:
             res["cfg1_error"] = f"{type(e).__name__}: {e}"[:200]
     if "cfg4" in which and world > 1:
