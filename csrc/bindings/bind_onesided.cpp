@@ -42,6 +42,14 @@ void bind_onesided(py::module_& m) {
            py::arg("part_bytes") = int64_t(256) << 10, py::arg("timeout_ms") = 30000, py::arg("threads") = 256,
            py::arg("role_wgs") = 0, py::arg("cu_keep") = 0)
       .def("handle", [](const OneSidedLane& l) { return py::bytes(l.handle()); })
+      .def("timeline", [](OneSidedLane& l) {
+        std::vector<uint64_t> v;
+        {
+          py::gil_scoped_release nogil;
+          v = l.timeline();
+        }
+        return v;
+      })
       .def("open", [](OneSidedLane& l, std::vector<std::string> handles) {
         py::gil_scoped_release nogil;
         l.open(handles);
@@ -127,6 +135,7 @@ void bind_onesided(py::module_& m) {
         d["threads"] = l.threads();
         d["ranks_on_this_gpu"] = l.shared_ranks();
         d["lane_cus"] = l.lane_cus();
+        d["clock_khz"] = l.clock_khz();
         d["pieces_per_part"] = l.pieces();
         const auto g = l.role_grid();
         d["role_wgs"] = py::dict(py::arg("push") = g[0], py::arg("reduce") = g[1], py::arg("copy") = g[2]);

@@ -725,11 +725,14 @@ __device__ void finish_if_last(const Args& a) {
 template <typename T, int NS, int LB>
 __global__ __launch_bounds__(LB) void os_round_kernel(Args a) {
   constexpr int ES = sizeof(T);
+  const uint64_t t0 = a.tl ? wall_clock64() : 0;
+  uint64_t t1 = t0;
   int32_t b = int32_t(blockIdx.x);
   if (b == 0) {
     begin_role(a);
   } else {
     const uint32_t r = wait_begun(a);
+    if (a.tl) t1 = wall_clock64();
     b -= 1;
     if (b < a.gp) {
       push_role<ES>(a, r, b, a.gp);
@@ -742,6 +745,12 @@ __global__ __launch_bounds__(LB) void os_round_kernel(Args a) {
     } else {
       copy_role<ES>(a, r, b - 1, a.gq);
     }
+  }
+  if (a.tl && threadIdx.x == 0) {  // vector stores (one lane)
+    unsigned long long* t = a.tl + 3 * int64_t(blockIdx.x);
+    t[0] = t0;
+    t[1] = t1;
+    t[2] = wall_clock64();
   }
   finish_if_last(a);
 }

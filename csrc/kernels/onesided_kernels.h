@@ -64,6 +64,9 @@ struct Args {
   const uint32_t* dead = nullptr;          // host-mapped [kMaxRanks]: peers marked dead
   const uint32_t* force = nullptr;         // host-mapped: rounds < *force are forced
   CallStatus* status = nullptr;            // host-mapped [kStatusSlots]
+  // measurement (AKKA_OS_TIMELINE=1): per workgroup [entry, round known,
+  // role done] wall-clock ticks of the last call; nullptr otherwise
+  unsigned long long* tl = nullptr;
 };
 
 // Enqueue one call on `s` (dtype: 0 fp32, 1 bf16).

@@ -174,6 +174,7 @@ OneSidedLane::OneSidedLane(int32_t device, int64_t S, int32_t N, int64_t C, int3
     AKKA_OS_HIP(hipDeviceSynchronize());
     int khz = 0;
     if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device_) != hipSuccess || khz <= 0) khz = 100000;
+    clock_khz_ = khz;
     timeout_ticks_ = uint64_t(std::max<int64_t>(1, p.timeout_ms)) * uint64_t(khz);
   } else {
     // one shared-memory segment: [flags | SD rows | GD rows]
@@ -225,6 +226,7 @@ OneSidedLane::~OneSidedLane() {
     hipDeviceSynchronize();  // none of our kernels may still touch a window
     for (void* m : opened_) hipIpcCloseMemHandle(m);
     if (cu_stream_) hipStreamDestroy(static_cast<hipStream_t>(cu_stream_));
+    if (tl_dev_) hipFree(tl_dev_);
     if (ev_in_) hipEventDestroy(static_cast<hipEvent_t>(ev_in_));
     if (ev_out_) hipEventDestroy(static_cast<hipEvent_t>(ev_out_));
     for (char* p : sd_)
@@ -441,6 +443,15 @@ void OneSidedLane::gpu_call(uintptr_t stream, const char* in, char* out, int32_t
   a.force = &hw_dev_->force;
   a.status = hw_dev_->status;
   AKKA_OS_HIP(hipSetDevice(device_));
+  if (const char* tv = std::getenv("AKKA_OS_TIMELINE"); tv && std::strcmp(tv, "1") == 0) {
+    const int64_t words = 3 * int64_t(os::onesided_grid(a));
+    if (words > tl_words_) {
+      if (tl_dev_) AKKA_OS_HIP(hipFree(tl_dev_));
+      AKKA_OS_HIP(hipMalloc(reinterpret_cast<void**>(&tl_dev_), size_t(words) * sizeof(unsigned long long)));
+      tl_words_ = words;
+    }
+    a.tl = tl_dev_;
+  }
   hipStream_t caller = reinterpret_cast<hipStream_t>(stream);
   if (cu_stream_) {
     // fork/join through events (graph capture follows the same edges)
@@ -844,5 +855,14 @@ void OneSidedLane::set_dead(int32_t peer, bool d) {
 }
 
 void OneSidedLane::force_below(uint32_t v) { __atomic_store_n(&hw_->force, v, __ATOMIC_RELEASE); }
+
+std::vector<uint64_t> OneSidedLane::timeline() {
+  std::vector<uint64_t> v(size_t(tl_words_), 0);
+  if (!tl_dev_ || device_ < 0) return v;
+  AKKA_OS_HIP(hipSetDevice(device_));
+  AKKA_OS_HIP(hipDeviceSynchronize());
+  AKKA_OS_HIP(hipMemcpy(v.data(), tl_dev_, v.size() * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  return v;
+}
 
 }  // namespace akka

@@ -121,6 +121,10 @@ class OneSidedLane {
   int32_t shared_ranks() const { return shared_ranks_; }
   // CUs the round launch may use when ranks share this GPU (0: all)
   int32_t lane_cus() const { return lane_cus_; }
+  // AKKA_OS_TIMELINE=1 at construction: per workgroup [entry, round known,
+  // role done] of the last call (waits for the device), and the clock rate
+  std::vector<uint64_t> timeline();
+  int64_t clock_khz() const { return clock_khz_; }
   std::array<int32_t, 3> role_grid() const { return {gp_, gr_, gq_}; }
   size_t window_bytes() const { return win_bytes_; }
   const std::string& memory_kind() const { return mem_kind_; }
@@ -178,6 +182,9 @@ class OneSidedLane {
   void* ev_in_ = nullptr;      // hipEvent_t
   void* ev_out_ = nullptr;     // hipEvent_t
   int32_t lane_cus_ = 0;
+  unsigned long long* tl_dev_ = nullptr;  // AKKA_OS_TIMELINE=1: [grid][3]
+  int64_t tl_words_ = 0;
+  int64_t clock_khz_ = 0;
   std::string my_bus_;
   int64_t slot_ = 0, part_len_ = 64;
   size_t flag_bytes_ = 0, row_bytes_ = 0, win_bytes_ = 0;
