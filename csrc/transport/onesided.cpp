@@ -75,13 +75,13 @@ int64_t round_up(int64_t x, int64_t m) { return (x + m - 1) / m * m; }
 // resident at once on a GPU of its own, so the copies of landed chunks run
 // while later chunks are still crossing the links.  Fixed once open() ran (the reduce pieces'
 // counters count modulo nsub_).
-void OneSidedLane::size_roles(int64_t wgs) {
+void OneSidedLane::size_roles(int64_t wgs, int64_t push_wgs, int64_t copy_wgs) {
   const int32_t N = g_.N;
   wgs = std::max<int64_t>(1, wgs);
   const int64_t push_items = int64_t(N - 1) * Kmax_ * P_;
   const int64_t red_parts = int64_t(g_.num_chunks(me_)) * P_;
-  gp_ = int32_t(std::clamp<int64_t>(push_items, 1, wgs));
-  gq_ = gp_;
+  gp_ = int32_t(std::clamp<int64_t>(push_items, 1, push_wgs > 0 ? push_wgs : wgs));
+  gq_ = int32_t(std::clamp<int64_t>(push_items, 1, copy_wgs > 0 ? copy_wgs : wgs));
   // pieces of >= 4096 elements; twice the workgroups of the other roles:
   // the reduce reads N sources per element (bench/onesided_role.py: 512
   // 256-thread workgroups reach 5.0 TB/s at N=8 where 256 reach 3.7)
@@ -367,7 +367,14 @@ void OneSidedLane::open(const std::vector<std::string>& handles) {
       const char* bv = std::getenv("AKKA_OS_SHARED_BUDGET");  // measurement knob (resident 256-thread WGs)
       const int64_t total = bv ? std::max(16, std::atoi(bv)) : total_default;
       const int64_t budget = total / share - 2 - g_.num_chunks(me_);
-      size_roles(std::max<int64_t>(2, budget / 4));  // push, copy: 1 share each; reduce: 2
+      // shares of the budget, push / reduce / copy (AKKA_OS_SHARES="p,r,c" to measure)
+      int64_t sp = 1, sr = 2, sc = 1;
+      if (const char* sv = std::getenv("AKKA_OS_SHARES")) {
+        long a = 0, b = 0, c2 = 0;
+        if (std::sscanf(sv, "%ld,%ld,%ld", &a, &b, &c2) == 3 && a > 0 && b > 0 && c2 > 0) sp = a, sr = b, sc = c2;
+      }
+      const int64_t unit = std::max<int64_t>(1, budget / (sp + sr + sc));
+      size_roles(std::max<int64_t>(1, unit * sr / 2), unit * sp, unit * sc);
     }
   }
   if (device_ >= 0) {

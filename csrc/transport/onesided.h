@@ -157,7 +157,8 @@ class OneSidedLane {
     int64_t deadline_ms = 0;
   };
   static constexpr int64_t kDefaultRoleWgs = 256;
-  void size_roles(int64_t wgs);
+  // wgs: reduce = 2 x wgs; push / copy = wgs unless given
+  void size_roles(int64_t wgs, int64_t push_wgs = 0, int64_t copy_wgs = 0);
   void gpu_call(uintptr_t stream, const char* in, char* out, int32_t* counts, int32_t kcols);
   // CPU roles
   void push(int32_t phase, int32_t dst, int32_t k, int32_t j, uint32_t r, uint32_t cnt, const char* src);
