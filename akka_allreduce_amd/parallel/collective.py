@@ -556,6 +556,7 @@ class ThresholdAllreduce:
         if self.transport != "stream" or self.world_size < 2:
             raise ValueError("lane tuning needs the stream transport and N > 1")
         res: dict = {}
+        os_made_here = False  # tune() mapped the one-sided lane (and may drop it again)
         ipc_open = bool(self.state().get("link", {}).get("ipc"))
         cands = list(candidates) if candidates is not None else None
         if cands is None:
@@ -580,6 +581,7 @@ class ThresholdAllreduce:
                               "ipc_lite", "ipc_bcast_lite", "ipc_fused_lite", "ipc_fused_bcast_lite"]
                 if self._th_exact:
                     err = None
+                    os_made_here = self._exact_os is None
                     try:
                         self.enable_onesided()
                     except Exception as e:  # noqa: BLE001 - the candidate is skipped on every rank
@@ -648,6 +650,14 @@ class ThresholdAllreduce:
         if not good:
             raise RuntimeError(f"no exact lane: {res}")
         pick = min(good, key=lambda n: res[n]["ms"])
+        if pick != "onesided" and os_made_here and self._exact_os is not None:
+            # the one-sided windows (2 x rows x the buffer) are not kept for
+            # a lane that lost: every rank is past its last round on them
+            # (the agreement below is the barrier), then each frees its own
+            if cuda:
+                torch.cuda.synchronize(self.device)
+            self._agree_max([0.0])
+            self._exact_os = None
         self.use_lane(pick)
         res["chosen"] = pick
         self.tuned = res
