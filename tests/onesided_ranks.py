@@ -67,6 +67,7 @@ def check_sets(o, world, me, dtype, detail=None):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--mode", default="exact", choices=["exact", "straggler", "chaos"])
+    ap.add_argument("--timeline", action="store_true", help="exact: AKKA_OS_TIMELINE=1, check the stamps")
     ap.add_argument("--async-op", action="store_true", help="exact: async rounds (side stream), wait() then read")
     ap.add_argument("--jitter-ms", type=float, default=2.0, help="chaos: every call waits U(0, jitter) first")
     ap.add_argument("--device", default="cpu")
@@ -95,6 +96,8 @@ def main():
     dtype = torch.float32 if a.dtype == "float32" else torch.bfloat16
     from akka_allreduce_amd.parallel.onesided import OneSidedAllreduce
 
+    if a.timeline:
+        os.environ["AKKA_OS_TIMELINE"] = "1"  # read by each call's launch
     th = 1.0 if a.mode == "exact" else a.th
     ar = OneSidedAllreduce(a.size, max_chunk_size=a.chunk, dtype=dtype, th_reduce=th, th_complete=th,
                            max_lag=a.max_lag, device=dev, rows=a.rows, part_bytes=a.part_bytes,
@@ -121,6 +124,14 @@ def main():
             ok = torch.equal(o.data.cpu(), want.to(dtype)) and bool((o.count.cpu() == world).all())
             res["exact"].append(bool(ok))
             res["rounds"].append(o.iteration)
+        if a.timeline:
+            tl = ar.lane.timeline()
+            g = ar.info()["role_wgs"]
+            grid = 1 + g["push"] + ar.geometry.num_chunks(rank) + g["reduce"] + 1 + g["copy"]
+            w = [tl[i:i + 3] for i in range(0, len(tl), 3)][:grid]
+            res["timeline"] = {"words": len(tl), "grid": grid,
+                               "ordered": all(0 < t[0] <= t[1] <= t[2] for t in w),
+                               "span_ticks": (max(t[2] for t in w) - min(t[0] for t in w)) if w else 0}
     elif a.mode == "chaos":
         # every rank waits a random time before each call (its own seeded
         # stream): arrival orders, lags, catch-ups and overwrite conflicts

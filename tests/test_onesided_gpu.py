@@ -40,6 +40,17 @@ def test_onesided_gpu_exact_rounds_async():
         assert d["exact"] == [True] * 4 and d["error"] == 0, d
 
 
+def test_onesided_gpu_timeline_stamps():
+    """AKKA_OS_TIMELINE=1: every workgroup of the last call stamped [entry,
+    round known, role done] in order (bench/onesided_timeline.py's input)."""
+    r, rows = run_ranks(2, "--mode", "exact", "--size", str(1 << 20), "--chunk", str(1 << 16), "--rounds", "2",
+                        "--timeline", "--timeout-s", "10", device="cuda", timeout=180)
+    assert r.returncode == 0, r.stderr[-3000:]
+    for d in rows:
+        t = d["timeline"]
+        assert d["exact"] == [True] * 2 and t["words"] >= 3 * t["grid"] and t["ordered"] and t["span_ticks"] > 0, t
+
+
 def test_onesided_gpu_straggler_steady_state():
     """N=4 on the card, 0.75 / 0.75, maxLag 1, rank 3 sleeps 50 ms per call,
     64 rounds: fast ranks' median round within 2x of the straggler-free phase,
