@@ -141,17 +141,21 @@ def main():
         rng = random.Random(1234 + rank)
         x = torch.full((a.size,), float(1 << rank), dtype=dtype, device=dev)
         out = torch.empty_like(x)
-        bad, detail, rounds, reasons, last = 0, [], [], [], -1
+        bad, detail, rounds, reasons, last, partial = 0, [], [], [], -1, 0
         while last < a.rounds - 1:
             time.sleep(rng.uniform(0.0, a.jitter_ms) / 1e3)
             o = ar(x, out=out)
             sync()
             b, _ = check_sets(o, world, rank, dtype, detail)
             bad += b
+            cnt, g = o.counts_per_chunk.cpu(), o.geometry  # a chunk short of N contributors?
+            partial += int(any(int(cnt[p, k]) != world for p in range(world) for k in range(g.num_chunks(p))
+                               if g.chunk_range(p, k)[1] > g.chunk_range(p, k)[0]))
             last = o.iteration
             rounds.append(last)
             reasons.append(o.status["reason"])
         res["chaos"] = {"rounds": rounds, "bad_chunks": bad, "bad_detail": detail, "reasons": reasons,
+                        "calls_with_partial_chunks": partial,
                         "stats": ar.stats()}
         ar.retire()
         sync()

@@ -86,7 +86,7 @@ def test_onesided_gpu_straggler_killed_mid_run():
 
 
 @pytest.mark.parametrize("n,th,max_lag,dtype", [(4, 0.75, 1, "float32"), (8, 0.5, 2, "bfloat16"),
-                                                (3, 0.67, 1, "float32")])
+                                                (3, 0.67, 1, "float32"), (4, 1.0, 1, "float32")])
 def test_onesided_gpu_chaos_jitter(n, th, max_lag, dtype):
     """Every rank waits a random 0-2 ms before each call, 200 rounds, 16 MiB
     (fp32) with 1 MiB chunks: arrival orders, lags, catch-ups and overwrite
@@ -101,3 +101,5 @@ def test_onesided_gpu_chaos_jitter(n, th, max_lag, dtype):
         assert c["bad_chunks"] == 0, (d["rank"], c["bad_detail"], c["stats"])
         assert d["error"] == 0 and c["stats"]["timeouts"] == 0, c["stats"]
         assert c["rounds"][-1] >= 199, c["rounds"][-5:]
+        if th == 1.0:  # exact thresholds: whatever the timing, every round is complete
+            assert c["calls_with_partial_chunks"] == 0 and c["rounds"] == list(range(200)), c["stats"]
