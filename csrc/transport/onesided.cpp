@@ -338,7 +338,10 @@ void OneSidedLane::open(const std::vector<std::string>& handles) {
     }
     shared_ranks_ = share;
     if (share > 1) {
-      nt_ = 256;
+      // 256-thread workgroups (AKKA_OS_THREADS=1024 to measure: the budget
+      // then counts 1024-thread workgroups, a quarter as many)
+      const char* tv = std::getenv("AKKA_OS_THREADS");
+      nt_ = (tv && std::atoi(tv) >= 1024) ? 1024 : 256;
       const char* kv = std::getenv("AKKA_OS_CU_KEEP");  // CUs kept of every 8 (measurement knob)
       const int32_t keep = kv ? std::clamp(std::atoi(kv), 0, 8) : std::clamp(p_.cu_keep, 0, 8);
       int64_t total_default = 768;
@@ -366,7 +369,7 @@ void OneSidedLane::open(const std::vector<std::string>& handles) {
       }
       const char* bv = std::getenv("AKKA_OS_SHARED_BUDGET");  // measurement knob (resident 256-thread WGs)
       const int64_t total = bv ? std::max(16, std::atoi(bv)) : total_default;
-      const int64_t budget = total / share - 2 - g_.num_chunks(me_);
+      const int64_t budget = total * 256 / nt_ / share - 2 - g_.num_chunks(me_);
       // shares of the budget, push / reduce / copy (AKKA_OS_SHARES="p,r,c" to measure)
       int64_t sp = 1, sr = 2, sc = 1;
       if (const char* sv = std::getenv("AKKA_OS_SHARES")) {
