@@ -205,7 +205,7 @@ enum Stat : int32_t {
 enum Verdict : int32_t {
   kWait = 0,
   kThreshold = 1,    // the reference's trigger
-  kUnreachable = 2,  // landed + still-possible < needed: nothing left to wait for
+  kUnreachable = 2,  // landed + still-possible < needed, and every possible one landed
   kCatchUp = 3,      // a peer pushed a round beyond r + maxLag (W:100-106)
   kHostForce = 4,    // the host forced the round (close / dead peers)
   kTimeout = 5,      // bounded wait expired: forced, and the lane reports an error
@@ -215,7 +215,10 @@ enum Verdict : int32_t {
 OS_HD inline int32_t evaluate(int32_t landed, int32_t pending, int32_t need, uint32_t r, int64_t seen_max,
                               int32_t max_lag, uint32_t force_through, bool timed_out) {
   if (landed >= need) return kThreshold;
-  if (landed + pending < need) return kUnreachable;
+  // short of the threshold for good (dead or departed peers): still take
+  // everything that can arrive before ending the wait -- ending it at once
+  // would drop live peers' chunks still in flight
+  if (landed + pending < need && pending == 0) return kUnreachable;
   if (seen_max > int64_t(r) + max_lag) return kCatchUp;
   if (force_through > r) return kHostForce;
   if (timed_out) return kTimeout;

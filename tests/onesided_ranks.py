@@ -66,7 +66,7 @@ def check_sets(o, world, me, dtype, detail=None):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--mode", default="exact", choices=["exact", "straggler", "chaos"])
+    ap.add_argument("--mode", default="exact", choices=["exact", "straggler", "chaos", "dead"])
     ap.add_argument("--timeline", action="store_true", help="exact: AKKA_OS_TIMELINE=1, check the stamps")
     ap.add_argument("--async-op", action="store_true", help="exact: async rounds (side stream), wait() then read")
     ap.add_argument("--jitter-ms", type=float, default=2.0, help="chaos: every call waits U(0, jitter) first")
@@ -98,7 +98,7 @@ def main():
 
     if a.timeline:
         os.environ["AKKA_OS_TIMELINE"] = "1"  # read by each call's launch
-    th = 1.0 if a.mode == "exact" else a.th
+    th = 1.0 if a.mode in ("exact", "dead") else a.th
     ar = OneSidedAllreduce(a.size, max_chunk_size=a.chunk, dtype=dtype, th_reduce=th, th_complete=th,
                            max_lag=a.max_lag, device=dev, rows=a.rows, part_bytes=a.part_bytes,
                            timeout_s=a.timeout_s)
@@ -132,6 +132,50 @@ def main():
             res["timeline"] = {"words": len(tl), "grid": grid,
                                "ordered": all(0 < t[0] <= t[1] <= t[2] for t in w),
                                "span_ticks": (max(t[2] for t in w) - min(t[0] for t in w)) if w else 0}
+    elif a.mode == "dead":
+        # exact thresholds; rank N-1 serves `kill_after` rounds, then vanishes
+        # without retiring (its window stays mapped); the survivors learn it
+        # out of band (the master's WorkerTerminated, M:46-52) and mark it
+        # dead: later rounds complete over the live ranks, the dead rank's
+        # block 0 with count 0, every live block the exact live sum
+        victim, k = world - 1, max(1, a.kill_after)
+        x = torch.full((a.size,), float(1 << rank), dtype=dtype, device=dev)
+        out = torch.empty_like(x)
+        res["dead"] = {"before": [], "after": [], "reasons": []}
+        for i in range(k):
+            o = ar(x, out=out)
+            sync()
+            res["dead"]["before"].append(o.iteration)
+        if rank == victim:
+            dist.barrier()  # the survivors are past round k-1 too
+            with open(os.path.join(a.out_dir, f"rank{rank}.json"), "w") as f:
+                json.dump(res, f)
+            os._exit(0)
+        dist.barrier()
+        ar.mark_dead(victim)
+        live = sum(1 << q for q in range(world) if q != victim)
+        g = ar.geometry
+        bad = 0
+        for i in range(a.rounds):
+            o = ar(x, out=out)
+            sync()
+            data, cnt = o.data.float().cpu(), o.counts_per_chunk.cpu()
+            for p in range(world):
+                for kk in range(g.num_chunks(p)):
+                    s0, e0 = g.chunk_range(p, kk)
+                    if e0 <= s0:
+                        continue
+                    want_v, want_c = (0.0, 0) if p == victim else (float(live), world - 1)
+                    if not (bool((data[s0:e0] == want_v).all()) and int(cnt[p, kk]) == want_c):
+                        bad += 1
+            res["dead"]["after"].append(o.iteration)
+            res["dead"]["reasons"].append(o.status["reason"])
+        res["dead"]["bad_chunks"] = bad
+        res["error"] = ar.error()
+        res["stats"] = ar.stats()
+        with open(os.path.join(a.out_dir, f"rank{rank}.json"), "w") as f:
+            json.dump(res, f)
+        os._exit(0)  # a peer is gone: no collective teardown
     elif a.mode == "chaos":
         # every rank waits a random time before each call (its own seeded
         # stream): arrival orders, lags, catch-ups and overwrite conflicts

@@ -183,3 +183,19 @@ def test_onesided_chaos_jitter(n, th, max_lag):
         assert c["rounds"][-1] >= 59 and c["rounds"] == sorted(c["rounds"]), c["rounds"]
         if th == 1.0:  # exact thresholds: whatever the timing, every round is complete
             assert c["calls_with_partial_chunks"] == 0 and c["rounds"] == list(range(60)), c
+
+
+def test_onesided_dead_peer_marked():
+    """Exact thresholds; rank 3 serves 3 rounds, then vanishes without
+    retiring; the survivors mark it dead (the master's WorkerTerminated,
+    M:46-52) and serve 10 more rounds: each completes without waiting for it
+    -- the dead rank's block 0 with count 0, every live block the exact live
+    sum with count 3 -- and no wait times out."""
+    r, rows = run_ranks(4, "--mode", "dead", "--kill-after", "3", "--rounds", "10", "--size", str(1 << 14),
+                        "--chunk", str(1 << 10), "--timeout-s", "20")
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert rows[3]["dead"]["before"] == [0, 1, 2]
+    for d in rows[:3]:
+        dd = d["dead"]
+        assert dd["before"] == [0, 1, 2] and dd["after"] == list(range(3, 13)), dd
+        assert dd["bad_chunks"] == 0 and d["error"] == 0 and d["stats"]["timeouts"] == 0, (dd, d["stats"])

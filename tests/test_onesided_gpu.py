@@ -103,3 +103,16 @@ def test_onesided_gpu_chaos_jitter(n, th, max_lag, dtype):
         assert c["rounds"][-1] >= 199, c["rounds"][-5:]
         if th == 1.0:  # exact thresholds: whatever the timing, every round is complete
             assert c["calls_with_partial_chunks"] == 0 and c["rounds"] == list(range(200)), c["stats"]
+
+
+def test_onesided_gpu_dead_peer_marked():
+    """GPU twin of tests/test_onesided_cpu.py::test_onesided_dead_peer_marked:
+    a rank vanishes without retiring, the survivors mark it dead and keep
+    completing exact rounds over the live ranks, no wait times out."""
+    r, rows = run_ranks(4, "--mode", "dead", "--kill-after", "3", "--rounds", "10", "--size", str(1 << 20),
+                        "--chunk", str(1 << 16), "--timeout-s", "10", device="cuda", timeout=180)
+    assert r.returncode == 0, r.stderr[-3000:]
+    for d in rows[:3]:
+        dd = d["dead"]
+        assert dd["before"] == [0, 1, 2] and dd["after"] == list(range(3, 13)), dd
+        assert dd["bad_chunks"] == 0 and d["error"] == 0 and d["stats"]["timeouts"] == 0, (dd, d["stats"])
