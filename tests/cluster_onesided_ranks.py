@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--delay-ms", type=float, default=0.0)
     ap.add_argument("--out-dir", required=True)
     ap.add_argument("--timeout-s", type=float, default=240.0)
+    ap.add_argument("--die-after", type=int, default=-1, help="exit abruptly once this round reached the sink")
     a = ap.parse_args()
     import faulthandler
     import logging
@@ -49,6 +50,8 @@ def main():
         kept.append((int(o.iteration), o.data.float().cpu(),
                      o.counts_per_chunk.cpu() if o.counts_per_chunk is not None else None, o.geometry))
         recs.append({"round": int(o.iteration), "t": time.perf_counter(), "t_src": src_t[-1] if src_t else 0.0})
+        if 0 <= a.die_after <= int(o.iteration):
+            os._exit(0)  # abrupt: no Shutdown, no retire -- the master's failure detector must notice
 
     def check(rec, item):
         _, data, cpc, g = item

@@ -29,7 +29,7 @@ def _port() -> int:
 
 
 def run_job(device="cpu", delay_ms=0.0, rounds=64, size=1 << 14, chunk=1 << 10, workers=4, timeout=240,
-            log_dir=None):
+            log_dir=None, die_after=-1, env=None):
     port = _port()
     base = [sys.executable, "-m", "akka_allreduce_amd", "--log-level", "WARNING"]
     with tempfile.TemporaryDirectory() as out:
@@ -42,7 +42,7 @@ def run_job(device="cpu", delay_ms=0.0, rounds=64, size=1 << 14, chunk=1 << 10, 
                                           str(size), "--max-chunk-size", str(chunk), "--max-round", str(rounds - 1),
                                           "--max-lag", "1", "--th-allreduce", "0.75", "--th-reduce", "0.75",
                                           "--th-complete", "0.75", "--transport", "onesided"],
-                                  cwd=ROOT, stdout=subprocess.DEVNULL, stderr=mlog)
+                                  cwd=ROOT, stdout=subprocess.DEVNULL, stderr=mlog, env=env)
         t_end = time.time() + 60
         while time.time() < t_end:
             try:
@@ -54,10 +54,12 @@ def run_job(device="cpu", delay_ms=0.0, rounds=64, size=1 << 14, chunk=1 << 10, 
         for i in range(workers):
             d = delay_ms if i == workers - 1 else 0.0
             wlogs.append(os.path.join(logs, f"worker{i}_d{int(delay_ms)}.log"))
+            extra = ["--die-after", str(die_after)] if die_after >= 0 and i == workers - 1 else []
             procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "cluster_onesided_ranks.py"),
                                            "--master", f"127.0.0.1:{port}", "--size", str(size), "--device", device,
-                                           "--delay-ms", str(d), "--out-dir", out, "--timeout-s", str(timeout - 30)],
-                                          cwd=ROOT, stdout=subprocess.DEVNULL, stderr=open(wlogs[-1], "w")))
+                                           "--delay-ms", str(d), "--out-dir", out, "--timeout-s", str(timeout - 30),
+                                           *extra],
+                                          cwd=ROOT, stdout=subprocess.DEVNULL, stderr=open(wlogs[-1], "w"), env=env))
             if i < workers - 1:
                 time.sleep(0.3)  # join order = ids: the straggler joins last (id 3)
         errs = []
@@ -119,3 +121,22 @@ def check_job(device, rounds=64, slack_ms=2.0, **kw):
 
 def test_cluster_onesided_master_pacing_cpu():
     check_job("cpu")
+
+
+def test_cluster_onesided_worker_dies():
+    """A worker process exits abruptly after round 10 (no Shutdown, no
+    retire).  The master notices (WorkerTerminated, M:46-52), paces the
+    remaining rounds on the live count, the survivors mark the rank dead in
+    their lanes and serve every round to maxRound with consistent contributor
+    sets -- the dead rank's block 0 with count 0 (C1e)."""
+    env = dict(os.environ, AKKA_CLUSTER_UNREACHABLE_AFTER_S="2", AKKA_CLUSTER_HEARTBEAT_INTERVAL_S="0.25")
+    rows, errs = run_job("cpu", 0.0, 48, die_after=10, env=env)
+    assert len(rows) == 3, errs  # the dead worker writes no record
+    for r in rows:
+        assert r["finished"] and not r["errors"], (r["errors"], errs)
+        assert all(x["bad"] == 0 for x in r["records"]), r["id"]
+        rs = [x["round"] for x in r["records"]]
+        assert rs == sorted(rs) and rs[-1] == 47, rs[-5:]
+        # rounds after the death: 3 contributors at most per chunk
+        late = [x for x in r["records"] if x["round"] >= 20]
+        assert late and max(x["mean_count"] for x in late) <= 3.0, late[:3]
