@@ -611,12 +611,15 @@ class ThresholdAllreduce:
             o = self(x, async_op=cuda, out=buf)
             o.wait()
             sync()
-            t0 = time.perf_counter()
-            for _ in range(rounds):  # the ranks are coupled by the rounds themselves
-                o = self(x, async_op=cuda, out=buf)
-            o.wait()
-            sync()
-            return (time.perf_counter() - t0) / rounds * 1e3
+            best = float("inf")
+            for _ in range(2):  # the better of two blocks: one noisy block does not decide the lane
+                t0 = time.perf_counter()
+                for _ in range(rounds):  # the ranks are coupled by the rounds themselves
+                    o = self(x, async_op=cuda, out=buf)
+                o.wait()
+                sync()
+                best = min(best, (time.perf_counter() - t0) / rounds * 1e3)
+            return best
 
         for name in cands:
             ok, ms, err = True, 0.0, None
