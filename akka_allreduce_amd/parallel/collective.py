@@ -342,7 +342,9 @@ class ThresholdAllreduce:
         if self.transport == "onesided":
             if self.pacer is None:
                 self._round += 1
-                return self._os(x, out=out, async_op=async_op)
+                # (async_op: the round is valid in the caller's stream order,
+                # which satisfies wait(); a side stream only adds hand-offs)
+                return self._os(x, out=out)
             # paced: wait for round r, call, then report every round this call
             # completed -- the served one and any it skipped by catch-up (the
             # reference force-completes those, W:100-106) -- like
@@ -361,7 +363,7 @@ class ThresholdAllreduce:
         if self._lane_os:
             # exact rounds on the one-sided lane (tune candidate "onesided"):
             # valid in the caller's stream order, like an async round
-            out = self._exact_os(x, out=out, async_op=async_op)
+            out = self._exact_os(x, out=out)  # (async_op: see the onesided transport above)
         else:
             out = self.worker.allreduce(x, async_op=async_op, out=out)
         if out is None:
