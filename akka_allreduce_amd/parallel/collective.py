@@ -192,6 +192,8 @@ class ThresholdAllreduce:
         # "onesided" or lane "onesided"), e.g. {"cu_keep": 6} on a shared GPU
         self.onesided_options = dict(onesided_options or {})
         self._lane_os = False  # exact rounds on the one-sided lane (use_lane("onesided"))
+        self._ipc_direct = False  # exact ipc rounds straight on the caller's stream (use_lane("*_direct"))
+        self._ipc_dev_on = False  # the ipc lane's round id lives on the device
         self._direct = None    # an open CapturableExact view
         if transport == "onesided":
             # thresholds over mapped peer windows: no send ever waits for a
@@ -364,6 +366,8 @@ class ThresholdAllreduce:
             # exact rounds on the one-sided lane (tune candidate "onesided"):
             # valid in the caller's stream order, like an async round
             out = self._exact_os(x, out=out)  # (async_op: see the onesided transport above)
+        elif getattr(self, "_ipc_direct", False):
+            out = self._ipc_direct_round(x, out)  # valid in the caller's stream order (satisfies wait())
         else:
             out = self.worker.allreduce(x, async_op=async_op, out=out)
         if out is None:
@@ -382,7 +386,7 @@ class ThresholdAllreduce:
         (bench/ddp_overlap.py, 2 ranks: 3.11 ms per DDP step sync vs 4.57
         async; profiles/r04/README.md).  ``OneSidedAllreduce(async_op=True)``
         stays available."""
-        if self.transport == "onesided" or self._lane_os:
+        if self.transport == "onesided" or self._lane_os or getattr(self, "_ipc_direct", False):
             return False
         return self.transport == "stream"
 
@@ -400,7 +404,33 @@ class ThresholdAllreduce:
         if self.transport != "stream":
             raise ValueError("lanes belong to the scheduled (stream) transport")
         self._lane_os = False
+        self._ipc_direct_off()
         self.worker.set_lane(lane)
+
+    def _ipc_direct_off(self) -> None:
+        """Back from direct ipc rounds: the lane's round id returns to the host
+        (every rank at the same round, like any lane switch)."""
+        if getattr(self, "_ipc_dev_on", False):
+            torch.cuda.synchronize(self.device)
+            self.worker._core.ipc_device_rounds(False)
+            self._ipc_dev_on = False
+        self._ipc_direct = False
+
+    def _ipc_direct_round(self, x: torch.Tensor, out: Optional[torch.Tensor]) -> AllReduceOutput:
+        core = self.worker._core
+        if not getattr(self, "_ipc_dev_on", False):
+            core.ipc_device_rounds(True)  # collective in effect: every rank switches at the same round
+            self._ipc_dev_on = True
+        g = self.worker.geometry
+        if getattr(self, "_full_counts", None) is None:
+            self._full_counts = torch.full((g.workerNum, g.kmax), g.workerNum, dtype=torch.int32, device=self.device)
+        if x.dtype != self.worker.dtype or not x.is_contiguous() or x.device != self.device:
+            x = x.to(device=self.device, dtype=self.worker.dtype).contiguous()
+        if out is None:
+            out = torch.empty_like(x)
+        core.ipc_round_direct(x.data_ptr(), out.data_ptr(), torch.cuda.current_stream(self.device).cuda_stream)
+        return AllReduceOutput(out.view(-1), iteration=self._round, counts_per_chunk=self._full_counts, geometry=g,
+                               expander=self.worker._expand_counts)
 
     def enable_ipc(self) -> None:
         """Open the one-sided xGMI lane (csrc/transport/ipc_lane.h): every
@@ -486,6 +516,11 @@ class ThresholdAllreduce:
         # store can beat a remote read, which the shared-card rehearsals cannot
         # show (both stay inside one card's HBM there)
         "ipc_fused_bcast_lite": ("ipc", -1, "bcast", True, 1024, True),
+        # the same ipc rounds launched straight on the caller's stream with a
+        # device-resident round id (no engine bookkeeping, no cross-stream
+        # events; exact rounds only -- every count is N): "<lane>_direct"
+        "ipc_fused_lite_direct": ("ipc", -1, "pull", True, 1024, True),
+        "ipc_lite_direct": ("ipc", -1, "pull", False, 1024, True),
         # the one-sided threshold lane at thresholds 1 (enable_onesided): one
         # role-partitioned launch, each chunk reduced and pushed as soon as
         # its copies landed, peer chunks copied out as they land
@@ -529,16 +564,23 @@ class ThresholdAllreduce:
         """Switch to a named lane candidate (see LANES); every rank must do the
         same at the same round."""
         if name == "onesided":
+            self._ipc_direct_off()
             self.enable_onesided()
             self._lane_os = True
             return
         self._lane_os = False
         ln, unit, mode, fused, threads, lite = self.LANES[name]
+        if name.endswith("_direct"):
+            if not self._th_exact or self.device.type != "cuda" or self.world_size < 2 or self.pacer is not None:
+                raise ValueError("direct ipc rounds are exact, unpaced, on GPUs with N > 1")
+        else:
+            self._ipc_direct_off()
         self.set_lane(ln)
         if ln == "ipc":
             self.set_ipc_mode(mode, fused, threads, lite)
         elif self.world_size > 1:
             self.set_exact_unit_bytes(unit)
+        self._ipc_direct = name.endswith("_direct")
 
     def tune(self, candidates=None, rounds: int = 8, try_ipc: bool = True) -> dict:
         """Pick the fastest exact lane for this buffer on this job (collective).
@@ -581,6 +623,8 @@ class ThresholdAllreduce:
                 if ipc_open:
                     cands += ["ipc", "ipc_bcast", "ipc_fused", "ipc_fused_bcast", "ipc_wide", "ipc_bcast_wide",
                               "ipc_lite", "ipc_bcast_lite", "ipc_fused_lite", "ipc_fused_bcast_lite"]
+                    if self._th_exact and self.pacer is None:
+                        cands += ["ipc_lite_direct", "ipc_fused_lite_direct"]
                 if self._th_exact:
                     err = None
                     os_made_here = self._exact_os is None
@@ -765,6 +809,7 @@ class CapturableExact:
         elif ar.state().get("link", {}).get("ipc"):
             self.lane = "ipc"
             ar.worker._core.ipc_device_rounds(True)  # collective in effect: same round on every rank
+            ar._ipc_dev_on = True
             self.counts = torch.full((g.workerNum, g.kmax), g.workerNum, dtype=torch.int32, device=ar.device)
         else:
             raise ValueError("capturable rounds run on the ipc or onesided lane: use_lane() one of them first")
@@ -791,6 +836,7 @@ class CapturableExact:
 
     def close(self) -> None:
         """Back to the engine's own calls (every rank, same round)."""
-        if self.lane == "ipc":
+        if self.lane == "ipc" and not getattr(self.ar, "_ipc_direct", False):
             self.ar.worker._core.ipc_device_rounds(False)
+            self.ar._ipc_dev_on = False
         self.ar._direct = None

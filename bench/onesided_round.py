@@ -87,6 +87,23 @@ def main() -> None:
                     ar.retire()
                     torch.cuda.synchronize()
                     dist.barrier()
+                elif lane == "ipc_direct":
+                    # the same ipc lane, its rounds launched straight on the
+                    # caller's stream (device round ids, ThresholdAllreduce.capturable())
+                    ar = ThresholdAllreduce(S, max_chunk_size=min(C, S), device=dev, data_plane="ipc")
+                    ar.use_lane(a.ipc_lane)
+                    torch.cuda.synchronize()
+                    cap = ar.capturable()
+                    case["lane"] = a.ipc_lane + "_direct"
+                    y = torch.full((S,), float(rank + 1), device=dev)
+                    o = cap(y, out=torch.empty_like(y))
+                    torch.cuda.synchronize()
+                    case["exact"] = bool((o.data == world * (world + 1) / 2).all())
+                    case["ms"] = _time(lambda: cap(x, out=out), a.warmup, a.steps)
+                    case["error"] = ar.ipc_error()
+                    torch.cuda.synchronize()
+                    dist.barrier()
+                    cap.close()
                 else:
                     ar = ThresholdAllreduce(S, max_chunk_size=min(C, S), device=dev, data_plane="ipc")
                     ar.use_lane(a.ipc_lane)

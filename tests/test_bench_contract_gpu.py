@@ -96,7 +96,8 @@ def test_bench_multirank_on_one_card(plane):
     else:
         # the ipc lane's variants and the one-sided lane (exact rounds)
         assert set(cands) == {"ipc", "ipc_bcast", "ipc_fused", "ipc_fused_bcast", "ipc_wide", "ipc_bcast_wide",
-                              "ipc_lite", "ipc_bcast_lite", "ipc_fused_lite", "ipc_fused_bcast_lite", "onesided"}
+                              "ipc_lite", "ipc_bcast_lite", "ipc_fused_lite", "ipc_fused_bcast_lite",
+                              "ipc_lite_direct", "ipc_fused_lite_direct", "onesided"}
 
 
 def test_bench_rccl_init_failure_falls_back_to_ipc():
