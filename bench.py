@@ -615,7 +615,7 @@ def run_extras(world: int, dev, barrier, which=("cfg1", "cfg3", "cfg4", "cfg5"),
                 dt = timed(lambda: wstep(wx, wy, 0.05, None), steps, 5, world, barrier)
                 res["cfg5_mlp_dp_sgd_bf16_whole_graph"] = {
                     "steps_per_s": round(steps / dt, 3), "samples_per_s": round(steps * batch * world / dt, 1),
-                    "lane": chosen, "compute_dtype": "bf16 autocast, fp32 master weights/grads; forward, backward, "
+                    "lane": lane or chosen, "compute_dtype": "bf16 autocast, fp32 master weights/grads; forward, backward, "
                                                      "allreduce and update as one HIP graph replay"}
             finally:
                 _sync()
