@@ -428,7 +428,11 @@ class ThresholdAllreduce:
             x = x.to(device=self.device, dtype=self.worker.dtype).contiguous()
         if out is None:
             out = torch.empty_like(x)
-        core.ipc_round_direct(x.data_ptr(), out.data_ptr(), torch.cuda.current_stream(self.device).cuda_stream)
+        # (raises once an earlier round's wait failed; a failing round zeroes
+        # the fixed counts table on the device, so no output of a dead lane
+        # reads as exact)
+        core.ipc_round_direct(x.data_ptr(), out.data_ptr(), torch.cuda.current_stream(self.device).cuda_stream,
+                              self._full_counts.data_ptr(), self._full_counts.numel())
         return AllReduceOutput(out.view(-1), iteration=self._round, counts_per_chunk=self._full_counts, geometry=g,
                                expander=self.worker._expand_counts)
 
@@ -521,11 +525,46 @@ class ThresholdAllreduce:
         # events; exact rounds only -- every count is N): "<lane>_direct"
         "ipc_fused_lite_direct": ("ipc", -1, "pull", True, 1024, True),
         "ipc_lite_direct": ("ipc", -1, "pull", False, 1024, True),
+        # the fenced twin of ipc_fused_lite_direct: plain window stores behind
+        # system release / acquire fences (the HIP memory model's protocol),
+        # for a link on which write-through + drain is not proven
+        "ipc_fused_direct": ("ipc", -1, "pull", True, 1024, False),
         # the one-sided threshold lane at thresholds 1 (enable_onesided): one
         # role-partitioned launch, each chunk reduced and pushed as soon as
         # its copies landed, peer chunks copied out as they land
         "onesided": ("onesided", -1, None, False, 0, False),
+        # ... with fenced hand-offs (OneSidedAllreduce(handoff="fenced"))
+        "onesided_fenced": ("onesided", -1, None, False, 0, True),
     }
+
+    @staticmethod
+    def lane_candidates(*, two_sided: bool, ipc_open: bool, onesided_ok: bool, exact: bool = True,
+                        paced: bool = False, lane_set: str = "default") -> list:
+        """The lanes tune() tries.  ``default``: at most six -- the p2p
+        schedule (RCCL p2p + the gfx950 reduce), the direct ipc rounds (lite,
+        fused lite, and the fused round's FENCED twin) and the one-sided lane
+        in both hand-off modes -- so a job on a node it has never run on
+        chooses among few lanes, each exact fast lane next to a fenced one.
+        ``all`` adds the engine-path ipc variants and p2p_block (measurement).
+        Paced or threshold jobs cannot take direct rounds: the engine-path
+        fused ipc round (lite + fenced) stands in."""
+        if lane_set not in ("default", "all"):
+            raise ValueError("lane_set must be 'default' or 'all'")
+        allset = lane_set == "all"
+        c: list = []
+        if two_sided:
+            c += ["p2p", "p2p_block"] if allset else ["p2p"]
+        if ipc_open:
+            if allset:
+                c += ["ipc", "ipc_bcast", "ipc_fused", "ipc_fused_bcast", "ipc_wide", "ipc_bcast_wide",
+                      "ipc_lite", "ipc_bcast_lite", "ipc_fused_lite", "ipc_fused_bcast_lite"]
+            if exact and not paced:
+                c += ["ipc_lite_direct", "ipc_fused_lite_direct", "ipc_fused_direct"]
+            elif not allset:
+                c += ["ipc_fused_lite", "ipc_fused"]
+        if onesided_ok and exact:
+            c += ["onesided", "onesided_fenced"]
+        return c
 
     def capturable(self) -> "CapturableExact":
         """A graph-capturable view of this engine's exact rounds (GPU, N > 1):
@@ -563,9 +602,10 @@ class ThresholdAllreduce:
     def use_lane(self, name: str) -> None:
         """Switch to a named lane candidate (see LANES); every rank must do the
         same at the same round."""
-        if name == "onesided":
+        if name in ("onesided", "onesided_fenced"):
             self._ipc_direct_off()
             self.enable_onesided()
+            self._exact_os.set_handoff("fenced" if name == "onesided_fenced" else "lite")
             self._lane_os = True
             return
         self._lane_os = False
@@ -582,7 +622,7 @@ class ThresholdAllreduce:
             self.set_exact_unit_bytes(unit)
         self._ipc_direct = name.endswith("_direct")
 
-    def tune(self, candidates=None, rounds: int = 8, try_ipc: bool = True) -> dict:
+    def tune(self, candidates=None, rounds: int = 8, try_ipc: bool = True, lane_set: str = "default") -> dict:
         """Pick the fastest exact lane for this buffer on this job (collective).
 
         Every candidate runs three exact rounds with different integer data (the
@@ -592,7 +632,8 @@ class ThresholdAllreduce:
         fails on any rank ends the candidate on every rank.  The
         one-sided lanes join when every rank could map every other rank's
         window.  Leaves the object on the winner; returns every candidate's
-        result and the choice.  Needs thresholds 1 (exact rounds)."""
+        result and the choice.  Needs thresholds 1 (exact rounds).
+        ``lane_set``: the candidates when none are given (lane_candidates)."""
         import time
 
         import torch.distributed as dist
@@ -608,7 +649,7 @@ class ThresholdAllreduce:
             # framework lanes only: the p2p schedule (gfx950 reduce) and the
             # one-sided ipc kernels.  RCCL's own reduce-scatter + all-gather
             # ("collective") is a comparator, never a candidate.  "none": ipc-only job
-            cands = [] if spec[0] == "none" else ["p2p", "p2p_block"]
+            os_ok = False
             if self.device.type == "cuda" and try_ipc:
                 if not ipc_open:
                     err = None
@@ -620,11 +661,6 @@ class ThresholdAllreduce:
                     if not ipc_open:
                         res["ipc"] = {"exact": None, "ms": None,
                                       "error": err or "another rank could not open its windows"}
-                if ipc_open:
-                    cands += ["ipc", "ipc_bcast", "ipc_fused", "ipc_fused_bcast", "ipc_wide", "ipc_bcast_wide",
-                              "ipc_lite", "ipc_bcast_lite", "ipc_fused_lite", "ipc_fused_bcast_lite"]
-                    if self._th_exact and self.pacer is None:
-                        cands += ["ipc_lite_direct", "ipc_fused_lite_direct"]
                 if self._th_exact:
                     err = None
                     os_made_here = self._exact_os is None
@@ -633,10 +669,14 @@ class ThresholdAllreduce:
                     except Exception as e:  # noqa: BLE001 - the candidate is skipped on every rank
                         err = f"{type(e).__name__}: {e}"[:200]
                     if self._agree_max([1.0 if err else 0.0])[0] == 0.0:
-                        cands.append("onesided")
+                        os_ok = True
                     else:
                         res["onesided"] = {"exact": None, "ms": None,
                                            "error": err or "another rank could not map its one-sided windows"}
+            cands = self.lane_candidates(two_sided=spec[0] != "none",
+                                         ipc_open=ipc_open and self.device.type == "cuda" and try_ipc,
+                                         onesided_ok=os_ok, exact=self._th_exact, paced=self.pacer is not None,
+                                         lane_set=lane_set)
         S, N, r = self.data_size, self.world_size, self.rank
         dtype = self.worker.dtype
         x = torch.randn(S, device=self.device).to(dtype)
@@ -682,7 +722,7 @@ class ThresholdAllreduce:
                         val = float(v)
                     elif not v:
                         ok = False
-                    if name == "onesided" and self._exact_os is not None and self._exact_os.error():
+                    if name.startswith("onesided") and self._exact_os is not None and self._exact_os.error():
                         ok, err = False, f"{tag}: a bounded wait of the onesided lane expired"
                 except Exception as e:  # noqa: BLE001 - the candidate is rejected
                     ok, err = False, f"{tag}: {type(e).__name__}: {e}"[:160]
@@ -699,7 +739,7 @@ class ThresholdAllreduce:
         if not good:
             raise RuntimeError(f"no exact lane: {res}")
         pick = min(good, key=lambda n: res[n]["ms"])
-        if pick != "onesided" and os_made_here and self._exact_os is not None:
+        if not pick.startswith("onesided") and os_made_here and self._exact_os is not None:
             # the one-sided windows (2 x rows x the buffer) are not kept for
             # a lane that lost: every rank is past its last round on them
             # (the agreement below is the barrier), then each frees its own
@@ -740,7 +780,7 @@ class ThresholdAllreduce:
         if self._lane_os:
             st = self.worker.state()
             link = dict(st.get("link", {}))
-            link["lane"] = "onesided"
+            link["lane"] = "onesided_fenced" if self._exact_os.handoff == "fenced" else "onesided"
             link["onesided"] = {**self._exact_os.info(), "stats": self._exact_os.stats()}
             return {**st, "link": link}
         if self.transport == "onesided":
@@ -822,6 +862,11 @@ class CapturableExact:
     def note_replays(self, n: int) -> None:
         if self.lane == "onesided":
             self.ar._exact_os.note_replays(n)
+        elif self.ar.worker._core.ipc_error_now():
+            # a replayed round's wait failed (the fixed counts table now reads
+            # 0): the lane is dead, like the engine path's next round
+            raise RuntimeError("ipc lane: a wait of a replayed round timed out (peer missing?); "
+                               "its rounds are not trustworthy")
 
     def __call__(self, x: torch.Tensor, out: Optional[torch.Tensor] = None) -> AllReduceOutput:
         if self.lane == "onesided":
@@ -830,7 +875,8 @@ class CapturableExact:
         if out is None:
             out = torch.empty_like(x)
         stream = torch.cuda.current_stream(self.ar.device)
-        self.ar.worker._core.ipc_round_direct(x.data_ptr(), out.data_ptr(), stream.cuda_stream)
+        self.ar.worker._core.ipc_round_direct(x.data_ptr(), out.data_ptr(), stream.cuda_stream,
+                                              self.counts.data_ptr(), self.counts.numel())
         return AllReduceOutput(out, iteration=-1, counts_per_chunk=self.counts, geometry=g,
                                expander=self.ar.worker._expand_counts)
 

@@ -47,6 +47,12 @@ from ..data import AllReduceOutput, Geometry
 from .collective import _handle_exchange, env_rank_world
 
 _DTYPES = {torch.float32: "float32", torch.bfloat16: "bfloat16"}
+# Hand-off of window bytes between ranks (csrc/kernels/onesided.hip): "lite"
+# = write-through stores + drain before each flag, system-coherent loads (no
+# cache maintenance); "fenced" = plain stores behind a system-scope release,
+# a system-scope acquire after each observed flag -- the HIP memory model's
+# own protocol, the fallback for a link on which lite is not proven.
+_HANDOFFS = ("lite", "fenced")
 
 
 class OneSidedOutput(AllReduceOutput):
@@ -82,6 +88,8 @@ class OneSidedOutput(AllReduceOutput):
         was reused (64 or more later calls)."""
         if self._status is not None:
             return self._status
+        if self._call < 0:
+            raise RuntimeError("a call captured into a graph has no status record (its replays do)")
         st = self._lane.status(self._call)
         if st["round"] >= 0:
             self._status = st
@@ -89,6 +97,8 @@ class OneSidedOutput(AllReduceOutput):
 
     @property
     def status(self) -> dict:
+        if self._call < 0:
+            raise RuntimeError("a call captured into a graph has no status record (its replays do)")
         if self._status is None:
             if self._stream is not None:
                 self._stream.synchronize()
@@ -124,9 +134,12 @@ class OneSidedAllreduce:
         role_wgs: int = 0,
         cu_keep: int = 0,
         data_sink: Any = None,
+        handoff: str = "lite",
     ):
         if dtype not in _DTYPES:
             raise ValueError("dtype must be float32 or bfloat16")
+        if handoff not in _HANDOFFS:
+            raise ValueError(f"handoff must be one of {_HANDOFFS}")
         r, w, local = env_rank_world()
         import torch.distributed as dist
 
@@ -164,7 +177,8 @@ class OneSidedAllreduce:
                                        _DTYPES[dtype], th_reduce=float(th_reduce), th_complete=float(th_complete),
                                        max_lag=int(max_lag), rows=int(rows), part_bytes=int(part_bytes),
                                        timeout_ms=int(timeout_s * 1000), threads=int(threads),
-                                       role_wgs=int(role_wgs), cu_keep=int(cu_keep))
+                                       role_wgs=int(role_wgs), cu_keep=int(cu_keep),
+                                       fenced=handoff == "fenced")
             mine = self.lane.handle()
         except Exception as e:  # noqa: BLE001 - re-raised after the exchange
             mine, err = b"", e
@@ -180,7 +194,9 @@ class OneSidedAllreduce:
         exchange_done(b"1")
         self.lane.unlink()
         self._kmax = self.geometry.kmax
-        self._counts: Optional[torch.Tensor] = None
+        # counts tables reused with caller-owned outputs, one per output buffer
+        # (a caller alternating buffers keeps each round's counts with its data)
+        self._counts: dict = {}
         self._side: Optional[torch.cuda.Stream] = None  # async_op rounds
         self.calls = 0
 
@@ -205,10 +221,14 @@ class OneSidedAllreduce:
             raise ValueError("out must be a contiguous tensor of the buffer's size and dtype")
         if reuse:
             # the caller manages the output's lifetime (``out`` given): the
-            # counts table is reused with it, like the output buffer itself
-            if self._counts is None:
-                self._counts = torch.empty((self.world_size, self._kmax), dtype=torch.int32, device=self.device)
-            counts = self._counts
+            # counts table is reused with THAT buffer, like the buffer itself
+            key = out.data_ptr()
+            counts = self._counts.get(key)
+            if counts is None:
+                if len(self._counts) >= 16:  # bounded: buffers a caller dropped
+                    self._counts.pop(next(iter(self._counts)))
+                counts = torch.empty((self.world_size, self._kmax), dtype=torch.int32, device=self.device)
+                self._counts[key] = counts
         else:
             counts = torch.empty((self.world_size, self._kmax), dtype=torch.int32, device=self.device)
         stream = torch.cuda.current_stream(self.device) if self.device.type == "cuda" else None
@@ -226,7 +246,8 @@ class OneSidedAllreduce:
         if async_op and stream is not None:
             event = torch.cuda.Event()
             event.record(stream)
-        self.calls += 1
+        if call >= 0:  # (a captured call counts once per replay: note_replays)
+            self.calls += 1
         o = OneSidedOutput(out.view(-1), lane=self.lane, call=call, stream=stream, counts_per_chunk=counts,
                            geometry=self.geometry, expander=self._expand if stream is not None else None,
                            event=event)
@@ -246,6 +267,17 @@ class OneSidedAllreduce:
         call sequence lives in device memory.  After each replay of a captured
         call, ``note_replays(1)`` keeps the host's call ids in step."""
         return self.device.type == "cuda" and self.data_sink is None
+
+    @property
+    def handoff(self) -> str:
+        return "fenced" if self.lane.fenced else "lite"
+
+    def set_handoff(self, mode: str) -> None:
+        """Hand-off mode of this rank's later calls ("lite" / "fenced"); the
+        modes share the protocol's tags, so ranks may switch independently."""
+        if mode not in _HANDOFFS:
+            raise ValueError(f"handoff must be one of {_HANDOFFS}")
+        self.lane.set_fenced(mode == "fenced")
 
     def note_replays(self, n: int) -> None:
         self.lane.note_replays(int(n))

@@ -126,3 +126,14 @@ def env_phase_stall(rank: int, phase: str) -> None:
         raise RuntimeError(f"injected fault on rank {rank} in phase {phase}")
     while True:
         time.sleep(3600)
+
+
+def env_bad_handoff(rank: int, handoff: str) -> bool:
+    """``AKKA_FAULT_BAD_HANDOFF=<mode>`` (e.g. ``lite``): this rank's
+    validation rounds of config 4 count one chunk as torn while the lane runs
+    in that hand-off mode -- exercises the switch to the fenced hand-off
+    without a link that actually reorders (``AKKA_FAULT_BAD_HANDOFF_RANK``
+    narrows it to one rank)."""
+    want = os.environ.get("AKKA_FAULT_BAD_HANDOFF")
+    who = os.environ.get("AKKA_FAULT_BAD_HANDOFF_RANK")
+    return want == handoff and (who is None or int(who) == int(rank))

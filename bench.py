@@ -84,6 +84,9 @@ def parse():
                    help="ipc: no RCCL communicator, every exact round on the one-sided xGMI lane; ipc_p2p: the "
                         "p2p schedules over mailboxes in mapped peer memory (with AKKA_SHARE_GPU=1 either rehearses "
                         "the N-rank flow with N processes on one card)")
+    p.add_argument("--lane-set", choices=["default", "all"], default="default",
+                   help="lane selection candidates: default = p2p, the direct ipc rounds (lite, fused lite, fused "
+                        "fenced) and the one-sided lane (lite, fenced); all = also every engine-path ipc variant")
     p.add_argument("--ipc", choices=["on", "off"], default="on",
                    help="lane selection also tries the one-sided xGMI lane (mapped peer windows, ipc_lane.h)")
     p.add_argument("--async-op", choices=["auto", "on", "off"], default="auto",
@@ -153,11 +156,16 @@ def run_cfg4(world: int, rank: int, dev, barrier, size_mb: float, delay_ms: floa
     every rank contributes the constant 2^rank, so every output chunk must be
     one integer whose set bits are its contributors, as many as its count --
     a torn, stale or mixed chunk shows (on a node: the cross-device hand-offs
-    of the one-sided lane, checked on the job itself)."""
-    import statistics
+    of the one-sided lane, checked on the job itself).
 
+    The lane starts with its fast "lite" hand-offs (write-through stores +
+    drain).  If the validation finds a bad chunk on any rank, every rank
+    switches to the FENCED hand-off (system release / acquire, the HIP memory
+    model's own protocol) and runs both phases and the validation again: the
+    line then says ``handoff: fenced`` and keeps the lite run under
+    ``handoff_fallback`` -- the straggler path stays available whatever the
+    link does (reference: AllreduceWorker.scala:170-186)."""
     import torch
-    import torch.distributed as dist
 
     from akka_allreduce_amd.parallel import ThresholdAllreduce
 
@@ -176,6 +184,8 @@ def run_cfg4(world: int, rank: int, dev, barrier, size_mb: float, delay_ms: floa
            "lane": ar.state()["link"]["onesided"]}
     res["lane"].pop("stats", None)
     res.update(cfg4_threshold_needs(world, S, C, 0.75, 0.75, straggler))
+    res["handoff"] = ar._os.handoff
+    res["handoff_fallback"] = None
 
     def sync():
         if dev.type == "cuda":
@@ -186,9 +196,41 @@ def run_cfg4(world: int, rank: int, dev, barrier, size_mb: float, delay_ms: floa
     # rank's setup kernels need (docs/DESIGN.md §4c, cu_keep)
     sync()
     barrier()
-    last = -1
+    last = cfg4_phases(ar, res, x, out, world, rank, straggler, delay_ms, rounds, -1, sync)
+    res["validation"] = cfg4_validate(ar, world, rank, straggler, delay_ms, last, max(8, rounds // 4), dev)
+    last = res["validation"].pop("last_round")
+    if not res["validation"]["contributor_sets_consistent"] and ar._os.handoff != "fenced":
+        # a torn, stale or mixed chunk on the lite hand-offs (the verdict is
+        # the same on every rank: the validation gathers every rank's count)
+        lite = {k: res.pop(k) for k in ("no_straggler", "with_straggler", "fast_rank_slowdown", "validation")}
+        ar._os.set_handoff("fenced")
+        sync()
+        barrier()
+        last = cfg4_phases(ar, res, x, out, world, rank, straggler, delay_ms, rounds, last, sync)
+        res["validation"] = cfg4_validate(ar, world, rank, straggler, delay_ms, last, max(8, rounds // 4), dev)
+        res["validation"].pop("last_round")
+        res["handoff"] = "fenced"
+        res["handoff_fallback"] = {"from": "lite", "reason": "validation found torn / stale / mixed chunks",
+                                   "lite": lite}
+    ar.retire()  # the job's end: nobody waits for this rank's later rounds
+    sync()
+    barrier()
+    return res
+
+
+def cfg4_phases(ar, res: dict, x, out, world: int, rank: int, straggler: int, delay_ms: float, rounds: int,
+                last: int, sync) -> int:
+    """Config 4's two timed phases (run_cfg4), each ending at a common round
+    past ``last`` (the same on every rank); fills ``res``, returns this
+    rank's last round served."""
+    import statistics
+
+    import torch
+    import torch.distributed as dist
+
+    base = last + 1
     for pi, key in enumerate(("no_straggler", "with_straggler")):
-        target = (pi + 1) * rounds - 1
+        target = base + (pi + 1) * rounds - 1
         st0 = ar._os.stats()
         ms, outs, calls = [], [], 0
         while last < target:
@@ -231,14 +273,14 @@ def run_cfg4(world: int, rank: int, dev, barrier, size_mb: float, delay_ms: floa
             "forced_completions": sum(v["complete_forced"] for v in allv),
             "timeouts": sum(v["timeouts"] for v in allv),
         }
+        # the next phase starts past the largest round any rank served
+        lasts = [None] * world
+        dist.all_gather_object(lasts, last)
+        last = max(lasts)
     a, b = res["no_straggler"], res["with_straggler"]
     res["fast_rank_slowdown"] = round(b["fast_rank_median_ms_per_round"] / max(1e-9, a["fast_rank_median_ms_per_round"]),
                                       3)
-    res["validation"] = cfg4_validate(ar, world, rank, straggler, delay_ms, last, max(8, rounds // 4), dev)
-    ar.retire()  # the job's end: nobody waits for this rank's later rounds
-    sync()
-    barrier()
-    return res
+    return last
 
 
 def cfg4_validate(ar, world: int, rank: int, straggler: int, delay_ms: float, last: int, rounds: int, dev) -> dict:
@@ -247,8 +289,11 @@ def cfg4_validate(ar, world: int, rank: int, straggler: int, delay_ms: float, la
     import torch
     import torch.distributed as dist
 
+    from akka_allreduce_amd.utils.faults import env_bad_handoff
+
     os_ = ar._os
     g = os_.geometry
+    inject = env_bad_handoff(rank, os_.handoff)  # fault injection: one torn chunk per call
     S = ar.data_size
     x = torch.full((S,), float(1 << rank), device=dev)
     out = torch.empty_like(x)
@@ -276,14 +321,17 @@ def cfg4_validate(ar, world: int, rank: int, straggler: int, delay_ms: float, la
                 v, c = float(seg[0]), int(counts[p, k])
                 iv = int(v)
                 ok = bool((seg == v).all()) and float(iv) == v and 0 <= iv < (1 << world) and bin(iv).count("1") == c
+                if inject and p == 0 and k == 0:
+                    ok = False
                 if not ok:
                     bad += 1
                     if first_bad is None:
                         first_bad = {"round": last, "block": p, "chunk": k, "count": c, "value": v}
-    mine = {"bad": bad, "chunks": chunks, "calls": calls, "first_bad": first_bad}
+    mine = {"bad": bad, "chunks": chunks, "calls": calls, "first_bad": first_bad, "last": last}
     allv = [None] * world
     dist.all_gather_object(allv, mine)
-    return {"rounds": rounds, "calls": [v["calls"] for v in allv], "chunks_checked": sum(v["chunks"] for v in allv),
+    return {"rounds": rounds, "handoff": os_.handoff, "last_round": max(v["last"] for v in allv),
+            "calls": [v["calls"] for v in allv], "chunks_checked": sum(v["chunks"] for v in allv),
             "bad_chunks": sum(v["bad"] for v in allv),
             "first_bad": next((dict(v["first_bad"], rank=i) for i, v in enumerate(allv) if v["first_bad"]), None),
             "contributor_sets_consistent": all(v["bad"] == 0 for v in allv)}
@@ -451,7 +499,7 @@ def apply_lane_choice(ar, name) -> None:
     chose (ThresholdAllreduce.LANES); None: leave auto."""
     if not name or ar.world_size < 2 or ar.transport != "stream":
         return
-    if name == "onesided":
+    if name.startswith("onesided"):
         try:
             ar.enable_onesided()  # collective; a failure on any rank raises on every rank
         except Exception as e:  # noqa: BLE001 - keep the job on the framework's p2p lane
@@ -604,7 +652,7 @@ def run_extras(world: int, dev, barrier, which=("cfg1", "cfg3", "cfg4", "cfg5"),
         # backward, the allreduce and the fused average + SGD update -- as one
         # replay (device-resident round ids, ThresholdAllreduce.capturable())
         chosen = (ar.state().get("link", {}) or {}).get("lane") if world > 1 else None
-        if world > 1 and chosen is not None and (str(chosen).startswith("ipc") or chosen == "onesided"):
+        if world > 1 and chosen is not None and (str(chosen).startswith("ipc") or str(chosen).startswith("onesided")):
             _sync()
             barrier()
             progress(f"rank {rank}: cfg5 whole step graphed ({chosen})")
@@ -882,9 +930,9 @@ def main() -> int:
 
     def lane_select():
         env_phase_stall(rank, "lane_select")
-        if ipc_only:  # the two-sided lane failed its preflight: ipc lanes only
-            return ar.tune(candidates=[k for k in ar.LANES if k.startswith("ipc")])
-        return ar.tune(try_ipc=args.ipc == "on")
+        # (ipc_only: the two-sided lane failed its preflight; the engine on the
+        # ipc data plane has no p2p lane, so the window lanes alone compete)
+        return ar.tune(try_ipc=args.ipc == "on" or ipc_only, lane_set=args.lane_set)
 
     lane_sel = None
     if world > 1 and ar.transport == "stream" and args.lane == "auto" and args.lane_select == "on":
@@ -1038,7 +1086,7 @@ def main() -> int:
     line["config"] = dict(base["config"])
     line["config"].update({
         "transport": ("xgmi-ipc" if str(lane_used).startswith("ipc") else
-                      "xgmi-onesided" if lane_used == "onesided" else
+                      "xgmi-onesided" if str(lane_used).startswith("onesided") else
                       "xgmi-mailbox-p2p" if args.data_plane == "ipc_p2p" else
                       "rccl-pair-reactive" if ar.transport == "reactive" else "rccl-p2p-xgmi")
         if world > 1 and dev.type == "cuda" else ("gloo-p2p" if world > 1 else "local"),

@@ -23,7 +23,7 @@ void bind_onesided(py::module_& m) {
   py::class_<OneSidedLane>(m, "OneSidedLane")
       .def(py::init([](int32_t device, int64_t S, int32_t N, int64_t C, int32_t me, const std::string& dtype,
                        float th_reduce, float th_complete, int32_t max_lag, int32_t rows, int64_t part_bytes,
-                       int64_t timeout_ms, int32_t threads, int32_t role_wgs, int32_t cu_keep) {
+                       int64_t timeout_ms, int32_t threads, int32_t role_wgs, int32_t cu_keep, bool fenced) {
              OneSidedParams p;
              p.th_reduce = th_reduce;
              p.th_complete = th_complete;
@@ -34,13 +34,16 @@ void bind_onesided(py::module_& m) {
              p.threads = threads;
              p.role_wgs = role_wgs;
              p.cu_keep = cu_keep;
+             p.fenced = fenced;
              const DType dt = (dtype == "bfloat16" || dtype == "bf16") ? DType::BF16 : DType::F32;
              return std::make_unique<OneSidedLane>(device, S, N, C, me, dt, p);
            }),
            py::arg("device"), py::arg("S"), py::arg("N"), py::arg("C"), py::arg("me"), py::arg("dtype") = "float32",
            py::arg("th_reduce") = 1.f, py::arg("th_complete") = 1.f, py::arg("max_lag") = 1, py::arg("rows") = 0,
            py::arg("part_bytes") = int64_t(256) << 10, py::arg("timeout_ms") = 30000, py::arg("threads") = 256,
-           py::arg("role_wgs") = 0, py::arg("cu_keep") = 0)
+           py::arg("role_wgs") = 0, py::arg("cu_keep") = 0, py::arg("fenced") = false)
+      .def("set_fenced", &OneSidedLane::set_fenced)
+      .def_property_readonly("fenced", &OneSidedLane::fenced)
       .def("handle", [](const OneSidedLane& l) { return py::bytes(l.handle()); })
       .def("timeline", [](OneSidedLane& l) {
         std::vector<uint64_t> v;
@@ -137,6 +140,7 @@ void bind_onesided(py::module_& m) {
         d["lane_cus"] = l.lane_cus();
         d["clock_khz"] = l.clock_khz();
         d["pieces_per_part"] = l.pieces();
+        d["handoff"] = l.fenced() ? "fenced" : "lite";
         const auto g = l.role_grid();
         d["role_wgs"] = py::dict(py::arg("push") = g[0], py::arg("reduce") = g[1], py::arg("copy") = g[2]);
         return d;

@@ -284,11 +284,22 @@ class WorkerCore final : public EngineHost {
   // Exact ipc round straight on `stream`, none of the engine's round
   // bookkeeping (exact rounds: every count is N) -- the graph-capturable
   // path, with device-resident round ids (ipc_device_rounds(true)).
-  void ipc_round_direct(uintptr_t in, uintptr_t out, uintptr_t stream) {
+  // `counts` ([n] int32, optional): the fixed counts table the caller hands
+  // out with direct rounds; a failed wait zeroes it on the device.  A wait of
+  // an earlier round that failed makes this call raise, like the engine path
+  // (StreamLink::ipc_round).
+  void ipc_round_direct(uintptr_t in, uintptr_t out, uintptr_t stream, uintptr_t counts, int64_t n) {
     AKKA_CHECK(stream_link_ && stream_link_->ipc(), "ipc_round_direct: the ipc lane is not open");
     AKKA_CHECK(stream_link_->ipc()->device_rounds(), "ipc_round_direct: switch device rounds on first");
+    AKKA_CHECK(stream_link_->ipc()->error_now() == 0,
+               "ipc lane: a wait of an earlier round timed out (peer missing?); its rounds are not trustworthy");
     stream_link_->ipc()->round(reinterpret_cast<StreamH>(stream), reinterpret_cast<const void*>(in),
-                               reinterpret_cast<void*>(out));
+                               reinterpret_cast<void*>(out), reinterpret_cast<int32_t*>(counts), counts ? n : 0);
+  }
+  // The lane's error word as far as the kernels got (no synchronisation).
+  uint32_t ipc_error_now() {
+    AKKA_CHECK(stream_link_ && stream_link_->ipc(), "ipc_error_now: the ipc lane is not open");
+    return stream_link_->ipc()->error_now();
   }
   void ipc_device_rounds(bool on) {
     AKKA_CHECK(stream_link_ && stream_link_->ipc(), "ipc_device_rounds: the ipc lane is not open");
@@ -746,7 +757,9 @@ PYBIND11_MODULE(_native, m) {
       .def("ipc_open", &WorkerCore::ipc_open)
       .def("ipc_error", &WorkerCore::ipc_error)
       .def("ipc_close", &WorkerCore::ipc_close)
-      .def("ipc_round_direct", &WorkerCore::ipc_round_direct)
+      .def("ipc_round_direct", &WorkerCore::ipc_round_direct, py::arg("in_ptr"), py::arg("out_ptr"), py::arg("stream"),
+           py::arg("counts") = 0, py::arg("n") = 0)
+      .def("ipc_error_now", &WorkerCore::ipc_error_now)
       .def("ipc_device_rounds", &WorkerCore::ipc_device_rounds)
       .def("ipc_current_round", &WorkerCore::ipc_current_round)
       .def("ipc_set_mode", &WorkerCore::ipc_set_mode, py::arg("mode"), py::arg("fused") = false,

@@ -244,7 +244,18 @@ void DataPlane::bind_input(int32_t round, const void* input, StreamH ready_strea
 StreamH DataPlane::exec_stream(int32_t round) const {
   auto it = bind_.find(round);
   if (it != bind_.end() && it->second.exec_on_producer) return it->second.exec;
+  if (it != bind_.end() && it->second.exec_on_comm) return dev_->comm_stream();
   return dev_->compute_stream();
+}
+
+void DataPlane::set_exec_comm(int32_t round) {
+  Binding& b = binding_mut(round);
+  if (!b.exec_on_producer) b.exec_on_comm = true;
+}
+
+bool DataPlane::exec_on_comm(int32_t round) const {
+  auto it = bind_.find(round);
+  return it != bind_.end() && it->second.exec_on_comm;
 }
 
 bool DataPlane::exec_on_producer(int32_t round) const {
@@ -276,6 +287,9 @@ void DataPlane::bind_output(int32_t round, void* output, int32_t* counts, Stream
   }
   if (!b.done) b.done = binding_event();
   b.finalized = false;
+  // (exec_on_comm may already be set: bulk rounds bind their output lazily,
+  // after the link chose the comm stream; a fresh round's binding starts clear)
+  b.counts_poisoned = false;
 }
 
 bool DataPlane::has_input(int32_t round) const {
@@ -438,7 +452,15 @@ void DataPlane::upload_counts(int32_t round, const std::vector<int32_t>& blocks,
     for (int32_t j = 0; j < g_.N && same; ++j)
       for (int32_t k = 0; k < g_.num_chunks(j) && same; ++k) same = row[size_t(j) * kmax_ + k] == v;
     if (same) {
-      dev_->fill_i32(s, b.counts, v, size_t(g_.N) * kmax_);
+      if (poison_flag_ && b.exec_on_comm && s == dev_->comm_stream()) {
+        // the lane's error word decides the value when the stream gets there
+        // (v, or 0 after a failed wait): fill + poison in one launch, in the
+        // order of the stream that ran the lane's kernels
+        dev_->fill_counts_unless(s, poison_flag_, b.counts, v, size_t(g_.N) * kmax_);
+        binding_mut(round).counts_poisoned = true;
+      } else {
+        dev_->fill_i32(s, b.counts, v, size_t(g_.N) * kmax_);
+      }
       if (s == dev_->comm_stream()) binding_mut(round).comm_used = true;
       return;
     }
@@ -467,8 +489,9 @@ void DataPlane::finalize(int32_t round, const std::vector<uint8_t>& landed) {
   const StreamH cs = exec_stream(round);
   // cs writes the caller's output/counts below
   if (!b.exec_on_producer && !fault_skip_output_wait_) wait_input(round, cs);
-  // Join: everything the comm stream wrote into this round's output.
-  if (b.comm_used) {
+  // Join: everything the comm stream wrote into this round's output (a round
+  // executing on the comm stream is already in its order).
+  if (b.comm_used && !b.exec_on_comm) {
     EventH ce = record_comm();
     dev_->wait(cs, ce);
   }
@@ -519,12 +542,17 @@ void DataPlane::finalize(int32_t round, const std::vector<uint8_t>& landed) {
   }
   // a round of a lane that failed (a wait timed out / the lane was aborted)
   // never comes back as exact: its counts read 0 everywhere
-  if (poison_flag_ && b.counts) dev_->poison_counts_if(cs, poison_flag_, b.counts, size_t(g_.N) * kmax_);
+  if (poison_flag_ && b.counts && !b.counts_poisoned)
+    dev_->poison_counts_if(cs, poison_flag_, b.counts, size_t(g_.N) * kmax_);
   if (b.exec_on_producer) {
     dev_->flush(cs);  // the round's launch must not wait for the next round to merge into
     b.done_lazy = true;
   } else {
     dev_->record(b.done, cs);
+    // async callers record their event on the compute stream (worker.py
+    // _deliver / the DDP hook's async_stream): it follows the comm stream's
+    // done point -- off the comm stream's path, which never waits for it
+    if (b.exec_on_comm) dev_->wait(dev_->compute_stream(), b.done);
   }
   b.finalized = true;
 }

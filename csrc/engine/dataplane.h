@@ -101,6 +101,12 @@ class DataPlane {
   // or -- for a purely local round (N == 1) -- the input producer's stream.
   StreamH exec_stream(int32_t round) const;
   bool exec_on_producer(int32_t round) const;
+  // A bulk (whole exact) round whose every write ends in comm-stream order
+  // (ipc kernels, the exact step schedule, RCCL's collectives): its counts and
+  // finalize run on the comm stream too, so the round needs no comm -> compute
+  // -> comm event hop before its done point (profiles/r05/engine_path/).
+  void set_exec_comm(int32_t round);
+  bool exec_on_comm(int32_t round) const;
   // Make `s` wait (once per round) for the stream that produced the input and
   // for the point where the output/counts memory was handed over: every
   // stream that reads the input or writes the output/counts calls it first.
@@ -151,6 +157,8 @@ class DataPlane {
     bool comm_used = false;  // the comm stream wrote into this round (join at finalize)
     StreamH exec = nullptr;  // stream running this round's compute when exec_on_producer
     bool exec_on_producer = false;
+    bool exec_on_comm = false;     // set_exec_comm: counts + finalize on the comm stream
+    bool counts_poisoned = false;  // the counts fill already applied the poison flag
     EventH done = nullptr;
     // Producer-stream rounds record `done` only when someone asks for it: the
     // round is already in that stream's order, and a marker between two

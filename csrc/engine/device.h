@@ -86,6 +86,12 @@ class Device {
   // counts[0..n) = 0 if *flag != 0 when the stream gets there (a failed
   // one-sided round).  Host devices never run those rounds.
   virtual void poison_counts_if(StreamH, const uint32_t* /*flag*/, int32_t* /*counts*/, size_t /*n*/) {}
+  // counts[0..n) = (*flag != 0 ? 0 : value) when the stream gets there: the
+  // counts fill of an exact round and its poison check as one operation.
+  virtual void fill_counts_unless(StreamH s, const uint32_t* flag, int32_t* counts, int32_t value, size_t n) {
+    fill_i32(s, counts, value, n);
+    poison_counts_if(s, flag, counts, n);
+  }
   // Issue any work held back on `s` (reduce launches kept open for merging).
   virtual void flush(StreamH) {}
 

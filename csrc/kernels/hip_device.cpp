@@ -222,6 +222,11 @@ class HipDevice final : public Device {
     flush_if(s);
     launch_poison_counts(static_cast<hipStream_t>(s), flag, counts, int64_t(n));
   }
+  void fill_counts_unless(StreamH s, const uint32_t* flag, int32_t* counts, int32_t value, size_t n) override {
+    if (!n) return;
+    flush_if(s);
+    launch_fill_counts(static_cast<hipStream_t>(s), flag, counts, value, int64_t(n));
+  }
   void flush(StreamH s) override { flush_if(s); }
 
  private:

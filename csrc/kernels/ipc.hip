@@ -41,6 +41,13 @@ using namespace xgmi;
 // earlier timeout of this rank, makes every later wait fail too; the failed
 // round's counts are then poisoned to 0 (DataPlane::finalize) and the next
 // round on the lane raises.
+// Lane 0: this rank's round failed -- error word, and the direct rounds'
+// counts table reads 0 from now on (vector stores, one lane).
+__device__ void fail_round(const IpcArgs& a) {
+  sys_store(a.err, 1u);
+  for (int64_t i = 0; i < a.fail_n; ++i) a.fail_counts[i] = 0;
+}
+
 __device__ bool wait_flag(const IpcArgs& a, uint32_t* f, uint32_t want, uint64_t deadline) {
   uint32_t* abort_me = a.flags[a.me] + ipc_flag_error(a.N, a.nportions);
   uint32_t spins = 0;
@@ -49,18 +56,18 @@ __device__ bool wait_flag(const IpcArgs& a, uint32_t* f, uint32_t want, uint64_t
       // a producer that aborted stored the abort before its flag (release)
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
       if (sys_load(abort_me) != 0) {
-        sys_store(a.err, 1u);
+        fail_round(a);
         return false;
       }
       return true;
     }
     if ((++spins & 63) == 0) {
       if (sys_load(a.err) != 0 || sys_load(abort_me) != 0) {
-        sys_store(a.err, 1u);
+        fail_round(a);
         return false;
       }
       if (wall_clock64() > deadline) {
-        sys_store(a.err, 1u);
+        fail_round(a);
         for (int32_t p = 0; p < a.N; ++p) sys_store(a.flags[p] + ipc_flag_error(a.N, a.nportions), 1u);
         return false;
       }

@@ -59,6 +59,11 @@ struct IpcArgs {
   const char* in = nullptr;  // round input [S]
   char* out = nullptr;       // round output [S]
   uint32_t* err = nullptr;   // host-mapped error word: set on a timed-out wait (read by the host each round)
+  // direct rounds' fixed counts table [fail_n]: zeroed by a failed wait, so
+  // an output of a failed round never reads as exact (nullptr: engine rounds,
+  // whose counts are poisoned behind the round instead)
+  int32_t* fail_counts = nullptr;
+  int64_t fail_n = 0;
 };
 
 // Flag words of one rank's flag area (uint32 index).

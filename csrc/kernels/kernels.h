@@ -48,6 +48,8 @@ void launch_xent_bwd(hipStream_t s, const void* x, const int64_t* y, int64_t B, 
 // counts[0..n) = 0 if *flag != 0 (read when the kernel runs): poisons the
 // counts of a one-sided round whose waits failed.
 void launch_poison_counts(hipStream_t s, const uint32_t* flag, int32_t* counts, int64_t n);
+// counts[0..n) = (*flag != 0 ? 0 : value): fill + poison of an exact round in one launch.
+void launch_fill_counts(hipStream_t s, const uint32_t* flag, int32_t* counts, int32_t value, int64_t n);
 // Standalone kernels for tests/bench: out = a (+ b ...) via a pointer table on device.
 ReduceImpl reduce_impl_from_env();
 const char* reduce_impl_name(ReduceImpl i);

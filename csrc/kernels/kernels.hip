@@ -840,6 +840,23 @@ __global__ void poison_counts_kernel(const uint32_t* flag, int32_t* counts, int6
 }
 }  // namespace
 
+namespace {
+// An exact round's counts table in one launch: value everywhere, or 0 when
+// the lane's error word is set by the time the stream gets here.
+__global__ void fill_counts_kernel(const uint32_t* flag, int32_t* counts, int64_t n, int32_t value) {
+  const int32_t v =
+      __hip_atomic_load(const_cast<uint32_t*>(flag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == 0 ? value : 0;
+  for (int64_t i = blockIdx.x * int64_t(blockDim.x) + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
+    counts[i] = v;
+}
+}  // namespace
+
+void launch_fill_counts(hipStream_t s, const uint32_t* flag, int32_t* counts, int32_t value, int64_t n) {
+  if (n <= 0) return;
+  hipLaunchKernelGGL(fill_counts_kernel, dim3(unsigned(std::min<int64_t>(64, (n + 255) / 256))), dim3(256), 0, s,
+                     flag, counts, n, value);
+}
+
 void launch_poison_counts(hipStream_t s, const uint32_t* flag, int32_t* counts, int64_t n) {
   if (n <= 0) return;
   hipLaunchKernelGGL(poison_counts_kernel, dim3(unsigned(std::min<int64_t>(64, (n + 255) / 256))), dim3(256), 0, s,

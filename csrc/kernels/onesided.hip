@@ -13,6 +13,13 @@
 // issues (the announce -> look hand-shake).  No buffer_wbl2 / buffer_inv on
 // the aligned paths; unaligned spans (odd chunk sizes) fall back to plain
 // stores + a system release.
+//
+// Args::fenced selects the conservative twin for every span: plain stores, a
+// system-scope release (cache write-back) before each flag store and a
+// system-scope acquire after each observed flag (xgmi_device.h release_wg /
+// acquire) -- the ordering the HIP memory model guarantees across devices,
+// for links where write-through + drain is not known to order data before
+// the flag.  Both modes share the tags, so ranks may differ in mode.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -161,7 +168,7 @@ __device__ void push_role(const Args& a, uint32_t r, int32_t w0, int32_t stride)
       const int64_t off = part_off(a, k, j);
       char* dst = a.tab->sd[row][p] + (int64_t(a.me) * a.slot + off) * ES;
       const char* src = a.in + (a.tab->bstart[p] + off) * ES;
-      const bool lite = ((uintptr_t(dst) | uintptr_t(src) | uintptr_t(n * ES)) & 15) == 0;
+      const bool lite = !a.fenced && ((uintptr_t(dst) | uintptr_t(src) | uintptr_t(n * ES)) & 15) == 0;
       if (n > 0) {
         if (lite) copy_out_sys(dst, src, n * ES);
         else copy_bytes(dst, src, n * ES);
@@ -335,9 +342,15 @@ __device__ void masked_sum_n(const Args& a, const char* mine, const char* sd, ch
         const uint4 w = Elt<T>::pack(acc);
         if (a.own_wt) store_sys16(sys_rsrc(o, nv * 16), i * 16, w);
         else store_nt16(reinterpret_cast<uint4*>(o) + i, w);
+        if (a.fenced) {  // plain stores, released before the tags (reduce_piece)
 #pragma unroll
-        for (int q = 0; q < NS; ++q)
-          if ((okq >> q) & 1u) store_sys16(sys_rsrc(a.tab->gd[row][q] + goff, nv * 16), i * 16, w);
+          for (int q = 0; q < NS; ++q)
+            if ((okq >> q) & 1u) reinterpret_cast<uint4*>(a.tab->gd[row][q] + goff)[i] = w;
+        } else {
+#pragma unroll
+          for (int q = 0; q < NS; ++q)
+            if ((okq >> q) & 1u) store_sys16(sys_rsrc(a.tab->gd[row][q] + goff, nv * 16), i * 16, w);
+        }
       }
     }
   }
@@ -360,7 +373,7 @@ __device__ bool masked_sum(const Args& a, int32_t row, uint32_t mask, uint32_t o
   if ((al & 15) == 0) {
     if constexpr (NS > 0) {
       masked_sum_n<T, NS>(a, mine, sd, o, goff, row, mask, okq, off, n);
-      return false;
+      return a.fenced != 0;
     }
     const int64_t nv = n / PV;
     for (int64_t i0 = threadIdx.x; i0 < nv; i0 += kUnroll * int(blockDim.x)) {
@@ -442,6 +455,10 @@ __device__ void reduce_piece(const Args& a, uint32_t r, int32_t k, int32_t j, in
     }
     mask_s = uint32_t(d >> 32);
     okq_s = gated ? sys_load(a.loc + L.okq(k, j)) : 0u;
+    if (a.fenced) {  // the decision stands for the landed tags: acquire before reading their bytes
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
   }
   __syncthreads();
   const int64_t n = part_len_of(a, me, k, j);
@@ -610,10 +627,18 @@ __device__ void copy_role(const Args& a, uint32_t r, int32_t w0, int32_t stride)
         // have counted them in
         if (tag_state(DevMem::ld(fl + L.gtag(row, p, k, j)), r) == kLanded) {
           v = 1;
+          if (a.fenced) {  // acquire after the observed tag, before the bytes
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          }
           break;
         }
         if (sys_load(a.loc + L.state(kComp)) == r + 1u) {
           v = sys_load(a.loc + L.cmask(p, k)) != 0u ? 1 : 0;
+          if (v && a.fenced) {
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          }
           break;
         }
         if (wall_clock64() > deadline) {

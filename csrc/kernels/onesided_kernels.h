@@ -56,7 +56,12 @@ struct Args {
   // workgroup on another XCD zeroes it after its reduce pieces -- two XCDs'
   // L2s holding the same dirty lines would write back in any order
   int32_t own_wt = 0;
-  uint64_t timeout = 0;                    // per wait, wall-clock ticks
+  // hand-off mode of window bytes: 0 "lite" (write-through stores + drain
+  // before the flag, system-coherent loads), 1 "fenced" (plain stores, a
+  // system-scope release before every flag, a system-scope acquire after
+  // every observed flag: the HIP memory model's protocol, xgmi_device.h)
+  int32_t fenced = 0;
+  uint64_t timeout = 0;                 // per wait, wall-clock ticks
   const char* in = nullptr;                // round input [S]
   char* out = nullptr;                     // round output [S]
   int32_t* counts = nullptr;               // [N][kcols] per-chunk contributor counts

@@ -213,7 +213,7 @@ void IpcLane::open(const std::vector<std::string>& handles) {
   ready_ = true;
 }
 
-void IpcLane::round(StreamH s, const void* in, void* out) {
+void IpcLane::round(StreamH s, const void* in, void* out, int32_t* fail_counts, int64_t fail_n) {
   AKKA_CHECK(ready_, "ipc lane: open() the peer windows first");
   IpcArgs a;
   std::memset(&a, 0, sizeof(a));
@@ -243,6 +243,8 @@ void IpcLane::round(StreamH s, const void* in, void* out) {
   a.in = static_cast<const char*>(in);
   a.out = static_cast<char*>(out);
   a.err = err_dev_;
+  a.fail_counts = fail_counts;
+  a.fail_n = fail_counts ? fail_n : 0;
   launch_ipc_round(static_cast<hipStream_t>(s), a, dt_);
   AKKA_IPC_HIP(hipGetLastError());
   ++stats_.rounds;

@@ -110,7 +110,10 @@ class IpcLane {
   void set_lite(bool on) { lite_ = on; }
   bool lite() const { return lite_; }
   // Enqueue one exact round on `s`: in[S] from every rank summed into out[S].
-  void round(StreamH s, const void* in, void* out);
+  // `fail_counts` (optional, [fail_n] int32): zeroed by the kernel that
+  // finds a wait failed -- the fixed counts table of direct rounds then reads
+  // 0 for this and every later round (the lane is dead; calls raise).
+  void round(StreamH s, const void* in, void* out, int32_t* fail_counts = nullptr, int64_t fail_n = 0);
   // Device-resident round ids (graph capture): on, the round id lives in a
   // device word that a bump launch in front of every round advances -- a
   // captured round replays with a fresh id.  Switching copies the id across

@@ -103,6 +103,10 @@ OneSidedLane::OneSidedLane(int32_t device, int64_t S, int32_t N, int64_t C, int3
   AKKA_CHECK(me >= 0 && me < N, "onesided lane: rank out of range");
   AKKA_CHECK(S >= 1, "onesided lane: empty buffer");
   AKKA_CHECK(p.max_lag >= 0, "onesided lane: maxLag must be >= 0");
+  if (const char* hv = std::getenv("AKKA_OS_HANDOFF")) {  // lite | fenced
+    if (std::strcmp(hv, "fenced") == 0) p_.fenced = true;
+    else if (std::strcmp(hv, "lite") == 0) p_.fenced = false;
+  }
   D_ = p.rows > 0 ? p.rows : std::max(3, p.max_lag + 2);
   D_ = std::clamp(D_, 2, kMaxRows);
   Kmax_ = std::max(1, g_.max_block_len_chunks());
@@ -410,7 +414,13 @@ int64_t OneSidedLane::round(uintptr_t stream, const void* in, void* out, int32_t
   AKKA_CHECK(ready_, "onesided lane: open() the peer windows first");
   AKKA_CHECK(kcols >= Kmax_, "onesided lane: counts table has too few columns");
   if (device_ >= 0) {
-    const int64_t call = calls_++;
+    // A call captured into a graph runs no kernel now: the device's call
+    // sequence advances once per REPLAY (note_replays), so the host's call
+    // ids must not advance here -- the captured call has no id (-1).
+    hipStreamCaptureStatus cst = hipStreamCaptureStatusNone;
+    const bool capturing = hipStreamIsCapturing(reinterpret_cast<hipStream_t>(stream), &cst) == hipSuccess &&
+                           cst == hipStreamCaptureStatusActive;
+    const int64_t call = capturing ? -1 : calls_++;
     gpu_call(stream, static_cast<const char*>(in), static_cast<char*>(out), counts, kcols);
     return call;
   }
@@ -444,6 +454,7 @@ void OneSidedLane::gpu_call(uintptr_t stream, const char* in, char* out, int32_t
   a.gq = gq_;
   a.nsub = nsub_;
   a.own_wt = need_c_ < g_.total_chunks() ? 1 : 0;
+  a.fenced = p_.fenced ? 1 : 0;
   a.timeout = timeout_ticks_;
   a.in = in;
   a.out = out;

@@ -55,6 +55,10 @@ struct OneSidedParams {
   // (a rank on a GPU of its own never needs one; the mask costs the
   // shared-card round ~0.25 ms at 64 MiB, profiles/r04/README.md)
   int32_t cu_keep = 0;
+  // Hand-off mode of window bytes (os::Args::fenced): false "lite"
+  // (write-through + drain), true "fenced" (plain stores + system release /
+  // acquire).  AKKA_OS_HANDOFF=fenced|lite overrides it at construction.
+  bool fenced = false;
 };
 
 class OneSidedLane {
@@ -90,6 +94,10 @@ class OneSidedLane {
   // Calls a captured (graphed) call ran in addition to round()'s own: keeps
   // the host's call ids in step with the device's sequence.
   void note_replays(int64_t n) { calls_ += n; }
+  // Switch the hand-off mode between calls (every later call; both modes
+  // share the tags, so ranks may switch independently).
+  void set_fenced(bool on) { p_.fenced = on; }
+  bool fenced() const { return p_.fenced; }
 
   // ---- CPU backend, step by step (the deterministic replay harness) ----------
   // begin(): start a round (non-blocking), returns its call id; progress():

@@ -213,6 +213,10 @@ bool StreamLink::bulk_round(int32_t r) {
   // Auto = the framework's own p2p schedule (gfx950 reduce); RCCL's
   // reduce-scatter + all-gather runs only when asked for by name.
   dp_->set_poison_flag(lane_ == Lane::Ipc && ipc_ ? ipc_->error_word_device() : nullptr);
+  // every write of a bulk round ends in comm-stream order (ipc kernels; the
+  // step schedule's last broadcasts wait for every reduce; RCCL's
+  // collectives): its counts and done point go there too, no stream hop
+  dp_->set_exec_comm(r);
   if (lane_ == Lane::Ipc) ipc_round(r);
   else if (lane_ == Lane::Collective) collective_round(r, native);
   else exact_steps(r);
@@ -237,7 +241,8 @@ void StreamLink::ipc_round(int32_t r) {
   Device* dev = dp_->device();
   engine_->ensure_output(r);
   StreamH comm = dev->comm_stream();
-  dp_->comm_wait(dp_->row_release_event(r));
+  // (no ring row: the ipc kernels move the bytes through the lane's own
+  // windows, so the round does not wait for the compute stream's readers)
   dp_->wait_input(r, comm);
   dp_->mark_comm_used(r);
   ipc_->round(comm, dp_->input_chunk(r, 0, 0).ptr, dp_->output_at(r, 0, 0));

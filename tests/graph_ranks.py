@@ -74,6 +74,13 @@ def main():
     if a.lane == "onesided":
         st = ar.stats()
         extra = {"calls": ar.calls - calls0, "error": ar.error(), "forced": st["complete_forced"]}
+        # an eager call after the captured ones: the host's call ids stayed in
+        # step with the device's call sequence (the capture itself ran no
+        # call), so this call's record is found and names its round
+        w = dist.get_world_size()
+        o = ar(torch.full((b1.numel,), float(rank + 1), device=dev))
+        extra.update({"eager_after_round": o.iteration, "eager_after_call": o.call, "calls_total": ar.calls,
+                      "eager_after_exact": bool((o.data == w * (w + 1) / 2).all().item())})
     else:
         r_after = ar.worker._core.ipc_current_round()
         cap.close()

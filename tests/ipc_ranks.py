@@ -42,6 +42,9 @@ def main():
     ap.add_argument("--pre-del", action="store_true", help="delete the --pre-size engine before the timed one")
     ap.add_argument("--mode", default="pull", choices=["pull", "bcast", "alternate", "fused", "fused_bcast", "rotate"])
     ap.add_argument("--out-dir", default="", help="write rank<i>.json there (stdout lines of ranks interleave)")
+    ap.add_argument("--lane-seq", default="",
+                    help="comma list of lane names (ThresholdAllreduce.LANES): use_lane(name) before round r "
+                         "(cycled); records the lane's round id after each round")
     ap.add_argument("--poison", action="store_true",
                     help="round 0 runs on a fresh stream whose only free block is still being written by a "
                          "pending spin + fill: the round's output/counts are carved from it")
@@ -78,7 +81,10 @@ def main():
             import time
 
             time.sleep(a.late_s)  # arrives after the peers' waits timed out
-        if a.mode != "pull":
+        if a.lane_seq:
+            seq = a.lane_seq.split(",")
+            ar.use_lane(seq[r % len(seq)])
+        elif a.mode != "pull":
             variants = [("pull", False), ("bcast", False), ("pull", True), ("bcast", True)]
             mode, fused = {"bcast": ("bcast", False), "fused": ("pull", True), "fused_bcast": ("bcast", True),
                            "alternate": variants[r % 2], "rotate": variants[r % 4]}[a.mode]
@@ -104,6 +110,8 @@ def main():
         want = expected(a.size, world, r, dtype, 5)
         res["exact"].append(bool(torch.equal(o.data.cpu(), want)) and bool((o.count.cpu() == world).all()))
         res.setdefault("counts_all_zero", []).append(bool((o.counts_per_chunk.cpu() == 0).all()))
+        if a.lane_seq:  # the lane's round id, host or device resident (synchronises)
+            res.setdefault("lane_round", []).append(int(ar.worker._core.ipc_current_round()))
     res["ipc_error"] = ar.ipc_error()
     if ((a.skip_rank >= 0 and rank != a.skip_rank) or a.late_rank >= 0) and res["ipc_error"]:
         # the next round on this lane refuses to run (like an RCCL async error)

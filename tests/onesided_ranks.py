@@ -84,6 +84,7 @@ def main():
     ap.add_argument("--compute-ms", type=float, default=0.0, help="every rank 'computes' this long before a call")
     ap.add_argument("--part-bytes", type=int, default=256 << 10)
     ap.add_argument("--timeout-s", type=float, default=30.0)
+    ap.add_argument("--handoff", default="lite", choices=["lite", "fenced"])
     ap.add_argument("--out-dir", required=True)
     a = ap.parse_args()
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
@@ -101,7 +102,7 @@ def main():
     th = 1.0 if a.mode in ("exact", "dead") else a.th
     ar = OneSidedAllreduce(a.size, max_chunk_size=a.chunk, dtype=dtype, th_reduce=th, th_complete=th,
                            max_lag=a.max_lag, device=dev, rows=a.rows, part_bytes=a.part_bytes,
-                           timeout_s=a.timeout_s)
+                           timeout_s=a.timeout_s, handoff=a.handoff)
     res = {"rank": rank, "info": ar.info()}
 
     def sync():

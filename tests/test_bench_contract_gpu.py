@@ -83,8 +83,11 @@ def test_bench_multirank_on_one_card(plane):
     assert "share ONE GPU" in lp["note"] and len(lp["push_GBps"]) == n and len(lp["pull_GBps"][0]) == n
     assert all(lp["push_GBps"][i][j] > 0 for i in range(n) for j in range(n) if i != j)
     if plane == "ipc_p2p":
-        assert {"p2p", "p2p_block", "ipc", "ipc_bcast", "ipc_fused", "ipc_fused_bcast", "ipc_wide",
-                "ipc_bcast_wide"} <= set(cands) and "collective" not in cands
+        # the default (pruned) lane set: the p2p schedule, the direct ipc
+        # rounds with the fused round's fenced twin, the one-sided lane in
+        # both hand-off modes (<= 6 candidates at first contact)
+        assert cands == ["p2p", "ipc_lite_direct", "ipc_fused_lite_direct", "ipc_fused_direct", "onesided",
+                         "onesided_fenced"], cands
         assert d["lane_is_framework"] is True
         c4 = d["extra_configs"]["cfg4_threshold_straggler"]
         w = c4["with_straggler"]
@@ -93,11 +96,11 @@ def test_bench_multirank_on_one_card(plane):
         # the untimed validation rounds (2^rank inputs): every chunk's set matches its count
         v = c4["validation"]
         assert v["contributor_sets_consistent"] is True and v["bad_chunks"] == 0, v
+        assert c4["handoff"] == "lite" and c4["handoff_fallback"] is None, c4
     else:
-        # the ipc lane's variants and the one-sided lane (exact rounds)
-        assert set(cands) == {"ipc", "ipc_bcast", "ipc_fused", "ipc_fused_bcast", "ipc_wide", "ipc_bcast_wide",
-                              "ipc_lite", "ipc_bcast_lite", "ipc_fused_lite", "ipc_fused_bcast_lite",
-                              "ipc_lite_direct", "ipc_fused_lite_direct", "onesided"}
+        # ipc-only job: the window lanes of the default set
+        assert cands == ["ipc_lite_direct", "ipc_fused_lite_direct", "ipc_fused_direct", "onesided",
+                         "onesided_fenced"], cands
 
 
 def test_bench_rccl_init_failure_falls_back_to_ipc():
@@ -120,7 +123,7 @@ def test_bench_rccl_init_failure_falls_back_to_ipc():
     assert len(lines) == 1, r.stdout
     d = json.loads(lines[0])
     assert d["rccl_fallback"]["data_plane"] == "ipc" and set(d["rccl_fallback"]["rccl_init_errors"]) == {"0", "1"}
-    assert d["config"]["data_plane"] == "ipc" and (d["lane"].startswith("ipc") or d["lane"] == "onesided") \
+    assert d["config"]["data_plane"] == "ipc" and (d["lane"].startswith("ipc") or d["lane"].startswith("onesided")) \
         and d["lane_is_framework"] is True
     assert d["exact"] is True and d["value"] > 0
 
@@ -148,9 +151,10 @@ def test_bench_preflight_failure_falls_back_to_ipc():
     d = json.loads(lines[0])
     assert set(d["preflight_fallback"]["errors"]) == {"0", "1"}, d
     assert d["preflight"] == "passed on the ipc lane"
-    assert (d["lane"].startswith("ipc") or d["lane"] == "onesided") \
+    assert (d["lane"].startswith("ipc") or d["lane"].startswith("onesided")) \
         and d["lane_is_framework"] is True
-    assert all(k.startswith("ipc") or k == "onesided" for k in d["lane_select"] if k != "chosen"), d["lane_select"]
+    assert all(k.startswith("ipc") or k.startswith("onesided") for k in d["lane_select"] if k != "chosen"), \
+        d["lane_select"]
     assert d["exact"] is True and d["value"] > 0 and d["rccl_allreduce_algbw_GBps"] is None
 
 
@@ -179,6 +183,6 @@ def test_bench_cfg5_two_ranks_on_one_card():
     assert "cfg5_error" not in ex, ex.get("cfg5_error")
     for k in ("cfg5_mlp_dp_sgd", "cfg5_mlp_dp_sgd_bf16", "cfg5_mlp_dp_sgd_bf16_graph"):
         assert ex[k]["steps_per_s"] > 50, ex
-    if d["lane"] == "onesided" or d["lane"].startswith("ipc"):
+    if d["lane"].startswith("onesided") or d["lane"].startswith("ipc"):
         w = ex["cfg5_mlp_dp_sgd_bf16_whole_graph"]
         assert w["lane"] == d["lane"] and w["steps_per_s"] > 50, ex

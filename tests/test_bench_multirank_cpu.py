@@ -83,6 +83,11 @@ def test_bench_lane_select():
     comparator (other_lane)."""
     d = _run(3)
     sel = d["lane_select"]
+    # the default (pruned) set on CPU processes: the p2p schedule alone
+    assert [k for k in sel if k != "chosen"] == ["p2p"], sel
+    assert sel["chosen"] == "p2p" and d["lane"] == "p2p"
+    d = _run(3, "--lane-set", "all")
+    sel = d["lane_select"]
     cands = ("p2p", "p2p_block")
     assert all(sel[c]["exact"] is True and sel[c]["ms"] > 0 for c in cands)
     assert "collective" not in sel
@@ -96,7 +101,7 @@ def test_bench_n8_full_flow():
     """The driver's largest N: 8 ranks through preflight, lane selection,
     timed rounds, check, comparator and the other lane (uneven blocks: 0.3 MiB
     of fp32 = 78643 elements over 8 ranks, 16 KiB chunks)."""
-    d = _run(8, "--size-mb", "0.3", "--chunk-mb", "0.015625")
+    d = _run(8, "--size-mb", "0.3", "--chunk-mb", "0.015625", "--lane-set", "all")
     assert d["n_gpus"] == 8 and d["config"]["parallelism"] == "dp8" and d["exact"] is True
     assert d["p2p_nranks"] == 8 and [r["rank"] for r in d["rank_devices"]] == list(range(8))
     sel = d["lane_select"]

@@ -37,6 +37,11 @@ def test_fully_graphed_step_matches_eager(lane, dtype):
         rows = [torch.load(os.path.join(out, f"rank{i}.pt"), weights_only=True) for i in range(n)]
     for d in rows:
         assert d["replays"] == 20 and d["calls"] == 20 and d["error"] == 0 and d["forced"] == 0
+        if lane == "onesided":
+            # exact rounds: round id == call id; the eager call after the
+            # graph replays is the last call and its status record is found
+            assert d["eager_after_exact"] and d["eager_after_call"] == d["calls_total"] - 1, d
+            assert d["eager_after_round"] == d["eager_after_call"], d
         assert torch.equal(d["eager"], d["graphed"])
         assert torch.equal(d["eager_losses"], d["graph_losses"])
     for d in rows[1:]:

@@ -179,3 +179,32 @@ def test_ipc_lane_wide_workgroups(threads, n, size, dtype, mode):
     assert r.returncode == 0 and len(rows) == n, r.stderr[-3000:]
     for d in rows:
         assert all(d["exact"]) and d["ipc_error"] == 0, d
+
+
+def test_ipc_direct_lanes_switch_with_engine_lanes():
+    """Direct ipc rounds (device-resident round id, launched on the caller's
+    stream) alternating with the engine path and with the fenced direct
+    twin: every round exact on every rank, and the lane's round id -- handed
+    between host and device at every switch -- advances by one per round."""
+    seq = "ipc_lite_direct,ipc_lite_direct,ipc_fused_lite,ipc_fused_direct,ipc_fused_lite_direct,ipc,ipc_lite_direct"
+    r, rows = _run(4, "--size", str(1 << 20), "--rounds", "7", "--lane-seq", seq)
+    assert r.returncode == 0, r.stderr[-3000:]
+    for d in rows:
+        assert d["exact"] == [True] * 7, d
+        assert d["counts_all_zero"] == [False] * 7, d
+        lr = d["lane_round"]
+        assert lr == list(range(lr[0], lr[0] + 7)), lr
+    assert len({tuple(d["lane_round"]) for d in rows}) == 1
+
+
+def test_ipc_direct_lane_missing_peer_raises():
+    """Rank 1 leaves after round 0 of a direct ipc lane: rank 0's round 1
+    waits (bounded, 0.5 s), its counts table reads 0 (zeroed by the kernel
+    whose wait failed, not a fixed N), and its next call raises."""
+    r, rows = _run(2, "--size", str(1 << 16), "--rounds", "2", "--skip-rank", "1",
+                   "--lane-seq", "ipc_fused_lite_direct", env={"AKKA_IPC_TIMEOUT_MS": "500"})
+    assert r.returncode == 0, r.stderr[-3000:]
+    d0 = rows[0]
+    assert d0["exact"] == [True, False] and d0["ipc_error"] != 0, d0
+    assert d0["counts_all_zero"] == [False, True], d0
+    assert d0["next_round_raised"] is True, d0

@@ -19,12 +19,15 @@ pytestmark = pytest.mark.gpu
     (8, 1 << 22, 1 << 17, "float32"),     # a node's rank count: the N=8 masked-sum kernel
     (8, 1 << 22, 1 << 17, "bfloat16"),
 ])
-def test_onesided_gpu_exact_rounds(n, size, chunk, dtype):
+@pytest.mark.parametrize("handoff", ["lite", "fenced"])
+def test_onesided_gpu_exact_rounds(n, size, chunk, dtype, handoff):
+    """Both hand-off modes (write-through + drain; plain stores behind
+    system release / acquire): bitwise the fp32 sum, counts N."""
     r, rows = run_ranks(n, "--mode", "exact", "--size", str(size), "--chunk", str(chunk), "--dtype", dtype,
-                        "--rounds", "4", "--timeout-s", "10", device="cuda", timeout=180)
+                        "--rounds", "4", "--timeout-s", "10", "--handoff", handoff, device="cuda", timeout=180)
     assert r.returncode == 0, r.stderr[-3000:]
     for d in rows:
-        assert d["info"]["backend"] == "gpu"
+        assert d["info"]["backend"] == "gpu" and d["info"]["handoff"] == handoff
         assert d["exact"] == [True] * 4, d
         assert d["rounds"] == list(range(4)), d
         assert d["error"] == 0 and d["stats"]["missing_chunks"] == 0, d["stats"]
@@ -51,13 +54,15 @@ def test_onesided_gpu_timeline_stamps():
         assert d["exact"] == [True] * 2 and t["words"] >= 3 * t["grid"] and t["ordered"] and t["span_ticks"] > 0, t
 
 
-def test_onesided_gpu_straggler_steady_state():
+@pytest.mark.parametrize("handoff", ["lite", "fenced"])
+def test_onesided_gpu_straggler_steady_state(handoff):
     """N=4 on the card, 0.75 / 0.75, maxLag 1, rank 3 sleeps 50 ms per call,
     64 rounds: fast ranks' median round within 2x of the straggler-free phase,
-    contributor sets consistent with counts, straggler's pushes dropped."""
+    contributor sets consistent with counts, straggler's pushes dropped --
+    in both hand-off modes."""
     r, rows = run_ranks(4, "--mode", "straggler", "--straggler", "3", "--rounds", "64", "--compute-ms", "2",
                         "--delay-ms", "50", "--size", str(1 << 22), "--chunk", str(1 << 18), "--timeout-s", "10",
-                        device="cuda", timeout=180)
+                        "--handoff", handoff, device="cuda", timeout=180)
     assert r.returncode == 0, r.stderr[-3000:]
     for d in rows:
         assert d["error"] == 0, d["stats"]
@@ -87,14 +92,15 @@ def test_onesided_gpu_straggler_killed_mid_run():
 
 @pytest.mark.parametrize("n,th,max_lag,dtype", [(4, 0.75, 1, "float32"), (8, 0.5, 2, "bfloat16"),
                                                 (3, 0.67, 1, "float32"), (4, 1.0, 1, "float32")])
-def test_onesided_gpu_chaos_jitter(n, th, max_lag, dtype):
+@pytest.mark.parametrize("handoff", ["lite", "fenced"])
+def test_onesided_gpu_chaos_jitter(n, th, max_lag, dtype, handoff):
     """Every rank waits a random 0-2 ms before each call, 200 rounds, 16 MiB
     (fp32) with 1 MiB chunks: arrival orders, lags, catch-ups and overwrite
     conflicts vary from round to round across the card's XCDs.  Every output
     chunk of every call is one contributor set matching its count."""
     r, rows = run_ranks(n, "--mode", "chaos", "--th", str(th), "--max-lag", str(max_lag), "--rounds", "200",
                         "--jitter-ms", "2", "--size", str(1 << 22), "--chunk", str(1 << 18), "--dtype", dtype,
-                        "--timeout-s", "10", device="cuda", timeout=240)
+                        "--timeout-s", "10", "--handoff", handoff, device="cuda", timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
     for d in rows:
         c = d["chaos"]
