@@ -36,7 +36,8 @@ def _master(a: argparse.Namespace) -> int:
     wc = WorkerConfig(int(total), a.max_lag if a.max_lag is not None else cfg.workers.maxLag)
     m = start_master(th, data, wc, host=a.host or cfg.cluster.host, port=int(port),
                      heartbeat_interval_s=cfg.cluster.heartbeat_interval_s,
-                     unreachable_after_s=cfg.cluster.unreachable_after_s, transport=a.transport or cfg.engine.transport)
+                     unreachable_after_s=cfg.cluster.unreachable_after_s, transport=a.transport or cfg.engine.transport,
+                     min_workers=a.min_workers)
     print(f"-------\n Port = {m.node.port} \n Number of Workers = {wc.totalSize} \n Message Size = {data.dataSize} "
           f"\n Max Chunk Size = {data.maxChunkSize}", flush=True)
     try:
@@ -127,6 +128,9 @@ def main(argv=None) -> int:
     m.add_argument("--data-size", type=int)
     m.add_argument("--max-chunk-size", type=int)
     m.add_argument("--max-round", type=int)
+    m.add_argument("--min-workers", type=int,
+                   help="start round 0 once this many workers joined (default: all); the others join later and "
+                        "every worker gets a re-InitWorkers with the new peer map (SPEC:141-170)")
     m.add_argument("--max-lag", type=int)
     m.add_argument("--th-allreduce", type=float)
     m.add_argument("--th-reduce", type=float)

@@ -52,8 +52,14 @@ class AllreduceMaster:
         on_round_start: Optional[Callable[[int], None]] = None,
         on_finished: Optional[Callable[[], None]] = None,
         transport_info: Optional[Callable[[], Dict[str, Any]]] = None,
+        min_workers: Optional[int] = None,
     ):
         self.totalWorkers = int(totalWorkers)
+        # round 0 starts once this many workers joined (the reference waits
+        # for all, M:39); fewer starts with a partial peer map and the rest
+        # join later (T4/T5, SPEC:141-170: re-InitWorkers with the new map)
+        self.min_workers = self.totalWorkers if min_workers is None else max(1, min(int(min_workers),
+                                                                                     self.totalWorkers))
         self.thAllreduce = float(thAllreduce)
         self.thReduce = float(thReduce)
         self.thComplete = float(thComplete)
@@ -120,7 +126,7 @@ class AllreduceMaster:
         self.workers[new_id] = ref
         log.info("master: worker %d joined (%d/%d)", new_id, len(self.workers), self.totalWorkers)
         if self.round == -1:
-            if len(self.workers) >= self.totalWorkers:
+            if len(self.workers) >= self.min_workers:
                 self._init_workers(list(self.workers))
                 self.round = 0
                 self._start_allreduce()

@@ -92,7 +92,7 @@ class ThroughputSink:
 class MasterProcess:
     def __init__(self, thresholds: ThresholdConfig, data: DataConfig, workers: WorkerConfig, *,
                  host: str = "127.0.0.1", port: int = 2551, heartbeat_interval_s: float = 1.0,
-                 unreachable_after_s: float = 10.0, transport: str = "auto"):
+                 unreachable_after_s: float = 10.0, transport: str = "auto", min_workers: Optional[int] = None):
         self.node = Node(host, port, name="master")
         self.transport = transport
         self._store = None
@@ -104,7 +104,7 @@ class MasterProcess:
             self._store = TCPStore(host, 0, is_master=True, wait_for_workers=False)
         self._gpu_workers: Dict[str, bool] = {}  # worker address -> has a GPU
         self.master = AllreduceMaster.from_configs(thresholds, data, workers, on_finished=self._finished,
-                                                   transport_info=self._transport_info)
+                                                   transport_info=self._transport_info, min_workers=min_workers)
         self.unreachable_after_s = unreachable_after_s
         self.heartbeat_interval_s = heartbeat_interval_s
         self.last_seen: Dict[int, float] = {}

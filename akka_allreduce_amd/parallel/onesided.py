@@ -109,6 +109,17 @@ class OneSidedOutput(AllReduceOutput):
         return self._status
 
 
+def _member_exchange(rank: int, members: list, world: int, store: Any, key: str):
+    """Like _handle_exchange over ``members`` only: mine -> [bytes of every
+    rank], empty for ranks outside the member list."""
+
+    def exchange(mine: bytes) -> list:
+        store.set(f"{key}/{rank}", mine)
+        return [bytes(store.get(f"{key}/{i}")) if i in members else b"" for i in range(world)]
+
+    return exchange
+
+
 class OneSidedAllreduce:
     """Threshold allreduce over mapped peer windows (see module docstring)."""
 
@@ -135,6 +146,7 @@ class OneSidedAllreduce:
         cu_keep: int = 0,
         data_sink: Any = None,
         handoff: str = "lite",
+        members: Optional[list] = None,
     ):
         if dtype not in _DTYPES:
             raise ValueError("dtype must be float32 or bfloat16")
@@ -167,7 +179,17 @@ class OneSidedAllreduce:
         self.th_reduce, self.th_complete, self.max_lag = float(th_reduce), float(th_complete), int(max_lag)
         iid = OneSidedAllreduce._instances
         OneSidedAllreduce._instances += 1
-        exchange = _handle_exchange(self.rank, self.world_size, store, f"akka/onesided/{iid}")
+        # partial membership (the reference's partial peer map, W:213-216):
+        # only ``members`` exchange windows now; the others are never pushed
+        # to nor waited for until admit() maps them (re-init, W:87-89)
+        self.members = sorted(set(int(q) for q in members) | {self.rank}) if members is not None \
+            else list(range(self.world_size))
+        partial = len(self.members) < self.world_size
+        if partial and store is None:
+            raise ValueError("partial membership exchanges windows through a store (late ranks fetch them there)")
+        self._store, self._key = store, f"akka/onesided/{iid}"
+        exchange = _member_exchange(self.rank, self.members, self.world_size, store, self._key) if partial \
+            else _handle_exchange(self.rank, self.world_size, store, self._key)
         # every rank takes part in the exchange even if its own window failed
         # (an empty handle): a local failure raises on EVERY rank, none is
         # left blocked in the collective
@@ -185,14 +207,20 @@ class OneSidedAllreduce:
         handles = exchange(mine)
         if err is not None:
             raise err
-        missing = [i for i, h in enumerate(handles) if not h]
+        missing = [i for i, h in enumerate(handles) if not h and i in self.members]
         if missing:
             raise RuntimeError(f"onesided lane: ranks {missing} could not create their windows")
         self.lane.open(handles)
-        # every rank mapped every window: names may go (a killed rank leaves no shm behind)
-        exchange_done = _handle_exchange(self.rank, self.world_size, store, f"akka/onesided/{iid}/opened")
-        exchange_done(b"1")
-        self.lane.unlink()
+        if members is not None and store is not None:
+            # a membership that may grow (admit): ranks joining later open
+            # this window by name / handle, so it stays published (CPU: the
+            # shm name is removed when the lane goes)
+            _member_exchange(self.rank, self.members, self.world_size, store, f"{self._key}/opened")(b"1")
+        else:
+            # every rank mapped every window: names may go (a killed rank leaves no shm behind)
+            exchange_done = _handle_exchange(self.rank, self.world_size, store, f"{self._key}/opened")
+            exchange_done(b"1")
+            self.lane.unlink()
         self._kmax = self.geometry.kmax
         # counts tables reused with caller-owned outputs, one per output buffer
         # (a caller alternating buffers keeps each round's counts with its data)
@@ -278,6 +306,31 @@ class OneSidedAllreduce:
         if mode not in _HANDOFFS:
             raise ValueError(f"handoff must be one of {_HANDOFFS}")
         self.lane.set_fenced(mode == "fenced")
+
+    def admit(self, peer: int, timeout_s: float = 60.0) -> None:
+        """Re-init with a larger peer map (W:87-89): map ``peer``'s window
+        (published in the store when it created its lane) and push to / wait
+        for it from the next call on.  Between calls only (synchronises the
+        device).  A rank already mapped raises."""
+        import time
+
+        q = int(peer)
+        if q in self.members:
+            return
+        if self._store is None:
+            raise ValueError("admit: windows of late ranks come through the store given at construction")
+        t0 = time.monotonic()
+        while True:  # the joining rank may still be creating its window
+            try:
+                h = bytes(self._store.get(f"{self._key}/{q}"))
+                break
+            except Exception:  # noqa: BLE001 - store timeout: retry until ours expires
+                if time.monotonic() - t0 > timeout_s:
+                    raise
+        if not h:
+            raise RuntimeError(f"onesided lane: rank {q} could not create its window")
+        self.lane.add_peer(q, h)
+        self.members = sorted(self.members + [q])
 
     def note_replays(self, n: int) -> None:
         self.lane.note_replays(int(n))

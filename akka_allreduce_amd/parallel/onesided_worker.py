@@ -10,7 +10,11 @@ with the data plane on ``OneSidedAllreduce`` (csrc/transport/onesided.h):
 stores into mapped peer windows, device-side thresholds, no send ever waits.
 
   * ``InitWorkers`` (carrying the master's rendezvous store in
-    ``transport = {"kind": "onesided", ...}``) maps every worker's window;
+    ``transport = {"kind": "onesided", ...}``) maps the windows of the
+    workers in its peer map; the others are never pushed to nor waited for
+    (the reference scatters to known peers only, W:213-216).  A later
+    ``InitWorkers`` with a larger map (W:87-89) maps the newcomers' windows
+    at the next round boundary, and they take part from that round on;
   * ``StartAllreduce(r)`` raises ``maxRound`` (W:99); a round thread serves
     the worker's next rounds up to it: fetch (W:197-204), one lane call, the
     sink, ``CompleteAllreduce`` (W:270-277).  The master's start of round R
@@ -62,6 +66,7 @@ class OneSidedWorker:
         self._thread: Optional[threading.Thread] = None
         self._store = None
         self._max_lag = 0
+        self._joins: List[int] = []  # ranks of a re-init's larger peer map, mapped between rounds
 
     # ---- actor API ---------------------------------------------------------------
     @property
@@ -92,7 +97,15 @@ class OneSidedWorker:
 
     def _on_init(self, m: InitWorkers) -> None:
         if self.initialized:
-            return  # fixed membership per window set: a death is handled by mark_dead
+            # re-init: the peer map replaces the old one (W:87-89).  Ranks new
+            # to it are mapped by the round thread between two calls; a rank
+            # mapped before that departed stays dead (its window is gone)
+            new = [int(q) for q in m.workers if int(q) not in self.ar.members]
+            if new:
+                with self._cv:
+                    self._joins.extend(q for q in new if q not in self._joins)
+                    self._cv.notify_all()
+            return
         tinfo = getattr(m, "transport", None) or {}
         if tinfo.get("kind") != "onesided":
             raise RuntimeError("onesided worker: InitWorkers carries no onesided rendezvous (master --transport "
@@ -107,12 +120,13 @@ class OneSidedWorker:
         self.master = m.master
         self._max_lag = int(m.maxLag)
         self.geometry = Geometry(int(m.dataSize), int(m.workerNum), int(m.maxChunkSize))
-        # collective over the master's store: every worker gets InitWorkers
+        # collective over the master's store among the workers of the peer
+        # map (every one of them gets this InitWorkers); ranks outside it join later
         self.ar = OneSidedAllreduce(int(m.dataSize), max_chunk_size=int(m.maxChunkSize), dtype=self.dtype,
                                     th_reduce=float(m.thReduce), th_complete=float(m.thComplete),
                                     max_lag=int(m.maxLag), rank=self.id, world_size=int(m.workerNum),
                                     device=self.device, store=_PrefixStore(self._store, tinfo["key"]),
-                                    timeout_s=self.timeout_s)
+                                    timeout_s=self.timeout_s, members=sorted(int(q) for q in m.workers))
         log.info("%s: id=%d onesided lane %s", self.name, self.id, self.ar.info())
         self._thread = threading.Thread(target=self._run, name=f"{self.name}-rounds", daemon=True)
         self._thread.start()
@@ -136,12 +150,21 @@ class OneSidedWorker:
             log.error("%s: cannot select %s: %s", self.name, self.device, e)
         while True:
             with self._cv:
-                while not self._stop and self.next_round > self.max_round:
+                while not self._stop and self.next_round > self.max_round and not self._joins:
                     self._cv.wait(0.5)
                 if self._stop:
                     return
                 want = self.next_round
+                joins, self._joins = self._joins, []
             try:
+                # a round boundary: no call of this lane in flight.  Mapped at
+                # once, even with no round to serve yet: the newcomer learns
+                # where this rank is (OneSidedLane::add_peer) and catches up
+                for q in joins:
+                    self.ar.admit(q, timeout_s=self.timeout_s)
+                    log.info("%s: rank %d joined the lane (members %s)", self.name, q, self.ar.members)
+                if want > self.max_round:
+                    continue
                 inp = self.dataSource(AllReduceInputRequest(want))  # W:197-204
                 x = inp.data if isinstance(inp, AllReduceInput) else inp
                 x = torch.as_tensor(x).to(device=self.device, dtype=self.dtype).reshape(-1)

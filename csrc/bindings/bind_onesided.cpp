@@ -58,6 +58,13 @@ void bind_onesided(py::module_& m) {
         l.open(handles);
       })
       .def("unlink", &OneSidedLane::unlink)
+      .def("add_peer",
+           [](OneSidedLane& l, int32_t q, py::bytes h) {
+             std::string hs(h);
+             py::gil_scoped_release nogil;
+             l.add_peer(q, hs);
+           })
+      .def("members", &OneSidedLane::members)
       .def("round",
            [](OneSidedLane& l, uintptr_t stream, uintptr_t in, uintptr_t out, uintptr_t counts, int32_t kcols) {
              py::gil_scoped_release nogil;  // the CPU backend waits for other processes

@@ -783,7 +783,7 @@ __global__ __launch_bounds__(LB) void os_round_kernel(Args a) {
 // retire: tell every peer that this rank serves no round >= its next one
 __global__ void os_retire_kernel(Args a) {
   const int32_t q = threadIdx.x;
-  if (q >= a.L.N || q == a.me) return;
+  if (q >= a.L.N || q == a.me || a.tab->fl[q] == nullptr) return;  // (null: a rank that never joined)
   DevMem::st(a.tab->fl[q] + a.L.fin(a.me), sys_load(a.loc + a.L.state(kNext)) + 1u);
 }
 

@@ -279,52 +279,91 @@ std::string OneSidedLane::handle() const {
   return std::string(reinterpret_cast<const char*>(&b), sizeof(b));
 }
 
+// Parse and check one rank's window handle against this lane's geometry.
+static Blob parse_handle(const std::string& h, int32_t q, int32_t N, size_t es, int32_t D, int32_t P, int32_t Kmax,
+                         const Geometry& g, int64_t slot, int64_t part_len, bool gpu) {
+  AKKA_CHECK(h.size() == sizeof(Blob), "onesided lane: malformed handle");
+  Blob b;
+  std::memcpy(&b, h.data(), sizeof(b));
+  AKKA_CHECK(std::memcmp(b.magic, kMagic, sizeof(kMagic)) == 0, "onesided lane: not a onesided window handle");
+  AKKA_CHECK(b.rank == q && b.nranks == N && b.esize == int32_t(es) && b.rows == D && b.parts == P &&
+                 b.kmax == Kmax && b.S == g.S && b.C == g.C && b.slot == slot && b.part_len == part_len &&
+                 b.kind == (gpu ? 0 : 1),
+             "onesided lane: rank " + std::to_string(q) + "'s window was built for another geometry / ring");
+  return b;
+}
+
+void OneSidedLane::map_peer(int32_t q, const std::string& h) {
+  const Blob b = parse_handle(h, q, g_.N, es_, D_, P_, Kmax_, g_, slot_, part_len_, device_ >= 0);
+  if (device_ >= 0) {
+    void* f = nullptr;
+    AKKA_OS_HIP(hipIpcOpenMemHandle(&f, b.h[0], hipIpcMemLazyEnablePeerAccess));
+    opened_.push_back(f);
+    pfl_[size_t(q)] = static_cast<uint32_t*>(f);
+    for (int32_t d = 0; d < D_; ++d) {
+      void* sp = nullptr;
+      void* gp = nullptr;
+      AKKA_OS_HIP(hipIpcOpenMemHandle(&sp, b.h[1 + d], hipIpcMemLazyEnablePeerAccess));
+      opened_.push_back(sp);
+      AKKA_OS_HIP(hipIpcOpenMemHandle(&gp, b.h[1 + D_ + d], hipIpcMemLazyEnablePeerAccess));
+      opened_.push_back(gp);
+      psd_[size_t(d)][size_t(q)] = static_cast<char*>(sp);
+      pgd_[size_t(d)][size_t(q)] = static_cast<char*>(gp);
+    }
+  } else {
+    const size_t fb = size_t(round_up(int64_t(flag_bytes_), 4096));
+    const size_t rb = size_t(round_up(int64_t(row_bytes_), 4096));
+    const int fd = shm_open(b.shm, O_RDWR, 0600);
+    AKKA_CHECK(fd >= 0, std::string("onesided lane: cannot open rank ") + std::to_string(q) + "'s window " + b.shm);
+    void* m = mmap(nullptr, size_t(b.shm_bytes), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
+    close(fd);
+    AKKA_CHECK(m != MAP_FAILED, "onesided lane: mmap of a peer window failed");
+    char* base = static_cast<char*>(m);
+    peer_maps_.push_back({base, size_t(b.shm_bytes)});
+    pfl_[size_t(q)] = reinterpret_cast<uint32_t*>(base);
+    for (int32_t d = 0; d < D_; ++d) {
+      psd_[size_t(d)][size_t(q)] = base + fb + size_t(d) * rb;
+      pgd_[size_t(d)][size_t(q)] = base + fb + size_t(D_ + d) * rb;
+    }
+  }
+}
+
+void OneSidedLane::write_tables() {
+  if (device_ < 0) return;
+  Tables t;
+  std::memset(&t, 0, sizeof(t));
+  for (int32_t q = 0; q < g_.N; ++q) {
+    t.fl[q] = pfl_[size_t(q)];
+    t.bstart[q] = g_.block_start(q);
+    t.blen[q] = g_.block_len(q);
+    t.nch[q] = g_.num_chunks(q);
+    for (int32_t d = 0; d < D_; ++d) {
+      t.sd[d][q] = psd_[size_t(d)][size_t(q)];
+      t.gd[d][q] = pgd_[size_t(d)][size_t(q)];
+    }
+  }
+  AKKA_OS_HIP(hipMemcpy(tab_dev_, &t, sizeof(t), hipMemcpyHostToDevice));
+}
+
 void OneSidedLane::open(const std::vector<std::string>& handles) {
   AKKA_CHECK(!ready_, "onesided lane: windows already open");
   AKKA_CHECK(int32_t(handles.size()) == g_.N, "onesided lane: need one handle per rank");
   if (device_ >= 0) AKKA_OS_HIP(hipSetDevice(device_));
-  const size_t fb = size_t(round_up(int64_t(flag_bytes_), 4096));
-  const size_t rb = size_t(round_up(int64_t(row_bytes_), 4096));
+  absent_.assign(size_t(g_.N), 0);
   for (int32_t q = 0; q < g_.N; ++q) {
     const std::string& h = handles[size_t(q)];
-    AKKA_CHECK(h.size() == sizeof(Blob), "onesided lane: malformed handle");
-    Blob b;
-    std::memcpy(&b, h.data(), sizeof(b));
-    AKKA_CHECK(std::memcmp(b.magic, kMagic, sizeof(kMagic)) == 0, "onesided lane: not a onesided window handle");
-    AKKA_CHECK(b.rank == q && b.nranks == g_.N && b.esize == int32_t(es_) && b.rows == D_ && b.parts == P_ &&
-                   b.kmax == Kmax_ && b.S == g_.S && b.C == g_.C && b.slot == slot_ && b.part_len == part_len_ &&
-                   b.kind == (device_ >= 0 ? 0 : 1),
-               "onesided lane: rank " + std::to_string(q) + "'s window was built for another geometry / ring");
-    if (q == me_) continue;
-    if (device_ >= 0) {
-      void* f = nullptr;
-      AKKA_OS_HIP(hipIpcOpenMemHandle(&f, b.h[0], hipIpcMemLazyEnablePeerAccess));
-      opened_.push_back(f);
-      pfl_[size_t(q)] = static_cast<uint32_t*>(f);
-      for (int32_t d = 0; d < D_; ++d) {
-        void* s = nullptr;
-        void* g = nullptr;
-        AKKA_OS_HIP(hipIpcOpenMemHandle(&s, b.h[1 + d], hipIpcMemLazyEnablePeerAccess));
-        opened_.push_back(s);
-        AKKA_OS_HIP(hipIpcOpenMemHandle(&g, b.h[1 + D_ + d], hipIpcMemLazyEnablePeerAccess));
-        opened_.push_back(g);
-        psd_[size_t(d)][size_t(q)] = static_cast<char*>(s);
-        pgd_[size_t(d)][size_t(q)] = static_cast<char*>(g);
-      }
-    } else {
-      const int fd = shm_open(b.shm, O_RDWR, 0600);
-      AKKA_CHECK(fd >= 0, std::string("onesided lane: cannot open rank ") + std::to_string(q) + "'s window " + b.shm);
-      void* m = mmap(nullptr, size_t(b.shm_bytes), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0);
-      close(fd);
-      AKKA_CHECK(m != MAP_FAILED, "onesided lane: mmap of a peer window failed");
-      char* base = static_cast<char*>(m);
-      peer_maps_.push_back({base, size_t(b.shm_bytes)});
-      pfl_[size_t(q)] = reinterpret_cast<uint32_t*>(base);
-      for (int32_t d = 0; d < D_; ++d) {
-        psd_[size_t(d)][size_t(q)] = base + fb + size_t(d) * rb;
-        pgd_[size_t(d)][size_t(q)] = base + fb + size_t(D_ + d) * rb;
-      }
+    if (q == me_) {
+      (void)parse_handle(h, q, g_.N, es_, D_, P_, Kmax_, g_, slot_, part_len_, device_ >= 0);
+      continue;
     }
+    if (h.empty()) {
+      // not a member yet (partial peer map, W:213-216): never written to or
+      // waited for -- dead until add_peer() maps its window (re-init, W:87-89)
+      absent_[size_t(q)] = 1;
+      __atomic_store_n(&hw_->dead[q], 1u, __ATOMIC_RELEASE);
+      continue;
+    }
+    map_peer(q, h);
   }
   if (device_ >= 0 && p_.role_wgs <= 0 && !std::getenv("AKKA_OS_ROLE_WGS")) {
     // Ranks sharing this GPU (tests / rehearsals on a 1-GPU box): every
@@ -333,9 +372,11 @@ void OneSidedLane::open(const std::vector<std::string>& handles) {
     // Budget: 768 of the card's ~1024 resident 256-thread workgroups (103
     // VGPRs: 4 per CU) for all sharing ranks' grids together (pass F sweep,
     // profiles/r04/README.md: 512 / 768 / 1024 -> 1.26 / 1.15 / 1.44 ms at
-    // 256 MiB, 4 ranks).
+    // 256 MiB, 4 ranks).  (Members only: a rank joining later keeps the
+    // grid this one was sized for.)
     int32_t share = 0;
     for (int32_t q = 0; q < g_.N; ++q) {
+      if (handles[size_t(q)].empty()) continue;
       Blob b;
       std::memcpy(&b, handles[size_t(q)].data(), sizeof(b));
       share += std::strncmp(b.bus, my_bus_.c_str(), sizeof(b.bus)) == 0;
@@ -384,22 +425,49 @@ void OneSidedLane::open(const std::vector<std::string>& handles) {
       size_roles(std::max<int64_t>(1, unit * sr / 2), unit * sp, unit * sc);
     }
   }
-  if (device_ >= 0) {
-    Tables t;
-    std::memset(&t, 0, sizeof(t));
-    for (int32_t q = 0; q < g_.N; ++q) {
-      t.fl[q] = pfl_[size_t(q)];
-      t.bstart[q] = g_.block_start(q);
-      t.blen[q] = g_.block_len(q);
-      t.nch[q] = g_.num_chunks(q);
-      for (int32_t d = 0; d < D_; ++d) {
-        t.sd[d][q] = psd_[size_t(d)][size_t(q)];
-        t.gd[d][q] = pgd_[size_t(d)][size_t(q)];
-      }
-    }
-    AKKA_OS_HIP(hipMemcpy(tab_dev_, &t, sizeof(t), hipMemcpyHostToDevice));
-  }
+  write_tables();
   ready_ = true;
+}
+
+void OneSidedLane::add_peer(int32_t q, const std::string& handle) {
+  AKKA_CHECK(ready_, "onesided lane: open() the peer windows first");
+  AKKA_CHECK(q >= 0 && q < g_.N && q != me_, "onesided lane: bad peer");
+  AKKA_CHECK(absent_[size_t(q)], "onesided lane: rank " + std::to_string(q) +
+                                     " is already mapped (a rank's window is mapped once; a departed rank stays dead)");
+  AKKA_CHECK(!cr_.active, "onesided lane: add_peer between rounds only");
+  if (device_ >= 0) {
+    AKKA_OS_HIP(hipSetDevice(device_));
+    // a round boundary on the device too: no call of this lane still reads
+    // the pointer tables (they are rewritten below)
+    AKKA_OS_HIP(hipDeviceSynchronize());
+  }
+  map_peer(q, handle);
+  write_tables();
+  // Announce my position to the newcomer: I serve no round before my next
+  // one any more, so its waits for my copies of those rounds end at once
+  // (source_past) and its first call catches up to my window (select_round)
+  // -- without this, a newcomer serving an old round would wait for copies
+  // this rank already moved past until a force or its timeout.
+  uint32_t next = 0;
+  if (device_ >= 0) AKKA_OS_HIP(hipMemcpy(&next, loc_ + L_.state(kNext), sizeof(next), hipMemcpyDeviceToHost));
+  else next = loc_[L_.state(kNext)];
+  const uint32_t seen = next + 1u;
+  if (device_ >= 0) {
+    AKKA_OS_HIP(hipMemcpy(pfl_[size_t(q)] + L_.seen(me_), &seen, sizeof(seen), hipMemcpyHostToDevice));
+  } else {
+    HostMem::st(pfl_[size_t(q)] + L_.seen(me_), seen);
+  }
+  absent_[size_t(q)] = 0;
+  // from the next call on: pushed to and waited for (a fresh window: no
+  // word of this rank's window was ever written by it)
+  __atomic_store_n(&hw_->dead[q], 0u, __ATOMIC_RELEASE);
+}
+
+std::vector<int32_t> OneSidedLane::members() const {
+  std::vector<int32_t> v;
+  for (int32_t q = 0; q < g_.N; ++q)
+    if (q == me_ || (size_t(q) < absent_.size() && !absent_[size_t(q)])) v.push_back(q);
+  return v;
 }
 
 void OneSidedLane::unlink() {
@@ -539,6 +607,10 @@ int64_t OneSidedLane::begin(const void* in, void* out, int32_t* counts, int32_t 
 void OneSidedLane::push(int32_t phase, int32_t dst, int32_t k, int32_t j, uint32_t r, uint32_t cnt,
                         const char* src) {
   Msg m{phase, dst, k, j, r, cnt, {}};
+  if (__atomic_load_n(&hw_->dead[dst], __ATOMIC_ACQUIRE) != 0u) {  // as the kernels' push role: never queued
+    stats_host_[kDeadSkips] += 1;
+    return;
+  }
   if (!hold_) {
     exec(m, src);
     return;
@@ -834,7 +906,7 @@ void OneSidedLane::retire(uintptr_t stream) {
   } else {
     flush();
     for (int32_t q = 0; q < g_.N; ++q)
-      if (q != me_) HostMem::st(pfl_[size_t(q)] + L_.fin(me_), loc_[L_.state(kNext)] + 1u);
+      if (q != me_ && pfl_[size_t(q)]) HostMem::st(pfl_[size_t(q)] + L_.fin(me_), loc_[L_.state(kNext)] + 1u);
   }
 }
 

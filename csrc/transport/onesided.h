@@ -69,7 +69,17 @@ class OneSidedLane {
   OneSidedLane& operator=(const OneSidedLane&) = delete;
 
   std::string handle() const;
+  // An empty handle (q != me) is a rank not in the peer map yet (partial
+  // membership, W:213-216): it is never pushed to nor waited for (dead)
+  // until add_peer() maps its window.
   void open(const std::vector<std::string>& handles);
+  // Re-init with a larger peer map (W:87-89): map a rank that was absent at
+  // open() and treat it as live from the next call on.  Between rounds only
+  // (GPU: synchronises the device).  A rank mapped once stays mapped: a
+  // departed rank is marked dead (set_dead), not remapped.
+  void add_peer(int32_t q, const std::string& handle);
+  // Ranks whose windows are mapped (me included).
+  std::vector<int32_t> members() const;
   // CPU: remove this rank's shared-memory name (every peer mapped it already).
   void unlink();
   bool ready() const { return ready_; }
@@ -175,6 +185,8 @@ class OneSidedLane {
   bool try_complete(bool timed_out);
   void flush();
   void dump(const char* role, int32_t k) const;
+  void map_peer(int32_t q, const std::string& handle);
+  void write_tables();  // GPU: the device's pointer tables from pfl_ / psd_ / pgd_
 
   int32_t device_;
   Geometry g_;
@@ -199,6 +211,7 @@ class OneSidedLane {
   size_t flag_bytes_ = 0, row_bytes_ = 0, win_bytes_ = 0;
   std::string mem_kind_;
   bool ready_ = false;
+  std::vector<uint8_t> absent_;  // [N]: not mapped yet (partial membership)
   int64_t calls_ = 0;
   uint64_t timeout_ticks_ = 0;
 

@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--out-dir", required=True)
     ap.add_argument("--timeout-s", type=float, default=240.0)
     ap.add_argument("--die-after", type=int, default=-1, help="exit abruptly once this round reached the sink")
+    ap.add_argument("--compute-ms", type=float, default=0.0, help="every round's data source sleeps this long")
+    ap.add_argument("--progress-file", default="", help="the sink writes the last round it got here")
     a = ap.parse_args()
     import faulthandler
     import logging
@@ -38,8 +40,8 @@ def main():
 
     def source(req):
         src_t.append(time.perf_counter())
-        if a.delay_ms:
-            time.sleep(a.delay_ms / 1e3)
+        if a.delay_ms or a.compute_ms:
+            time.sleep((a.delay_ms + a.compute_ms) / 1e3)
         wid = holder["w"].worker.id
         return torch.full((a.size,), float(1 << wid))
 
@@ -50,6 +52,10 @@ def main():
         kept.append((int(o.iteration), o.data.float().cpu(),
                      o.counts_per_chunk.cpu() if o.counts_per_chunk is not None else None, o.geometry))
         recs.append({"round": int(o.iteration), "t": time.perf_counter(), "t_src": src_t[-1] if src_t else 0.0})
+        if a.progress_file:
+            with open(a.progress_file + ".tmp", "w") as f:
+                f.write(str(int(o.iteration)))
+            os.replace(a.progress_file + ".tmp", a.progress_file)
         if 0 <= a.die_after <= int(o.iteration):
             os._exit(0)  # abrupt: no Shutdown, no retire -- the master's failure detector must notice
 
@@ -68,8 +74,10 @@ def main():
             n = sum(g.num_chunks(p) for p in range(g.workerNum))
             rec["mean_count"] = float(sum(int(cpc[p, k]) for p in range(g.workerNum)
                                           for k in range(g.num_chunks(p)))) / max(1, n)
+            rec["block_counts"] = [int(cpc[p, 0]) if g.num_chunks(p) else 0 for p in range(g.workerNum)]
         else:
             rec["mean_count"] = 0.0
+            rec["block_counts"] = None  # a round force-completed by catch-up: zeros, count 0 (W:100-106)
         rec["bad"] = bad
 
     dev = a.device

@@ -29,7 +29,9 @@ def _port() -> int:
 
 
 def run_job(device="cpu", delay_ms=0.0, rounds=64, size=1 << 14, chunk=1 << 10, workers=4, timeout=240,
-            log_dir=None, die_after=-1, env=None):
+            log_dir=None, die_after=-1, env=None, th=0.75, min_workers=None, late_after=-1, compute_ms=0.0):
+    """``late_after`` >= 0: the last worker starts only once worker 0's sink
+    got that round (the master runs with ``--min-workers workers - 1``)."""
     port = _port()
     base = [sys.executable, "-m", "akka_allreduce_amd", "--log-level", "WARNING"]
     with tempfile.TemporaryDirectory() as out:
@@ -40,8 +42,9 @@ def run_job(device="cpu", delay_ms=0.0, rounds=64, size=1 << 14, chunk=1 << 10, 
         mlog = open(os.path.join(logs, f"master_d{int(delay_ms)}.log"), "w")
         master = subprocess.Popen(base + ["master", "--port", str(port), "--workers", str(workers), "--data-size",
                                           str(size), "--max-chunk-size", str(chunk), "--max-round", str(rounds - 1),
-                                          "--max-lag", "1", "--th-allreduce", "0.75", "--th-reduce", "0.75",
-                                          "--th-complete", "0.75", "--transport", "onesided"],
+                                          "--max-lag", "1", "--th-allreduce", str(th), "--th-reduce", str(th),
+                                          "--th-complete", str(th), "--transport", "onesided"]
+                                  + (["--min-workers", str(min_workers)] if min_workers else []),
                                   cwd=ROOT, stdout=subprocess.DEVNULL, stderr=mlog, env=env)
         t_end = time.time() + 60
         while time.time() < t_end:
@@ -51,10 +54,24 @@ def run_job(device="cpu", delay_ms=0.0, rounds=64, size=1 << 14, chunk=1 << 10, 
             except OSError:
                 time.sleep(0.1)
         procs, wlogs = [], []
+        progress = os.path.join(out, "progress0")
         for i in range(workers):
             d = delay_ms if i == workers - 1 else 0.0
             wlogs.append(os.path.join(logs, f"worker{i}_d{int(delay_ms)}.log"))
             extra = ["--die-after", str(die_after)] if die_after >= 0 and i == workers - 1 else []
+            if compute_ms:
+                extra += ["--compute-ms", str(compute_ms)]
+            if i == 0:
+                extra += ["--progress-file", progress]
+            if late_after >= 0 and i == workers - 1:
+                t_end = time.time() + timeout / 2
+                while time.time() < t_end:  # the others are past round `late_after`
+                    try:
+                        if int(open(progress).read() or -1) >= late_after:
+                            break
+                    except (OSError, ValueError):
+                        pass
+                    time.sleep(0.05)
             procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "cluster_onesided_ranks.py"),
                                            "--master", f"127.0.0.1:{port}", "--size", str(size), "--device", device,
                                            "--delay-ms", str(d), "--out-dir", out, "--timeout-s", str(timeout - 30),
@@ -92,7 +109,7 @@ def fast_median_ms(rows):
     return max(meds)
 
 
-def check_job(device, rounds=64, slack_ms=2.0, **kw):
+def check_job(device, rounds=64, slack_ms=1.0, **kw):
     import os as _os
 
     kw.setdefault("log_dir", _os.environ.get("AKKA_TEST_LOGS") or None)
@@ -140,3 +157,48 @@ def test_cluster_onesided_worker_dies():
         # rounds after the death: 3 contributors at most per chunk
         late = [x for x in r["records"] if x["round"] >= 20]
         assert late and max(x["mean_count"] for x in late) <= 3.0, late[:3]
+
+
+def check_late_join(device, rounds=300, join_after=5, compute_ms=25.0, **kw):
+    """Exact thresholds, maxLag 1; the master starts with 3 of 4 workers
+    (--min-workers 3, a partial peer map) and the 4th joins after round
+    ``join_after`` (re-InitWorkers with the full map, W:87-89).  Before the
+    join: blocks 0-2 reduce over the 3 members (count 3), block 3 is 0 with
+    count 0 (no rank owns it yet).  After it: every block of every round the
+    joiner serves has all 4 contributors.  Every chunk's value matches its
+    count on every worker (2^id inputs)."""
+    rows, errs = run_job(device, 0.0, rounds, th=1.0, min_workers=3, late_after=join_after, compute_ms=compute_ms,
+                         **kw)
+    assert len(rows) == 4, errs
+    for r in rows:
+        assert r["finished"] and not r["errors"], (r["id"], r["errors"], errs)
+        assert all(x["bad"] == 0 for x in r["records"]), r["id"]
+        rs = [x["round"] for x in r["records"]]
+        assert rs == sorted(rs) and len(set(rs)) == len(rs) and rs[-1] == rounds - 1, rs[-5:]
+    early = [r for r in rows if r["id"] != 3]
+    late = [r for r in rows if r["id"] == 3][0]
+    # the joiner force-completes the rounds it joined too late for (the
+    # reference's cold catch-up, SPEC:632-656: zeros, count 0): every member
+    # announced its position when it mapped the newcomer's window
+    # (OneSidedLane::add_peer), so its first call catches up at once; from
+    # then on every block of every round
+    first_full = next((x["round"] for x in late["records"] if x["block_counts"] == [4, 4, 4, 4]), rounds)
+    assert join_after < first_full < rounds - 20, first_full
+    assert late["forced_rounds"] >= first_full - 3, (late["forced_rounds"], first_full)
+    # no member waited for the joiner: the job kept its pace through the join
+    for r in early:
+        t = [x["t"] for x in r["records"]]
+        assert max(b - a for a, b in zip(t, t[1:])) < 2.0, r["id"]
+    for r in early:
+        recs = {x["round"]: x for x in r["records"]}
+        for rr in range(join_after + 1):  # served before the 4th worker existed
+            assert recs[rr]["block_counts"] == [3, 3, 3, 0], (r["id"], rr, recs[rr])
+        tail = [x for x in r["records"] if x["round"] >= rounds - 20]
+        assert tail and all(x["block_counts"] == [4, 4, 4, 4] for x in tail), (r["id"], tail[:3])
+    ltail = [x for x in late["records"] if x["round"] >= rounds - 20]
+    assert ltail and all(x["block_counts"] == [4, 4, 4, 4] for x in ltail), ltail[:3]
+    return rows
+
+
+def test_cluster_onesided_late_join_cpu():
+    check_late_join("cpu")

@@ -7,11 +7,19 @@ of the straggler-free job, sinks see consistent contributor sets, the
 straggler catches up by skipping rounds."""
 import pytest
 
-from test_cluster_onesided import check_job
+from test_cluster_onesided import check_job, check_late_join
 
 pytestmark = pytest.mark.gpu
 
 
 def test_cluster_onesided_master_pacing_gpu():
-    b, s = check_job("cuda", slack_ms=1.0, size=1 << 20, chunk=1 << 16)
+    b, s = check_job("cuda", slack_ms=0.2, size=1 << 20, chunk=1 << 16)
     print(f"fast workers' median ms per round: {b:.3f} without, {s:.3f} with the straggler")
+
+
+def test_cluster_onesided_late_join_gpu():
+    """The 4th worker joins after round 5 (master --min-workers 3): the
+    members map its window between rounds, it catches up, and from then on
+    every block of every round has all 4 contributors (exact thresholds),
+    on the card's gfx950 kernels."""
+    check_late_join("cuda", size=1 << 20, chunk=1 << 16)

@@ -42,7 +42,7 @@ from model_worker import Geometry
 class SpecHarness:
     """Rank ``me`` is the worker under test; the test plays every other rank."""
 
-    def __init__(self, N, S, C, th_reduce, th_complete, max_lag, me=0, rows=0):
+    def __init__(self, N, S, C, th_reduce, th_complete, max_lag, me=0, rows=0, members=None):
         nat = load()
         self.N, self.S, self.C, self.me = N, S, C, me
         self.g = Geometry(S, N, C)
@@ -52,10 +52,17 @@ class SpecHarness:
                                        max_lag=max_lag, rows=rows, part_bytes=1 << 40, timeout_ms=3_600_000)
                       for r in range(N)]
         hs = [ln.handle() for ln in self.lanes]
-        for ln in self.lanes:
-            ln.open(hs)
-        for ln in self.lanes:
-            ln.unlink()
+        self.handles = hs
+        for r, ln in enumerate(self.lanes):
+            # the worker under test may start with a partial peer map (T4):
+            # absent ranks get no window mapping (an empty handle) until admit()
+            if r == me and members is not None:
+                ln.open([h if q in members or q == me else b"" for q, h in enumerate(hs)])
+            else:
+                ln.open(hs)
+        if members is None:
+            for ln in self.lanes:
+                ln.unlink()
         self.w = self.lanes[me]
         self.w.set_hold(True)
         self.starts: list = []   # queued calls (input data), served in order
@@ -107,6 +114,11 @@ class SpecHarness:
         s = [m for m in self.sent if phase is None or m[0] == phase]
         self.sent = [m for m in self.sent if not (phase is None or m[0] == phase)]
         return s
+
+    def admit(self, q):
+        """Re-InitWorkers with a larger peer map (W:87-89): the worker maps
+        rank q's window between rounds."""
+        self.w.add_peer(q, self.handles[q])
 
     # ---- the peers ------------------------------------------------------------------
     def scatter(self, src, k, r, vals):
@@ -447,3 +459,45 @@ def test_random_orders_match_reference_rules(seed):
             assert data[g.chunk_offset(0, k)] == v
         for s, k, v in got_reduced:
             assert data[g.chunk_offset(s, k)] == v
+
+
+def test_t4_t5_partial_membership_then_reinit():
+    """SPEC:141-170 (N=4, S=8, C=2, thresholds 1, maxLag 5, worker 0).
+    T4: with the peer map {0} the worker scatters only to itself -- no push
+    to an absent rank (it is not mapped at all: dead until it joins).  T5: a
+    re-InitWorkers with the full map (the windows of ranks 1-3 mapped between
+    rounds) and StartAllreduce(1): the worker scatters round 1 to every
+    peer, chunk [2i+1, 2i+2] to rank i, rotated from itself.
+    By design (docs/DESIGN.md): round 0 cannot reach thReduce = 1 without
+    the absent ranks and nothing more can arrive, so it completes at once
+    (reason "unreachable") with the worker's own block (count 1) and zeros
+    with count 0 elsewhere, where the reference's round would wait forever."""
+    h = SpecHarness(4, 8, 2, 1.0, 1.0, 5, members=[0])
+    assert h.w.members() == [0]
+    h.start(basic(8, 0))
+    assert h.take_sent("scatter") == []            # only the self-scatter, delivered in place
+    # one chunk per absent peer in each phase (its scatter, then the forced
+    # reduce's broadcast), never pushed
+    assert h.stats()["dead_skips"] == 6
+    assert reduces(h, 0) == []
+    assert len(h.outputs) == 1
+    rnd, data, cnt, reason = h.outputs[0]
+    assert rnd == 0 and reason == "unreachable"
+    assert data[:2] == [0.0, 1.0] and cnt[:2] == [1, 1]
+    assert data[2:] == [0.0] * 6 and cnt[2:] == [0] * 6
+    for q in (1, 2, 3):
+        h.admit(q)
+    assert h.w.members() == [0, 1, 2, 3]
+    h.start(basic(8, 1))
+    sc = h.take_sent("scatter")
+    assert [(m[1], m[2], m[3], m[5]) for m in sc] == [(i, 0, 1, [2.0 * i + 1, 2.0 * i + 2]) for i in (1, 2, 3)]
+    # and the round now waits for the joined ranks' copies (thReduce = 1)
+    assert len(h.outputs) == 1
+    for src in (1, 2, 3):
+        h.scatter(src, 0, 1, [1.0, 2.0])
+    red = reduces(h, 1)
+    assert [(m[0], m[1], m[3]) for m in red] == [(1, 0, 4), (2, 0, 4), (3, 0, 4)]
+    assert red[0][4] == [4.0, 8.0]
+    # re-admitting a mapped rank is refused (a departed rank stays dead)
+    with pytest.raises(Exception):
+        h.admit(1)
