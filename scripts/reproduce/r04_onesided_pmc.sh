@@ -13,13 +13,13 @@ timeout -k 10 200 python -m torch.distributed.run --nnodes=1 --nproc-per-node=4 
   --master-port 29659 --no-python rocprofv3 --kernel-trace --stats --output-format csv -d $O/trace -o run_%pid% \
   -- python bench/onesided_round.py --sizes-mb 64,256 --lanes onesided,ipc --steps 8 --warmup 2 --out-dir $O/ot \
   > $O/trace.log 2>&1 || { echo "trace rc=$?"; tail -20 $O/trace.log; exit 1; }
-python scripts/r04/ktrace.py $O/trace 8 | tee $O/trace_summary.txt | head -40
-python scripts/r04/summarize_round.py $O/ot 4
+python scripts/ktrace.py $O/trace 8 | tee $O/trace_summary.txt | head -40
+python scripts/summarize_round.py $O/ot 4
 i=0
 for C in FETCH_SIZE WRITE_SIZE; do
   i=$((i+1)); mkdir -p $O/p$i $O/o$i
   PMC=$C PMC_DIR=$O/p$i timeout -k 10 150 python -m torch.distributed.run --nnodes=1 --nproc-per-node=4 \
-    --master-addr 127.0.0.1 --master-port $((29660+i)) --no-python bash scripts/r04/pmc_rank0.sh \
+    --master-addr 127.0.0.1 --master-port $((29660+i)) --no-python bash scripts/pmc_rank0.sh \
     bench/onesided_round.py --sizes-mb 64,256 --lanes onesided,ipc --steps 3 --warmup 1 --out-dir $O/o$i \
     > $O/p$i.log 2>&1 || { echo "pmc $C rc=$?"; grep -v "^    @" $O/p$i.log | tail -20; exit 1; }
 done
