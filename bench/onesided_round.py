@@ -105,14 +105,18 @@ def main() -> None:
                     dist.barrier()
                     cap.close()
                 else:
+                    # the engine path: async rounds (comm stream, event
+                    # hand-offs) or, "ipc_sync", synchronous calls (the round
+                    # runs on the caller's stream)
+                    sync_call = lane == "ipc_sync"
                     ar = ThresholdAllreduce(S, max_chunk_size=min(C, S), device=dev, data_plane="ipc")
                     ar.use_lane(a.ipc_lane)
-                    case["lane"] = a.ipc_lane
+                    case["lane"] = a.ipc_lane + ("_sync" if sync_call else "")
                     y = torch.full((S,), float(rank + 1), device=dev)
                     o = ar(y)
                     torch.cuda.synchronize()
                     case["exact"] = bool((o.data == world * (world + 1) / 2).all()) and bool((o.count == world).all())
-                    case["ms"] = _time(lambda: ar(x, out=out, async_op=True), a.warmup, a.steps)
+                    case["ms"] = _time(lambda: ar(x, out=out, async_op=not sync_call), a.warmup, a.steps)
                     case["error"] = ar.ipc_error()
                 case["algbw_GBps"] = round(S * 4 / (case["ms"] * 1e-3) / 1e9, 2)
             except Exception as e:  # noqa: BLE001 - recorded, the next case still runs

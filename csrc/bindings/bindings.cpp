@@ -585,6 +585,9 @@ class WorkerCore final : public EngineHost {
     // host devices: a modelled caller stream (stream race checking) counts too
     dp_->bind_input(round, reinterpret_cast<const void*>(it->second.in), reinterpret_cast<StreamH>(it->second.stream),
                     !dev_->is_host() || (dev_->models_streams() && it->second.stream != 0));
+    // a synchronous call: the caller's stream waits for the round anyway, so
+    // a lane that needs no stream of its own may run the round right there
+    if (it->second.stream_wait && !dev_->is_host()) dp_->set_caller_waits(round);
   }
   void alloc_output(int32_t round) override {
     auto it = pre_.find(round);

@@ -209,6 +209,8 @@ DataPlane::Binding& DataPlane::binding_mut(int32_t round) {
 void DataPlane::bind_input(int32_t round, const void* input, StreamH ready_stream, bool has_stream) {
   Binding& b = bind_[round];
   b.input = input;
+  b.ready = ready_stream;
+  b.has_ready = has_stream && (!dev_->is_host() || dev_->models_streams());
   b.input_waited_compute = b.input_waited_comm = false;
   if (staging_on_) {
     // Stage the input on the compute stream; afterwards nothing reads the
@@ -251,6 +253,24 @@ StreamH DataPlane::exec_stream(int32_t round) const {
 void DataPlane::set_exec_comm(int32_t round) {
   Binding& b = binding_mut(round);
   if (!b.exec_on_producer) b.exec_on_comm = true;
+}
+
+void DataPlane::set_counts_by_lane(int32_t round) { binding_mut(round).counts_by_lane = true; }
+
+void DataPlane::set_caller_waits(int32_t round) { binding_mut(round).caller_waits = true; }
+
+bool DataPlane::caller_waits(int32_t round) const {
+  auto it = bind_.find(round);
+  return it != bind_.end() && it->second.caller_waits && it->second.has_ready && !staging_on_;
+}
+
+StreamH DataPlane::run_on_caller(int32_t round) {
+  Binding& b = binding_mut(round);
+  AKKA_CHECK(b.caller_waits && b.has_ready, "run_on_caller: the round has no waiting caller stream");
+  b.exec = b.ready;
+  b.exec_on_producer = true;
+  b.exec_on_comm = false;
+  return b.exec;
 }
 
 bool DataPlane::exec_on_comm(int32_t round) const {
@@ -296,6 +316,11 @@ bool DataPlane::has_input(int32_t round) const {
   auto it = bind_.find(round);
   return it != bind_.end() && it->second.input != nullptr;
 }
+bool DataPlane::has_counts(int32_t round) const {
+  auto it = bind_.find(round);
+  return it != bind_.end() && it->second.counts != nullptr;
+}
+
 bool DataPlane::has_output(int32_t round) const {
   auto it = bind_.find(round);
   return it != bind_.end() && it->second.output != nullptr;
@@ -435,7 +460,7 @@ void DataPlane::set_count(int32_t round, int32_t block, int32_t k, int32_t count
 void DataPlane::upload_counts(int32_t round, const std::vector<int32_t>& blocks, StreamH s) {
   Row& r = row_for(round);
   const Binding& b = binding(round);
-  if (!b.counts) return;
+  if (!b.counts || b.counts_by_lane) return;
   // the counts memory is the caller's: write it only after the point where
   // the caller's stream handed it over (an exact round's compute stream has
   // not waited for anything of the caller's yet)
@@ -542,7 +567,7 @@ void DataPlane::finalize(int32_t round, const std::vector<uint8_t>& landed) {
   }
   // a round of a lane that failed (a wait timed out / the lane was aborted)
   // never comes back as exact: its counts read 0 everywhere
-  if (poison_flag_ && b.counts && !b.counts_poisoned)
+  if (poison_flag_ && b.counts && !b.counts_poisoned && !b.counts_by_lane)
     dev_->poison_counts_if(cs, poison_flag_, b.counts, size_t(g_.N) * kmax_);
   if (b.exec_on_producer) {
     dev_->flush(cs);  // the round's launch must not wait for the next round to merge into

@@ -57,6 +57,7 @@ class DataPlane {
                    bool has_stream = false);
   bool has_input(int32_t round) const;
   bool has_output(int32_t round) const;
+  bool has_counts(int32_t round) const;
   void unbind(int32_t round);
 
   // --- views ---------------------------------------------------------------
@@ -93,6 +94,7 @@ class DataPlane {
   void read_payload(const Payload& p, void* host_dst) const;
 
   // Stream hooks for the scheduled link.
+  EventH pooled_event_public() { return pooled_event(); }
   EventH record_compute();
   EventH record_comm();
   void compute_wait(EventH e) { dev_->wait(dev_->compute_stream(), e); }
@@ -106,6 +108,16 @@ class DataPlane {
   // finalize run on the comm stream too, so the round needs no comm -> compute
   // -> comm event hop before its done point (profiles/r05/engine_path/).
   void set_exec_comm(int32_t round);
+  // The lane's own kernels write this round's counts (and apply the poison
+  // flag themselves): upload_counts / finalize leave them alone.
+  void set_counts_by_lane(int32_t round);
+  // The caller's stream will wait for this round (a synchronous call).
+  void set_caller_waits(int32_t round);
+  bool caller_waits(int32_t round) const;
+  // Run the round on the stream that produced its input (the caller's): it
+  // is then in that stream's order with no event hop either way, like a
+  // purely local round.  Needs caller_waits() and a producer stream.
+  StreamH run_on_caller(int32_t round);
   bool exec_on_comm(int32_t round) const;
   // Make `s` wait (once per round) for the stream that produced the input and
   // for the point where the output/counts memory was handed over: every
@@ -159,6 +171,10 @@ class DataPlane {
     bool exec_on_producer = false;
     bool exec_on_comm = false;     // set_exec_comm: counts + finalize on the comm stream
     bool counts_poisoned = false;  // the counts fill already applied the poison flag
+    bool counts_by_lane = false;   // set_counts_by_lane
+    bool caller_waits = false;     // set_caller_waits
+    StreamH ready = nullptr;       // the producer stream given at bind_input (has_ready)
+    bool has_ready = false;
     EventH done = nullptr;
     // Producer-stream rounds record `done` only when someone asks for it: the
     // round is already in that stream's order, and a marker between two

@@ -376,7 +376,8 @@ void Engine::finalize_round(int32_t r) {
   std::vector<int32_t> all(static_cast<size_t>(N_), 0);
   for (int32_t j = 0; j < N_; ++j) all[size_t(j)] = j;
   // (bulk rounds whose writes all end on the comm stream finalize there)
-  dp_->upload_counts(r, all, dp_->exec_on_comm(r) ? dp_->device()->comm_stream() : dp_->device()->compute_stream());
+  dp_->upload_counts(r, all, dp_->exec_on_comm(r) || dp_->exec_on_producer(r) ? dp_->exec_stream(r)
+                                                                                  : dp_->device()->compute_stream());
   dp_->finalize(r, rw.rd_landed);
   host_->deliver(r);
 }

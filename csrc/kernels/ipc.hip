@@ -351,10 +351,31 @@ __global__ __launch_bounds__(LB) void ipc_reduce_kernel(IpcArgs a) {
   for (int32_t w = blockIdx.x; w < items; w += gridDim.x) reduce_item<T, NS>(a, w / kReduceSplit, w % kReduceSplit);
 }
 
+// Every workgroup of the round's LAST kernel, at its end: the last one out
+// writes the round's counts (N, or 0 after a failed wait of this round --
+// every wait of the round ended before its workgroup took a ticket) and
+// resets the ticket for the next round (same stream: nothing overlaps).
+__device__ void finish_counts(const IpcArgs& a) {
+  if (!a.counts_out) return;
+  __shared__ int32_t last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const uint32_t prev = __hip_atomic_fetch_add(a.fin_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    last = prev + 1u == gridDim.x ? 1 : 0;
+  }
+  __syncthreads();
+  if (!last) return;
+  const int32_t v = sys_load(a.err) != 0 ? 0 : a.counts_value;
+  for (int64_t i = threadIdx.x; i < a.counts_n; i += blockDim.x) a.counts_out[i] = v;
+  if (threadIdx.x == 0) sys_store(a.fin_ctr, 0u);
+}
+
 template <int ES>
 __global__ __launch_bounds__(kMaxThreads) void ipc_phase2_kernel(IpcArgs a) {
   const int32_t items = a.nportions * (a.N - 1);
   for (int32_t w = blockIdx.x; w < items; w += gridDim.x) phase2_item<ES>(a, w / (a.N - 1), item_peer(a, w));
+  finish_counts(a);
 }
 
 // ---- one fused launch -----------------------------------------------------
@@ -380,6 +401,7 @@ __global__ __launch_bounds__(kMaxThreads) void ipc_fused_kernel(IpcArgs a, int32
     const int32_t items = a.nportions * (a.N - 1);
     for (int32_t w = b - gp - gr; w < items; w += gq) phase2_item<ES>(a, w / (a.N - 1), item_peer(a, w));
   }
+  finish_counts(a);
 }
 
 template <typename T, int NS>

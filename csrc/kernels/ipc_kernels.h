@@ -64,6 +64,15 @@ struct IpcArgs {
   // whose counts are poisoned behind the round instead)
   int32_t* fail_counts = nullptr;
   int64_t fail_n = 0;
+  // engine-path rounds: the round's counts table [counts_n], written by the
+  // last workgroup of the round's last kernel -- counts_value everywhere, or
+  // 0 when a wait of this round failed (no counts fill launch behind the
+  // round).  fin_ctr: this lane's finisher ticket (uncached, reset by the
+  // finisher)
+  int32_t* counts_out = nullptr;
+  int64_t counts_n = 0;
+  int32_t counts_value = 0;
+  uint32_t* fin_ctr = nullptr;
 };
 
 // Flag words of one rank's flag area (uint32 index).

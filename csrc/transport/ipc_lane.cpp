@@ -147,6 +147,7 @@ IpcLane::~IpcLane() {
   if (flags_) hipFree(flags_);
   if (err_host_) hipHostFree(err_host_);
   if (round_dev_) hipFree(round_dev_);
+  if (fin_ctr_) hipFree(fin_ctr_);
   // win_: freed by its last owner (IpcWindows::~IpcWindows)
 }
 
@@ -213,7 +214,8 @@ void IpcLane::open(const std::vector<std::string>& handles) {
   ready_ = true;
 }
 
-void IpcLane::round(StreamH s, const void* in, void* out, int32_t* fail_counts, int64_t fail_n) {
+void IpcLane::round(StreamH s, const void* in, void* out, int32_t* fail_counts, int64_t fail_n, int32_t* counts_out,
+                    int64_t counts_n, int32_t counts_value) {
   AKKA_CHECK(ready_, "ipc lane: open() the peer windows first");
   IpcArgs a;
   std::memset(&a, 0, sizeof(a));
@@ -245,6 +247,19 @@ void IpcLane::round(StreamH s, const void* in, void* out, int32_t* fail_counts, 
   a.err = err_dev_;
   a.fail_counts = fail_counts;
   a.fail_n = fail_counts ? fail_n : 0;
+  if (counts_out && counts_n > 0) {
+    if (!fin_ctr_) {
+      if (hipExtMallocWithFlags(reinterpret_cast<void**>(&fin_ctr_), 64, hipDeviceMallocUncached) != hipSuccess) {
+        (void)hipGetLastError();
+        AKKA_IPC_HIP(hipMalloc(reinterpret_cast<void**>(&fin_ctr_), 64));
+      }
+      AKKA_IPC_HIP(hipMemset(fin_ctr_, 0, 64));
+    }
+    a.counts_out = counts_out;
+    a.counts_n = counts_n;
+    a.counts_value = counts_value;
+    a.fin_ctr = fin_ctr_;
+  }
   launch_ipc_round(static_cast<hipStream_t>(s), a, dt_);
   AKKA_IPC_HIP(hipGetLastError());
   ++stats_.rounds;

@@ -113,7 +113,8 @@ class IpcLane {
   // `fail_counts` (optional, [fail_n] int32): zeroed by the kernel that
   // finds a wait failed -- the fixed counts table of direct rounds then reads
   // 0 for this and every later round (the lane is dead; calls raise).
-  void round(StreamH s, const void* in, void* out, int32_t* fail_counts = nullptr, int64_t fail_n = 0);
+  void round(StreamH s, const void* in, void* out, int32_t* fail_counts = nullptr, int64_t fail_n = 0,
+             int32_t* counts_out = nullptr, int64_t counts_n = 0, int32_t counts_value = 0);
   // Device-resident round ids (graph capture): on, the round id lives in a
   // device word that a bump launch in front of every round advances -- a
   // captured round replays with a fresh id.  Switching copies the id across
@@ -156,6 +157,7 @@ class IpcLane {
   std::vector<void*> opened_flags_;
   uint32_t round_ = 0;
   uint32_t* round_dev_ = nullptr;  // uncached device word (device rounds)
+  uint32_t* fin_ctr_ = nullptr;    // uncached: the round's counts finisher ticket (IpcArgs::fin_ctr)
   bool round_dev_on_ = false;
   int32_t max_wgs_ = 1024, sharers_ = 1;
   int32_t threads_ = 256;  // workgroup size of the round kernels (AKKA_IPC_THREADS)

@@ -228,8 +228,19 @@ bool StreamLink::bulk_round(int32_t r) {
 }
 
 void StreamLink::set_ipc(std::unique_ptr<IpcLane> ipc) {
-  if (ipc_ && dp_) dp_->device()->sync_stream(dp_->device()->comm_stream());
+  if (ipc_ && dp_) {
+    dp_->device()->sync_stream(dp_->device()->comm_stream());
+    if (ipc_last_stream_set_ && ipc_last_stream_ != dp_->device()->comm_stream()) {
+      // the last round ran on a caller's stream: wait for it through an event
+      // recorded there now (the stream handle is the caller's, still alive
+      // while its rounds are in flight)
+      EventH e = dp_->pooled_event_public();
+      dp_->device()->record(e, ipc_last_stream_);
+      dp_->device()->sync_event(e);
+    }
+  }
   ipc_ = std::move(ipc);
+  ipc_last_stream_set_ = false;
 }
 
 void StreamLink::ipc_round(int32_t r) {
@@ -241,11 +252,33 @@ void StreamLink::ipc_round(int32_t r) {
   Device* dev = dp_->device();
   engine_->ensure_output(r);
   StreamH comm = dev->comm_stream();
+  // A synchronous call runs its round on the caller's own stream: the ipc
+  // kernels need no stream of the engine's, and the caller waits anyway --
+  // no input event, no done event (the direct rounds' cost, through the
+  // engine's bookkeeping).  Async calls keep the comm stream (overlap).
+  StreamH s = comm;
+  if (dp_->caller_waits(r)) s = dp_->run_on_caller(r);
+  // Rounds of the lane run one at a time: a round on another stream than
+  // the previous one's orders behind it first (windows are reused)
+  if (ipc_last_stream_set_ && ipc_last_stream_ != s) {
+    EventH e = dp_->pooled_event_public();
+    dev->record(e, ipc_last_stream_);
+    dev->wait(s, e);
+  }
+  ipc_last_stream_ = s;
+  ipc_last_stream_set_ = true;
   // (no ring row: the ipc kernels move the bytes through the lane's own
   // windows, so the round does not wait for the compute stream's readers)
-  dp_->wait_input(r, comm);
-  dp_->mark_comm_used(r);
-  ipc_->round(comm, dp_->input_chunk(r, 0, 0).ptr, dp_->output_at(r, 0, 0));
+  if (s == comm) {
+    dp_->wait_input(r, comm);
+    dp_->mark_comm_used(r);
+  }
+  // the round's counts (N everywhere, 0 if a wait failed) are written by the
+  // round's last kernel: no fill launch behind it (profiles/r05/engine_path/)
+  int32_t* counts = dp_->has_counts(r) ? dp_->counts_row(r, 0) : nullptr;
+  if (counts) dp_->set_counts_by_lane(r);
+  ipc_->round(s, dp_->input_chunk(r, 0, 0).ptr, dp_->output_at(r, 0, 0), nullptr, 0, counts,
+              int64_t(dp_->geometry().N) * dp_->kmax(), dp_->geometry().N);
   const Geometry& g = dp_->geometry();
   stats_.bytes_sent += int64_t(2) * (g.S - g.block_len(dp_->me())) * int64_t(dp_->esize());
   ++stats_.ipc_rounds;

@@ -128,6 +128,8 @@ class StreamLink final : public Link {
   void collective_round(int32_t round, bool native);
   void ipc_round(int32_t round);
   std::unique_ptr<IpcLane> ipc_;
+  StreamH ipc_last_stream_ = nullptr;  // stream of the lane's last engine-path round
+  bool ipc_last_stream_set_ = false;
   std::vector<std::vector<OpT>> exact_;  // [step] -> ops
   Geometry gx_;                          // exact rounds' transfer units (unit_chunks_ chunks each)
   int32_t unit_chunks_ = 1;

@@ -23,8 +23,8 @@ import os
 import re
 import statistics
 
-MAIN = re.compile(r"ipc_\w*kernel|os_round_kernel")
-ENGINE = re.compile(r"poison_counts|fillBuffer|finish_counts")
+MAIN = re.compile(r"ipc_(?!round_bump)\w*kernel|os_round_kernel")
+ENGINE = re.compile(r"poison_counts|fillBuffer|fill_counts")
 
 
 def runs_of(rows, split_ns, min_rounds):
