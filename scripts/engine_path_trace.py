@@ -10,8 +10,8 @@ at least --min-rounds launches:
   gap_us      median idle time between one main kernel's end and the next start
   between     every other kernel launched in those gaps: calls per round and
               median duration (the engine path's counts fill / poison / ...)
-A run whose gaps contain the engine's bookkeeping kernels is labelled
-"engine", else "direct".
+Runs are listed in time order (bench/onesided_round.py: one run per size,
+in --sizes-mb order; its warm-up launches fall below --min-rounds).
 
     python scripts/engine_path_trace.py <trace dir> [--split-ms 3] [--json out.json]
 """
@@ -24,7 +24,6 @@ import re
 import statistics
 
 MAIN = re.compile(r"ipc_(?!round_bump)\w*kernel|os_round_kernel")
-ENGINE = re.compile(r"poison_counts|fillBuffer|fill_counts")
 
 
 def runs_of(rows, split_ns, min_rounds):
@@ -55,7 +54,6 @@ def summarize(rows, run):
            "kernel_us": round(statistics.median(dur), 1), "gap_us": round(statistics.median(gap), 1),
            "between": {k[:60]: {"per_round": round(len(v) / n, 2), "median_us": round(statistics.median(v), 1)}
                        for k, v in sorted(between.items())}}
-    out["path"] = "engine" if any(ENGINE.search(k) for k in between) else "direct"
     return out
 
 
@@ -78,7 +76,7 @@ def main():
     for f, runs in res.items():
         print(f"== {f}")
         for i, s in enumerate(runs):
-            print(f"  run {i}: {s['path']:6s} rounds {s['rounds']:3d} period {s['period_us']:8.1f} us  kernel "
+            print(f"  run {i}: rounds {s['rounds']:3d} period {s['period_us']:8.1f} us  kernel "
                   f"{s['kernel_us']:8.1f}  gap {s['gap_us']:7.1f}  {s['main']}")
             for k, v in s["between"].items():
                 print(f"      {v['per_round']:5.2f}/round {v['median_us']:7.1f} us  {k}")
