@@ -93,6 +93,31 @@ void bind_onesided(py::module_& m) {
              for (size_t i = 0; i < sizeof(kStatNames) / sizeof(kStatNames[0]); ++i) d[kStatNames[i]] = v[i];
              return d;
            })
+      .def("stats_nowait",
+           [](OneSidedLane& l) {
+             std::vector<uint64_t> v;
+             {
+               py::gil_scoped_release nogil;
+               v = l.stats_nowait();
+             }
+             py::dict d;
+             for (size_t i = 0; i < sizeof(kStatNames) / sizeof(kStatNames[0]); ++i) d[kStatNames[i]] = v[i];
+             return d;
+           })
+      .def("peek_flags",
+           [](OneSidedLane& l) {
+             py::gil_scoped_release nogil;
+             return l.peek_flags();
+           })
+      .def("peek_part",
+           [](OneSidedLane& l, int32_t phase, int32_t row, int32_t src, int32_t k, int32_t j) {
+             std::string s;
+             {
+               py::gil_scoped_release nogil;
+               s = l.peek_part(phase, row, src, k, j);
+             }
+             return py::bytes(s);
+           })
       .def("begin",
            [](OneSidedLane& l, uintptr_t in, uintptr_t out, uintptr_t counts, int32_t kcols) {
              return l.begin(reinterpret_cast<const void*>(in), reinterpret_cast<void*>(out),

@@ -42,7 +42,32 @@ struct Blob {
   char bus[32];
   char shm[64];
   hipIpcMemHandle_t h[1 + 2 * kMaxRows];  // flags, SD rows, GD rows
+  // GPU: the creating process and its raw pointers -- lanes of ONE process
+  // (the single-process spec harness) map each other without IPC, which
+  // refuses a process's own allocations
+  int64_t pid;
+  uint64_t p_flags, p_sd[kMaxRows], p_gd[kMaxRows];
 };
+
+// Memory policy of the protocol functions for HOST code acting on DEVICE
+// words (the GPU spec harness's injected peer messages): blocking copies on
+// a non-blocking stream, so they run while the lane's kernels spin.
+struct DevFromHost {
+  static hipStream_t s;
+  static uint32_t ld(const uint32_t* p) {
+    uint32_t v = 0;
+    AKKA_OS_HIP(hipMemcpyAsync(&v, p, sizeof(v), hipMemcpyDeviceToHost, s));
+    AKKA_OS_HIP(hipStreamSynchronize(s));
+    return v;
+  }
+  static void st(uint32_t* p, uint32_t v) {
+    AKKA_OS_HIP(hipMemcpyAsync(p, &v, sizeof(v), hipMemcpyHostToDevice, s));
+    AKKA_OS_HIP(hipStreamSynchronize(s));
+  }
+  static void st_sc(uint32_t* p, uint32_t v) { st(p, v); }
+  static uint32_t ld_sc(const uint32_t* p) { return ld(p); }
+};
+hipStream_t DevFromHost::s = nullptr;
 
 // Memory policy of the protocol functions on the host (shared memory between
 // processes): C++ atomics; the announce / look pair is sequentially consistent.
@@ -167,7 +192,12 @@ OneSidedLane::OneSidedLane(int32_t device, int64_t S, int32_t N, int64_t C, int3
       AKKA_OS_HIP(hipMalloc(reinterpret_cast<void**>(&loc_), size_t(L_.local_words) * sizeof(uint32_t)));
     }
     AKKA_OS_HIP(hipMemset(loc_, 0, size_t(L_.local_words) * sizeof(uint32_t)));
-    AKKA_OS_HIP(hipMalloc(reinterpret_cast<void**>(&stats_dev_), kNumStats * sizeof(unsigned long long)));
+    // uncached: the counters can be read while a call runs (stats_nowait)
+    if (hipExtMallocWithFlags(reinterpret_cast<void**>(&stats_dev_), kNumStats * sizeof(unsigned long long),
+                              hipDeviceMallocUncached) != hipSuccess) {
+      (void)hipGetLastError();
+      AKKA_OS_HIP(hipMalloc(reinterpret_cast<void**>(&stats_dev_), kNumStats * sizeof(unsigned long long)));
+    }
     AKKA_OS_HIP(hipMemset(stats_dev_, 0, kNumStats * sizeof(unsigned long long)));
     AKKA_OS_HIP(hipMalloc(&tab_dev_, sizeof(Tables)));
     AKKA_OS_HIP(hipHostMalloc(reinterpret_cast<void**>(&hw_), sizeof(HostWords),
@@ -228,8 +258,9 @@ OneSidedLane::~OneSidedLane() {
   if (device_ >= 0) {
     hipSetDevice(device_);
     hipDeviceSynchronize();  // none of our kernels may still touch a window
-    for (void* m : opened_) hipIpcCloseMemHandle(m);
+    for (void* m : opened_) hipIpcCloseMemHandle(m);  // (same-process peers: nothing opened)
     if (cu_stream_) hipStreamDestroy(static_cast<hipStream_t>(cu_stream_));
+    if (side_stream_) hipStreamDestroy(static_cast<hipStream_t>(side_stream_));
     if (tl_dev_) hipFree(tl_dev_);
     if (ev_in_) hipEventDestroy(static_cast<hipEvent_t>(ev_in_));
     if (ev_out_) hipEventDestroy(static_cast<hipEvent_t>(ev_out_));
@@ -268,6 +299,12 @@ std::string OneSidedLane::handle() const {
   b.shm_bytes = int64_t(shm_bytes_);
   if (device_ >= 0) {
     std::memcpy(b.bus, my_bus_.c_str(), std::min(sizeof(b.bus) - 1, my_bus_.size()));
+    b.pid = int64_t(getpid());
+    b.p_flags = uint64_t(reinterpret_cast<uintptr_t>(flags_));
+    for (int32_t d = 0; d < D_; ++d) {
+      b.p_sd[d] = uint64_t(reinterpret_cast<uintptr_t>(sd_[size_t(d)]));
+      b.p_gd[d] = uint64_t(reinterpret_cast<uintptr_t>(gd_[size_t(d)]));
+    }
     AKKA_OS_HIP(hipIpcGetMemHandle(&b.h[0], flags_));
     for (int32_t d = 0; d < D_; ++d) {
       AKKA_OS_HIP(hipIpcGetMemHandle(&b.h[1 + d], sd_[size_t(d)]));
@@ -295,7 +332,14 @@ static Blob parse_handle(const std::string& h, int32_t q, int32_t N, size_t es, 
 
 void OneSidedLane::map_peer(int32_t q, const std::string& h) {
   const Blob b = parse_handle(h, q, g_.N, es_, D_, P_, Kmax_, g_, slot_, part_len_, device_ >= 0);
-  if (device_ >= 0) {
+  if (device_ >= 0 && b.pid == int64_t(getpid())) {
+    // a lane of this same process: its device pointers as they are
+    pfl_[size_t(q)] = reinterpret_cast<uint32_t*>(uintptr_t(b.p_flags));
+    for (int32_t d = 0; d < D_; ++d) {
+      psd_[size_t(d)][size_t(q)] = reinterpret_cast<char*>(uintptr_t(b.p_sd[d]));
+      pgd_[size_t(d)][size_t(q)] = reinterpret_cast<char*>(uintptr_t(b.p_gd[d]));
+    }
+  } else if (device_ >= 0) {
     void* f = nullptr;
     AKKA_OS_HIP(hipIpcOpenMemHandle(&f, b.h[0], hipIpcMemLazyEnablePeerAccess));
     opened_.push_back(f);
@@ -684,7 +728,7 @@ std::string OneSidedLane::outbox_bytes(int64_t i) const {
 
 void OneSidedLane::inject(int32_t phase, int32_t dst, int32_t k, int32_t j, uint32_t r, uint32_t cnt,
                           const std::string& bytes) {
-  AKKA_CHECK(ready_ && device_ < 0, "onesided lane: inject drives the CPU backend");
+  AKKA_CHECK(ready_, "onesided lane: open() the peer windows first");
   AKKA_CHECK(phase == 0 || phase == 1, "onesided lane: phase 0 (scatter) or 1 (gather)");
   AKKA_CHECK(dst >= 0 && dst < g_.N && dst != me_, "onesided lane: bad destination");
   const int32_t blk = phase == 0 ? dst : me_;
@@ -693,7 +737,108 @@ void OneSidedLane::inject(int32_t phase, int32_t dst, int32_t k, int32_t j, uint
   const int64_t n = std::max<int64_t>(0, std::min(part_len_, clen - int64_t(j) * part_len_));
   AKKA_CHECK(int64_t(bytes.size()) == n * int64_t(es_), "onesided lane: injected part has the wrong size");
   Msg m{phase, dst, k, j, r, cnt, std::vector<char>(bytes.begin(), bytes.end())};
-  exec(m, nullptr);
+  if (device_ >= 0) exec_gpu(m);
+  else exec(m, nullptr);
+}
+
+// inject() on a GPU lane: this rank (played by the host) pushes into the
+// receiver's device window through the same gates, while the receiver's
+// round kernel runs (the GPU spec harness, tests/test_onesided_spec_gpu.py).
+void OneSidedLane::exec_gpu(const Msg& m) {
+  AKKA_OS_HIP(hipSetDevice(device_));
+  if (!side_stream_) {
+    hipStream_t s = nullptr;
+    AKKA_OS_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    side_stream_ = s;
+  }
+  DevFromHost::s = static_cast<hipStream_t>(side_stream_);
+  const int32_t me = me_, q = m.dst, k = m.k, j = m.j;
+  const uint32_t r = m.r;
+  const int32_t row = int32_t(r % uint32_t(D_));
+  if (__atomic_load_n(&hw_->dead[q], __ATOMIC_ACQUIRE) != 0u) {
+    ++inj_stats_[kDeadSkips];
+    return;
+  }
+  uint32_t* qfl = pfl_[size_t(q)];
+  if (k == 0 && j == 0) DevFromHost::st(qfl + L_.seen(me), r + 1u);  // implicit start at the receiver
+  const int64_t tag = m.phase == 0 ? L_.stag(row, me, k, j) : L_.gtag(row, me, k, j);
+  if (DevFromHost::ld(qfl + tag) >= tag_writing(r + 1u)) {  // the slot's single writer moved past r
+    ++inj_stats_[m.phase == 0 ? kScatterOutdated : kGatherOutdated];
+    return;
+  }
+  const int32_t g = m.phase == 0 ? scatter_gate<DevFromHost>(qfl, L_, row, me, k, j, r)
+                                 : gather_gate<DevFromHost>(qfl, L_, row, me, k, j, r);
+  if (m.phase == 0) ++inj_stats_[g == kGo ? kScatterPushed : g == kOutdated ? kScatterOutdated : kScatterConflict];
+  else ++inj_stats_[g == kGo ? kGatherPushed : g == kOutdated ? kGatherOutdated : kGatherConflict];
+  if (g != kGo) return;
+  const int64_t off = int64_t(k) * g_.C + int64_t(j) * part_len_;
+  if (m.phase == 1) DevFromHost::st(qfl + tag + 1, m.cnt);  // count before the "done" tag
+  char* dst = (m.phase == 0 ? psd_ : pgd_)[size_t(row)][size_t(q)] + (int64_t(me) * slot_ + off) * int64_t(es_);
+  if (!m.bytes.empty()) {
+    AKKA_OS_HIP(hipMemcpyAsync(dst, m.bytes.data(), m.bytes.size(), hipMemcpyHostToDevice, DevFromHost::s));
+    AKKA_OS_HIP(hipStreamSynchronize(DevFromHost::s));
+  }
+  DevFromHost::st(qfl + tag, tag_done(r));  // after the bytes (the copy completed)
+}
+
+std::vector<uint32_t> OneSidedLane::peek_flags() {
+  std::vector<uint32_t> v(size_t(L_.flag_words), 0u);
+  if (device_ < 0) {
+    for (size_t i = 0; i < v.size(); ++i) v[i] = HostMem::ld(flags_ + i);
+    return v;
+  }
+  AKKA_OS_HIP(hipSetDevice(device_));
+  if (!side_stream_) {
+    hipStream_t s = nullptr;
+    AKKA_OS_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    side_stream_ = s;
+  }
+  AKKA_OS_HIP(hipMemcpyAsync(v.data(), flags_, v.size() * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                             static_cast<hipStream_t>(side_stream_)));
+  AKKA_OS_HIP(hipStreamSynchronize(static_cast<hipStream_t>(side_stream_)));
+  return v;
+}
+
+std::string OneSidedLane::peek_part(int32_t phase, int32_t row, int32_t src, int32_t k, int32_t j) {
+  AKKA_CHECK(row >= 0 && row < D_ && src >= 0 && src < g_.N && k >= 0 && k < Kmax_ && j >= 0 && j < P_,
+             "onesided lane: no such part");
+  const int32_t blk = phase == 0 ? me_ : src;  // SD holds my block's chunks, GD block src's
+  const int64_t clen = std::max<int64_t>(0, std::min(g_.C, g_.block_len(blk) - int64_t(k) * g_.C));
+  const int64_t n = std::max<int64_t>(0, std::min(part_len_, clen - int64_t(j) * part_len_));
+  const int64_t off = int64_t(k) * g_.C + int64_t(j) * part_len_;
+  const char* p = (phase == 0 ? sd_ : gd_)[size_t(row)] + (int64_t(src) * slot_ + off) * int64_t(es_);
+  std::string out(size_t(n) * es_, '\0');
+  if (n == 0) return out;
+  if (device_ < 0) {
+    std::memcpy(out.data(), p, out.size());
+    return out;
+  }
+  AKKA_OS_HIP(hipSetDevice(device_));
+  if (!side_stream_) {
+    hipStream_t s = nullptr;
+    AKKA_OS_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    side_stream_ = s;
+  }
+  AKKA_OS_HIP(hipMemcpyAsync(out.data(), p, out.size(), hipMemcpyDeviceToHost, static_cast<hipStream_t>(side_stream_)));
+  AKKA_OS_HIP(hipStreamSynchronize(static_cast<hipStream_t>(side_stream_)));
+  return out;
+}
+
+std::vector<uint64_t> OneSidedLane::stats_nowait() {
+  std::vector<uint64_t> v(kNumStats, 0);
+  if (device_ < 0) return stats();
+  AKKA_OS_HIP(hipSetDevice(device_));
+  if (!side_stream_) {
+    hipStream_t s = nullptr;
+    AKKA_OS_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    side_stream_ = s;
+  }
+  std::vector<unsigned long long> h(kNumStats, 0);
+  AKKA_OS_HIP(hipMemcpyAsync(h.data(), stats_dev_, kNumStats * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                             static_cast<hipStream_t>(side_stream_)));
+  AKKA_OS_HIP(hipStreamSynchronize(static_cast<hipStream_t>(side_stream_)));
+  for (int i = 0; i < kNumStats; ++i) v[size_t(i)] = h[size_t(i)] + inj_stats_[size_t(i)];
+  return v;
 }
 
 void OneSidedLane::drop(int64_t i) {
@@ -932,7 +1077,7 @@ std::vector<uint64_t> OneSidedLane::stats() {
     AKKA_OS_HIP(hipDeviceSynchronize());
     std::vector<unsigned long long> h(kNumStats, 0);
     AKKA_OS_HIP(hipMemcpy(h.data(), stats_dev_, kNumStats * sizeof(unsigned long long), hipMemcpyDeviceToHost));
-    for (int i = 0; i < kNumStats; ++i) v[size_t(i)] = h[size_t(i)];
+    for (int i = 0; i < kNumStats; ++i) v[size_t(i)] = h[size_t(i)] + inj_stats_[size_t(i)];
   } else {
     for (int i = 0; i < kNumStats; ++i) v[size_t(i)] = stats_host_[size_t(i)];
   }

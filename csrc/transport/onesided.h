@@ -126,7 +126,17 @@ class OneSidedLane {
   std::string outbox_bytes(int64_t i) const;
   // Play this rank as a TestKit-style peer (AllreduceSpec.scala:812-818): a
   // push of arbitrary bytes from this rank, through the same gates.
+  // GPU lanes: the host performs the push into the receiver's device window
+  // (blocking copies on a side stream) -- the receiver's kernel may be
+  // running; its decisions are the real os_round_kernel's.
   void inject(int32_t phase, int32_t dst, int32_t k, int32_t j, uint32_t r, uint32_t cnt, const std::string& bytes);
+  // stats() without synchronising the device (GPU: read while a call runs).
+  std::vector<uint64_t> stats_nowait();
+  // Test access to this rank's own window (GPU: copies on the side stream,
+  // while a call may run): the flag words, and part j of chunk k of source
+  // (SD, phase 0) or block (GD, phase 1) `src` in ring row `row`.
+  std::vector<uint32_t> peek_flags();
+  std::string peek_part(int32_t phase, int32_t row, int32_t src, int32_t k, int32_t j);
 
   bool on_gpu() const { return device_ >= 0; }
   int32_t rows() const { return D_; }
@@ -181,6 +191,7 @@ class OneSidedLane {
   // CPU roles
   void push(int32_t phase, int32_t dst, int32_t k, int32_t j, uint32_t r, uint32_t cnt, const char* src);
   void exec(const Msg& m, const char* src);
+  void exec_gpu(const Msg& m);
   bool try_decide(int32_t k, bool timed_out);
   bool try_complete(bool timed_out);
   void flush();
@@ -231,6 +242,8 @@ class OneSidedLane {
   HostWords* hw_dev_ = nullptr;         // device view of hw_ (GPU)
   std::vector<uint32_t> loc_host_;
   std::vector<unsigned long long> stats_host_;
+  std::array<unsigned long long, os::kNumStats> inj_stats_{};  // GPU: injected pushes' gate outcomes
+  void* side_stream_ = nullptr;  // hipStream_t (non-blocking): inject / stats_nowait copies
 
   // CPU progress state
   CpuRound cr_;
