@@ -69,6 +69,20 @@ struct DevFromHost {
 };
 hipStream_t DevFromHost::s = nullptr;
 
+// ONE non-blocking stream per device for every lane's host-side copies
+// (inject / peek / stats_nowait), created once for the process: streams
+// share the device's hardware queues (GPU_MAX_HW_QUEUES), and a copy queued
+// behind a lane's waiting round kernel on a shared queue would wait for it.
+hipStream_t host_side_stream(int32_t device) {
+  static hipStream_t streams[64] = {};
+  if (!streams[device]) {
+    hipStream_t s = nullptr;
+    AKKA_OS_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    streams[device] = s;
+  }
+  return streams[device];
+}
+
 // Memory policy of the protocol functions on the host (shared memory between
 // processes): C++ atomics; the announce / look pair is sequentially consistent.
 struct HostMem {
@@ -260,7 +274,7 @@ OneSidedLane::~OneSidedLane() {
     hipDeviceSynchronize();  // none of our kernels may still touch a window
     for (void* m : opened_) hipIpcCloseMemHandle(m);  // (same-process peers: nothing opened)
     if (cu_stream_) hipStreamDestroy(static_cast<hipStream_t>(cu_stream_));
-    if (side_stream_) hipStreamDestroy(static_cast<hipStream_t>(side_stream_));
+    // (side_stream_: the process-wide host_side_stream, never destroyed)
     if (tl_dev_) hipFree(tl_dev_);
     if (ev_in_) hipEventDestroy(static_cast<hipEvent_t>(ev_in_));
     if (ev_out_) hipEventDestroy(static_cast<hipEvent_t>(ev_out_));
@@ -746,11 +760,7 @@ void OneSidedLane::inject(int32_t phase, int32_t dst, int32_t k, int32_t j, uint
 // round kernel runs (the GPU spec harness, tests/test_onesided_spec_gpu.py).
 void OneSidedLane::exec_gpu(const Msg& m) {
   AKKA_OS_HIP(hipSetDevice(device_));
-  if (!side_stream_) {
-    hipStream_t s = nullptr;
-    AKKA_OS_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-    side_stream_ = s;
-  }
+  side_stream_ = host_side_stream(device_);
   DevFromHost::s = static_cast<hipStream_t>(side_stream_);
   const int32_t me = me_, q = m.dst, k = m.k, j = m.j;
   const uint32_t r = m.r;
@@ -788,11 +798,7 @@ std::vector<uint32_t> OneSidedLane::peek_flags() {
     return v;
   }
   AKKA_OS_HIP(hipSetDevice(device_));
-  if (!side_stream_) {
-    hipStream_t s = nullptr;
-    AKKA_OS_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-    side_stream_ = s;
-  }
+  side_stream_ = host_side_stream(device_);
   AKKA_OS_HIP(hipMemcpyAsync(v.data(), flags_, v.size() * sizeof(uint32_t), hipMemcpyDeviceToHost,
                              static_cast<hipStream_t>(side_stream_)));
   AKKA_OS_HIP(hipStreamSynchronize(static_cast<hipStream_t>(side_stream_)));
@@ -814,11 +820,7 @@ std::string OneSidedLane::peek_part(int32_t phase, int32_t row, int32_t src, int
     return out;
   }
   AKKA_OS_HIP(hipSetDevice(device_));
-  if (!side_stream_) {
-    hipStream_t s = nullptr;
-    AKKA_OS_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-    side_stream_ = s;
-  }
+  side_stream_ = host_side_stream(device_);
   AKKA_OS_HIP(hipMemcpyAsync(out.data(), p, out.size(), hipMemcpyDeviceToHost, static_cast<hipStream_t>(side_stream_)));
   AKKA_OS_HIP(hipStreamSynchronize(static_cast<hipStream_t>(side_stream_)));
   return out;
@@ -828,11 +830,7 @@ std::vector<uint64_t> OneSidedLane::stats_nowait() {
   std::vector<uint64_t> v(kNumStats, 0);
   if (device_ < 0) return stats();
   AKKA_OS_HIP(hipSetDevice(device_));
-  if (!side_stream_) {
-    hipStream_t s = nullptr;
-    AKKA_OS_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-    side_stream_ = s;
-  }
+  side_stream_ = host_side_stream(device_);
   std::vector<unsigned long long> h(kNumStats, 0);
   AKKA_OS_HIP(hipMemcpyAsync(h.data(), stats_dev_, kNumStats * sizeof(unsigned long long), hipMemcpyDeviceToHost,
                              static_cast<hipStream_t>(side_stream_)));

@@ -7,7 +7,8 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/../..}"
 export TMPDIR=/tmp
 O=gpurun_out/r05/e
 mkdir -p $O
-timeout -k 10 900 python -u -m pytest -x -v --timeout 150 --timeout-method thread -m gpu \
+# (clock_probe.py: lane timeouts match the wall clock, 510 / 2006 ms for 500 / 2000 ms)
+timeout -k 10 60 python scripts/r05/nowait_probe.py && timeout -k 10 900 python -u -m pytest -x -v --timeout 150 --timeout-method thread -m gpu \
   tests/test_onesided_spec_gpu.py > $O/pytest.txt 2>&1
 rc=$?
 grep -E "PASSED|FAILED|ERROR|passed|failed" $O/pytest.txt | tail -40

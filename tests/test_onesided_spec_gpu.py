@@ -15,9 +15,9 @@ the worker's kernel spins in its waits.  All N lanes live in this one process
 The worker's own pushes land in the peers' (passive) windows, where the
 harness reads them back as the probe reads the worker's messages: a "done r"
 tag of a part is one message of round r, its bytes and count word the
-payload.  Messages that appear in one step are ordered the way the CPU
-harness emits them (round, scatter before reduce, chunk, part, peers rotated
-from the worker), so every assertion of the CPU cases -- outputs
+payload.  The messages pending at a look are ordered the way the CPU harness
+emits them (round, scatter before reduce, chunk, part, peers rotated from the
+worker), so every assertion of the CPU cases -- outputs
 ``(round, data, counts, reason)``, emitted messages, counters -- holds
 verbatim on the device.  After every step the harness waits for the card to
 go quiet (no new output and no new message for a few polls), which is what
@@ -40,6 +40,13 @@ from akka_allreduce_amd._native_loader import load
 from model_worker import Geometry
 
 _OPEN: list = []  # harnesses of the running test (closed after it: every launched call must end)
+_STREAMS: dict = {}  # the worker's and the copy stream, created once (streams share hardware queues)
+
+
+def _streams(dev):
+    if dev not in _STREAMS:
+        _STREAMS[dev] = (torch.cuda.Stream(dev), torch.cuda.Stream(dev))
+    return _STREAMS[dev]
 
 
 class WindowSpecHarness:
@@ -80,8 +87,17 @@ class WindowSpecHarness:
         self.pending: list = []
         if dev >= 0:
             self.cuda = torch.device("cuda", dev)
-            self.stream = torch.cuda.Stream(self.cuda)
-            self.copy_stream = torch.cuda.Stream(self.cuda)
+            self.stream, self.copy_stream = _streams(self.cuda)
+            # first-time work of the runtime (side streams, staging buffers
+            # for pageable copies) may wait for the whole device: done here,
+            # before any call is in flight, not in the middle of a round
+            for ln in self.lanes:
+                ln.peek_flags()
+                ln.peek_part(0, 0, 0, 0, 0)
+                ln.stats_nowait()
+            with torch.cuda.stream(self.copy_stream):
+                torch.zeros(4, device=self.cuda).cpu()
+            torch.cuda.synchronize(self.cuda)
         _OPEN.append(self)
 
     # ---- layout (csrc/kernels/onesided_protocol.h, Layout::init) -----------------
@@ -100,8 +116,14 @@ class WindowSpecHarness:
         if self.device < 0:
             self.pending.append((x, out, counts))
         else:
-            with torch.cuda.stream(self.stream):
+            # the buffers are staged on the copy stream: a blocking copy on the
+            # worker's stream would wait for the call still running there
+            with torch.cuda.stream(self.copy_stream):
                 x, out, counts = (t.to(self.cuda, non_blocking=False) for t in (x, out, counts))
+            self.stream.wait_stream(self.copy_stream)
+            for t in (x, out, counts):
+                t.record_stream(self.stream)
+            with torch.cuda.stream(self.stream):
                 call = self.w.round(self.stream.cuda_stream, x.data_ptr(), out.data_ptr(), counts.data_ptr(),
                                     self.kmax)
                 ev = torch.cuda.Event()
@@ -163,9 +185,6 @@ class WindowSpecHarness:
                                              dtype=np.float32).tolist()
                         cnt = int(fl[w + 1]) if phase == 1 else 0
                         new.append(("scatter" if phase == 0 else "gather", q, k, r, cnt, vals))
-        # the CPU harness's emission order: a round's scatters (chunk-major,
-        # peers rotated from the worker), then its ReduceBlocks chunk by chunk
-        new.sort(key=lambda m: (m[3], 0 if m[0] == "scatter" else 1, m[2], (m[1] - self.me - 1) % self.N))
         self.sent.extend(new)
 
     def _sig(self):
@@ -185,6 +204,11 @@ class WindowSpecHarness:
             last = s
 
     def take_sent(self, phase=None):
+        # everything pending since the test's last look is one step for the
+        # test: order it as the CPU harness emits (the device publishes the
+        # parts of one decision to the peers in any order, and a look may
+        # fall between them)
+        self.sent.sort(key=lambda m: (m[3], 0 if m[0] == "scatter" else 1, m[2], (m[1] - self.me - 1) % self.N))
         s = [m for m in self.sent if phase is None or m[0] == phase]
         self.sent = [m for m in self.sent if not (phase is None or m[0] == phase)]
         return s
@@ -219,36 +243,62 @@ class CpuWindowSpecHarness(WindowSpecHarness):
 
 CASES = sorted(name for name, f in inspect.getmembers(spec, inspect.isfunction)
                if name.startswith("test_") and "seed" not in inspect.signature(f).parameters)
+SEEDS = range(4)
 
 
-def _run_case(name, harness, seed=None, monkeypatch=None):
-    monkeypatch.setattr(spec, "SpecHarness", harness)
-    f = getattr(spec, name)
+def run_case(name, harness, seed=None):
+    """One case of tests/test_onesided_spec.py with ``harness`` as its SpecHarness."""
+    saved = spec.SpecHarness
+    spec.SpecHarness = harness
     try:
+        f = getattr(spec, name)
         f(seed) if seed is not None else f()
     finally:
+        spec.SpecHarness = saved
         while _OPEN:
             _OPEN.pop().close()
 
 
 @pytest.mark.parametrize("name", CASES)
-def test_spec_case_on_window_harness_cpu(name, monkeypatch):
+def test_spec_case_on_window_harness_cpu(name):
     """The harness itself on CPU lanes: the same assertions hold when the
     worker's pushes are delivered to (and read back from) the peers' windows."""
-    _run_case(name, CpuWindowSpecHarness, monkeypatch=monkeypatch)
+    run_case(name, CpuWindowSpecHarness)
+
+
+@pytest.fixture(scope="module")
+def gpu_results():
+    """Every case on the GPU in ONE child process with GPU_MAX_HW_QUEUES=16:
+    the harness's copy stream and the lanes' host-side stream must not share
+    a hardware queue with the worker's stream, where a copy would queue behind
+    the round kernel it is meant to observe (4 queues by default)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    import tempfile
+
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    here = os.path.dirname(os.path.abspath(__file__))
+    with tempfile.TemporaryDirectory() as td:
+        out = os.path.join(td, "results.json")
+        env = dict(os.environ, GPU_MAX_HW_QUEUES="16")
+        r = subprocess.run([sys.executable, os.path.join(here, "spec_gpu_runner.py"), out], cwd=os.path.dirname(here),
+                           env=env, capture_output=True, text=True, timeout=900)
+        assert os.path.exists(out), (r.returncode, r.stdout[-3000:], r.stderr[-3000:])
+        return json.load(open(out))
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", CASES)
-def test_spec_case_on_gpu_kernel(name, monkeypatch):
-    if not torch.cuda.is_available():
-        pytest.skip("needs a GPU")
-    _run_case(name, WindowSpecHarness, monkeypatch=monkeypatch)
+def test_spec_case_on_gpu_kernel(name, gpu_results):
+    res = gpu_results[name]
+    assert res["ok"], res["error"]
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("seed", range(4))
-def test_spec_random_orders_on_gpu_kernel(seed, monkeypatch):
-    if not torch.cuda.is_available():
-        pytest.skip("needs a GPU")
-    _run_case("test_random_orders_match_reference_rules", WindowSpecHarness, seed=seed, monkeypatch=monkeypatch)
+@pytest.mark.parametrize("seed", SEEDS)
+def test_spec_random_orders_on_gpu_kernel(seed, gpu_results):
+    res = gpu_results[f"random_orders_{seed}"]
+    assert res["ok"], res["error"]
