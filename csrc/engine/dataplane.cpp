@@ -340,7 +340,10 @@ void DataPlane::wait_input(int32_t round, StreamH s) {
   // only if it actually reads the input (N=1 never touches the comm stream).
   Binding& b = binding_mut(round);
   const bool comm = s == dev_->comm_stream();
-  if (b.output_ready) {
+  // fault injection (AKKA_FAULT_SKIP_OUTPUT_WAIT): the stream that fills an
+  // exact round's counts (the comm stream since round 5) skips the caller's
+  // hand-over point -- the round-2 counts-fill race, re-created for the checker
+  if (b.output_ready && !(fault_skip_output_wait_ && comm && b.exec_on_comm)) {
     bool& od = comm ? b.output_waited_comm : b.output_waited_compute;
     if (!od) {
       dev_->wait(s, b.output_ready);

@@ -554,7 +554,7 @@ int64_t OneSidedLane::round(uintptr_t stream, const void* in, void* out, int32_t
   int us = 20;
   while (!progress()) {
     std::this_thread::sleep_for(std::chrono::microseconds(us));
-    us = std::min(us * 2, 1000);
+    us = std::min(us * 2, 200);  // (a coarser back-off adds up to its cap to a round that waited)
   }
   return call;
 }

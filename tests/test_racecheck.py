@@ -110,9 +110,11 @@ def test_threshold_schedule_is_race_free(n, S, C, th):
 
 
 def test_detects_the_counts_fill_race_when_reinjected():
-    """The round-2 bug: the exact round's counts fill on the compute stream did
-    not wait for the caller's hand-over point.  Re-injected, the checker names
-    it on every rank (fill vs the caller's pending write)."""
+    """The round-2 bug: the exact round's counts fill did not wait for the
+    caller's hand-over point.  Re-injected, the checker names it on every rank
+    (fill vs the caller's pending write).  (Since round 5 an exact bulk round
+    fills its counts on the comm stream, behind that stream's wait for the
+    hand-over, which the fault now skips.)"""
     d = _run({"n": 4, "S": 4096, "C": 256, "lane": "collective", "collectives": True},
              AKKA_FAULT_SKIP_OUTPUT_WAIT="1")
     assert all(r > 0 for r in d["races"]), d
