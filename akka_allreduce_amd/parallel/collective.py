@@ -377,6 +377,12 @@ class ThresholdAllreduce:
             self.pacer.completed(r)  # CompleteAllreduce(id, r) to the "master" (W:276)
         return out
 
+    def prefers_lane_output(self) -> bool:
+        """Calls without ``out`` skip a copy on this lane: the one-sided lane
+        with ``onesided_options={"window_output": True}`` returns its window
+        row (valid until the next call) instead of writing a caller buffer."""
+        return bool(self._lane_os and self._exact_os is not None and self._exact_os.window_output)
+
     def runs_async(self) -> bool:
         """Whether the DDP hook should issue ``async_op=True`` rounds (then
         ``async_stream()`` is where their results complete).  Not on the
@@ -694,14 +700,15 @@ class ThresholdAllreduce:
             return bool(torch.all(o.data == want).item()) and bool(torch.all(o.count == N).item())
 
         def timed_block() -> float:
-            o = self(x, async_op=cuda, out=buf)
+            ob = None if self.prefers_lane_output() else buf  # the lane's own output where it has one
+            o = self(x, async_op=cuda, out=ob)
             o.wait()
             sync()
             best = float("inf")
             for _ in range(2):  # the better of two blocks: one noisy block does not decide the lane
                 t0 = time.perf_counter()
                 for _ in range(rounds):  # the ranks are coupled by the rounds themselves
-                    o = self(x, async_op=cuda, out=buf)
+                    o = self(x, async_op=cuda, out=ob)
                 o.wait()
                 sync()
                 best = min(best, (time.perf_counter() - t0) / rounds * 1e3)

@@ -147,6 +147,7 @@ class OneSidedAllreduce:
         data_sink: Any = None,
         handoff: str = "lite",
         members: Optional[list] = None,
+        window_output: bool = False,
     ):
         if dtype not in _DTYPES:
             raise ValueError("dtype must be float32 or bfloat16")
@@ -200,7 +201,7 @@ class OneSidedAllreduce:
                                        max_lag=int(max_lag), rows=int(rows), part_bytes=int(part_bytes),
                                        timeout_ms=int(timeout_s * 1000), threads=int(threads),
                                        role_wgs=int(role_wgs), cu_keep=int(cu_keep),
-                                       fenced=handoff == "fenced")
+                                       fenced=handoff == "fenced", window_output=bool(window_output))
             mine = self.lane.handle()
         except Exception as e:  # noqa: BLE001 - re-raised after the exchange
             mine, err = b"", e
@@ -227,6 +228,17 @@ class OneSidedAllreduce:
         self._counts: dict = {}
         self._side: Optional[torch.cuda.Stream] = None  # async_op rounds
         self.calls = 0
+        # window output (exact rounds): a call without ``out`` returns the
+        # gather row of its call id in this rank's own window -- the peers'
+        # reduced parts land there in place, no copy -- valid until the NEXT
+        # call of this lane (like a reused ``out``)
+        self._rows: Optional[list] = None
+        if self.lane.info().get("window_output"):
+            from torch.utils.dlpack import from_dlpack
+
+            dname = _DTYPES[dtype]
+            self._rows = [from_dlpack(self.lane.gather_row_dlpack(d, dname, int(dev_index)))
+                          for d in range(int(self.lane.info()["rows"]))]
 
     def __call__(self, x: torch.Tensor, out: Optional[torch.Tensor] = None, async_op: bool = False) -> OneSidedOutput:
         """One round of this rank.  GPU: enqueued on the current stream (the
@@ -243,7 +255,10 @@ class OneSidedAllreduce:
             x = x.to(device=self.device, dtype=self.dtype)
         x = x.reshape(-1).contiguous()
         reuse = out is not None
-        if out is None:
+        lane_out = out is None and self._rows is not None and self.data_sink is None
+        if lane_out:
+            out = None  # the kernel writes the window row of this call's id
+        elif out is None:
             out = torch.empty_like(x)
         elif out.numel() != self.data_size or out.dtype != self.dtype or not out.is_contiguous():
             raise ValueError("out must be a contiguous tensor of the buffer's size and dtype")
@@ -264,13 +279,17 @@ class OneSidedAllreduce:
         if async_op and stream is not None:
             side = self._side_stream()
             side.wait_stream(stream)
-            for t in (x, out, counts):  # the caching allocator: in use on the side stream too
+            for t in (x, counts) + ((out,) if out is not None else ()):  # in use on the side stream too
                 t.record_stream(side)
             stream = side
         # roctx range around the enqueue (AKKA_TRACE=1; rocprofv3 --marker-trace)
         with _tracing.range_(f"akka.onesided call {self.calls}"):
-            call = self.lane.round(stream.cuda_stream if stream is not None else 0, x.data_ptr(), out.data_ptr(),
-                                   counts.data_ptr(), self._kmax)
+            call = self.lane.round(stream.cuda_stream if stream is not None else 0, x.data_ptr(),
+                                   0 if lane_out else out.data_ptr(), counts.data_ptr(), self._kmax)
+        if lane_out:
+            if call < 0:
+                raise RuntimeError("a captured call needs an output buffer (out=...)")
+            out = self._rows[call % len(self._rows)][: self.data_size]
         if async_op and stream is not None:
             event = torch.cuda.Event()
             event.record(stream)
@@ -295,6 +314,11 @@ class OneSidedAllreduce:
         call sequence lives in device memory.  After each replay of a captured
         call, ``note_replays(1)`` keeps the host's call ids in step."""
         return self.device.type == "cuda" and self.data_sink is None
+
+    @property
+    def window_output(self) -> bool:
+        """Calls without ``out`` return a window row (valid until the next call)."""
+        return self._rows is not None
 
     @property
     def handoff(self) -> str:

@@ -87,6 +87,9 @@ def parse():
     p.add_argument("--lane-set", choices=["default", "all"], default="default",
                    help="lane selection candidates: default = p2p, the direct ipc rounds (lite, fused lite, fused "
                         "fenced) and the one-sided lane (lite, fenced); all = also every engine-path ipc variant")
+    p.add_argument("--lane-output", choices=["on", "off"], default="on",
+                   help="on: a one-sided lane chosen for the timed rounds returns its window row (no copy into a "
+                        "caller buffer; the output of a round is valid until the next round)")
     p.add_argument("--ipc", choices=["on", "off"], default="on",
                    help="lane selection also tries the one-sided xGMI lane (mapped peer windows, ipc_lane.h)")
     p.add_argument("--async-op", choices=["auto", "on", "off"], default="auto",
@@ -799,12 +802,18 @@ def main() -> int:
                  and (not args.extras_only or "cfg3" in args.extras_only.split(",")))
     ipc_cap = max(S, (1 << 30) // esize) if will_cfg3 else 0
 
+    # the headline's one-sided lane (an exact tune candidate) returns its
+    # window row when called without ``out``: the peers' reduced parts land
+    # in place, no copy into a caller buffer (the line's config.output says
+    # which output the timed rounds used)
+    os_opts = {"window_output": True} if args.lane_output == "on" else None
+
     def rccl_init():
         env_phase_stall(rank, "rccl_init")
         return ThresholdAllreduce(S, max_chunk_size=C, dtype=dtype, th_reduce=args.th_reduce,
                                   th_complete=args.th_complete, max_lag=args.max_lag, broadcast_lag=args.bcast_lag,
                                   device=dev, transport=args.transport, lane=args.lane,
-                                  data_plane=args.data_plane, ipc_capacity=ipc_cap)
+                                  data_plane=args.data_plane, ipc_capacity=ipc_cap, onesided_options=os_opts)
 
     # RCCL failing on EVERY rank (agreed) does not cost the headline: the job
     # is rebuilt in this same process on the ipc data plane (one-sided xGMI,
@@ -820,7 +829,7 @@ def main() -> int:
             args.data_plane = "ipc"
             ar = guard.run("ipc_init", dl, lambda: ThresholdAllreduce(
                 S, max_chunk_size=C, dtype=dtype, max_lag=args.max_lag, broadcast_lag=args.bcast_lag, device=dev,
-                data_plane="ipc", ipc_capacity=ipc_cap))
+                data_plane="ipc", ipc_capacity=ipc_cap, onesided_options=os_opts))
         else:
             guard.fail("rccl_init", "error", init_errors)
 
@@ -890,7 +899,7 @@ def main() -> int:
                     failed_engines.append(ar)
                     ar = ThresholdAllreduce(S, max_chunk_size=C, dtype=dtype, max_lag=args.max_lag,
                                             broadcast_lag=args.bcast_lag, device=dev, data_plane="ipc",
-                                            ipc_capacity=ipc_cap)
+                                            ipc_capacity=ipc_cap, onesided_options=os_opts)
                     ar.use_lane("ipc_fused_lite")
                     if not exact_round("preflight_ipc"):
                         raise RuntimeError("ipc preflight round is not exact")
@@ -938,6 +947,12 @@ def main() -> int:
     if world > 1 and ar.transport == "stream" and args.lane == "auto" and args.lane_select == "on":
         lane_sel = guard.run("lane_select", dl, lane_select)
         chosen_lane = lane_sel["chosen"]
+
+    if out_buf is not None and ar.world_size > 1 and ar.prefers_lane_output():
+        out_buf = None  # the chosen lane's own output (window row, valid until the next round)
+        lane_output = True
+    else:
+        lane_output = False
 
     def warmup():
         env_phase_stall(rank, "warmup")
@@ -1093,7 +1108,8 @@ def main() -> int:
         # N=1 moves nothing between ranks: no data plane runs
         "data_plane": args.data_plane if world > 1 else "none (local reduce pass)",
         "async_op": args.async_op,
-        "output": "fresh tensor per round" if args.fresh_out else "preallocated, reused",
+        "output": ("the lane's window row, valid until the next round (no copy into a caller buffer)"
+                   if lane_output else "fresh tensor per round" if args.fresh_out else "preallocated, reused"),
     })
     if rccl_err:
         line["rccl_compare_error"] = rccl_err

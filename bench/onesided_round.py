@@ -73,15 +73,18 @@ def main() -> None:
         for lane in a.lanes.split(","):
             case = {"lane": lane, "size_mb": mb, "chunk_elems": min(C, S)}
             try:
-                if lane == "onesided":
+                if lane in ("onesided", "onesided_wo"):
+                    # onesided_wo: window output (calls without out return the
+                    # window row of the call: no copy into a caller buffer)
                     kw = {"threads": a.threads} if a.threads else {}
-                    ar = OneSidedAllreduce(S, max_chunk_size=min(C, S), device=dev, **kw)
+                    wo = lane == "onesided_wo"
+                    ar = OneSidedAllreduce(S, max_chunk_size=min(C, S), device=dev, window_output=wo, **kw)
                     # exactness once: integer data, sum in any order is exact
                     y = torch.full((S,), float(rank + 1), device=dev)
                     o = ar(y)
                     torch.cuda.synchronize()
                     case["exact"] = bool((o.data == world * (world + 1) / 2).all()) and bool((o.count == world).all())
-                    case["ms"] = _time(lambda: ar(x, out=out), a.warmup, a.steps)
+                    case["ms"] = _time(lambda: ar(x, out=None if wo else out), a.warmup, a.steps)
                     case["info"] = {k: v for k, v in ar.info().items() if k != "stats"}
                     case["error"] = ar.error()
                     ar.retire()

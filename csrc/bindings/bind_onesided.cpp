@@ -10,6 +10,57 @@ namespace py = pybind11;
 namespace akka {
 
 namespace {
+// Minimal DLPack (v0.x ABI) to hand a window row to torch without a copy.
+struct DLDevice {
+  int32_t device_type;
+  int32_t device_id;
+};
+struct DLDataType {
+  uint8_t code;
+  uint8_t bits;
+  uint16_t lanes;
+};
+struct DLTensor {
+  void* data;
+  DLDevice device;
+  int32_t ndim;
+  DLDataType dtype;
+  int64_t* shape;
+  int64_t* strides;
+  uint64_t byte_offset;
+};
+struct DLManagedTensor {
+  DLTensor dl_tensor;
+  void* manager_ctx;
+  void (*deleter)(DLManagedTensor*);
+};
+constexpr int32_t kDLROCM = 10;
+
+void dl_delete(DLManagedTensor* t) {
+  delete[] t->dl_tensor.shape;
+  delete t;
+}
+
+// A capsule over device memory the lane owns (no deleter of the memory).
+py::capsule window_capsule(void* data, int32_t device, int64_t n, bool bf16) {
+  auto* t = new DLManagedTensor();
+  t->dl_tensor.data = data;
+  t->dl_tensor.device = {kDLROCM, device};
+  t->dl_tensor.ndim = 1;
+  t->dl_tensor.dtype = bf16 ? DLDataType{4, 16, 1} : DLDataType{2, 32, 1};
+  t->dl_tensor.shape = new int64_t[1]{n};
+  t->dl_tensor.strides = nullptr;
+  t->dl_tensor.byte_offset = 0;
+  t->manager_ctx = nullptr;
+  t->deleter = dl_delete;
+  return py::capsule(t, "dltensor", [](PyObject* cap) {
+    // consumed capsules are renamed "used_dltensor" (the consumer owns them)
+    if (PyCapsule_IsValid(cap, "dltensor")) {
+      auto* m = static_cast<DLManagedTensor*>(PyCapsule_GetPointer(cap, "dltensor"));
+      if (m && m->deleter) m->deleter(m);
+    }
+  });
+}
 const char* kStatNames[] = {
     "rounds",           "skipped_rounds",     "scatter_pushed",  "scatter_outdated", "scatter_conflict",
     "gather_pushed",    "gather_outdated",    "gather_conflict", "reduce_threshold", "reduce_forced",
@@ -23,7 +74,8 @@ void bind_onesided(py::module_& m) {
   py::class_<OneSidedLane>(m, "OneSidedLane")
       .def(py::init([](int32_t device, int64_t S, int32_t N, int64_t C, int32_t me, const std::string& dtype,
                        float th_reduce, float th_complete, int32_t max_lag, int32_t rows, int64_t part_bytes,
-                       int64_t timeout_ms, int32_t threads, int32_t role_wgs, int32_t cu_keep, bool fenced) {
+                       int64_t timeout_ms, int32_t threads, int32_t role_wgs, int32_t cu_keep, bool fenced,
+                       bool window_output) {
              OneSidedParams p;
              p.th_reduce = th_reduce;
              p.th_complete = th_complete;
@@ -35,13 +87,21 @@ void bind_onesided(py::module_& m) {
              p.role_wgs = role_wgs;
              p.cu_keep = cu_keep;
              p.fenced = fenced;
+             p.window_output = window_output;
              const DType dt = (dtype == "bfloat16" || dtype == "bf16") ? DType::BF16 : DType::F32;
              return std::make_unique<OneSidedLane>(device, S, N, C, me, dt, p);
            }),
            py::arg("device"), py::arg("S"), py::arg("N"), py::arg("C"), py::arg("me"), py::arg("dtype") = "float32",
            py::arg("th_reduce") = 1.f, py::arg("th_complete") = 1.f, py::arg("max_lag") = 1, py::arg("rows") = 0,
            py::arg("part_bytes") = int64_t(256) << 10, py::arg("timeout_ms") = 30000, py::arg("threads") = 256,
-           py::arg("role_wgs") = 0, py::arg("cu_keep") = 0, py::arg("fenced") = false)
+           py::arg("role_wgs") = 0, py::arg("cu_keep") = 0, py::arg("fenced") = false,
+           py::arg("window_output") = false)
+      .def("gather_row_dlpack",
+           [](const OneSidedLane& l, int32_t row, const std::string& dtype, int32_t device) {
+             AKKA_CHECK(l.on_gpu() && l.window_output(), "onesided lane: no window output");
+             AKKA_CHECK(row >= 0 && row < l.rows(), "onesided lane: no such row");
+             return window_capsule(l.gather_row(row), device, l.geometry().S, dtype == "bfloat16");
+           })
       .def("set_fenced", &OneSidedLane::set_fenced)
       .def_property_readonly("fenced", &OneSidedLane::fenced)
       .def("handle", [](const OneSidedLane& l) { return py::bytes(l.handle()); })
@@ -173,6 +233,7 @@ void bind_onesided(py::module_& m) {
         d["clock_khz"] = l.clock_khz();
         d["pieces_per_part"] = l.pieces();
         d["handoff"] = l.fenced() ? "fenced" : "lite";
+        d["window_output"] = l.window_output();
         const auto g = l.role_grid();
         d["role_wgs"] = py::dict(py::arg("push") = g[0], py::arg("reduce") = g[1], py::arg("copy") = g[2]);
         return d;

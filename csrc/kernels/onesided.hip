@@ -106,16 +106,17 @@ __device__ void begin_role(const Args& a) {
   sys_store(loc + L.state(kBegun), seq + 1u);
 }
 
-// Every other role: wait for begin, return the call's round.
-__device__ uint32_t wait_begun(const Args& a) {
-  __shared__ uint32_t r_s;
+// Every other role: wait for begin, return the call's round and call id.
+__device__ uint2 wait_begun(const Args& a) {
+  __shared__ uint32_t r_s, seq_s;
   if (threadIdx.x == 0) {
     const uint32_t seq = sys_load(a.loc + a.L.state(kCallSeq));
     while (sys_load(a.loc + a.L.state(kBegun)) != seq + 1u) __builtin_amdgcn_s_sleep(1);
     r_s = sys_load(a.loc + a.L.state(kCur));
+    seq_s = seq;
   }
   __syncthreads();
-  return r_s;
+  return make_uint2(r_s, seq_s);
 }
 
 // ---- push: phase 1, fire and forget -----------------------------------------------
@@ -360,13 +361,13 @@ __device__ void masked_sum_n(const Args& a, const char* mine, const char* sd, ch
 // NS == 0: any N.  Returns whether the window stores need a release fence
 // before the tags (plain stores: runtime-N and unaligned bodies).
 template <typename T, int NS>
-__device__ bool masked_sum(const Args& a, int32_t row, uint32_t mask, uint32_t okq, int64_t off, int64_t n) {
+__device__ bool masked_sum(const Args& a, char* out, int32_t row, uint32_t mask, uint32_t okq, int64_t off, int64_t n) {
   constexpr int ES = sizeof(T);
   constexpr int PV = Elt<T>::kPerVec;
   const int32_t N = a.L.N, me = a.me;
   const char* mine = a.in + (a.tab->bstart[me] + off) * ES;
   const char* sd = a.tab->sd[row][me];
-  char* o = a.out + (a.tab->bstart[me] + off) * ES;
+  char* o = out + (a.tab->bstart[me] + off) * ES;
   const int64_t goff = (int64_t(me) * a.slot + off) * ES;  // same offset in every peer's GD row
   const uintptr_t al = uintptr_t(mine) | uintptr_t(o) | uintptr_t(n * ES) | uintptr_t(goff) | uintptr_t(off * ES) |
                        uintptr_t(a.slot * ES);
@@ -429,7 +430,8 @@ __device__ bool masked_sum(const Args& a, int32_t row, uint32_t mask, uint32_t o
 
 // Piece s of part j of my chunk k, once the chunk is decided.
 template <typename T, int NS>
-__device__ void reduce_piece(const Args& a, uint32_t r, int32_t k, int32_t j, int32_t s, bool wait_decision) {
+__device__ void reduce_piece(const Args& a, char* out, uint32_t r, int32_t k, int32_t j, int32_t s,
+                             bool wait_decision) {
   const Layout& L = a.L;
   const int32_t N = L.N, P = L.P, me = a.me;
   const int32_t row = int32_t(r % uint32_t(L.D));
@@ -465,7 +467,7 @@ __device__ void reduce_piece(const Args& a, uint32_t r, int32_t k, int32_t j, in
   const int64_t per = ((n + a.nsub - 1) / a.nsub + 63) / 64 * 64;
   const int64_t lo = min(n, int64_t(s) * per), hi = min(n, lo + per);
   bool fenced = false;
-  if (hi > lo && mask_s != 0u) fenced = masked_sum<T, NS>(a, row, mask_s, okq_s, part_off(a, k, j) + lo, hi - lo);
+  if (hi > lo && mask_s != 0u) fenced = masked_sum<T, NS>(a, out, row, mask_s, okq_s, part_off(a, k, j) + lo, hi - lo);
   // (uniform: the alignment of a piece is the same for every thread)
   if (fenced) release_wg();
   else drain_wg();
@@ -485,12 +487,12 @@ __device__ void reduce_piece(const Args& a, uint32_t r, int32_t k, int32_t j, in
 }
 
 template <typename T, int NS>
-__device__ void reduce_role(const Args& a, uint32_t r, int32_t w0, int32_t stride) {
+__device__ void reduce_role(const Args& a, char* out, uint32_t r, int32_t w0, int32_t stride) {
   const int32_t P = a.L.P, ns = a.nsub;
   const int32_t items = a.kme * P * ns;
   for (int32_t w = w0; w < items; w += stride) {
     const int32_t k = w / (P * ns), j = (w / ns) % P, s = w % ns;
-    reduce_piece<T, NS>(a, r, k, j, s, true);
+    reduce_piece<T, NS>(a, out, r, k, j, s, true);
   }
 }
 
@@ -599,7 +601,7 @@ __device__ void complete_role(const Args& a, uint32_t r) {
 // that never landed, my own chunk reduced too late -- so the zeroing is
 // spread over the copy workgroups instead of a pass of its own.
 template <int ES>
-__device__ void copy_role(const Args& a, uint32_t r, int32_t w0, int32_t stride) {
+__device__ void copy_role(const Args& a, char* out, bool in_place, uint32_t r, int32_t w0, int32_t stride) {
   const Layout& L = a.L;
   const int32_t N = L.N, P = L.P, me = a.me;
   const int32_t peer_items = (N - 1) * L.Kmax * P;
@@ -614,7 +616,8 @@ __device__ void copy_role(const Args& a, uint32_t r, int32_t w0, int32_t stride)
     }
     return Item{me, (w - peer_items) / P, (w - peer_items) % P};
   };
-  for (int32_t w = w0; w < peer_items; w += stride) {
+  // (window output, in place: the peers' parts landed at their final offsets)
+  for (int32_t w = in_place ? peer_items : w0; w < peer_items; w += stride) {
     const auto [p, k, j] = item(w);
     if (k >= a.tab->nch[p]) continue;
     if (threadIdx.x == 0) {
@@ -653,7 +656,7 @@ __device__ void copy_role(const Args& a, uint32_t r, int32_t w0, int32_t stride)
     const int64_t n = part_len_of(a, p, k, j);
     if (act && n > 0) {
       const int64_t off = part_off(a, k, j);
-      copy_in(a.out + (a.tab->bstart[p] + off) * ES, a.tab->gd[row][me] + (int64_t(p) * a.slot + off) * ES, n * ES);
+      copy_in(out + (a.tab->bstart[p] + off) * ES, a.tab->gd[row][me] + (int64_t(p) * a.slot + off) * ES, n * ES);
     }
     __syncthreads();  // `act` is rewritten by the next item
   }
@@ -695,7 +698,7 @@ __device__ void copy_role(const Args& a, uint32_t r, int32_t w0, int32_t stride)
     __syncthreads();
     const int64_t n = part_len_of(a, p, k, j);
     if (act && n > 0) {
-      char* o = a.out + (a.tab->bstart[p] + part_off(a, k, j)) * ES;
+      char* o = out + (a.tab->bstart[p] + part_off(a, k, j)) * ES;
       if (p == me && a.own_wt && ((uintptr_t(o) | uintptr_t(n * ES)) & 15) == 0) {
         // my own part: written through, after the reduce pieces' own
         // write-through stores (another XCD's): memory ends with the zeros
@@ -756,19 +759,32 @@ __global__ __launch_bounds__(LB) void os_round_kernel(Args a) {
   if (b == 0) {
     begin_role(a);
   } else {
-    const uint32_t r = wait_begun(a);
+    const uint2 rs = wait_begun(a);
+    const uint32_t r = rs.x;
     if (a.tl) t1 = wall_clock64();
+    // Window output (exact rounds, no caller buffer): the call's output is
+    // the gather row of ITS call id in my own window, where the peers'
+    // reduced parts land at their final offsets (slot == block step) and my
+    // reduce writes my block -- no copy.  A call that served another round
+    // (catch-up) copies into that row like a caller buffer.
+    char* out = a.out;
+    bool in_place = false;
+    if (a.wo) {
+      const int32_t vrow = int32_t(rs.y % uint32_t(a.L.D));
+      out = a.tab->gd[vrow][a.me];
+      in_place = vrow == int32_t(r % uint32_t(a.L.D));
+    }
     b -= 1;
     if (b < a.gp) {
       push_role<ES>(a, r, b, a.gp);
     } else if ((b -= a.gp) < a.kme) {
       decide_role(a, r, b);
     } else if ((b -= a.kme) < a.gr) {
-      reduce_role<T, NS>(a, r, b, a.gr);
+      reduce_role<T, NS>(a, out, r, b, a.gr);
     } else if ((b -= a.gr) == 0) {
       complete_role(a, r);
     } else {
-      copy_role<ES>(a, r, b - 1, a.gq);
+      copy_role<ES>(a, out, in_place, r, b - 1, a.gq);
     }
   }
   if (a.tl && threadIdx.x == 0) {  // vector stores (one lane)
@@ -793,7 +809,7 @@ __global__ __launch_bounds__(LB) void os_reduce_bench_kernel(Args a, uint32_t r)
   const int32_t P = a.L.P, ns = a.nsub;
   const int32_t items = a.kme * P * ns;
   for (int32_t w = blockIdx.x; w < items; w += gridDim.x)
-    reduce_piece<T, NS>(a, r, w / (P * ns), (w / ns) % P, w % ns, false);
+    reduce_piece<T, NS>(a, a.out, r, w / (P * ns), (w / ns) % P, w % ns, false);
 }
 
 template <typename F>

@@ -61,6 +61,9 @@ struct Args {
   // system-scope release before every flag, a system-scope acquire after
   // every observed flag: the HIP memory model's protocol, xgmi_device.h)
   int32_t fenced = 0;
+  // window output: the call's output is the gather row (call id % D) of my
+  // own window (exact rounds; `out` unused), see os_round_kernel
+  int32_t wo = 0;
   uint64_t timeout = 0;                 // per wait, wall-clock ticks
   const char* in = nullptr;                // round input [S]
   char* out = nullptr;                     // round output [S]

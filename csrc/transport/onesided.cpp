@@ -161,6 +161,12 @@ OneSidedLane::OneSidedLane(int32_t device, int64_t S, int32_t N, int64_t C, int3
   need_r_ = std::clamp(float_threshold(p.th_reduce, N), 1, N);
   const int64_t total = g_.total_chunks();
   need_c_ = int32_t(std::clamp<int64_t>(float_threshold(p.th_complete, total), 1, std::max<int64_t>(total, 1)));
+  // window output: gather rows laid out as the output itself (slot = step,
+  // block p at p * step), exact thresholds only (nothing is ever zeroed in
+  // place while a late writer could still be storing into the row)
+  wo_ = p.window_output && device >= 0 && need_r_ == N && need_c_ == total && g_.step > 0 &&
+        (g_.step * int64_t(es_)) % 16 == 0;
+  if (wo_) slot_ = g_.step;
   AKKA_CHECK(P_ <= kMaxParts, "onesided lane: too many parts per chunk");
   AKKA_CHECK(int64_t(D_) * N * Kmax_ * P_ <= (int64_t(1) << 22),
              "onesided lane: " + std::to_string(int64_t(D_) * N * Kmax_ * P_) +
@@ -539,6 +545,7 @@ void OneSidedLane::unlink() {
 int64_t OneSidedLane::round(uintptr_t stream, const void* in, void* out, int32_t* counts, int32_t kcols) {
   AKKA_CHECK(ready_, "onesided lane: open() the peer windows first");
   AKKA_CHECK(kcols >= Kmax_, "onesided lane: counts table has too few columns");
+  AKKA_CHECK(out != nullptr || wo_, "onesided lane: a call without an output buffer needs the window output");
   if (device_ >= 0) {
     // A call captured into a graph runs no kernel now: the device's call
     // sequence advances once per REPLAY (note_replays), so the host's call
@@ -581,6 +588,7 @@ void OneSidedLane::gpu_call(uintptr_t stream, const char* in, char* out, int32_t
   a.nsub = nsub_;
   a.own_wt = need_c_ < g_.total_chunks() ? 1 : 0;
   a.fenced = p_.fenced ? 1 : 0;
+  a.wo = (wo_ && out == nullptr) ? 1 : 0;
   a.timeout = timeout_ticks_;
   a.in = in;
   a.out = out;

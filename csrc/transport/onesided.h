@@ -59,6 +59,12 @@ struct OneSidedParams {
   // (write-through + drain), true "fenced" (plain stores + system release /
   // acquire).  AKKA_OS_HANDOFF=fenced|lite overrides it at construction.
   bool fenced = false;
+  // Exact rounds only: a call without a caller buffer returns the gather row
+  // of its call id in this rank's own window -- the peers' reduced parts
+  // land there at their final offsets, so no copy (Python: the output of
+  // call c stays valid until call c + 1).  Taken when the thresholds are 1
+  // and a block's byte size is a 16-byte multiple; window_output() says.
+  bool window_output = false;
 };
 
 class OneSidedLane {
@@ -108,6 +114,9 @@ class OneSidedLane {
   // share the tags, so ranks may switch independently).
   void set_fenced(bool on) { p_.fenced = on; }
   bool fenced() const { return p_.fenced; }
+  bool window_output() const { return wo_; }
+  // Base of my own gather row `row` (window output: call c's output is row c % D).
+  void* gather_row(int32_t row) const { return gd_[size_t(row)]; }
 
   // ---- CPU backend, step by step (the deterministic replay harness) ----------
   // begin(): start a round (non-blocking), returns its call id; progress():
@@ -223,6 +232,7 @@ class OneSidedLane {
   std::string mem_kind_;
   bool ready_ = false;
   std::vector<uint8_t> absent_;  // [N]: not mapped yet (partial membership)
+  bool wo_ = false;              // window output (OneSidedParams::window_output, granted)
   int64_t calls_ = 0;
   uint64_t timeout_ticks_ = 0;
 

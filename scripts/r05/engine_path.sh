@@ -14,7 +14,7 @@ LANE=${2:-ipc_fused_lite}
 SIZES=${3:-64,256}
 mkdir -p $O
 port=29701
-for L in ipc ipc_sync ipc_direct onesided; do
+for L in ${LANES:-ipc ipc_sync ipc_direct onesided}; do
   mkdir -p $O/time_$L $O/trace_$L $O/ot_$L
   port=$((port+1))
   timeout -k 10 200 python -m torch.distributed.run --nnodes=1 --nproc-per-node=4 --master-addr 127.0.0.1 \
@@ -31,7 +31,7 @@ done
 python - <<PY | tee $O/summary.txt
 import json, glob
 rows = {}
-for L in ("ipc", "ipc_sync", "ipc_direct", "onesided"):
+for L in "${LANES:-ipc ipc_sync ipc_direct onesided}".split():
     for f in sorted(glob.glob("$O/time_%s/rank*.json" % L)):
         d = json.load(open(f))
         for c in d["cases"]:

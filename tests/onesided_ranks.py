@@ -85,6 +85,7 @@ def main():
     ap.add_argument("--part-bytes", type=int, default=256 << 10)
     ap.add_argument("--timeout-s", type=float, default=30.0)
     ap.add_argument("--handoff", default="lite", choices=["lite", "fenced"])
+    ap.add_argument("--window-output", action="store_true", help="exact: calls without out return window rows")
     ap.add_argument("--out-dir", required=True)
     a = ap.parse_args()
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
@@ -102,7 +103,7 @@ def main():
     th = 1.0 if a.mode in ("exact", "dead") else a.th
     ar = OneSidedAllreduce(a.size, max_chunk_size=a.chunk, dtype=dtype, th_reduce=th, th_complete=th,
                            max_lag=a.max_lag, device=dev, rows=a.rows, part_bytes=a.part_bytes,
-                           timeout_s=a.timeout_s, handoff=a.handoff)
+                           timeout_s=a.timeout_s, handoff=a.handoff, window_output=a.window_output)
     res = {"rank": rank, "info": ar.info()}
 
     def sync():
@@ -125,6 +126,9 @@ def main():
             ok = torch.equal(o.data.cpu(), want.to(dtype)) and bool((o.count.cpu() == world).all())
             res["exact"].append(bool(ok))
             res["rounds"].append(o.iteration)
+            if ar.window_output:  # the output IS the window row of this call's id
+                res.setdefault("in_window", []).append(
+                    o.data.data_ptr() == ar._rows[r % len(ar._rows)].data_ptr())
         if a.timeline:
             tl = ar.lane.timeline()
             g = ar.info()["role_wgs"]

@@ -33,6 +33,28 @@ def test_onesided_gpu_exact_rounds(n, size, chunk, dtype, handoff):
         assert d["error"] == 0 and d["stats"]["missing_chunks"] == 0, d["stats"]
 
 
+@pytest.mark.parametrize("n,size,chunk,dtype,wo", [
+    (2, 1 << 20, 1 << 16, "float32", True),
+    (4, 1 << 24, 1 << 20, "float32", True),    # 64 MiB, 4 MiB chunks
+    (8, 1 << 22, 1 << 17, "bfloat16", True),
+    (3, 1_000_003, 40_000, "float32", False),  # a block's bytes not a 16-B multiple: the classic copy
+])
+@pytest.mark.parametrize("handoff", ["lite", "fenced"])
+def test_onesided_gpu_window_output(n, size, chunk, dtype, wo, handoff):
+    """Exact rounds whose output is the gather row of the call in the rank's
+    own window (no copy): bitwise the fp32 sum, counts N, rounds in order,
+    each output the row of its call id (rows cycle)."""
+    r, rows = run_ranks(n, "--mode", "exact", "--size", str(size), "--chunk", str(chunk), "--dtype", dtype,
+                        "--rounds", "5", "--timeout-s", "10", "--window-output", "--handoff", handoff,
+                        device="cuda", timeout=180)
+    assert r.returncode == 0, r.stderr[-3000:]
+    for d in rows:
+        assert d["info"]["window_output"] is wo, d["info"]
+        assert d["exact"] == [True] * 5 and d["rounds"] == list(range(5)), d
+        assert d.get("in_window", [True] * 5 if wo else None) == ([True] * 5 if wo else None), d
+        assert d["error"] == 0 and d["stats"]["missing_chunks"] == 0, d["stats"]
+
+
 def test_onesided_gpu_exact_rounds_async():
     """async_op=True: the round runs on the lane's side stream behind the
     caller's stream (the input's host-to-device copy); wait() joins it."""
