@@ -22,6 +22,10 @@ def main():
     ap.add_argument("--cu-keep", type=int, default=6)
     ap.add_argument("--transport", default="onesided", choices=["onesided", "stream"])
     ap.add_argument("--data-plane", default="ipc", help="stream transport: rccl | ipc")
+    ap.add_argument("--modes", default="sync,async", help="comma list (one process per mode avoids the second "
+                                                          "mode inheriting the first one's engines and windows)")
+    ap.add_argument("--lane", default="", help="stream transport: the hook's lane for every bucket engine "
+                                                  "(ThresholdAllreduce.LANES), e.g. ipc_fused_lite")
     a = ap.parse_args()
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     dist.init_process_group("gloo")
@@ -30,13 +34,15 @@ def main():
     from akka_allreduce_amd.models.mlp import MLP, synthetic_batch
     from akka_allreduce_amd.parallel.ddp import ThresholdHookState, threshold_allreduce_hook
 
-    for mode in ("sync", "async"):
+    for mode in a.modes.split(","):
         torch.manual_seed(0)
         model = torch.nn.parallel.DistributedDataParallel(MLP(4096, 8192, 1000).to(dev), device_ids=[dev.index],
                                                           bucket_cap_mb=a.bucket_mb)
         state = ThresholdHookState(transport=a.transport, max_chunk_size=1 << 20, async_op=(mode == "async"),
                                    bucket_cap_mb=a.bucket_mb, onesided_options={"cu_keep": a.cu_keep},
                                    data_plane=a.data_plane if a.transport == "stream" else "rccl")
+        if a.lane:
+            state.lane = a.lane  # applied to every bucket's engine (ThresholdHookState.engine)
         model.register_comm_hook(state, threshold_allreduce_hook)
         opt = torch.optim.SGD(model.parameters(), lr=0.05)
         g = torch.Generator(device=dev).manual_seed(100 + rank)
@@ -60,7 +66,8 @@ def main():
         dist.all_gather_object(t, dt)
         errs = [ar._os.error() if ar.transport == "onesided" else ar.ipc_error() for ar in state.engines.values()]
         if rank == 0:
-            print(json.dumps({"mode": mode, "transport": a.transport, "world": world, "ms_per_step": round(max(t) / a.steps * 1e3, 3),
+            print(json.dumps({"mode": mode, "transport": a.transport, "lane": a.lane or None, "world": world,
+                              "ms_per_step": round(max(t) / a.steps * 1e3, 3),
                               "buckets": len(state.engines), "async_rounds": state.async_rounds,
                               "rounds": state.rounds, "lane_errors": errs}), flush=True)
         del model, state, opt
