@@ -97,9 +97,15 @@ def _demo(a: argparse.Namespace) -> int:
                                         "--checkpoint", str(a.checkpoint), "--assert-multiple",
                                         str(a.assert_multiple), "--device", "cpu"]) for _ in range(a.workers)]
     rc = 0
-    for p in workers:
-        rc |= p.wait(timeout=a.timeout)
-    rc |= master.wait(timeout=a.timeout)
+    try:
+        for p in workers:
+            rc |= p.wait(timeout=a.timeout)
+        rc |= master.wait(timeout=a.timeout)
+    finally:  # a timeout or ^C must not leave the master or a worker behind
+        for p in [master, *workers]:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
     return rc
 
 

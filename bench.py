@@ -441,6 +441,9 @@ def run_cfg1(rounds: int = 300, gpu: bool = False) -> dict:
     import subprocess
     import tempfile
 
+    from akka_allreduce_amd._native_loader import load as _load_native
+
+    wd = _load_native()
     base = [sys.executable, "-m", "akka_allreduce_amd", "--log-level", "WARNING"]
     cp = max(1, rounds // 3)
     res = {"workers": 2, "data_size": 10, "max_chunk_size": 2, "max_lag": 1, "rounds": rounds,
@@ -459,6 +462,7 @@ def run_cfg1(rounds: int = 300, gpu: bool = False) -> dict:
                                               "--th-reduce", "1.0", "--th-complete", str(thc), "--transport",
                                               mtransport],
                                       stdout=logs[0], stderr=subprocess.STDOUT, cwd=os.path.dirname(__file__) or ".")]
+            wd.watchdog_track_child(procs[0].pid)  # a watchdog exit of this rank takes the job down too
             t_end = time.time() + 20
             while time.time() < t_end:  # master listening?
                 try:
@@ -471,6 +475,8 @@ def run_cfg1(rounds: int = 300, gpu: bool = False) -> dict:
                                                "--checkpoint", str(cp), "--assert-multiple", str(mult), "--device",
                                                wdev, *wextra], stdout=logs[i], stderr=subprocess.STDOUT,
                                        cwd=os.path.dirname(__file__) or ".") for i in (1, 2)]
+            for p in procs[1:]:
+                wd.watchdog_track_child(p.pid)
             rcs = []
             try:
                 for p in procs:
@@ -480,6 +486,7 @@ def run_cfg1(rounds: int = 300, gpu: bool = False) -> dict:
                     if p.poll() is None:
                         p.kill()
                         p.wait()
+                    wd.watchdog_untrack_child(p.pid)
             entry = {"rcs": rcs, "rounds_per_s": [], "sink_MBps": [], "failures": [], "workers_on": wdev,
                      "data_plane": "one-sided lane (GPU windows)" if wtransport == "onesided" else "tcp"}
             for f in logs[1:]:

@@ -793,6 +793,8 @@ PYBIND11_MODULE(_native, m) {
   m.def("watchdog_disarm", &watchdog_disarm);
   m.def("watchdog_set_out_fd", &watchdog_set_out_fd);
   m.def("watchdog_install_sigterm", &watchdog_install_sigterm);
+  m.def("watchdog_track_child", &watchdog_track_child, py::arg("pid"));
+  m.def("watchdog_untrack_child", &watchdog_untrack_child, py::arg("pid"));
   m.def("json_escape", &json_escape);
   m.def("hw_queue_probe", [](int32_t kmax, int32_t wait_ms) {
     // How many streams can be parked on a wait-value before a fresh stream

@@ -30,6 +30,10 @@ struct State {
   int tail_bytes = 4096;
   int pipe_r = -1, pipe_w = -1;
   bool started = false;
+  // child processes to take down with this one (watchdog_track_child): a
+  // watchdog exit skips every Python `finally`, and a child left behind (a
+  // master of bench.py's cluster configs) would run on without its parent
+  std::atomic<int> children[16] = {};
 };
 
 State& st() {
@@ -67,6 +71,13 @@ void replace_token(std::string& s, const std::string& token, const std::string& 
   if (pos != std::string::npos) s.replace(pos, token.size(), value);
 }
 
+void kill_children() {
+  for (auto& c : st().children) {
+    const int pid = c.exchange(0);
+    if (pid > 0) ::kill(pid, SIGKILL);
+  }
+}
+
 [[noreturn]] void fire(const std::string& reason) {
   State& S = st();
   std::string line, path;
@@ -88,6 +99,7 @@ void replace_token(std::string& s, const std::string& token, const std::string& 
   write_all(2, "akka watchdog: " + reason + "; exiting " + std::to_string(code) + "\n");
   if (!tail.empty()) write_all(2, "---- tail of " + path + " ----\n" + tail + "\n");
   ::fsync(1);
+  kill_children();
   ::_exit(code);
 }
 
@@ -153,6 +165,7 @@ void loop() {
           fire("SIGTERM after a failure reported by a rank: " + what);
         }
         if (was_armed) fire("SIGTERM");
+        kill_children();
         ::_exit(128 + SIGTERM);
       }
     }
@@ -233,6 +246,21 @@ void watchdog_disarm() {
     S.armed = false;
   }
   wake();
+}
+
+bool watchdog_track_child(int pid) {
+  for (auto& c : st().children) {
+    int z = 0;
+    if (c.compare_exchange_strong(z, pid)) return true;
+  }
+  return false;
+}
+
+void watchdog_untrack_child(int pid) {
+  for (auto& c : st().children) {
+    int v = pid;
+    c.compare_exchange_strong(v, 0);
+  }
 }
 
 void watchdog_install_sigterm() {

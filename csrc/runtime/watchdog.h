@@ -34,6 +34,10 @@ void watchdog_disarm();
 // Route SIGTERM through the watchdog: the armed line is written (reason
 // "SIGTERM") before the process exits; unarmed, it exits with 128+15.
 void watchdog_install_sigterm();
+// Child processes killed (SIGKILL) when the watchdog ends this process
+// (deadline, beacon or SIGTERM).  At most 16; false when the table is full.
+bool watchdog_track_child(int pid);
+void watchdog_untrack_child(int pid);
 // Expose the escaping used for the tail (tests).
 std::string json_escape(const std::string& s);
 

@@ -111,9 +111,24 @@ def test_bench_n8_full_flow():
 
 
 def test_bench_multirank_extras_deadline():
+    """The extras' deadline ends every rank mid-config: the processes rank 0
+    started for config 1 (a master and 2 workers, bench.run_cfg1) must not
+    outlive it (the native watchdog kills the children it tracks)."""
+    import time
+
+    import psutil
+
+    t0 = time.time()
     d = _run(2, "--extras", "on", "--extras-deadline-s", "0.05")
     assert d["exact"] is True and "extras_error" in d and "extra_configs" not in d
     assert d["value"] > 0
+    time.sleep(0.5)
+    left = []
+    for p in psutil.process_iter(["pid", "ppid", "cmdline", "create_time"]):
+        cmd = " ".join(p.info["cmdline"] or [])
+        if p.info["ppid"] == 1 and "akka_allreduce_amd" in cmd and p.info["create_time"] >= t0 - 1:
+            left.append((p.info["pid"], cmd[:120]))
+    assert not left, left
 
 
 def test_bench_stalled_rank_fails_legibly():
