@@ -386,13 +386,19 @@ class ThresholdAllreduce:
     def runs_async(self) -> bool:
         """Whether the DDP hook should issue ``async_op=True`` rounds (then
         ``async_stream()`` is where their results complete).  Not on the
-        one-sided lane: its round keeps a wave on every SIMD while it waits
-        for peers, so the backward kernels an async round would overlap wait
-        for it anyway, and the side-stream hand-offs cost more than they save
-        (bench/ddp_overlap.py, 2 ranks: 3.11 ms per DDP step sync vs 4.57
-        async; profiles/r04/README.md).  ``OneSidedAllreduce(async_op=True)``
-        stays available."""
-        if self.transport == "onesided" or self._lane_os or getattr(self, "_ipc_direct", False):
+        one-sided lane with its full grid: its round keeps a wave on every
+        SIMD while it waits for peers, so the backward kernels an async round
+        would overlap wait for it anyway, and the side-stream hand-offs cost
+        more than they save (bench/ddp_overlap.py, 2 ranks: 3.11 ms per DDP
+        step sync vs 4.57 async; profiles/r04/README.md).  Yes with a bounded
+        footprint on a GPU of its own (``onesided_options={"cu_keep": k}``):
+        the round then holds k of every 8 CUs and the backward runs on the
+        rest.  Not on the direct ipc lanes (full grid, caller's stream)."""
+        if self.transport == "onesided":
+            return self._os.bounded_footprint
+        if self._lane_os:
+            return self._exact_os.bounded_footprint
+        if getattr(self, "_ipc_direct", False):
             return False
         return self.transport == "stream"
 

@@ -27,7 +27,10 @@ protocol code, so multi-process CPU tests cover the GPU's decisions.
 Ranks sharing one GPU (tests, rehearsals) that also run compute between
 calls should pass ``cu_keep=6``: the round then runs on 6 of every 8 CUs, so
 a round waiting on its peers cannot hold every SIMD while a peer's GEMM
-needs one (csrc/transport/onesided.h, ``OneSidedParams::cu_keep``).
+needs one (csrc/transport/onesided.h, ``OneSidedParams::cu_keep``).  On a
+GPU of its own ``cu_keep=k`` bounds the round's footprint to k of every 8
+CUs (its grid sized for them): ``async_op=True`` rounds then overlap compute
+on the other CUs (``bounded_footprint``; the DDP hook issues async rounds).
 
 Usage::
 
@@ -319,6 +322,15 @@ class OneSidedAllreduce:
     def window_output(self) -> bool:
         """Calls without ``out`` return a window row (valid until the next call)."""
         return self._rows is not None
+
+    @property
+    def bounded_footprint(self) -> bool:
+        """The round runs on a subset of the CUs of a GPU of its own
+        (``cu_keep``): an async round leaves the other CUs to the kernels it
+        overlaps (the DDP backward), so a hook should issue async rounds."""
+        i = self.lane.info()
+        dedicated = int(i.get("ranks_on_this_gpu", 1)) <= 1 or os.environ.get("AKKA_OS_DEDICATED") == "1"
+        return int(i.get("lane_cus", 0)) > 0 and dedicated
 
     @property
     def handoff(self) -> str:

@@ -429,16 +429,8 @@ void OneSidedLane::open(const std::vector<std::string>& handles) {
     }
     map_peer(q, h);
   }
-  if (device_ >= 0 && p_.role_wgs <= 0 && !std::getenv("AKKA_OS_ROLE_WGS")) {
-    // Ranks sharing this GPU (tests / rehearsals on a 1-GPU box): every
-    // rank's round launch must fit on the card at once, or one rank's
-    // waiting workgroups could hold the slots another rank's pushers need.
-    // Budget: 768 of the card's ~1024 resident 256-thread workgroups (103
-    // VGPRs: 4 per CU) for all sharing ranks' grids together (pass F sweep,
-    // profiles/r04/README.md: 512 / 768 / 1024 -> 1.26 / 1.15 / 1.44 ms at
-    // 256 MiB, 4 ranks).  (Members only: a rank joining later keeps the
-    // grid this one was sized for.)
-    int32_t share = 0;
+  if (device_ >= 0) {
+    int32_t share = 0;  // member ranks on this GPU (tests / rehearsals on a 1-GPU box)
     for (int32_t q = 0; q < g_.N; ++q) {
       if (handles[size_t(q)].empty()) continue;
       Blob b;
@@ -446,36 +438,28 @@ void OneSidedLane::open(const std::vector<std::string>& handles) {
       share += std::strncmp(b.bus, my_bus_.c_str(), sizeof(b.bus)) == 0;
     }
     shared_ranks_ = share;
-    if (share > 1) {
+    const char* kv = std::getenv("AKKA_OS_CU_KEEP");  // CUs kept of every 8 (measurement knob)
+    const int32_t keep = kv ? std::clamp(std::atoi(kv), 0, 8) : std::clamp(p_.cu_keep, 0, 8);
+    // (AKKA_OS_DEDICATED=1: size as on a GPU of its own although ranks share
+    // this one -- the tests' way to run that path on a 1-GPU box)
+    const bool dedicated = share <= 1 || (std::getenv("AKKA_OS_DEDICATED") &&
+                                          std::strcmp(std::getenv("AKKA_OS_DEDICATED"), "1") == 0);
+    int32_t ncu = 0;
+    if (keep > 0 && keep < 8) ncu = make_cu_stream(keep);
+    const bool auto_roles = p_.role_wgs <= 0 && !std::getenv("AKKA_OS_ROLE_WGS");
+    if (auto_roles && !dedicated) {
+      // Ranks sharing this GPU: every rank's round launch must fit on the
+      // card at once, or one rank's waiting workgroups could hold the slots
+      // another rank's pushers need.  Budget: 768 of the card's ~1024
+      // resident 256-thread workgroups (103 VGPRs: 4 per CU) for all sharing
+      // ranks' grids together (pass F sweep, profiles/r04/README.md: 512 /
+      // 768 / 1024 -> 1.26 / 1.15 / 1.44 ms at 256 MiB, 4 ranks).  (Members
+      // only: a rank joining later keeps the grid this one was sized for.)
       // 256-thread workgroups (AKKA_OS_THREADS=1024 to measure: the budget
       // then counts 1024-thread workgroups, a quarter as many)
       const char* tv = std::getenv("AKKA_OS_THREADS");
       nt_ = (tv && std::atoi(tv) >= 1024) ? 1024 : 256;
-      const char* kv = std::getenv("AKKA_OS_CU_KEEP");  // CUs kept of every 8 (measurement knob)
-      const int32_t keep = kv ? std::clamp(std::atoi(kv), 0, 8) : std::clamp(p_.cu_keep, 0, 8);
-      int64_t total_default = 768;
-      if (keep > 0 && keep < 8) {
-        hipDeviceProp_t prop;
-        AKKA_OS_HIP(hipGetDeviceProperties(&prop, device_));
-        const int32_t ncu = std::max(1, prop.multiProcessorCount);
-        std::vector<uint32_t> mask(size_t((ncu + 31) / 32), 0u);
-        int32_t on = 0;
-        for (int32_t cu = 0; cu < ncu; ++cu)
-          if (cu % 8 < keep) {  // spread over every XCD / SE, the rest of each group left free
-            mask[size_t(cu / 32)] |= 1u << (cu % 32);
-            ++on;
-          }
-        hipStream_t s = nullptr;
-        AKKA_OS_HIP(hipExtStreamCreateWithCUMask(&s, uint32_t(mask.size()), mask.data()));
-        cu_stream_ = s;
-        hipEvent_t e0 = nullptr, e1 = nullptr;
-        AKKA_OS_HIP(hipEventCreateWithFlags(&e0, hipEventDisableTiming));
-        AKKA_OS_HIP(hipEventCreateWithFlags(&e1, hipEventDisableTiming));
-        ev_in_ = e0;
-        ev_out_ = e1;
-        lane_cus_ = on;
-        total_default = 768 * int64_t(on) / ncu;  // the same density on the masked CUs
-      }
+      const int64_t total_default = ncu > 0 ? 768 * int64_t(lane_cus_) / ncu : 768;  // same density on masked CUs
       const char* bv = std::getenv("AKKA_OS_SHARED_BUDGET");  // measurement knob (resident 256-thread WGs)
       const int64_t total = bv ? std::max(16, std::atoi(bv)) : total_default;
       const int64_t budget = total * 256 / nt_ / share - 2 - g_.num_chunks(me_);
@@ -487,6 +471,11 @@ void OneSidedLane::open(const std::vector<std::string>& handles) {
       }
       const int64_t unit = std::max<int64_t>(1, budget / (sp + sr + sc));
       size_roles(std::max<int64_t>(1, unit * sr / 2), unit * sp, unit * sc);
+    } else if (auto_roles && ncu > 0) {
+      // A GPU of its own with a bounded footprint (comm/compute overlap):
+      // the default grid's density on the kept CUs, the rest of every group
+      // of 8 left to the compute kernels the round overlaps
+      size_roles(std::max<int64_t>(8, kDefaultRoleWgs * lane_cus_ / ncu));
     }
   }
   write_tables();
@@ -564,6 +553,32 @@ int64_t OneSidedLane::round(uintptr_t stream, const void* in, void* out, int32_t
     us = std::min(us * 2, 200);  // (a coarser back-off adds up to its cap to a round that waited)
   }
   return call;
+}
+
+// The round launch's CU-masked stream: `keep` of every 8 CUs, spread over
+// every XCD / shader engine, plus the fork / join events.  Returns the
+// device's CU count (lane_cus_ = CUs kept).
+int32_t OneSidedLane::make_cu_stream(int32_t keep) {
+  hipDeviceProp_t prop;
+  AKKA_OS_HIP(hipGetDeviceProperties(&prop, device_));
+  const int32_t ncu = std::max(1, prop.multiProcessorCount);
+  std::vector<uint32_t> mask(size_t((ncu + 31) / 32), 0u);
+  int32_t on = 0;
+  for (int32_t cu = 0; cu < ncu; ++cu)
+    if (cu % 8 < keep) {
+      mask[size_t(cu / 32)] |= 1u << (cu % 32);
+      ++on;
+    }
+  hipStream_t s = nullptr;
+  AKKA_OS_HIP(hipExtStreamCreateWithCUMask(&s, uint32_t(mask.size()), mask.data()));
+  cu_stream_ = s;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  AKKA_OS_HIP(hipEventCreateWithFlags(&e0, hipEventDisableTiming));
+  AKKA_OS_HIP(hipEventCreateWithFlags(&e1, hipEventDisableTiming));
+  ev_in_ = e0;
+  ev_out_ = e1;
+  lane_cus_ = on;
+  return ncu;
 }
 
 void OneSidedLane::gpu_call(uintptr_t stream, const char* in, char* out, int32_t* counts, int32_t kcols) {

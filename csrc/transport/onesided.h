@@ -48,12 +48,14 @@ struct OneSidedParams {
   int64_t timeout_ms = 30000;            // bound of every wait (then forced + error)
   int32_t threads = 256;                 // workgroup size of the round launch (256 or 1024)
   int32_t role_wgs = 0;                  // workgroups per data role (push / reduce / copy); 0: automatic
-  // Ranks sharing one GPU that also run compute kernels (a DP step): keep the
-  // round launch on `cu_keep` of every 8 CUs (a CU-masked stream), so a round
+  // Keep the round launch on `cu_keep` of every 8 CUs (a CU-masked stream).
+  // Ranks sharing one GPU that also run compute kernels (a DP step): a round
   // waiting on its peers cannot hold every SIMD while a PEER's kernels that
-  // need a whole SIMD's registers (fp32 MFMA GEMMs) wait for one.  0: no mask
-  // (a rank on a GPU of its own never needs one; the mask costs the
-  // shared-card round ~0.25 ms at 64 MiB, profiles/r04/README.md)
+  // need a whole SIMD's registers (fp32 MFMA GEMMs) wait for one (the mask
+  // costs the shared-card round ~0.25 ms at 64 MiB, profiles/r04/README.md).
+  // A rank on a GPU of its own: the bounded footprint that lets an async
+  // round overlap the backward on the other CUs (the role grid is sized for
+  // the kept CUs).  0: no mask.
   int32_t cu_keep = 0;
   // Hand-off mode of window bytes (os::Args::fenced): false "lite"
   // (write-through + drain), true "fenced" (plain stores + system release /
@@ -156,7 +158,7 @@ class OneSidedLane {
   int32_t pieces() const { return nsub_; }
   int32_t threads() const { return nt_; }
   int32_t shared_ranks() const { return shared_ranks_; }
-  // CUs the round launch may use when ranks share this GPU (0: all)
+  // CUs the round launch may use (cu_keep; 0: all)
   int32_t lane_cus() const { return lane_cus_; }
   // AKKA_OS_TIMELINE=1 at construction: per workgroup [entry, round known,
   // role done] of the last call (waits for the device), and the clock rate
@@ -197,6 +199,7 @@ class OneSidedLane {
   // wgs: reduce = 2 x wgs; push / copy = wgs unless given
   void size_roles(int64_t wgs, int64_t push_wgs = 0, int64_t copy_wgs = 0);
   void gpu_call(uintptr_t stream, const char* in, char* out, int32_t* counts, int32_t kcols);
+  int32_t make_cu_stream(int32_t keep);
   // CPU roles
   void push(int32_t phase, int32_t dst, int32_t k, int32_t j, uint32_t r, uint32_t cnt, const char* src);
   void exec(const Msg& m, const char* src);
@@ -217,8 +220,8 @@ class OneSidedLane {
   os::Layout L_;
   int32_t D_ = 0, P_ = 1, Kmax_ = 0, need_r_ = 1, need_c_ = 1;
   int32_t nsub_ = 1, nt_ = 256, gp_ = 1, gr_ = 0, gq_ = 1, shared_ranks_ = 1;
-  // OneSidedParams::cu_keep on a shared GPU: the round launch goes to a
-  // CU-masked stream, joined to the caller's stream by events
+  // OneSidedParams::cu_keep: the round launch goes to a CU-masked stream,
+  // joined to the caller's stream by events
   void* cu_stream_ = nullptr;  // hipStream_t
   void* ev_in_ = nullptr;      // hipEvent_t
   void* ev_out_ = nullptr;     // hipEvent_t

@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--model", choices=["mlp", "deep"], default="mlp")
     ap.add_argument("--bucket-mb", type=float, default=0.25)
     ap.add_argument("--transport", choices=["stream", "onesided"], default="stream")
+    ap.add_argument("--cu-keep", type=int, default=0, help="onesided: CUs kept of every 8 (bounded footprint)")
     a = ap.parse_args()
     rank = int(os.environ["RANK"])
     dist.init_process_group("gloo")
@@ -43,7 +44,8 @@ def main():
     torch.manual_seed(0)
     model = torch.nn.parallel.DistributedDataParallel(build_model(a.model).to(dev), device_ids=[0],
                                                       bucket_cap_mb=a.bucket_mb)
-    state = ThresholdHookState(data_plane="ipc", max_chunk_size=1 << 14, tune=a.tune, transport=a.transport)
+    state = ThresholdHookState(data_plane="ipc", max_chunk_size=1 << 14, tune=a.tune, transport=a.transport,
+                               onesided_options={"cu_keep": a.cu_keep} if a.cu_keep else None)
     model.register_comm_hook(state, threshold_allreduce_hook)
     opt = torch.optim.SGD(model.parameters(), lr=0.1)
     for s in range(a.steps):
@@ -62,7 +64,10 @@ def main():
         windows = sorted({ar.state()["link"]["ipc"]["windows_id"] for ar in state.engines.values()})
     # tuned once per hook (the first engine), every engine on the chosen lane
     chosen = [state.lane] if a.tune else []
+    lane_cus = [int(ar._os.info().get("lane_cus", 0)) for ar in state.engines.values()] \
+        if a.transport == "onesided" else []
     torch.save({"flat": flat, "buckets": len(state.engines), "rounds": state.rounds, "ipc_errors": errs,
+                "async_rounds": state.async_rounds, "lane_cus": lane_cus,
                 "chosen": chosen, "transports": state.transports(), "window_sets": len(windows)},
                os.path.join(a.out_dir, f"rank{rank}.pt"))
     dist.barrier()

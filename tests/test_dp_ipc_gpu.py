@@ -110,22 +110,35 @@ def test_torch_ddp_hook_multiprocess(tune, model):
     torch.testing.assert_close(res[0]["flat"], want, rtol=1e-4, atol=1e-5)
 
 
-def test_torch_ddp_hook_onesided_multiprocess():
+@pytest.mark.parametrize("bounded", [False, True])
+def test_torch_ddp_hook_onesided_multiprocess(bounded):
     """The DDP hook on the one-sided threshold lane (thresholds 1 here, so
     every bucket's mean must equal the mean-gradient reference), 2 processes,
-    3 bucket sizes."""
+    3 bucket sizes.  ``bounded``: cu_keep=4 sized as on a GPU of its own
+    (AKKA_OS_DEDICATED=1 on this 1-GPU box): every round runs on 4 of each 8
+    CUs and the hook issues them async (runs_async), overlapping the
+    backward on the other CUs."""
     n, steps = 2, 3
+    env = dict(os.environ)
     with tempfile.TemporaryDirectory() as out:
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
                "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
                os.path.join(ROOT, "tests", "ddp_ranks.py"), "--out-dir", out, "--steps", str(steps),
                "--model", "deep", "--bucket-mb", "0.3", "--transport", "onesided"]
-        r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT)
+        if bounded:
+            cmd += ["--cu-keep", "4"]
+            env["AKKA_OS_DEDICATED"] = "1"
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT, env=env)
         assert r.returncode == 0, r.stderr[-3000:]
         res = [torch.load(os.path.join(out, f"rank{i}.pt"), weights_only=True) for i in range(n)]
+    kept = sum(1 for c in range(torch.cuda.get_device_properties(0).multi_processor_count) if c % 8 < 4)
     for d in res:
         assert d["ipc_errors"] and all(e == 0 for e in d["ipc_errors"]), d
         assert d["buckets"] >= 3 and d["rounds"] >= steps
+        if bounded:
+            assert d["async_rounds"] == d["rounds"] and all(c == kept for c in d["lane_cus"]), d
+        else:
+            assert d["async_rounds"] == 0 and all(c == 0 for c in d["lane_cus"]), d
         assert torch.equal(d["flat"], res[0]["flat"])
     want = _reference(n, steps, torch.device("cuda", 0), "deep")
     torch.testing.assert_close(res[0]["flat"], want, rtol=1e-4, atol=1e-5)
