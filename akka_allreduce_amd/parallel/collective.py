@@ -345,8 +345,9 @@ class ThresholdAllreduce:
             if self.pacer is None:
                 self._round += 1
                 # (async_op: the round is valid in the caller's stream order,
-                # which satisfies wait(); a side stream only adds hand-offs)
-                return self._os(x, out=out)
+                # which satisfies wait(); a side stream only adds hand-offs --
+                # unless the round's footprint is bounded, see runs_async)
+                return self._os(x, out=out, async_op=async_op and self._os.bounded_footprint)
             # paced: wait for round r, call, then report every round this call
             # completed -- the served one and any it skipped by catch-up (the
             # reference force-completes those, W:100-106) -- like
@@ -365,7 +366,7 @@ class ThresholdAllreduce:
         if self._lane_os:
             # exact rounds on the one-sided lane (tune candidate "onesided"):
             # valid in the caller's stream order, like an async round
-            out = self._exact_os(x, out=out)  # (async_op: see the onesided transport above)
+            out = self._exact_os(x, out=out, async_op=async_op and self._exact_os.bounded_footprint)  # (see above)
         elif getattr(self, "_ipc_direct", False):
             out = self._ipc_direct_round(x, out)  # valid in the caller's stream order (satisfies wait())
         else:
@@ -394,8 +395,8 @@ class ThresholdAllreduce:
         footprint on a GPU of its own (``onesided_options={"cu_keep": k}``):
         the round then holds k of every 8 CUs and the backward runs on the
         rest.  Not on the direct ipc lanes (full grid, caller's stream)."""
-        if self.transport == "onesided":
-            return self._os.bounded_footprint
+        if self.transport == "onesided":  # (paced calls wait for their round on the caller's side)
+            return self.pacer is None and self._os.bounded_footprint
         if self._lane_os:
             return self._exact_os.bounded_footprint
         if getattr(self, "_ipc_direct", False):

@@ -328,9 +328,12 @@ class OneSidedAllreduce:
         """The round runs on a subset of the CUs of a GPU of its own
         (``cu_keep``): an async round leaves the other CUs to the kernels it
         overlaps (the DDP backward), so a hook should issue async rounds."""
-        i = self.lane.info()
-        dedicated = int(i.get("ranks_on_this_gpu", 1)) <= 1 or os.environ.get("AKKA_OS_DEDICATED") == "1"
-        return int(i.get("lane_cus", 0)) > 0 and dedicated
+        b = getattr(self, "_bounded", None)
+        if b is None:  # fixed once the windows are open
+            i = self.lane.info()
+            dedicated = int(i.get("ranks_on_this_gpu", 1)) <= 1 or os.environ.get("AKKA_OS_DEDICATED") == "1"
+            b = self._bounded = int(i.get("lane_cus", 0)) > 0 and dedicated
+        return b
 
     @property
     def handoff(self) -> str:
