@@ -64,3 +64,32 @@ def test_sigterm_writes_the_line():
     out, _ = p.communicate(timeout=60)
     assert p.returncode == 4
     assert json.loads(out.strip().splitlines()[-1])["why"] == "SIGTERM"
+
+
+def test_fire_kills_tracked_children():
+    """A watchdog exit skips Python's `finally` blocks: the children a rank
+    registered (bench.py config 1's master and workers) are killed with it,
+    untracked ones are not."""
+    p = _child("import subprocess\n"
+               "def sl(): return subprocess.Popen(['sleep', '120'], stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)\n"
+               "a = sl(); b = sl(); c = sl()\n"
+               "assert n.watchdog_track_child(a.pid) and n.watchdog_track_child(b.pid) and n.watchdog_track_child(c.pid)\n"
+               "n.watchdog_untrack_child(c.pid)\n"
+               "print(a.pid, b.pid, c.pid, flush=True)\n"
+               "n.watchdog_arm(0.5, '{}', True, '', 6, 64)\n"
+               "time.sleep(30)\n")
+    out, _ = p.communicate(timeout=60)
+    assert p.returncode == 6
+    a, b, c = (int(v) for v in out.split()[:3])
+    time.sleep(0.3)
+
+    def alive(pid):
+        try:  # (an orphan killed by SIGKILL is reaped by init: gone, or a zombie)
+            with open(f"/proc/{pid}/stat") as f:
+                return f.read().split(")")[-1].split()[0] != "Z"
+        except FileNotFoundError:
+            return False
+
+    assert not alive(a) and not alive(b)
+    assert alive(c)
+    os.kill(c, signal.SIGKILL)
