@@ -307,7 +307,12 @@ class OneSidedAllreduce:
 
     def _side_stream(self) -> "torch.cuda.Stream":
         if self._side is None:
-            self._side = torch.cuda.Stream(self.device)
+            if self.bounded_footprint:
+                # the lane's CU-masked stream itself (shared by the process's
+                # lanes): async rounds launch there with no fork / join
+                self._side = torch.cuda.ExternalStream(int(self.lane.cu_stream()), device=self.device)
+            else:
+                self._side = torch.cuda.Stream(self.device)
         return self._side
 
     @property

@@ -153,6 +153,7 @@ void bind_onesided(py::module_& m) {
              for (size_t i = 0; i < sizeof(kStatNames) / sizeof(kStatNames[0]); ++i) d[kStatNames[i]] = v[i];
              return d;
            })
+      .def("cu_stream", &OneSidedLane::cu_stream)
       .def("stats_nowait",
            [](OneSidedLane& l) {
              std::vector<uint64_t> v;

@@ -14,6 +14,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <map>
+#include <mutex>
 #include <random>
 #include <thread>
 
@@ -75,12 +77,41 @@ hipStream_t DevFromHost::s = nullptr;
 // behind a lane's waiting round kernel on a shared queue would wait for it.
 hipStream_t host_side_stream(int32_t device) {
   static hipStream_t streams[64] = {};
+  AKKA_CHECK(device >= 0 && device < 64, "onesided lane: device index out of range");
   if (!streams[device]) {
     hipStream_t s = nullptr;
     AKKA_OS_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     streams[device] = s;
   }
   return streams[device];
+}
+
+// The round launches' CU-masked stream of a device: `keep` of every 8 CUs,
+// spread over every XCD / shader engine.  One per (device, keep) for the
+// whole process, never destroyed: every such stream is a hardware queue of
+// its own, and a DP job's lanes (one per bucket size) each with its own
+// would oversubscribe the GPU's queues (then the scheduler time-slices
+// them: 10-20 ms stalls, profiles/r05/bounded/).  Returns the stream and
+// the CUs kept.
+std::pair<hipStream_t, int32_t> cu_mask_stream(int32_t device, int32_t keep) {
+  static std::mutex mu;
+  static std::map<std::pair<int32_t, int32_t>, std::pair<hipStream_t, int32_t>> streams;
+  std::lock_guard<std::mutex> lk(mu);
+  auto it = streams.find({device, keep});
+  if (it != streams.end()) return it->second;
+  hipDeviceProp_t prop;
+  AKKA_OS_HIP(hipGetDeviceProperties(&prop, device));
+  const int32_t ncu = std::max(1, prop.multiProcessorCount);
+  std::vector<uint32_t> mask(size_t((ncu + 31) / 32), 0u);
+  int32_t on = 0;
+  for (int32_t cu = 0; cu < ncu; ++cu)
+    if (cu % 8 < keep) {
+      mask[size_t(cu / 32)] |= 1u << (cu % 32);
+      ++on;
+    }
+  hipStream_t s = nullptr;
+  AKKA_OS_HIP(hipExtStreamCreateWithCUMask(&s, uint32_t(mask.size()), mask.data()));
+  return streams[{device, keep}] = {s, on};
 }
 
 // Memory policy of the protocol functions on the host (shared memory between
@@ -279,8 +310,7 @@ OneSidedLane::~OneSidedLane() {
     hipSetDevice(device_);
     hipDeviceSynchronize();  // none of our kernels may still touch a window
     for (void* m : opened_) hipIpcCloseMemHandle(m);  // (same-process peers: nothing opened)
-    if (cu_stream_) hipStreamDestroy(static_cast<hipStream_t>(cu_stream_));
-    // (side_stream_: the process-wide host_side_stream, never destroyed)
+    // (cu_stream_ / side_stream_: process-wide streams, never destroyed)
     if (tl_dev_) hipFree(tl_dev_);
     if (ev_in_) hipEventDestroy(static_cast<hipEvent_t>(ev_in_));
     if (ev_out_) hipEventDestroy(static_cast<hipEvent_t>(ev_out_));
@@ -441,7 +471,9 @@ void OneSidedLane::open(const std::vector<std::string>& handles) {
     const char* kv = std::getenv("AKKA_OS_CU_KEEP");  // CUs kept of every 8 (measurement knob)
     const int32_t keep = kv ? std::clamp(std::atoi(kv), 0, 8) : std::clamp(p_.cu_keep, 0, 8);
     // (AKKA_OS_DEDICATED=1: size as on a GPU of its own although ranks share
-    // this one -- the tests' way to run that path on a 1-GPU box)
+    // this one -- the tests' way to run that path on a 1-GPU box, with grids
+    // small enough for every sharing rank's to be resident at once: small
+    // buffers or AKKA_OS_ROLE_WGS, see the budget below)
     const bool dedicated = share <= 1 || (std::getenv("AKKA_OS_DEDICATED") &&
                                           std::strcmp(std::getenv("AKKA_OS_DEDICATED"), "1") == 0);
     int32_t ncu = 0;
@@ -555,22 +587,14 @@ int64_t OneSidedLane::round(uintptr_t stream, const void* in, void* out, int32_t
   return call;
 }
 
-// The round launch's CU-masked stream: `keep` of every 8 CUs, spread over
-// every XCD / shader engine, plus the fork / join events.  Returns the
+// The round launch's CU-masked stream (cu_mask_stream, shared by the
+// process's lanes) plus this lane's fork / join events.  Returns the
 // device's CU count (lane_cus_ = CUs kept).
 int32_t OneSidedLane::make_cu_stream(int32_t keep) {
   hipDeviceProp_t prop;
   AKKA_OS_HIP(hipGetDeviceProperties(&prop, device_));
   const int32_t ncu = std::max(1, prop.multiProcessorCount);
-  std::vector<uint32_t> mask(size_t((ncu + 31) / 32), 0u);
-  int32_t on = 0;
-  for (int32_t cu = 0; cu < ncu; ++cu)
-    if (cu % 8 < keep) {
-      mask[size_t(cu / 32)] |= 1u << (cu % 32);
-      ++on;
-    }
-  hipStream_t s = nullptr;
-  AKKA_OS_HIP(hipExtStreamCreateWithCUMask(&s, uint32_t(mask.size()), mask.data()));
+  const auto [s, on] = cu_mask_stream(device_, keep);
   cu_stream_ = s;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   AKKA_OS_HIP(hipEventCreateWithFlags(&e0, hipEventDisableTiming));
@@ -623,7 +647,7 @@ void OneSidedLane::gpu_call(uintptr_t stream, const char* in, char* out, int32_t
     a.tl = tl_dev_;
   }
   hipStream_t caller = reinterpret_cast<hipStream_t>(stream);
-  if (cu_stream_) {
+  if (cu_stream_ && caller != static_cast<hipStream_t>(cu_stream_)) {
     // fork/join through events (graph capture follows the same edges)
     hipStream_t ls = static_cast<hipStream_t>(cu_stream_);
     AKKA_OS_HIP(hipEventRecord(static_cast<hipEvent_t>(ev_in_), caller));
@@ -634,7 +658,7 @@ void OneSidedLane::gpu_call(uintptr_t stream, const char* in, char* out, int32_t
     AKKA_OS_HIP(hipStreamWaitEvent(caller, static_cast<hipEvent_t>(ev_out_), 0));
     return;
   }
-  launch_onesided_call(caller, a, dt_ == DType::F32 ? 0 : 1);
+  launch_onesided_call(caller, a, dt_ == DType::F32 ? 0 : 1);  // (the caller's stream, or the masked one itself)
   AKKA_OS_HIP(hipGetLastError());
 }
 

@@ -160,6 +160,9 @@ class OneSidedLane {
   int32_t shared_ranks() const { return shared_ranks_; }
   // CUs the round launch may use (cu_keep; 0: all)
   int32_t lane_cus() const { return lane_cus_; }
+  // the CU-masked stream (hipStream_t as an integer; 0 without cu_keep): a
+  // call enqueued on it runs there directly, without the fork / join
+  uintptr_t cu_stream() const { return reinterpret_cast<uintptr_t>(cu_stream_); }
   // AKKA_OS_TIMELINE=1 at construction: per workgroup [entry, round known,
   // role done] of the last call (waits for the device), and the clock rate
   std::vector<uint64_t> timeline();
