@@ -1,8 +1,11 @@
 """torch DDP communication hook: gradient buckets through the threshold allreduce.
 
     from akka_allreduce_amd.parallel.ddp import ThresholdHookState, threshold_allreduce_hook
-    model = DistributedDataParallel(model)
+    model = DistributedDataParallel(model, gradient_as_bucket_view=True)
     model.register_comm_hook(ThresholdHookState(th_reduce=0.75, th_complete=0.75), threshold_allreduce_hook)
+
+(``gradient_as_bucket_view=True``: the hook writes the mean into the bucket
+in place, so the gradients -- views of the buckets -- need no copy back.)
 
 Every DDP bucket becomes one round of a ``ThresholdAllreduce`` (one per
 distinct bucket size, created lazily -- all ranks see the same bucket sequence,
@@ -118,7 +121,16 @@ def threshold_allreduce_hook(state: ThresholdHookState, bucket: dist.GradBucket)
     # the backward pass -- only waits where DDP consumes the bucket.
     side = ar.async_stream() if async_op else torch.cuda.current_stream(work.device)
     with torch.cuda.stream(side):
-        mean = out.mean().to(t.dtype).view_as(t)
+        if work is flat and t.is_contiguous() and ar.transport != "reactive":
+            # the mean straight into the bucket (the round is done with its
+            # input by then, in this stream's order): no allocation, and the
+            # result aliases the bucket, so DDP's copy of it into the
+            # gradients is a no-op with gradient_as_bucket_view=True.  (Not
+            # reactive: its round may complete while a send of the input to
+            # a straggler is still in flight.)
+            mean = out.mean(out=flat).view_as(t)
+        else:
+            mean = out.mean().to(t.dtype).view_as(t)
         fut = torch.futures.Future(devices=[work.device])
         fut.set_result(mean)
     return fut

@@ -24,6 +24,8 @@ def main():
     ap.add_argument("--data-plane", default="ipc", help="stream transport: rccl | ipc")
     ap.add_argument("--modes", default="sync,async", help="comma list (one process per mode avoids the second "
                                                           "mode inheriting the first one's engines and windows)")
+    ap.add_argument("--bucket-view", type=int, default=1, help="DDP gradient_as_bucket_view (1: grads are views "
+                                                                  "of the buckets, the hook's in-place mean needs no copy)")
     ap.add_argument("--lane", default="", help="stream transport: the hook's lane for every bucket engine "
                                                   "(ThresholdAllreduce.LANES), e.g. ipc_fused_lite")
     a = ap.parse_args()
@@ -37,7 +39,8 @@ def main():
     for mode in a.modes.split(","):
         torch.manual_seed(0)
         model = torch.nn.parallel.DistributedDataParallel(MLP(4096, 8192, 1000).to(dev), device_ids=[dev.index],
-                                                          bucket_cap_mb=a.bucket_mb)
+                                                          bucket_cap_mb=a.bucket_mb,
+                                                          gradient_as_bucket_view=bool(a.bucket_view))
         state = ThresholdHookState(transport=a.transport, max_chunk_size=1 << 20, async_op=(mode == "async"),
                                    bucket_cap_mb=a.bucket_mb, onesided_options={"cu_keep": a.cu_keep},
                                    data_plane=a.data_plane if a.transport == "stream" else "rccl")
@@ -67,6 +70,7 @@ def main():
         errs = [ar._os.error() if ar.transport == "onesided" else ar.ipc_error() for ar in state.engines.values()]
         if rank == 0:
             print(json.dumps({"mode": mode, "transport": a.transport, "lane": a.lane or None, "world": world,
+                              "bucket_view": bool(a.bucket_view),
                               "ms_per_step": round(max(t) / a.steps * 1e3, 3),
                               "buckets": len(state.engines), "async_rounds": state.async_rounds,
                               "rounds": state.rounds, "lane_errors": errs}), flush=True)
