@@ -66,8 +66,11 @@ def main():
     chosen = [state.lane] if a.tune else []
     lane_cus = [int(ar._os.info().get("lane_cus", 0)) for ar in state.engines.values()] \
         if a.transport == "onesided" else []
+    # the process's lanes share ONE CU-masked stream (a hardware queue each)
+    cu_streams = sorted({int(ar._os.lane.cu_stream()) for ar in state.engines.values()}) \
+        if a.transport == "onesided" else []
     torch.save({"flat": flat, "buckets": len(state.engines), "rounds": state.rounds, "ipc_errors": errs,
-                "async_rounds": state.async_rounds, "lane_cus": lane_cus,
+                "async_rounds": state.async_rounds, "lane_cus": lane_cus, "cu_streams": cu_streams,
                 "chosen": chosen, "transports": state.transports(), "window_sets": len(windows)},
                os.path.join(a.out_dir, f"rank{rank}.pt"))
     dist.barrier()

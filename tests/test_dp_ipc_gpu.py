@@ -137,6 +137,7 @@ def test_torch_ddp_hook_onesided_multiprocess(bounded):
         assert d["buckets"] >= 3 and d["rounds"] >= steps
         if bounded:
             assert d["async_rounds"] == d["rounds"] and all(c == kept for c in d["lane_cus"]), d
+            assert len(d["cu_streams"]) == 1 and d["cu_streams"][0] != 0, d  # one masked stream per process
         else:
             assert d["async_rounds"] == 0 and all(c == 0 for c in d["lane_cus"]), d
         assert torch.equal(d["flat"], res[0]["flat"])
