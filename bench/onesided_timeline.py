@@ -44,6 +44,7 @@ def main():
     ap.add_argument("--chunk-mb", type=float, default=4.0)
     ap.add_argument("--calls", type=int, default=5)
     ap.add_argument("--out-dir", required=True)
+    ap.add_argument("--window-output", action="store_true", help="calls without out: the lane's window row")
     a = ap.parse_args()
     rank = int(os.environ["RANK"])
     dist.init_process_group("gloo")
@@ -55,11 +56,11 @@ def main():
     for mb in [float(s) for s in a.sizes_mb.split(",")]:
         S = int(mb * (1 << 20)) // 4
         C = min(S, int(a.chunk_mb * (1 << 20)) // 4)
-        ar = OneSidedAllreduce(S, max_chunk_size=C, device=dev)
+        ar = OneSidedAllreduce(S, max_chunk_size=C, device=dev, window_output=a.window_output)
         info = ar.info()
         info["kme"] = ar.geometry.num_chunks(rank)
         x = torch.randn(S, device=dev)
-        out = torch.empty_like(x)
+        out = None if a.window_output else torch.empty_like(x)
         for _ in range(3):
             ar(x, out=out)
         torch.cuda.synchronize()
@@ -70,7 +71,8 @@ def main():
             torch.cuda.synchronize()
             per.append(spans(ar.lane.timeline(), info, info["clock_khz"]))
         best = min(per, key=lambda s: s["kernel"])
-        rows.append({"rank": rank, "size_mb": mb, "role_wgs": info["role_wgs"], "kme": info["kme"],
+        rows.append({"rank": rank, "size_mb": mb, "window_output": ar.window_output, "role_wgs": info["role_wgs"],
+                     "kme": info["kme"],
                      "kernel_us_per_call": [s["kernel"] for s in per], "fastest_call": best})
         dist.barrier()
         del ar

@@ -125,6 +125,11 @@ __device__ uint2 wait_begun(const Args& a) {
 // announcement: ~µs each over xGMI) overlap instead of preceding every copy;
 // then the workgroup copies its items one by one.
 constexpr int kGateBatch = 256;
+// 16-B vectors per thread per batch of a push (copy_out_sys): 128 B, twice
+// the default, half the waits for write-through acks per part -- for the
+// xGMI acks of a node; on one card the batch size does not matter
+// (profiles/r05/push_batch/; 16 puts some round kernels on scratch)
+constexpr int kPushUnroll = 8;
 
 template <int ES>
 __device__ void push_role(const Args& a, uint32_t r, int32_t w0, int32_t stride) {
@@ -171,7 +176,7 @@ __device__ void push_role(const Args& a, uint32_t r, int32_t w0, int32_t stride)
       const char* src = a.in + (a.tab->bstart[p] + off) * ES;
       const bool lite = !a.fenced && ((uintptr_t(dst) | uintptr_t(src) | uintptr_t(n * ES)) & 15) == 0;
       if (n > 0) {
-        if (lite) copy_out_sys(dst, src, n * ES);
+        if (lite) copy_out_sys<kPushUnroll>(dst, src, n * ES);
         else copy_bytes(dst, src, n * ES);
       }
       if (lite) drain_wg();

@@ -155,17 +155,22 @@ __device__ inline void store_sys16(__amdgpu_buffer_rsrc_t r, int64_t off, const 
 }
 
 // dst (a window, read by a peer) <- src (local), 16-byte aligned.
+// U vectors per thread per batch: the vmcnt counter is in order and counts
+// stores too, so a batch's loads wait for the previous batch's write-through
+// stores to be acknowledged (by the peer's memory, over xGMI on a node) --
+// the bytes moved per such wait set the push rate of a workgroup.
+template <int U = kUnroll>
 __device__ inline void copy_out_sys(char* __restrict__ dst, const char* __restrict__ src, int64_t bytes) {
   const auto r = sys_rsrc(dst, bytes);
   const uint4* s = reinterpret_cast<const uint4*>(src);
   const int64_t n = bytes >> 4;
   int64_t i = threadIdx.x;
-  for (; i + (kUnroll - 1) * int(blockDim.x) < n; i += kUnroll * int(blockDim.x)) {
-    uint4 v[kUnroll];
+  for (; i + (U - 1) * int(blockDim.x) < n; i += U * int(blockDim.x)) {
+    uint4 v[U];
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) v[u] = s[i + u * int(blockDim.x)];
+    for (int u = 0; u < U; ++u) v[u] = s[i + u * int(blockDim.x)];
 #pragma unroll
-    for (int u = 0; u < kUnroll; ++u) store_sys16(r, (i + u * int(blockDim.x)) * 16, v[u]);
+    for (int u = 0; u < U; ++u) store_sys16(r, (i + u * int(blockDim.x)) * 16, v[u]);
   }
   for (; i < n; i += int(blockDim.x)) store_sys16(r, i * 16, s[i]);
 }
