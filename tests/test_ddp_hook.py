@@ -110,3 +110,69 @@ def test_share_transport_refuses_reactive():
     with pytest.raises(ValueError, match="only the scheduled"):
         ThresholdAllreduce(16, transport="reactive", rank=0, world_size=2, device=torch.device("cpu"),
                            share_transport_with=_Fake())
+
+
+def _straggler_main(rank, world, port, q, delay_ms, steps):
+    try:
+        os.environ["MASTER_ADDR"] = "127.0.0.1"
+        os.environ["MASTER_PORT"] = str(port)
+        os.environ["AKKA_FAULT_RANK"] = "1"
+        os.environ["AKKA_FAULT_DELAY_MS"] = str(delay_ms)
+        torch.set_num_threads(1)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        import time
+
+        from torch.nn.parallel import DistributedDataParallel as DDP
+
+        from akka_allreduce_amd.parallel.ddp import ThresholdHookState, threshold_allreduce_hook
+
+        torch.manual_seed(0)
+        model = torch.nn.Sequential(torch.nn.Linear(64, 128), torch.nn.ReLU(), torch.nn.Linear(128, 8))
+        ddp = DDP(model, bucket_cap_mb=0.02, gradient_as_bucket_view=True)
+        # thresholds 1/2 of 2 ranks: a round completes on this rank's own data
+        state = ThresholdHookState(max_chunk_size=1024, transport="onesided", th_reduce=0.5, th_complete=0.5,
+                                   max_lag=1)
+        ddp.register_comm_hook(state, threshold_allreduce_hook)
+        opt = torch.optim.SGD(ddp.parameters(), lr=0.05)
+        g = torch.Generator().manual_seed(100 + rank)
+        times = []
+        for _ in range(steps):
+            x = torch.randn(8, 64, generator=g)
+            y = torch.randn(8, 8, generator=g)
+            t0 = time.perf_counter()
+            opt.zero_grad()
+            torch.nn.functional.mse_loss(ddp(x), y).backward()
+            opt.step()
+            times.append(time.perf_counter() - t0)
+        finite = all(bool(torch.isfinite(p).all()) for p in model.parameters())
+        errs = [ar._os.error() for ar in state.engines.values()]
+        q.put((rank, times, state.rounds, finite, errs))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover
+        q.put((rank, repr(e), 0, False, []))
+
+
+def test_ddp_hook_onesided_straggler_does_not_hold_the_fast_rank():
+    """The straggler case the reference exists for, through torch DDP: rank 1
+    sleeps 40 ms before each of its bucket rounds; at thresholds 1/2 the
+    one-sided rounds of rank 0 complete on what arrived, so its DDP steps
+    (after the first two: engine creation and DDP's bucket rebuild are
+    collective) take a small fraction of one straggler delay."""
+    delay_ms, steps = 40, 8
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_straggler_main, args=(r, 2, port, q, delay_ms, steps)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=240) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+    (r0, t0, rounds0, fin0, err0), (r1, t1, rounds1, fin1, err1) = res
+    assert isinstance(t0, list) and isinstance(t1, list), res
+    assert fin0 and fin1 and rounds0 >= steps and rounds1 >= steps
+    fast = sorted(t0[2:])[len(t0[2:]) // 2]  # median of the steady steps
+    slow = sorted(t1[2:])[len(t1[2:]) // 2]
+    assert slow >= delay_ms / 1e3, (t0, t1)  # the straggler pays its delay per round
+    assert fast < 0.25 * delay_ms / 1e3, (fast, t0, t1)  # the fast rank never waits for it
