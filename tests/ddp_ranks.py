@@ -33,6 +33,7 @@ def main():
     ap.add_argument("--bucket-mb", type=float, default=0.25)
     ap.add_argument("--transport", choices=["stream", "onesided"], default="stream")
     ap.add_argument("--cu-keep", type=int, default=0, help="onesided: CUs kept of every 8 (bounded footprint)")
+    ap.add_argument("--th", type=float, default=1.0, help="onesided: th_reduce = th_complete")
     a = ap.parse_args()
     rank = int(os.environ["RANK"])
     dist.init_process_group("gloo")
@@ -44,16 +45,23 @@ def main():
     torch.manual_seed(0)
     model = torch.nn.parallel.DistributedDataParallel(build_model(a.model).to(dev), device_ids=[0],
                                                       bucket_cap_mb=a.bucket_mb)
+    th = {"th_reduce": a.th, "th_complete": a.th, "max_lag": 1} if a.th < 1.0 else {}
     state = ThresholdHookState(data_plane="ipc", max_chunk_size=1 << 14, tune=a.tune, transport=a.transport,
-                               onesided_options={"cu_keep": a.cu_keep} if a.cu_keep else None)
+                               onesided_options={"cu_keep": a.cu_keep} if a.cu_keep else None, **th)
     model.register_comm_hook(state, threshold_allreduce_hook)
     opt = torch.optim.SGD(model.parameters(), lr=0.1)
+    import time
+
+    times = []
     for s in range(a.steps):
+        t0 = time.perf_counter()
         g = torch.Generator(device=dev).manual_seed(100 * s + rank)
         x, y = synthetic_batch(64, 256, 10, device=dev, generator=g)
         opt.zero_grad(set_to_none=True)
         torch.nn.functional.cross_entropy(model(x), y).backward()
         opt.step()
+        torch.cuda.synchronize()
+        times.append(time.perf_counter() - t0)
     torch.cuda.synchronize()
     flat = torch.cat([p.detach().reshape(-1).float().cpu() for p in model.parameters()])
     if a.transport == "onesided":  # one lane (window set) per bucket size
@@ -71,6 +79,7 @@ def main():
         if a.transport == "onesided" else []
     torch.save({"flat": flat, "buckets": len(state.engines), "rounds": state.rounds, "ipc_errors": errs,
                 "async_rounds": state.async_rounds, "lane_cus": lane_cus, "cu_streams": cu_streams,
+                "step_s": times,
                 "chosen": chosen, "transports": state.transports(), "window_sets": len(windows)},
                os.path.join(a.out_dir, f"rank{rank}.pt"))
     dist.barrier()

@@ -143,3 +143,27 @@ def test_torch_ddp_hook_onesided_multiprocess(bounded):
         assert torch.equal(d["flat"], res[0]["flat"])
     want = _reference(n, steps, torch.device("cuda", 0), "deep")
     torch.testing.assert_close(res[0]["flat"], want, rtol=1e-4, atol=1e-5)
+
+
+def test_torch_ddp_hook_onesided_straggler():
+    """The reference's straggler case through torch DDP on the GPU: rank 1
+    sleeps 30 ms before each of its bucket rounds; at thresholds 1/2 the
+    one-sided rounds of rank 0 complete on what arrived, so rank 0's DDP
+    steps (after the first two: engine creation and DDP's bucket rebuild are
+    collective) stay far below one straggler delay, with no wait timing out."""
+    n, steps, delay_ms = 2, 8, 30
+    env = dict(os.environ, AKKA_FAULT_RANK="1", AKKA_FAULT_DELAY_MS=str(delay_ms))
+    with tempfile.TemporaryDirectory() as out:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+               "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+               os.path.join(ROOT, "tests", "ddp_ranks.py"), "--out-dir", out, "--steps", str(steps),
+               "--model", "deep", "--bucket-mb", "0.3", "--transport", "onesided", "--th", "0.5"]
+        r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT, env=env)
+        assert r.returncode == 0, r.stderr[-3000:]
+        res = [torch.load(os.path.join(out, f"rank{i}.pt"), weights_only=True) for i in range(n)]
+    med = [sorted(d["step_s"][2:])[len(d["step_s"][2:]) // 2] for d in res]
+    for d in res:
+        assert all(e == 0 for e in d["ipc_errors"]), d  # no bounded wait expired
+        assert bool(torch.isfinite(d["flat"]).all())
+    assert med[1] >= delay_ms / 1e3, med  # the straggler pays its delay per round
+    assert med[0] < 0.25 * delay_ms / 1e3, (med, res[0]["step_s"])  # the fast rank never waits for it
