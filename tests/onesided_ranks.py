@@ -70,6 +70,7 @@ def main():
     ap.add_argument("--timeline", action="store_true", help="exact: AKKA_OS_TIMELINE=1, check the stamps")
     ap.add_argument("--async-op", action="store_true", help="exact: async rounds (side stream), wait() then read")
     ap.add_argument("--jitter-ms", type=float, default=2.0, help="chaos: every call waits U(0, jitter) first")
+    ap.add_argument("--seed", type=int, default=0, help="chaos: seed offset of the ranks' jitter streams")
     ap.add_argument("--device", default="cpu")
     ap.add_argument("--size", type=int, default=1 << 16)
     ap.add_argument("--chunk", type=int, default=1 << 12)
@@ -187,13 +188,13 @@ def main():
         # all vary from round to round; every output chunk is checked
         import random
 
-        rng = random.Random(1234 + rank)
+        rng = random.Random(1234 + rank + 1000 * a.seed)
         x = torch.full((a.size,), float(1 << rank), dtype=dtype, device=dev)
         out = torch.empty_like(x)
         bad, detail, rounds, reasons, last, partial = 0, [], [], [], -1, 0
         while last < a.rounds - 1:
             time.sleep(rng.uniform(0.0, a.jitter_ms) / 1e3)
-            o = ar(x, out=out)
+            o = ar(x) if a.window_output else ar(x, out=out)
             sync()
             b, _ = check_sets(o, world, rank, dtype, detail)
             bad += b
