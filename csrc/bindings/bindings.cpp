@@ -583,8 +583,12 @@ class WorkerCore final : public EngineHost {
       return;
     }
     // host devices: a modelled caller stream (stream race checking) counts too
+    // (a synchronous call: its round completes inside this call, so the
+    // input-ready marker can wait until a stream of the engine needs it --
+    // none does when the round runs on the caller's stream)
     dp_->bind_input(round, reinterpret_cast<const void*>(it->second.in), reinterpret_cast<StreamH>(it->second.stream),
-                    !dev_->is_host() || (dev_->models_streams() && it->second.stream != 0));
+                    !dev_->is_host() || (dev_->models_streams() && it->second.stream != 0),
+                    it->second.stream_wait && !dev_->is_host());
     // a synchronous call: the caller's stream waits for the round anyway, so
     // a lane that needs no stream of its own may run the round right there
     if (it->second.stream_wait && !dev_->is_host()) dp_->set_caller_waits(round);

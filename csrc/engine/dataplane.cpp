@@ -206,9 +206,10 @@ DataPlane::Binding& DataPlane::binding_mut(int32_t round) {
   return const_cast<Binding&>(static_cast<const DataPlane*>(this)->binding(round));
 }
 
-void DataPlane::bind_input(int32_t round, const void* input, StreamH ready_stream, bool has_stream) {
+void DataPlane::bind_input(int32_t round, const void* input, StreamH ready_stream, bool has_stream, bool defer_record) {
   Binding& b = bind_[round];
   b.input = input;
+  b.input_pending = false;
   b.ready = ready_stream;
   b.has_ready = has_stream && (!dev_->is_host() || dev_->models_streams());
   b.input_waited_compute = b.input_waited_comm = false;
@@ -239,7 +240,8 @@ void DataPlane::bind_input(int32_t round, const void* input, StreamH ready_strea
       return;
     }
     if (!b.input_ready) b.input_ready = binding_event();
-    dev_->record(b.input_ready, ready_stream);
+    if (defer_record) b.input_pending = true;  // recorded by the first wait_input, if any
+    else dev_->record(b.input_ready, ready_stream);
   }
 }
 
@@ -270,6 +272,7 @@ StreamH DataPlane::run_on_caller(int32_t round) {
   b.exec = b.ready;
   b.exec_on_producer = true;
   b.exec_on_comm = false;
+  b.input_pending = false;  // the round runs in the producer's order: nothing waits for the input event
   return b.exec;
 }
 
@@ -351,6 +354,10 @@ void DataPlane::wait_input(int32_t round, StreamH s) {
     }
   }
   if (!b.input_ready) return;
+  if (b.input_pending) {
+    dev_->record(b.input_ready, b.ready);
+    b.input_pending = false;
+  }
   bool& done = comm ? b.input_waited_comm : b.input_waited_compute;
   if (done) return;
   dev_->wait(s, b.input_ready);

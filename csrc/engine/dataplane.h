@@ -47,7 +47,11 @@ class DataPlane {
   // --- per-round bindings (memory owned by the embedding layer) ------------
   // `ready_stream` is the stream that produced `input`; it may be the null
   // stream (handle 0), so `has_stream` says whether there is one at all.
-  void bind_input(int32_t round, const void* input, StreamH ready_stream, bool has_stream);
+  // defer_record: record the input-ready event only when a stream first
+  // waits for it (a synchronous call whose round may run on the producer's
+  // own stream needs none: one marker less per round).  Only for rounds whose
+  // consumers all wait inside the call that binds them (fast_round).
+  void bind_input(int32_t round, const void* input, StreamH ready_stream, bool has_stream, bool defer_record = false);
   // `alloc_stream` (optional): the stream in whose order output/counts were
   // allocated (a caching allocator may hand out memory that earlier work on
   // that stream still uses).  Every other stream that writes them waits for
@@ -163,6 +167,7 @@ class DataPlane {
     EventH input_ready = nullptr;  // recorded on the producer stream
     bool input_waited_compute = false;
     bool input_waited_comm = false;
+    bool input_pending = false;    // input_ready not recorded yet (bind_input defer_record)
     EventH output_ready = nullptr;  // recorded on the stream that allocated output/counts
     bool output_waited_compute = false;
     bool output_waited_comm = false;
