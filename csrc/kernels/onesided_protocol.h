@@ -273,6 +273,19 @@ OS_HD inline bool source_past(const uint32_t* fl, const Layout& L, int32_t s, ui
 
 enum Gate : int32_t { kGo = 0, kOutdated = 1, kConflict = 2, kDead = 3 };
 
+// A write dropped by the overwrite hand-shake (kConflict) never happens: its
+// "writing r" marker would read as PENDING once the receiver serves round r
+// in that row -- a wait only the writer's next round (source_past) or the
+// timeout could end, and a writer that stops at r (the end of a job's phase)
+// has no next round.  The writer moves the tag to "writing r + 1" instead: a
+// round no writer ever writes in this row (D >= 2), read as LOST for round r
+// and for every older round, as PENDING for the row's later rounds -- and the
+// writer's own later rounds there (r + D, ...) still move the tag forward.
+template <class M>
+OS_HD inline void retract(uint32_t* tag, uint32_t r) {
+  M::st(tag, tag_writing(r + 1u));
+}
+
 // Phase 1 sender: may I write round r's part j of chunk k into the owner's
 // SD[row][me]?  Leaves the "writing r" marker behind on kGo / kConflict.
 template <class M>
@@ -281,7 +294,10 @@ OS_HD inline int32_t scatter_gate(uint32_t* owner_fl, const Layout& L, int32_t r
   if (M::ld(owner_fl + L.fired(row, k)) >= r + 1u) return kOutdated;  // owner reduced round >= r already
   M::st_sc(owner_fl + L.stag(row, me, k, j), tag_writing(r));
   const uint32_t rd = M::ld_sc(owner_fl + L.sread(row, k));
-  if (rd != 0u && rd != r + 1u) return kConflict;  // owner is reading this row for another round
+  if (rd != 0u && rd != r + 1u) {  // owner is reading this row for another round
+    retract<M>(owner_fl + L.stag(row, me, k, j), r);
+    return kConflict;
+  }
   return kGo;
 }
 
@@ -293,7 +309,10 @@ OS_HD inline int32_t gather_gate(uint32_t* q_fl, const Layout& L, int32_t row, i
   if (M::ld(q_fl + L.done()) >= r + 1u) return kOutdated;  // q completed round >= r already
   M::st_sc(q_fl + L.gtag(row, me, k, j), tag_writing(r));
   const uint32_t rd = M::ld_sc(q_fl + L.gread(row));
-  if (rd != 0u && rd != r + 1u) return kConflict;
+  if (rd != 0u && rd != r + 1u) {
+    retract<M>(q_fl + L.gtag(row, me, k, j), r);
+    return kConflict;
+  }
   return kGo;
 }
 

@@ -411,6 +411,41 @@ def test_overwrite_handshake_drops_writes_into_a_row_being_read():
     assert data[6:8] == [7.0, 7.0] and counts[2:6] == [0, 0, 0, 0]
 
 
+def test_dropped_write_leaves_no_phantom_for_its_own_round():
+    """A write dropped by the overwrite hand-shake must read as LOST when its
+    own round comes up in that row, not as "being written".  Ring depth 2,
+    exact thresholds: rank 1 writes round 2 into the row the worker is still
+    reading for round 0 and drops it (conflict); it never writes that part
+    again.  Rank 1 does not move past round 2 (it stops there, as a rank does
+    at the end of a job's phase), so only the tag can tell the worker that
+    the copy is gone.  When the worker serves round 2 its wait must end on
+    what landed (a phantom "writing 2" tag held it until the lane's timeout:
+    a 30 s stall of bench config 4 on the CPU, about once in 150 phase ends)."""
+    h = SpecHarness(4, 8, 2, 1.0, 1.0, 5, rows=2)
+    h.start(basic(8, 0))
+    h.scatter(1, 0, 2, [100.0, 100.0])  # round 2 -> row 0 while it is read for round 0: dropped
+    assert h.stats(1)["scatter_conflict"] == 1
+    for r in (0, 1):  # ranks 2 and 3 deliver everything; rank 1 is past rounds 0 and 1
+        if r == 1:
+            h.start(basic(8, 1))
+        for src in (2, 3):
+            h.scatter(src, 0, r, [float(src), float(src)])
+        for src in (2, 3):
+            h.reduce(src, 0, r, 3, [10.0 * src, 10.0 * src])
+        assert len(h.outputs) == r + 1, (r, h.outputs)
+    h.start(basic(8, 2))
+    for src in (2, 3):
+        h.scatter(src, 0, 2, [float(src), float(src)])
+    h.reduce(1, 0, 2, 3, [11.0, 11.0])  # rank 1 completes round 2's phase 2 normally
+    for src in (2, 3):
+        h.reduce(src, 0, 2, 3, [10.0 * src, 10.0 * src])
+    assert len(h.outputs) == 3, "round 2 still waits for the dropped copy"
+    r, data, counts, _ = h.outputs[2]
+    assert r == 2 and 100.0 not in data
+    assert data[:2] == [2.0 + 2 + 3, 3.0 + 2 + 3] and counts[:2] == [3, 3]  # own + ranks 2, 3
+    assert data[2:4] == [11.0, 11.0] and counts[2:4] == [3, 3]
+
+
 @pytest.mark.parametrize("seed", range(6))
 def test_random_orders_match_reference_rules(seed):
     """Random arrival orders of one round's messages (N=4, thresholds 0.75):
