@@ -123,8 +123,16 @@ def check_job(device, rounds=64, slack_ms=1.0, **kw):
             assert all(x["bad"] == 0 for x in r["records"]), r["id"]
             rs = [x["round"] for x in r["records"]]
             assert rs == sorted(rs) and len(set(rs)) == len(rs), rs[:20]
+    # every round in order (rounds skipped by catch-up are force-completed
+    # records too); the master ends the job once thAllreduce * N workers
+    # completed the last round, so a worker still behind may stop one round
+    # short -- but at least that many served every round
+    full = 0
     for r in base:
-        assert [x["round"] for x in r["records"]] == list(range(rounds))
+        rs = [x["round"] for x in r["records"]]
+        assert rs == list(range(len(rs))) and len(rs) >= rounds - 1, rs[-5:]
+        full += len(rs) == rounds
+    assert full >= 3, [len(r["records"]) for r in base]
     b, s = fast_median_ms(base), fast_median_ms(strag)
     assert s <= 2 * b + slack_ms, (b, s)
     st = [r for r in strag if r["straggler"]][0]
