@@ -26,6 +26,8 @@ def main():
                                                           "mode inheriting the first one's engines and windows)")
     ap.add_argument("--bucket-view", type=int, default=1, help="DDP gradient_as_bucket_view (1: grads are views "
                                                                   "of the buckets, the hook's in-place mean needs no copy)")
+    ap.add_argument("--window-output", type=int, default=0, help="onesided: exact rounds return the lane's window row "
+                                                                      "(no gather copy)")
     ap.add_argument("--lane", default="", help="stream transport: the hook's lane for every bucket engine "
                                                   "(ThresholdAllreduce.LANES), e.g. ipc_fused_lite")
     a = ap.parse_args()
@@ -42,7 +44,8 @@ def main():
                                                           bucket_cap_mb=a.bucket_mb,
                                                           gradient_as_bucket_view=bool(a.bucket_view))
         state = ThresholdHookState(transport=a.transport, max_chunk_size=1 << 20, async_op=(mode == "async"),
-                                   bucket_cap_mb=a.bucket_mb, onesided_options={"cu_keep": a.cu_keep},
+                                   bucket_cap_mb=a.bucket_mb, onesided_options={"cu_keep": a.cu_keep,
+                                                                    "window_output": bool(a.window_output)},
                                    data_plane=a.data_plane if a.transport == "stream" else "rccl")
         if a.lane:
             state.lane = a.lane  # applied to every bucket's engine (ThresholdHookState.engine)

@@ -446,6 +446,37 @@ def test_dropped_write_leaves_no_phantom_for_its_own_round():
     assert data[2:4] == [11.0, 11.0] and counts[2:4] == [3, 3]
 
 
+def test_dropped_gather_write_leaves_no_phantom_either():
+    """The gather side of the same rule: rank 2 writes round 2 (its scatter
+    copy and its reduced chunk) into the rows the worker still reads for
+    round 0, both writes are dropped, and rank 2 never writes them again.
+    Serving round 2 the worker reduces without rank 2's copy and completes
+    without its chunk (0, count 0) instead of waiting for either."""
+    h = SpecHarness(4, 8, 2, 1.0, 1.0, 5, rows=2)
+    h.start(basic(8, 0))
+    h.scatter(2, 0, 2, [100.0, 100.0])
+    h.reduce(2, 0, 2, 4, [200.0, 200.0])
+    assert h.stats(2)["scatter_conflict"] == 1 and h.stats(2)["gather_conflict"] == 1
+    for r in (0, 1):  # ranks 1 and 3 deliver everything; rank 2 is past rounds 0 and 1
+        if r == 1:
+            h.start(basic(8, 1))
+        for src in (1, 3):
+            h.scatter(src, 0, r, [float(src), float(src)])
+        for src in (1, 3):
+            h.reduce(src, 0, r, 3, [10.0 * src, 10.0 * src])
+        assert len(h.outputs) == r + 1, (r, h.outputs)
+    h.start(basic(8, 2))
+    for src in (1, 3):
+        h.scatter(src, 0, 2, [float(src), float(src)])
+    for src in (1, 3):
+        h.reduce(src, 0, 2, 3, [10.0 * src, 10.0 * src])
+    assert len(h.outputs) == 3, "round 2 still waits for a dropped copy"
+    r, data, counts, _ = h.outputs[2]
+    assert r == 2 and 100.0 not in data and 200.0 not in data
+    assert data[:2] == [2.0 + 1 + 3, 3.0 + 1 + 3] and counts[:2] == [3, 3]
+    assert data[4:6] == [0.0, 0.0] and counts[4:6] == [0, 0]  # rank 2's block: never arrived
+
+
 @pytest.mark.parametrize("seed", range(6))
 def test_random_orders_match_reference_rules(seed):
     """Random arrival orders of one round's messages (N=4, thresholds 0.75):
