@@ -77,7 +77,11 @@ def test_onesided_straggler_steady_state():
     phase), every chunk's value encodes a contributor set whose size is its
     count, the straggler's late pushes are dropped by the senders (outdated)
     and its calls catch up (skipped rounds)."""
-    r, rows = run_ranks(4, "--mode", "straggler", "--straggler", "3", "--rounds", "64", "--compute-ms", "2",
+    # (compute 0.5 ms per call: the fast ranks need each other at 0.75, and
+    # their compute phases drift apart by up to one compute time -- waiting
+    # for each other that long is no straggler wait, so keep it under the
+    # bound's 1 ms slack)
+    r, rows = run_ranks(4, "--mode", "straggler", "--straggler", "3", "--rounds", "64", "--compute-ms", "0.5",
                         "--delay-ms", "50")
     assert r.returncode == 0, r.stderr[-3000:]
     for d in rows:
