@@ -69,6 +69,57 @@ def _stale(obj: str, src: str, headers: list[str]) -> bool:
     return os.path.getmtime(src) > t or any(os.path.getmtime(h) > t for h in headers)
 
 
+def source_hash(root: str | None = None) -> str | None:
+    """sha256 over every source and header the module is built from (names +
+    contents) and the target arch, or None when the sources are not there
+    (an installed copy without ``csrc/``).  Contents, not mtimes: a snapshot
+    copied to another machine keeps its hash whatever its timestamps."""
+    import hashlib
+
+    csrc = os.path.join(root or ROOT, "csrc")
+    files = [os.path.join(csrc, r) for r in HOST_SOURCES + HIP_SOURCES]
+    files += sorted(glob.glob(os.path.join(csrc, "**", "*.h"), recursive=True))
+    if not all(os.path.exists(f) for f in files[: len(HOST_SOURCES) + len(HIP_SOURCES)]):
+        return None
+    h = hashlib.sha256(ARCH.encode())
+    for f in files:
+        if not os.path.exists(f):
+            continue
+        h.update(os.path.relpath(f, csrc).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+        h.update(b"\0")
+    return h.hexdigest()
+
+
+def hash_path(ext: str | None = None) -> str:
+    """Sidecar file holding the source hash the module at ``ext`` was linked from."""
+    return (ext or ext_path()) + ".srchash"
+
+
+def stale_reason(ext: str | None = None, root: str | None = None) -> str | None:
+    """Why the module at ``ext`` does not match the sources (None: it does,
+    or there are no sources to compare with)."""
+    ext = ext or ext_path()
+    if not os.path.exists(ext):
+        return "not built"
+    want = source_hash(root)
+    if want is None:
+        return None
+    try:
+        with open(hash_path(ext)) as f:
+            have = f.read().strip()
+    except OSError:
+        return "no source hash recorded next to the module"
+    return None if have == want else "sources changed since the module was built"
+
+
+def have_compiler() -> bool:
+    import shutil
+
+    return os.path.exists(os.path.join(ROCM, "bin", "hipcc")) and shutil.which("g++") is not None
+
+
 def _run(cmd: list[str], verbose: bool) -> None:
     if verbose:
         print(" ".join(shlex.quote(c) for c in cmd), flush=True)
@@ -81,12 +132,31 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False, s
     """Compile and link.  ``sanitize`` (e.g. ``"address,undefined"``) builds an
     instrumented HOST-code variant into ``build/native-<san>/`` (never the
     in-tree module); device code is not instrumented (no GPU sanitizers on
-    this pool).  Load it with ``AKKA_NATIVE_PATH=<path>``."""
-    import pybind11
+    this pool).  Load it with ``AKKA_NATIVE_PATH=<path>``.
+
+    Objects are rebuilt when their source or a header is newer; a module
+    whose recorded source hash (``hash_path``) disagrees with the sources
+    while no timestamp says so (a copied tree) is rebuilt from scratch.
+    Concurrent builds (several ranks importing at once) serialise on a lock
+    file and the later ones find the module current."""
+    import fcntl
 
     tag = sanitize.replace(",", "-") if sanitize else None
     bdir = os.path.join(ROOT, "build", f"native-{tag}") if tag else BUILD
     os.makedirs(bdir, exist_ok=True)
+    with open(os.path.join(bdir, ".lock"), "w") as lk:
+        fcntl.flock(lk, fcntl.LOCK_EX)
+        try:
+            return _build_locked(bdir, tag, force, jobs, verbose, sanitize)
+        finally:
+            fcntl.flock(lk, fcntl.LOCK_UN)
+
+
+def _build_locked(bdir: str, tag, force: bool, jobs, verbose: bool, sanitize) -> str:
+    import pybind11
+
+    out = os.path.join(bdir, "_native" + sysconfig.get_config_var("EXT_SUFFIX")) if tag else ext_path()
+    digest = source_hash()
     py_inc = sysconfig.get_paths()["include"]
     opt = ["-O1", "-g", "-fno-omit-frame-pointer", f"-fsanitize={sanitize}"] if sanitize else ["-O3"]
     common = ["-fPIC", "-std=c++17", "-Wall", "-Wno-unused-function", "-I" + CSRC]
@@ -99,26 +169,27 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False, s
     ]
     hip_flags = ["-O3"] + common + [f"--offload-arch={ARCH}", "-I" + os.path.join(ROCM, "include")]
     headers = _headers()
-    steps = []
-    objs = []
-    for rel in HOST_SOURCES:
-        src = os.path.join(CSRC, rel)
-        obj = os.path.join(bdir, rel.replace("/", "_") + ".o")
-        objs.append(obj)
-        if force or _stale(obj, src, headers):
-            steps.append(["g++", *host_flags, "-c", src, "-o", obj])
-    for rel in HIP_SOURCES:
-        src = os.path.join(CSRC, rel)
-        obj = os.path.join(bdir, rel.replace("/", "_") + ".o")
-        objs.append(obj)
-        if force or _stale(obj, src, headers):
-            steps.append([os.path.join(ROCM, "bin", "hipcc"), *hip_flags, "-c", src, "-o", obj])
+
+    def plan(everything: bool):
+        steps, objs = [], []
+        for rel in HOST_SOURCES + HIP_SOURCES:
+            src = os.path.join(CSRC, rel)
+            obj = os.path.join(bdir, rel.replace("/", "_") + ".o")
+            objs.append(obj)
+            if everything or _stale(obj, src, headers):
+                cc = [os.path.join(ROCM, "bin", "hipcc"), *hip_flags] if rel.endswith(".hip") else ["g++", *host_flags]
+                steps.append([*cc, "-c", src, "-o", obj])
+        return steps, objs
+
+    steps, objs = plan(force)
+    mismatch = os.path.exists(out) and stale_reason(out) is not None
+    if mismatch and not steps:
+        steps, objs = plan(True)  # the hash says the module is old, no timestamp says which object
     jobs = jobs or min(8, os.cpu_count() or 4)
     with cf.ThreadPoolExecutor(max_workers=jobs) as ex:
         for f in [ex.submit(_run, s, verbose) for s in steps]:
             f.result()
-    out = os.path.join(bdir, "_native" + sysconfig.get_config_var("EXT_SUFFIX")) if tag else ext_path()
-    if force or steps or not os.path.exists(out):
+    if force or steps or not os.path.exists(out) or mismatch:
         tlib = _torch_lib()
         linker = ["g++", f"-fsanitize={sanitize}"] if sanitize else [os.path.join(ROCM, "bin", "hipcc")]
         link = [
@@ -135,6 +206,12 @@ def build(force: bool = False, jobs: int | None = None, verbose: bool = False, s
         ]
         _run(link, verbose)
         os.replace(out + ".tmp", out)
+        if digest is not None:
+            # written after the module: a crash in between leaves a mismatch
+            # (rebuild), never a new hash next to an old module
+            with open(hash_path(out) + ".tmp", "w") as f:
+                f.write(digest + "\n")
+            os.replace(hash_path(out) + ".tmp", hash_path(out))
     return out
 
 

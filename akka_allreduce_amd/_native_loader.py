@@ -37,7 +37,14 @@ def load():
 
         from . import _build
 
-        if not os.path.exists(_build.ext_path()) or os.environ.get("AKKA_REBUILD") == "1":
+        # A module built from other sources than the ones in the tree (edited
+        # kernels, an old .so next to new code) is rebuilt before it is
+        # imported -- never silently run; with no compiler here it is an error.
+        why = "AKKA_REBUILD=1" if os.environ.get("AKKA_REBUILD") == "1" else _build.stale_reason()
+        if why is not None:
+            if not _build.have_compiler():
+                raise RuntimeError(f"akka_allreduce_amd: the native extension at {_build.ext_path()} must be rebuilt "
+                                   f"({why}) but hipcc / g++ are not available here")
             _build.build()
         _mod = importlib.import_module("akka_allreduce_amd._native")
         return _mod

@@ -105,6 +105,16 @@ class AllReduceOutput:
         self._expander = expander
         self._event = event
 
+    @classmethod
+    def _make(cls, data: torch.Tensor, iteration: int, counts_per_chunk: torch.Tensor, geometry: "Geometry",
+              expander: Any, event: Any) -> "AllReduceOutput":
+        """The engine's per-round constructor: positional, no keyword parsing
+        (one of these per round; small rounds are priced by their host path)."""
+        o = cls.__new__(cls)
+        o.data, o.iteration, o.counts_per_chunk, o.geometry = data, iteration, counts_per_chunk, geometry
+        o._count, o._expander, o._event = None, expander, event
+        return o
+
     def wait(self) -> "AllReduceOutput":
         """Async rounds: make the current stream wait for the result (no-op otherwise)."""
         if self._event is not None:

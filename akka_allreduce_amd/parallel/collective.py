@@ -48,7 +48,7 @@ import torch
 from .._native_loader import load as _load
 from ..data import AllReduceOutput
 from ..messages import InitWorkers
-from ..worker import AllreduceWorker
+from ..worker import AllreduceWorker, _raw_stream
 
 
 class _RemoteRank:
@@ -195,6 +195,10 @@ class ThresholdAllreduce:
         self._ipc_direct = False  # exact ipc rounds straight on the caller's stream (use_lane("*_direct"))
         self._ipc_dev_on = False  # the ipc lane's round id lives on the device
         self._direct = None    # an open CapturableExact view
+        # direct ipc rounds: the last workgroup writes the counts table (like
+        # an engine round) instead of zeroing it on failure only (measurement
+        # knob of bench/small_rounds.py, AKKA_IPC_DIRECT_FINISH=1)
+        self._ipc_finish = os.environ.get("AKKA_IPC_DIRECT_FINISH") == "1"
         if transport == "onesided":
             # thresholds over mapped peer windows: no send ever waits for a
             # peer (parallel/onesided.py, csrc/transport/onesided.h)
@@ -336,6 +340,16 @@ class ThresholdAllreduce:
         ``out``: preallocated output buffer (reused across rounds)."""
         if x.numel() != self.data_size:
             raise ValueError(f"expected {self.data_size} elements, got {x.numel()}")
+        w = self.worker
+        if (w is not None and self.pacer is None and self._direct is None and not self._lane_os
+                and not self._ipc_direct and not self.fault_delay_s and w._fast_ok(x)):
+            # the common call: straight into the worker's native fast path
+            # (small rounds are priced by this host path, profiles/r06/small_rounds/)
+            o = w._fast_allreduce(x, async_op, out)
+            if o is None:
+                raise RuntimeError("round did not complete (thresholds need every rank in the scheduled transport)")
+            self._round += 1
+            return o
         if self.fault_delay_s:
             import time
 
@@ -444,8 +458,8 @@ class ThresholdAllreduce:
         # (raises once an earlier round's wait failed; a failing round zeroes
         # the fixed counts table on the device, so no output of a dead lane
         # reads as exact)
-        core.ipc_round_direct(x.data_ptr(), out.data_ptr(), torch.cuda.current_stream(self.device).cuda_stream,
-                              self._full_counts.data_ptr(), self._full_counts.numel())
+        core.ipc_round_direct(x.data_ptr(), out.data_ptr(), _raw_stream(self.device.index),
+                              self._full_counts.data_ptr(), self._full_counts.numel(), self._ipc_finish)
         return AllReduceOutput(out.view(-1), iteration=self._round, counts_per_chunk=self._full_counts, geometry=g,
                                expander=self.worker._expand_counts)
 
@@ -513,68 +527,50 @@ class ThresholdAllreduce:
 
     # ---- lane tuning -------------------------------------------------------
     LANES = {  # candidate -> (lane, exact transfer-unit bytes or -1, ipc mode, ipc fused, ipc workgroup size, lite)
+        # RCCL's own reduce-scatter + all-gather: the comparator, never chosen by tune()
         "collective": ("collective", -1, None, False, 0, False),
+        # the chunk-pipelined p2p schedule (RCCL send/recv + the gfx950 reduce)
         "p2p": ("p2p", -1, None, False, 0, False),
-        "p2p_block": ("p2p", 1 << 40, None, False, 0, False),
-        "ipc": ("ipc", -1, "pull", False, 256, False),
-        "ipc_bcast": ("ipc", -1, "bcast", False, 256, False),
-        "ipc_fused": ("ipc", -1, "pull", True, 256, False),
-        "ipc_fused_bcast": ("ipc", -1, "bcast", True, 256, False),
-        # 1024-thread workgroups: 4x the loads / stores in flight per CU when a
-        # rank has its GPU to itself (profiles/r02/ipc: -10 % at N=2 on one card)
-        "ipc_wide": ("ipc", -1, "pull", False, 1024, False),
-        "ipc_bcast_wide": ("ipc", -1, "bcast", False, 1024, False),
-        # fence-free hand-offs: write-through window stores, system-coherent
-        # loads, no buffer_wbl2 / buffer_inv per portion (IpcLane::set_lite)
-        "ipc_lite": ("ipc", -1, "pull", False, 1024, True),
-        "ipc_bcast_lite": ("ipc", -1, "bcast", False, 1024, True),
+        # the ipc round through the engine's bookkeeping: the exact lane of
+        # paced jobs (thAllreduce pacing needs the engine's round ids); its
+        # safe alternative there is p2p
         "ipc_fused_lite": ("ipc", -1, "pull", True, 1024, True),
-        # phase 2 as remote WRITES in the fused, fence-free form: over xGMI a
-        # store can beat a remote read, which the shared-card rehearsals cannot
-        # show (both stay inside one card's HBM there)
-        "ipc_fused_bcast_lite": ("ipc", -1, "bcast", True, 1024, True),
-        # the same ipc rounds launched straight on the caller's stream with a
+        # ipc rounds launched straight on the caller's stream with a
         # device-resident round id (no engine bookkeeping, no cross-stream
-        # events; exact rounds only -- every count is N): "<lane>_direct"
-        "ipc_fused_lite_direct": ("ipc", -1, "pull", True, 1024, True),
+        # events; exact rounds only -- every count is N): fence-free
+        # hand-offs (write-through window stores, system-coherent loads),
+        # unfused and fused ...
         "ipc_lite_direct": ("ipc", -1, "pull", False, 1024, True),
-        # the fenced twin of ipc_fused_lite_direct: plain window stores behind
-        # system release / acquire fences (the HIP memory model's protocol),
-        # for a link on which write-through + drain is not proven
+        "ipc_fused_lite_direct": ("ipc", -1, "pull", True, 1024, True),
+        # ... and their FENCED twin: plain window stores behind system release /
+        # acquire fences (the HIP memory model's protocol), for a link on which
+        # write-through + drain is not proven (or fails tune()'s validation burst)
         "ipc_fused_direct": ("ipc", -1, "pull", True, 1024, False),
         # the one-sided threshold lane at thresholds 1 (enable_onesided): one
         # role-partitioned launch, each chunk reduced and pushed as soon as
-        # its copies landed, peer chunks copied out as they land
+        # its copies landed, peer chunks copied out as they land; lite and fenced
         "onesided": ("onesided", -1, None, False, 0, False),
-        # ... with fenced hand-offs (OneSidedAllreduce(handoff="fenced"))
         "onesided_fenced": ("onesided", -1, None, False, 0, True),
     }
 
+    BURST_ROUNDS = 32  # tune(): back-to-back validation rounds every candidate must pass
+
     @staticmethod
     def lane_candidates(*, two_sided: bool, ipc_open: bool, onesided_ok: bool, exact: bool = True,
-                        paced: bool = False, lane_set: str = "default") -> list:
-        """The lanes tune() tries.  ``default``: at most six -- the p2p
-        schedule (RCCL p2p + the gfx950 reduce), the direct ipc rounds (lite,
-        fused lite, and the fused round's FENCED twin) and the one-sided lane
-        in both hand-off modes -- so a job on a node it has never run on
-        chooses among few lanes, each exact fast lane next to a fenced one.
-        ``all`` adds the engine-path ipc variants and p2p_block (measurement).
-        Paced or threshold jobs cannot take direct rounds: the engine-path
-        fused ipc round (lite + fenced) stands in."""
-        if lane_set not in ("default", "all"):
-            raise ValueError("lane_set must be 'default' or 'all'")
-        allset = lane_set == "all"
+                        paced: bool = False) -> list:
+        """The lanes tune() tries (every entry of LANES but the comparator):
+        the p2p schedule (RCCL p2p + the gfx950 reduce), the direct ipc rounds
+        (lite, fused lite, and the fused round's FENCED twin) and the one-sided
+        lane in both hand-off modes -- each fast lite lane next to a fenced
+        one, so a job on a node it has never run on never depends on an
+        unproven hand-off.  Paced jobs cannot take direct rounds: the
+        engine-path fused ipc round stands in (p2p is its safe alternative)."""
         c: list = []
         if two_sided:
-            c += ["p2p", "p2p_block"] if allset else ["p2p"]
+            c.append("p2p")
         if ipc_open:
-            if allset:
-                c += ["ipc", "ipc_bcast", "ipc_fused", "ipc_fused_bcast", "ipc_wide", "ipc_bcast_wide",
-                      "ipc_lite", "ipc_bcast_lite", "ipc_fused_lite", "ipc_fused_bcast_lite"]
-            if exact and not paced:
-                c += ["ipc_lite_direct", "ipc_fused_lite_direct", "ipc_fused_direct"]
-            elif not allset:
-                c += ["ipc_fused_lite", "ipc_fused"]
+            c += ["ipc_lite_direct", "ipc_fused_lite_direct", "ipc_fused_direct"] if exact and not paced \
+                else ["ipc_fused_lite"]
         if onesided_ok and exact:
             c += ["onesided", "onesided_fenced"]
         return c
@@ -596,8 +592,8 @@ class ThresholdAllreduce:
         Collective, like enable_ipc."""
         if self._exact_os is not None:
             return
-        if self.device.type != "cuda" or self.world_size < 2:
-            raise ValueError("the onesided lane needs GPUs and N > 1")
+        if self.world_size < 2:
+            raise ValueError("the onesided lane needs N > 1")
         if not self._th_exact:
             raise ValueError("lane 'onesided' of this engine runs exact rounds (thresholds 1); use "
                              "transport='onesided' for threshold rounds")
@@ -635,18 +631,20 @@ class ThresholdAllreduce:
             self.set_exact_unit_bytes(unit)
         self._ipc_direct = name.endswith("_direct")
 
-    def tune(self, candidates=None, rounds: int = 8, try_ipc: bool = True, lane_set: str = "default") -> dict:
+    def tune(self, candidates=None, rounds: int = 8, try_ipc: bool = True) -> dict:
         """Pick the fastest exact lane for this buffer on this job (collective).
 
         Every candidate runs three exact rounds with different integer data (the
-        last after `rounds` timed rounds of other data, so a stale read shows)
-        and the timed rounds.  Each step runs inside a try and is agreed on
+        last after `rounds` timed rounds of other data, so a stale read shows),
+        the timed rounds, and a validation burst of BURST_ROUNDS back-to-back
+        rounds with distinct per-rank, per-round data compared on the device:
+        one wrong element in any round on any rank disqualifies it (a fast
+        lite lane then loses to its fenced twin).  Each step runs inside a try and is agreed on
         (max over ranks of failure and time) before the next: a step that
         fails on any rank ends the candidate on every rank.  The
         one-sided lanes join when every rank could map every other rank's
         window.  Leaves the object on the winner; returns every candidate's
-        result and the choice.  Needs thresholds 1 (exact rounds).
-        ``lane_set``: the candidates when none are given (lane_candidates)."""
+        result and the choice.  Needs thresholds 1 (exact rounds)."""
         import time
 
         import torch.distributed as dist
@@ -688,8 +686,7 @@ class ThresholdAllreduce:
                                            "error": err or "another rank could not map its one-sided windows"}
             cands = self.lane_candidates(two_sided=spec[0] != "none",
                                          ipc_open=ipc_open and self.device.type == "cuda" and try_ipc,
-                                         onesided_ok=os_ok, exact=self._th_exact, paced=self.pacer is not None,
-                                         lane_set=lane_set)
+                                         onesided_ok=os_ok, exact=self._th_exact, paced=self.pacer is not None)
         S, N, r = self.data_size, self.world_size, self.rank
         dtype = self.worker.dtype
         x = torch.randn(S, device=self.device).to(dtype)
@@ -705,6 +702,34 @@ class ThresholdAllreduce:
             o = self(y)
             want = float((salt + 1) * N * (N + 1) // 2)
             return bool(torch.all(o.data == want).item()) and bool(torch.all(o.count == N).item())
+
+        # Validation burst (first contact with a node, docs/DESIGN.md 4f rule 4):
+        # BURST_ROUNDS back-to-back rounds, no host sync in between, every
+        # rank's input distinct per round -- (rank + 1) * 2^(k % 8) times a
+        # 1 / 2 pattern that flips every 61 elements -- and every output
+        # compared on the device with its exact sum (integers of at most
+        # 9 bits times a power of two: exact in fp32 and bf16 for N <= 16).
+        # A stale, torn or misplaced chunk in any round makes it non-zero.
+        pattern = (1 + (torch.arange(S, device=self.device) // 61) % 2).to(dtype)
+        tot = N * (N + 1) // 2
+
+        def burst(name: str) -> int:
+            from ..utils.faults import env_corrupt_round
+
+            hit = env_corrupt_round(r, name)
+            xin = torch.empty(S, device=self.device, dtype=dtype)
+            want = torch.empty(S, device=self.device, dtype=dtype)
+            bad = torch.zeros((), dtype=torch.int64, device=self.device)
+            for k in range(self.BURST_ROUNDS):
+                sc = float(1 << (k % 8))
+                torch.mul(pattern, (r + 1) * sc, out=xin)
+                o = self(xin, out=None if self.prefers_lane_output() else buf)
+                d = o.data.view(-1)
+                if k == hit and S > 0:
+                    d[(k * 7919) % S] += 1  # injected fault: one element of one round on this rank
+                torch.mul(pattern, tot * sc, out=want)
+                bad += torch.ne(d, want).sum()
+            return int(bad.item())
 
         def timed_block() -> float:
             ob = None if self.prefers_lane_output() else buf  # the lane's own output where it has one
@@ -727,13 +752,17 @@ class ThresholdAllreduce:
             # raised on one rank only ends the candidate on EVERY rank, so no
             # rank issues rounds its peers will never match (p2p lanes).
             steps = [("lane", lambda: (self.use_lane(name), True)[1]), ("exact1", lambda: exact(1)),
-                     ("exact2", lambda: exact(2)), ("timed", timed_block), ("exact3", lambda: exact(3))]
+                     ("exact2", lambda: exact(2)), ("timed", timed_block), ("exact3", lambda: exact(3)),
+                     ("burst", lambda: burst(name))]
+            burst_bad = None
             for tag, step in steps:
                 val = 0.0
                 try:
                     v = step()
-                    if tag == "timed":
+                    if tag in ("timed", "burst"):
                         val = float(v)
+                        if tag == "burst" and v:
+                            ok, err = False, f"burst: {int(v)} wrong elements on this rank"
                     elif not v:
                         ok = False
                     if name.startswith("onesided") and self._exact_os is not None and self._exact_os.error():
@@ -743,10 +772,14 @@ class ThresholdAllreduce:
                 bad, worst = self._agree_max([0.0 if ok else 1.0, val])
                 if tag == "timed":
                     ms = worst
+                elif tag == "burst":
+                    burst_bad = int(worst)  # the worst rank's count
                 if bad != 0.0:
                     ok = False
                     break
             res[name] = {"exact": ok, "ms": round(ms, 4) if ok else None}
+            if burst_bad is not None:
+                res[name]["burst"] = {"rounds": self.BURST_ROUNDS, "bad_elements_max_rank": burst_bad}
             if err:
                 res[name]["error"] = err
         good = [n for n in cands if res[n]["exact"]]
@@ -888,8 +921,7 @@ class CapturableExact:
         g = self.geometry
         if out is None:
             out = torch.empty_like(x)
-        stream = torch.cuda.current_stream(self.ar.device)
-        self.ar.worker._core.ipc_round_direct(x.data_ptr(), out.data_ptr(), stream.cuda_stream,
+        self.ar.worker._core.ipc_round_direct(x.data_ptr(), out.data_ptr(), _raw_stream(self.ar.device.index),
                                               self.counts.data_ptr(), self.counts.numel())
         return AllReduceOutput(out, iteration=-1, counts_per_chunk=self.counts, geometry=g,
                                expander=self.ar.worker._expand_counts)

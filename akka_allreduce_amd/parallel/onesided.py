@@ -47,6 +47,7 @@ import torch
 from .._native_loader import load as _load
 from ..utils import tracing as _tracing
 from ..data import AllReduceOutput, Geometry
+from ..worker import _raw_stream
 from .collective import _handle_exchange, env_rank_world
 
 _DTYPES = {torch.float32: "float32", torch.bfloat16: "bfloat16"}
@@ -103,8 +104,11 @@ class OneSidedOutput(AllReduceOutput):
         if self._call < 0:
             raise RuntimeError("a call captured into a graph has no status record (its replays do)")
         if self._status is None:
-            if self._stream is not None:
-                self._stream.synchronize()
+            if self._stream is not None:  # the raw handle of the stream the call ran on
+                dev = self.data.device
+                s = torch.cuda.ExternalStream(self._stream, device=dev) if self._stream \
+                    else torch.cuda.default_stream(dev)
+                s.synchronize()
             st = self._lane.status(self._call)
             if st["round"] < 0:
                 raise RuntimeError("onesided call has not finished")
@@ -172,6 +176,9 @@ class OneSidedAllreduce:
         self.device = torch.device(device)
         if self.device.type == "cuda":
             torch.cuda.set_device(self.device)
+        self._cuda = self.device.type == "cuda"
+        self._dev_index = (self.device.index if self.device.index is not None else torch.cuda.current_device()) \
+            if self._cuda else -1
         self.dtype = dtype
         self.data_size = int(data_size)
         self.geometry = Geometry(self.data_size, self.world_size, int(max_chunk_size))
@@ -256,7 +263,8 @@ class OneSidedAllreduce:
             raise ValueError(f"expected {self.data_size} elements, got {x.numel()}")
         if x.dtype != self.dtype or x.device != self.device:
             x = x.to(device=self.device, dtype=self.dtype)
-        x = x.reshape(-1).contiguous()
+        if x.dim() != 1 or not x.is_contiguous():
+            x = x.reshape(-1).contiguous()
         reuse = out is not None
         lane_out = out is None and self._rows is not None and self.data_sink is None
         if lane_out:
@@ -277,17 +285,23 @@ class OneSidedAllreduce:
                 self._counts[key] = counts
         else:
             counts = torch.empty((self.world_size, self._kmax), dtype=torch.int32, device=self.device)
-        stream = torch.cuda.current_stream(self.device) if self.device.type == "cuda" else None
+        # (a raw stream handle: building a Stream object per call costs ~1.7 us,
+        # profiles/r06/small_rounds/)
+        stream = _raw_stream(self._dev_index) if self._cuda else None
         event = None
         if async_op and stream is not None:
             side = self._side_stream()
-            side.wait_stream(stream)
+            side.wait_stream(torch.cuda.current_stream(self.device))
             for t in (x, counts) + ((out,) if out is not None else ()):  # in use on the side stream too
                 t.record_stream(side)
-            stream = side
+            stream = side.cuda_stream
         # roctx range around the enqueue (AKKA_TRACE=1; rocprofv3 --marker-trace)
-        with _tracing.range_(f"akka.onesided call {self.calls}"):
-            call = self.lane.round(stream.cuda_stream if stream is not None else 0, x.data_ptr(),
+        if _tracing._enabled:
+            with _tracing.range_(f"akka.onesided call {self.calls}"):
+                call = self.lane.round(stream if stream is not None else 0, x.data_ptr(),
+                                       0 if lane_out else out.data_ptr(), counts.data_ptr(), self._kmax)
+        else:
+            call = self.lane.round(stream if stream is not None else 0, x.data_ptr(),
                                    0 if lane_out else out.data_ptr(), counts.data_ptr(), self._kmax)
         if lane_out:
             if call < 0:
@@ -295,7 +309,7 @@ class OneSidedAllreduce:
             out = self._rows[call % len(self._rows)][: self.data_size]
         if async_op and stream is not None:
             event = torch.cuda.Event()
-            event.record(stream)
+            event.record(self._side)
         if call >= 0:  # (a captured call counts once per replay: note_replays)
             self.calls += 1
         o = OneSidedOutput(out.view(-1), lane=self.lane, call=call, stream=stream, counts_per_chunk=counts,

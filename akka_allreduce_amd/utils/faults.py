@@ -137,3 +137,17 @@ def env_bad_handoff(rank: int, handoff: str) -> bool:
     want = os.environ.get("AKKA_FAULT_BAD_HANDOFF")
     who = os.environ.get("AKKA_FAULT_BAD_HANDOFF_RANK")
     return want == handoff and (who is None or int(who) == int(rank))
+
+
+def env_corrupt_round(rank: int, lane: str) -> int:
+    """``AKKA_FAULT_CORRUPT_LANE=<lane>``: the index of the round of
+    ``ThresholdAllreduce.tune()``'s validation burst in which this rank
+    corrupts one element of the lane's output (``AKKA_FAULT_CORRUPT_ROUND``,
+    default 7), or -1.  ``AKKA_FAULT_CORRUPT_RANK`` (default 0) picks the
+    rank.  Stands in for a data-after-flag reorder on a real link: the
+    candidate must be disqualified and its fenced twin chosen."""
+    if os.environ.get("AKKA_FAULT_CORRUPT_LANE") != lane:
+        return -1
+    if int(os.environ.get("AKKA_FAULT_CORRUPT_RANK", "0")) != int(rank):
+        return -1
+    return int(os.environ.get("AKKA_FAULT_CORRUPT_ROUND", "7"))

@@ -47,6 +47,18 @@ DataSink = Callable[[AllReduceOutput], None]
 _DTYPES = {torch.float32: "float32", torch.bfloat16: "bfloat16"}
 
 
+def _raw_stream(index: int) -> int:
+    """The current stream of device ``index`` as a raw handle: ~0.1 us, where
+    ``torch.cuda.current_stream(dev).cuda_stream`` builds a Stream object
+    (~1.7 us, a sixth of a small round's host time on MI355X)."""
+    return torch._C._cuda_getCurrentRawStream(index)
+
+
+if not hasattr(torch._C, "_cuda_getCurrentRawStream"):  # pragma: no cover - older torch builds
+    def _raw_stream(index: int) -> int:  # noqa: F811
+        return torch.cuda.current_stream(index).cuda_stream
+
+
 def _native():
     from . import _native_loader
 
@@ -124,6 +136,9 @@ class AllreduceWorker:
         self._fast_source = dataSource is None  # rounds fed by allreduce(): eligible for the native fast path
         self._fast_pending: Dict[int, Tuple[torch.Tensor, torch.Tensor]] = {}
         self.fast_rounds = 0  # rounds that took the native fast path
+        self._cuda = self.device.type == "cuda"
+        self._dev_index = self.device.index if self._cuda else -1
+        self._counts_by_out: Dict[int, torch.Tensor] = {}
         self.epochs = 0  # RCCL membership epochs after the first (re-InitWorkers with a new unique id)
         self.reactive_timeout: Optional[float] = None  # reactive allreduce(): max seconds to wait
 
@@ -427,24 +442,55 @@ class AllreduceWorker:
     def _fast_ok(self, tensor: torch.Tensor) -> bool:
         """Collective-style call on the scheduled transport, whose rounds
         complete inside the call: buffers can be bound natively."""
-        return (self.transport == "stream" and not self._deferred and self.initialized
+        return (self.transport == "stream" and not self._deferred and self.id >= 0
                 and self.dataSink is None and self._fast_source and not self._pre_init and not self._rounds
-                and isinstance(tensor, torch.Tensor) and tensor.device == self.device and tensor.dtype == self.dtype
-                and tensor.is_contiguous() and tensor.numel() == self.geometry.dataSize)
+                and isinstance(tensor, torch.Tensor) and self._buffer_ok(tensor))
+
+    def _buffer_ok(self, t: torch.Tensor) -> bool:
+        """A contiguous tensor of dataSize elements of the worker's dtype on its
+        device (plain int / identity compares: this runs twice per round)."""
+        return (t.dtype is self.dtype and t.get_device() == self._dev_index and t.numel() == self.geometry.dataSize
+                and t.is_contiguous())
+
+    def _counts_for(self, out: torch.Tensor) -> torch.Tensor:
+        """The [N, kmax] counts table that travels with a caller-owned output
+        buffer: reused with THAT buffer (the caller reuses the buffer only once
+        its previous round was consumed, which covers its counts too), so a
+        round with ``out`` given allocates nothing."""
+        key = out.data_ptr()
+        c = self._counts_by_out.get(key)
+        if c is None:
+            if len(self._counts_by_out) >= 16:  # bounded: buffers the caller dropped
+                self._counts_by_out.pop(next(iter(self._counts_by_out)))
+            g = self.geometry
+            c = self._counts_by_out[key] = torch.empty((g.workerNum, g.kmax), dtype=torch.int32, device=self.device)
+        return c
 
     def _fast_allreduce(self, x: torch.Tensor, async_op: bool, out: Optional[torch.Tensor]) -> Optional[AllReduceOutput]:
+        # The host cost of this call is the price of every small round (the
+        # reference's regime: maxChunkSize 2, M:104): raw stream handle, no
+        # allocation when ``out`` is given, one native call
+        # (profiles/r06/small_rounds/README.md).
         g = self.geometry
         if out is None:
             out = torch.empty(g.dataSize, dtype=self.dtype, device=self.device)
-        elif out.numel() != g.dataSize or out.dtype != self.dtype or out.device != self.device \
-                or not out.is_contiguous():
+            counts = torch.empty((g.workerNum, g.kmax), dtype=torch.int32, device=self.device)
+        elif not self._buffer_ok(out):
             raise ValueError("out must be a contiguous tensor of dataSize elements, worker dtype and device")
-        counts = self._alloc_counts()
+        else:
+            counts = self._counts_by_out.get(out.data_ptr())
+            if counts is None:
+                counts = self._counts_for(out)
         r = self._next_round
         self._next_round += 1
-        cuda = self.device.type == "cuda"
+        cuda = self._cuda
         async_op = bool(async_op) and cuda
-        stream = torch.cuda.current_stream(self.device) if cuda else None
+        if cuda:
+            sptr = _raw_stream(self._dev_index)
+            wait = not async_op
+        else:
+            sptr = self.host_stream or 0
+            wait = self.host_stream is not None
         local = g.workerNum == 1  # a purely local round runs on the caller's stream
         if async_op and not local:
             # the caller's stream will not wait: keep every buffer alive until
@@ -452,10 +498,11 @@ class AllreduceWorker:
             self._keep_alive_on_internal_streams(x, out, counts)
         self._fast_pending[r] = (out, counts)
         try:
-            with _tracing.range_(f"akka.round {r}"):
-                done = self._core.fast_round(r, x.data_ptr(), out.data_ptr(), counts.data_ptr(),
-                                             stream.cuda_stream if cuda else (self.host_stream or 0),
-                                             (cuda and not async_op) or (not cuda and self.host_stream is not None))
+            if _tracing._enabled:
+                with _tracing.range_(f"akka.round {r}"):
+                    done = self._core.fast_round(r, x.data_ptr(), out.data_ptr(), counts.data_ptr(), sptr, wait)
+            else:
+                done = self._core.fast_round(r, x.data_ptr(), out.data_ptr(), counts.data_ptr(), sptr, wait)
         except Exception as e:  # tryCatch semantics as in receive()
             self._fast_pending.pop(r, None)
             self.errors.append(e)
@@ -464,16 +511,20 @@ class AllreduceWorker:
                 raise
             return None
         self.fast_rounds += 1
+        expander = self._expand_counts if cuda else None
+        res = None
         for d in done:
             o, c = self._fast_pending.pop(d)
             event = None
             if async_op:
                 event = torch.cuda.Event()
-                event.record(stream if local else self._internal_streams()[1])
-            self._outputs[d] = AllReduceOutput(o, iteration=d, counts_per_chunk=c.view(g.workerNum, g.kmax),
-                                               geometry=g, expander=self._expand_counts if cuda else None,
-                                               event=event)
-        return self._outputs.pop(r, None)
+                event.record(torch.cuda.current_stream(self.device) if local else self._internal_streams()[1])
+            o = AllReduceOutput._make(o, d, c, g, expander, event)
+            if d == r:
+                res = o
+            else:
+                self._outputs[d] = o
+        return res
 
     # ------------------------------------------------------------------ reactive transport progress
     def _core_is_sim(self) -> bool:

@@ -84,9 +84,6 @@ def parse():
                    help="ipc: no RCCL communicator, every exact round on the one-sided xGMI lane; ipc_p2p: the "
                         "p2p schedules over mailboxes in mapped peer memory (with AKKA_SHARE_GPU=1 either rehearses "
                         "the N-rank flow with N processes on one card)")
-    p.add_argument("--lane-set", choices=["default", "all"], default="default",
-                   help="lane selection candidates: default = p2p, the direct ipc rounds (lite, fused lite, fused "
-                        "fenced) and the one-sided lane (lite, fenced); all = also every engine-path ipc variant")
     p.add_argument("--lane-output", choices=["on", "off"], default="on",
                    help="on: a one-sided lane chosen for the timed rounds returns its window row (no copy into a "
                         "caller buffer; the output of a round is valid until the next round)")
@@ -948,7 +945,7 @@ def main() -> int:
         env_phase_stall(rank, "lane_select")
         # (ipc_only: the two-sided lane failed its preflight; the engine on the
         # ipc data plane has no p2p lane, so the window lanes alone compete)
-        return ar.tune(try_ipc=args.ipc == "on" or ipc_only, lane_set=args.lane_set)
+        return ar.tune(try_ipc=args.ipc == "on" or ipc_only)
 
     lane_sel = None
     if world > 1 and ar.transport == "stream" and args.lane == "auto" and args.lane_select == "on":

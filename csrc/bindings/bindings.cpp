@@ -288,13 +288,21 @@ class WorkerCore final : public EngineHost {
   // out with direct rounds; a failed wait zeroes it on the device.  A wait of
   // an earlier round that failed makes this call raise, like the engine path
   // (StreamLink::ipc_round).
-  void ipc_round_direct(uintptr_t in, uintptr_t out, uintptr_t stream, uintptr_t counts, int64_t n) {
+  // `finish`: the round's last workgroup writes `counts` (N everywhere, 0 after
+  // a failed wait) like an engine-path round, instead of zeroing it only on
+  // failure (measurement knob, bench/small_rounds.py).
+  void ipc_round_direct(uintptr_t in, uintptr_t out, uintptr_t stream, uintptr_t counts, int64_t n, bool finish) {
     AKKA_CHECK(stream_link_ && stream_link_->ipc(), "ipc_round_direct: the ipc lane is not open");
     AKKA_CHECK(stream_link_->ipc()->device_rounds(), "ipc_round_direct: switch device rounds on first");
     AKKA_CHECK(stream_link_->ipc()->error_now() == 0,
                "ipc lane: a wait of an earlier round timed out (peer missing?); its rounds are not trustworthy");
-    stream_link_->ipc()->round(reinterpret_cast<StreamH>(stream), reinterpret_cast<const void*>(in),
-                               reinterpret_cast<void*>(out), reinterpret_cast<int32_t*>(counts), counts ? n : 0);
+    int32_t* c = reinterpret_cast<int32_t*>(counts);
+    if (finish && c)
+      stream_link_->ipc()->round(reinterpret_cast<StreamH>(stream), reinterpret_cast<const void*>(in),
+                                 reinterpret_cast<void*>(out), nullptr, 0, c, n, engine_->geometry().N);
+    else
+      stream_link_->ipc()->round(reinterpret_cast<StreamH>(stream), reinterpret_cast<const void*>(in),
+                                 reinterpret_cast<void*>(out), c, c ? n : 0);
   }
   // The lane's error word as far as the kernels got (no synchronisation).
   uint32_t ipc_error_now() {
@@ -563,12 +571,17 @@ class WorkerCore final : public EngineHost {
     AKKA_CHECK(!deferred_, "fast_round: deferred host streams complete rounds outside the call");
     pre_[r] = Prebound{in, out, counts, stream, stream_wait};
     fast_delivered_.clear();
+    // collective use has nobody to tell CompleteAllreduce: skip that Python
+    // callback per round (notify_complete); one attribute lookup per call
+    fast_no_master_ = host_.attr("master").is_none();
     try {
       engine_->start(r);
     } catch (...) {
       pre_.erase(r);
+      fast_no_master_ = false;
       throw;
     }
+    fast_no_master_ = false;
     std::vector<int32_t> got;
     got.swap(fast_delivered_);
     for (int32_t d : got) dp_->unbind(d);
@@ -612,7 +625,10 @@ class WorkerCore final : public EngineHost {
     fast_delivered_.push_back(round);
   }
   void notify_complete(int32_t round) override {
-    if (pre_.count(round) && host_.attr("master").is_none()) return;  // nobody to tell (collective use)
+    // (deliver() has already moved a prebound round to fast_delivered_)
+    if (fast_no_master_ && std::find(fast_delivered_.begin(), fast_delivered_.end(), round) != fast_delivered_.end())
+      return;  // nobody to tell (collective use)
+    if (pre_.count(round) && host_.attr("master").is_none()) return;
     host_.attr("_notify_complete")(round);
   }
   void release(int32_t round) override {
@@ -644,6 +660,7 @@ class WorkerCore final : public EngineHost {
   std::unordered_map<int32_t, Prebound> pre_;
   std::unique_ptr<IpcLane> ipc_pending_;  // created by ipc_handle, moved into the link by ipc_open
   std::vector<int32_t> fast_delivered_;
+  bool fast_no_master_ = false;  // inside fast_round, with no master to notify
 
   py::object host_;
   std::string link_kind_;
@@ -765,7 +782,7 @@ PYBIND11_MODULE(_native, m) {
       .def("ipc_error", &WorkerCore::ipc_error)
       .def("ipc_close", &WorkerCore::ipc_close)
       .def("ipc_round_direct", &WorkerCore::ipc_round_direct, py::arg("in_ptr"), py::arg("out_ptr"), py::arg("stream"),
-           py::arg("counts") = 0, py::arg("n") = 0)
+           py::arg("counts") = 0, py::arg("n") = 0, py::arg("finish") = false)
       .def("ipc_error_now", &WorkerCore::ipc_error_now)
       .def("ipc_device_rounds", &WorkerCore::ipc_device_rounds)
       .def("ipc_current_round", &WorkerCore::ipc_current_round)

@@ -238,9 +238,11 @@ bool Engine::bulk_eligible(int32_t r) const {
   // rank has to take it for the same rounds.  Local state that would make
   // this rank deviate (older rounds still open, part of r already received)
   // is an error rather than a silent switch to a different schedule.
-  if (!link_ || N_ < 2 || int32_t(peers_.size()) != N_) return false;
+  // (N = 1 too: the whole round is one local pass, no per-chunk bookkeeping)
+  if (!link_ || int32_t(peers_.size()) != N_) return false;
   if (min_scatter_ != N_ || int64_t(min_reduced_) != g_.total_chunks()) return false;
   const bool clean = r == round_ && r == max_round_ && !completed_.count(r) && find_row(r) == nullptr;
+  if (!clean && N_ == 1) return false;  // (catch-up at N = 1: the message flow, as before)
   if (!clean) {
     // outbox / reactive links run the message flow for every round anyway
     AKKA_CHECK(!link_->takes_exact_rounds(),

@@ -10,7 +10,7 @@
 //             workgroup barrier -> plain loads of the payload.
 // The explicit s_waitcnt after the release fence is there on purpose: the
 // compiler may drop its own when it proves the scoreboard empty, letting the
-// flag overtake the write-back (MI355X_MICROARCH.md, compiler hazard).
+// flag overtake the write-back (docs/DESIGN.md section 4f rule 2).
 // Every wait is bounded (wall clock, `timeout` ticks): on expiry the waiting
 // workgroup sets this rank's error word and the abort word of EVERY rank's
 // flag area (wait_flag), skips its data work and still signals, so every grid

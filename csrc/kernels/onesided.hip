@@ -4,8 +4,8 @@
 // functions of onesided_protocol.h, shared with the CPU backend; this file
 // maps them onto the roles of one launch and moves the bytes.
 //
-// Hand-offs are fence-free ("lite", MI355X_MICROARCH.md handoff-flag /
-// publish-large): every byte a peer reads is stored write-through (sc0 sc1)
+// Hand-offs are fence-free ("lite", docs/DESIGN.md section 4f rule 3):
+// every byte a peer reads is stored write-through (sc0 sc1)
 // or read system-coherent (sc0 sc1 loads), each storing wave drains
 // (s_waitcnt vmcnt(0)) before its workgroup's flag store, and flag / local
 // words live in uncached memory, accessed with system-scope atomics -- so a

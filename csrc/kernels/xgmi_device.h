@@ -11,7 +11,7 @@
 //             workgroup barrier -> system-coherent loads of the payload.
 // The explicit s_waitcnt after the release fence is there on purpose: the
 // compiler may drop its own when it proves the scoreboard empty, letting the
-// flag overtake the write-back (MI355X_MICROARCH.md, compiler hazard).
+// flag overtake the write-back (docs/DESIGN.md section 4f rule 2).
 // Only to be included by .hip translation units.
 #pragma once
 
@@ -142,9 +142,9 @@ __device__ inline void copy_in(char* __restrict__ dst, const char* __restrict__ 
 // (sc0 sc1, write-through) store; each storing wave waits for its stores
 // (s_waitcnt vmcnt(0)), the workgroup meets at a barrier, lane 0 stores the
 // flag.  Consumer: lane(s) poll the flag(s); after the barrier every load of
-// the bytes is a system-coherent load.  No buffer_wbl2 / buffer_inv at all --
-// MI355X_MICROARCH.md's "handoff-flag" / "publish-large" forms (write-through
-// stores + drained flag; sc loads in place of the acquire), at system scope.
+// the bytes is a system-coherent load.  No buffer_wbl2 / buffer_inv at all
+// (docs/DESIGN.md section 4f rule 3: write-through stores + drained flag; sc
+// loads in place of the acquire), at system scope.
 __device__ inline void store_sys16(__amdgpu_buffer_rsrc_t r, int64_t off, const uint4& v) {
   u32x4 w;
   w[0] = v.x;

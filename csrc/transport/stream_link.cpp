@@ -207,7 +207,29 @@ bool StreamLink::bulk_round(int32_t r) {
   AKKA_CHECK(dp_, "stream link has no data plane");
   const Geometry& g = dp_->geometry();
   const int32_t N = g.N;
-  if (N < 2) return false;  // a local round is already one pass
+  if (N < 2) {
+    // N = 1: input -> output in one launch on the producer's stream (bind_input
+    // put the round there), the counts fill riding in it (HipDevice::fill_i32);
+    // none of the per-chunk scatter / reduce / broadcast bookkeeping, whose
+    // host cost grows with the chunk count (profiles/r06/small_rounds/)
+    engine_->ensure_output(r);
+    // claim the round's ring row first: claiming it later (complete_bulk's
+    // set_count) flushes the pending reduce, and the counts fill could no
+    // longer ride in it -- a second launch per round
+    dp_->set_count(r, 0, 0, 1);
+    const StreamH s = dp_->exec_stream(r);
+    dp_->wait_input(r, s);
+    const void* in = dp_->input_chunk(r, 0, 0).ptr;
+    void* out = dp_->output_at(r, 0, 0);
+    if (in != out && g.S > 0) {
+      auto specs = split_reduce(out, {in}, g.S);
+      dp_->device()->reduce(s, specs.data(), int32_t(specs.size()), dp_->dtype());
+    }
+    stats_.rounds++;
+    stats_.bulk_rounds++;
+    mark_scheduled(r);
+    return true;
+  }
   AKKA_CHECK(p2p_->nranks() == N && p2p_->rank() == dp_->me(), "p2p communicator does not match the worker geometry");
   const bool native = p2p_->has_collectives() && g.S == int64_t(N) * g.step;
   // Auto = the framework's own p2p schedule (gfx950 reduce); RCCL's

@@ -78,6 +78,8 @@ def test_bench_multirank_on_one_card(plane):
     sel = d["lane_select"]
     cands = [k for k in sel if k != "chosen"]
     assert all(sel[k]["exact"] is True for k in cands), sel
+    # every candidate passed tune()'s validation burst (32 back-to-back rounds)
+    assert all(sel[k]["burst"] == {"rounds": 32, "bad_elements_max_rank": 0} for k in cands), sel
     assert d["lane"] == sel["chosen"]
     lp = d["link_probe"]  # the N x N matrix, labelled: ranks share one card, not xGMI
     assert "share ONE GPU" in lp["note"] and len(lp["push_GBps"]) == n and len(lp["pull_GBps"][0]) == n

@@ -86,13 +86,9 @@ def test_bench_lane_select():
     # the default (pruned) set on CPU processes: the p2p schedule alone
     assert [k for k in sel if k != "chosen"] == ["p2p"], sel
     assert sel["chosen"] == "p2p" and d["lane"] == "p2p"
-    d = _run(3, "--lane-set", "all")
-    sel = d["lane_select"]
-    cands = ("p2p", "p2p_block")
-    assert all(sel[c]["exact"] is True and sel[c]["ms"] > 0 for c in cands)
-    assert "collective" not in sel
-    faster = min(cands, key=lambda ln: sel[ln]["ms"])
-    assert sel["chosen"] == faster and d["lane"] == faster and d["lane_is_framework"] is True
+    assert sel["p2p"]["exact"] is True and sel["p2p"]["ms"] > 0
+    assert sel["p2p"]["burst"] == {"rounds": 32, "bad_elements_max_rank": 0}
+    assert "collective" not in sel and d["lane_is_framework"] is True
     assert d["other_lane"]["lane"] == "collective"
     assert d["exact"] is True and d["groups_per_round"] > 0
 
@@ -101,11 +97,11 @@ def test_bench_n8_full_flow():
     """The driver's largest N: 8 ranks through preflight, lane selection,
     timed rounds, check, comparator and the other lane (uneven blocks: 0.3 MiB
     of fp32 = 78643 elements over 8 ranks, 16 KiB chunks)."""
-    d = _run(8, "--size-mb", "0.3", "--chunk-mb", "0.015625", "--lane-set", "all")
+    d = _run(8, "--size-mb", "0.3", "--chunk-mb", "0.015625")
     assert d["n_gpus"] == 8 and d["config"]["parallelism"] == "dp8" and d["exact"] is True
     assert d["p2p_nranks"] == 8 and [r["rank"] for r in d["rank_devices"]] == list(range(8))
     sel = d["lane_select"]
-    assert all(sel[c]["exact"] is True for c in ("p2p", "p2p_block")) and "collective" not in sel
+    assert sel["p2p"]["exact"] is True and "collective" not in sel
     assert d["lane"] == sel["chosen"] and d["xgmi_bound_algbw_GBps"] == pytest.approx(612.0, abs=1.0)
     assert abs(d["busbw_GBps"] - d["value"] * 2 * 7 / 8) < 1e-2
 

@@ -186,7 +186,7 @@ def test_ipc_direct_lanes_switch_with_engine_lanes():
     stream) alternating with the engine path and with the fenced direct
     twin: every round exact on every rank, and the lane's round id -- handed
     between host and device at every switch -- advances by one per round."""
-    seq = "ipc_lite_direct,ipc_lite_direct,ipc_fused_lite,ipc_fused_direct,ipc_fused_lite_direct,ipc,ipc_lite_direct"
+    seq = "ipc_lite_direct,ipc_lite_direct,ipc_fused_lite,ipc_fused_direct,ipc_fused_lite_direct,ipc_fused_lite,ipc_lite_direct"
     r, rows = _run(4, "--size", str(1 << 20), "--rounds", "7", "--lane-seq", seq)
     assert r.returncode == 0, r.stderr[-3000:]
     for d in rows:

@@ -25,23 +25,33 @@ def test_default_candidates_are_pruned_with_fenced_twins():
     assert ThresholdAllreduce.LANES["ipc_fused_direct"][5] is False
     assert ThresholdAllreduce.LANES["ipc_fused_lite_direct"][5] is True
     assert ThresholdAllreduce.LANES["onesided_fenced"][0] == "onesided"
-    # the engine-path variants and p2p_block only behind lane_set="all"
-    allc = ThresholdAllreduce.lane_candidates(two_sided=True, ipc_open=True, onesided_ok=True, lane_set="all")
-    assert set(DEFAULT) <= set(allc) and "p2p_block" in allc and "ipc_bcast_wide" in allc
-    assert not ({"p2p_block", "ipc", "ipc_bcast", "ipc_wide"} & set(c))
+
+
+def test_lane_table_is_pruned():
+    """at most 8 lanes, the comparator included; no
+    measurement-only variants (engine-path ipc modes, p2p_block) and no
+    'all' candidate set."""
+    assert len(ThresholdAllreduce.LANES) <= 8
+    assert set(ThresholdAllreduce.LANES) == {"collective", "p2p", "ipc_fused_lite", "ipc_lite_direct",
+                                            "ipc_fused_lite_direct", "ipc_fused_direct", "onesided",
+                                            "onesided_fenced"}
+    with pytest.raises(TypeError):
+        ThresholdAllreduce.lane_candidates(two_sided=True, ipc_open=True, onesided_ok=True, lane_set="all")
+    # tune() never offers the comparator
+    for kw in ({}, {"paced": True}, {"exact": False}):
+        assert "collective" not in ThresholdAllreduce.lane_candidates(two_sided=True, ipc_open=True,
+                                                                      onesided_ok=True, **kw)
 
 
 def test_candidates_follow_what_the_job_can_run():
     # ipc-only job (no RCCL communicator): the window lanes alone
     assert ThresholdAllreduce.lane_candidates(two_sided=False, ipc_open=True, onesided_ok=True) == DEFAULT[1:]
     # paced job: no direct rounds (they bypass the pacer); the engine-path
-    # fused round in both hand-off modes stands in
+    # fused lite round stands in, p2p is its safe alternative
     c = ThresholdAllreduce.lane_candidates(two_sided=True, ipc_open=True, onesided_ok=True, paced=True)
-    assert c == ["p2p", "ipc_fused_lite", "ipc_fused", "onesided", "onesided_fenced"]
+    assert c == ["p2p", "ipc_fused_lite", "onesided", "onesided_fenced"]
     # windows unavailable: the two-sided lane only
     assert ThresholdAllreduce.lane_candidates(two_sided=True, ipc_open=False, onesided_ok=False) == ["p2p"]
-    with pytest.raises(ValueError):
-        ThresholdAllreduce.lane_candidates(two_sided=True, ipc_open=True, onesided_ok=True, lane_set="some")
 
 
 def test_cfg4_switches_to_fenced_handoff_on_bad_validation():

@@ -143,6 +143,148 @@ def reduces(h, r=None):
     return [m[1:] for m in h.take_sent("gather") if r is None or m[3] == r]
 
 
+def test_t1_sum_up_all_correct_data():
+    """SPEC:57-95 (N=2, S=3, C=2, thresholds 1, maxLag 5, worker 1 -- the
+    one case where the spec maps the worker's own id to the real worker, so
+    its self-delivery runs, W:228-232): two rounds of generator idx + iter.
+    Worker 1 owns [2, 3): it scatters block 0 to rank 0, reduces its own
+    element from both copies (count 2) and completes each round with 2 x
+    input and counts [2, 2, 2] (the spec's assertiveDataSink)."""
+    h = SpecHarness(2, 3, 2, 1.0, 1.0, 5, me=1)
+    for it in (0, 1):
+        x = basic(3, it)
+        h.start(x)
+        assert [(m[1], m[2], m[3], m[5]) for m in h.take_sent("scatter")] == [(0, 0, it, x[0:2])]
+        h.scatter(0, 0, it, [x[2]])  # rank 0's copy of my element (same generator)
+        assert reduces(h) == [(0, 0, it, 2, [2 * x[2]])]
+        h.reduce(0, 0, it, 2, [2 * x[0], 2 * x[1]])
+        assert h.outputs[-1] == (it, [2 * v for v in x], [2, 2, 2], "threshold")
+    assert len(h.outputs) == 2
+
+
+def _t2_early_reduce_of_a_future_round():
+    h = SpecHarness(4, 8, 2, 1.0, 0.8, 5)
+    h.start(basic(8, 0))
+    for s, v in ((1, [11.0, 10.0]), (2, [10.0, 20.0]), (3, [9.0, 10.0])):
+        h.reduce(s, 0, 3, 4, v)
+    for i in (1, 2, 3):
+        h.start(basic(8, i))
+    return h
+
+
+def test_t3_no_longer_act_on_completed_scatter():
+    """SPEC:133-138: after round 3 completed (T2's ReduceBlocks), the
+    ScatterBlocks of that round from every peer change nothing: no message,
+    no output (expectNoMsg); the senders count them as outdated."""
+    h = _t2_early_reduce_of_a_future_round()
+    assert [o[0] for o in h.outputs] == [0, 1, 2, 3]
+    h.take_sent()
+    for s in (1, 2, 3):
+        h.scatter(s, 0, 3, [2.0 * s, 2.0 * s])
+    assert h.take_sent() == [] and len(h.outputs) == 4
+    assert sum(h.stats(s)["scatter_outdated"] for s in (1, 2, 3)) == 3
+
+
+def test_t6_single_round_allreduce():
+    """SPEC:175-213 (N=4, S=8, C=2, thR 1, thC 0.75 -> 3): the worker's
+    scatters go out in the exact rotated order, self first (delivered in
+    place, W:228-232), then ranks 1, 2, 3 with [2i, 2i+1]; the reduce waits
+    for all four copies (count 4) and goes to ranks 1, 2, 3 in that order;
+    the round completes at the third reduced chunk (own + 2), the fourth is
+    outdated.  (The spec's probe plays the worker's own copy as [0, 0]; here
+    the worker's real input [0, 1] is summed: [12, 13].)"""
+    h = SpecHarness(4, 8, 2, 1.0, 0.75, 5)
+    h.start(basic(8, 0))
+    assert [(m[1], m[2], m[3], m[5]) for m in h.take_sent("scatter")] == \
+        [(i, 0, 0, [2.0 * i, 2.0 * i + 1]) for i in (1, 2, 3)]
+    for i in (1, 2):
+        h.scatter(i, 0, 0, [2.0 * i, 2.0 * i])
+        assert reduces(h) == []
+    h.scatter(3, 0, 0, [6.0, 6.0])
+    assert reduces(h) == [(d, 0, 0, 4, [12.0, 13.0]) for d in (1, 2, 3)]
+    h.reduce(1, 0, 0, 4, [11.0, 10.0])
+    assert h.outputs == []
+    h.reduce(2, 0, 0, 4, [10.0, 20.0])
+    assert h.outputs == [(0, [12.0, 13.0, 11.0, 10.0, 10.0, 20.0, 0.0, 0.0], [4, 4, 4, 4, 4, 4, 0, 0], "threshold")]
+    h.reduce(3, 0, 0, 4, [9.0, 10.0])
+    assert len(h.outputs) == 1 and h.stats(3)["gather_outdated"] == 1
+
+
+def test_t7_uneven_size_sending_to_self_first():
+    """SPEC:215-238 (N=2, S=3, C=1, thresholds 1, maxLag 1, worker 1):
+    blocks [0, 2) and [2, 3); worker 1 delivers its own element to itself
+    first (in place), then chunks 0 and 1 of block 0 to rank 0, in order."""
+    h = SpecHarness(2, 3, 1, 1.0, 1.0, 1, me=1)
+    h.start(basic(3, 0))
+    assert [(m[1], m[2], m[3], m[5]) for m in h.take_sent("scatter")] == [(0, 0, 0, [0.0]), (0, 1, 0, [1.0])]
+    assert reduces(h) == [] and h.outputs == []  # its own element waits for rank 0's copy
+
+
+def per_dest(msgs):
+    """Messages grouped by destination, each in emission order: the order the
+    reference's per-pair FIFO makes observable (W:213-237 sends every chunk to
+    a peer in ascending order; across peers -- different links -- the lane's
+    interleaving is its own)."""
+    out: dict = {}
+    for m in msgs:
+        out.setdefault(m[1], []).append(m)
+    return out
+
+
+def test_t18_rounds_complete_in_order_using_early_copies():
+    """SPEC:664-734 (N=3, S=9, C=2 -> chunks of 2 and 1, thR 0.75 -> 2, thC
+    0.75 -> 4 of 6), the lane's documented divergence pinned.  The reference
+    scatters round 1 as soon as it is started and completes round 1 BEFORE
+    round 0 (out-of-order completion, W:277-284).  The lane serves one round
+    per call, in order, and a peer's round-r pushes all precede its round-r+1
+    pushes (its call for r+1 starts after its call for r ended), so the
+    spec's exact interleaving cannot occur; its point -- a fast peer's next
+    round overtaking a slow one's current round -- does: rank 1 runs ahead
+    into round 1 while rank 2 still owes round 0.  Rank 1's round-1 copies
+    and reduced chunks land early in round 1's ring row; rounds reach the
+    sink as 0, then 1; round 1 -- served the moment round 0 completes --
+    reduces over the early copies and completes at once from the chunks that
+    had landed."""
+    h = SpecHarness(3, 9, 2, 0.75, 0.75, 5)
+    h.start(basic(9, 0))
+    sc = per_dest(h.take_sent("scatter"))
+    assert {d: [(m[2], m[3], m[5]) for m in v] for d, v in sc.items()} == \
+        {1: [(0, 0, [3.0, 4.0]), (1, 0, [5.0])], 2: [(0, 0, [6.0, 7.0]), (1, 0, [8.0])]}
+    # rank 1 (fast): its round-0 copies -> the reduces fire at 2 copies
+    h.scatter(1, 0, 0, [0.0, 1.0])
+    assert reduces(h) == [(1, 0, 0, 2, [0.0, 2.0]), (2, 0, 0, 2, [0.0, 2.0])]
+    h.scatter(1, 1, 0, [2.0])
+    assert reduces(h) == [(1, 1, 0, 2, [4.0]), (2, 1, 0, 2, [4.0])]
+    h.reduce(1, 0, 0, 2, [11.0, 11.0])  # one reduced chunk of round 0, then rank 1 moves on
+    h.start(basic(9, 1))  # the master starts round 1 while round 0 is open
+    h.scatter(1, 0, 1, [10.0, 11.0])  # rank 1's round 1, early
+    h.scatter(1, 1, 1, [12.0])
+    h.reduce(1, 0, 1, 2, [21.0, 21.0])
+    h.reduce(1, 1, 1, 2, [22.0])
+    # round 0 has own 2 + 1 = 3 < 4 reduced chunks; round 1 is not served yet
+    assert h.take_sent() == [] and h.outputs == []
+    # rank 2 (slow): its round-0 copies (outdated: the reduces fired) and one reduced chunk
+    h.scatter(2, 0, 0, [0.0, 1.0])
+    h.scatter(2, 1, 0, [2.0])
+    h.reduce(2, 0, 0, 2, [31.0, 31.0])
+    assert [o[0] for o in h.outputs] == [0, 1]  # in order, round 1 right behind round 0
+    assert h.outputs[0] == (0, [0.0, 2.0, 4.0, 11.0, 11.0, 0.0, 31.0, 31.0, 0.0], [2, 2, 2, 2, 2, 0, 2, 2, 0],
+                            "threshold")
+    assert h.outputs[1] == (1, [11.0, 13.0, 15.0, 21.0, 21.0, 22.0, 0.0, 0.0, 0.0], [2, 2, 2, 2, 2, 2, 0, 0, 0],
+                            "threshold")
+    # round 1 went out only once it was served: its scatters, then its
+    # reduces over own + rank 1's early copy (count 2)
+    sc = per_dest(h.take_sent("scatter"))
+    assert {d: [(m[2], m[3], m[5]) for m in v] for d, v in sc.items()} == \
+        {1: [(0, 1, [4.0, 5.0]), (1, 1, [6.0])], 2: [(0, 1, [7.0, 8.0]), (1, 1, [9.0])]}
+    red = per_dest(h.take_sent("gather"))
+    assert {d: [(m[2], m[3], m[4], m[5]) for m in v] for d, v in red.items()} == \
+        {d: [(0, 1, 2, [11.0, 13.0]), (1, 1, 2, [15.0])] for d in (1, 2)}
+    h.reduce(2, 1, 0, 2, [32.0])  # round 0 complete: outdated
+    assert len(h.outputs) == 2 and h.stats(2)["gather_outdated"] == 1
+    assert h.stats(2)["scatter_outdated"] == 2
+
+
 def test_t8_nasty_chunk_size():
     """SPEC:240-284 (N=2, S=6, C=2, thR 0.9 -> 1, thC 0.8 -> 3): both chunks
     of the worker's block reduce on the first copy (count 1, W:177-181);
@@ -366,29 +508,20 @@ def test_t17_cold_catchup():
 
 
 def test_t2_early_reduce_of_a_future_round():
-    """SPEC:113-138 (N=4, S=8, C=2, thR 1, thC 0.8 -> 3): ReduceBlocks of
+    """SPEC:113-131 (N=4, S=8, C=2, thR 1, thC 0.8 -> 3): ReduceBlocks of
     round 3 arrive while the worker is at round 0.  They land in round 3's
     row; every peer announced round 3, so rounds 0-2 can get no copy from
     them and end at once (forced, unreachable -- the reference leaves them
     open).  Round 3 completes at the third landed chunk without the
-    worker's own chunk, which is then never reduced: the round's later
-    scatters are outdated (SPEC:133-138, no more messages)."""
-    h = SpecHarness(4, 8, 2, 1.0, 0.8, 5)
-    h.start(basic(8, 0))
-    for s, v in ((1, [11.0, 10.0]), (2, [10.0, 20.0]), (3, [9.0, 10.0])):
-        h.reduce(s, 0, 3, 4, v)
-    for i in (1, 2, 3):
-        h.start(basic(8, i))
+    worker's own chunk, which is then never reduced (T3 below: the round's
+    later scatters are outdated, SPEC:133-138)."""
+    h = _t2_early_reduce_of_a_future_round()
     assert [o[0] for o in h.outputs] == [0, 1, 2, 3]
     assert [o[3] for o in h.outputs[:3]] == ["unreachable"] * 3
     r, data, counts, reason = h.outputs[3]
     assert reason == "threshold" and data == [0.0, 0.0, 11.0, 10.0, 10.0, 20.0, 9.0, 10.0]
     assert counts == [0, 0, 4, 4, 4, 4, 4, 4]
     assert h.stats()["reduce_abandoned"] == 1
-    h.take_sent()
-    for s in (1, 2, 3):
-        h.scatter(s, 0, 3, [2.0 * s, 2.0 * s])
-    assert h.take_sent() == [] and len(h.outputs) == 4
 
 
 def test_overwrite_handshake_drops_writes_into_a_row_being_read():
