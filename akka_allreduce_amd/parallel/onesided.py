@@ -31,6 +31,11 @@ needs one (csrc/transport/onesided.h, ``OneSidedParams::cu_keep``).  On a
 GPU of its own ``cu_keep=k`` bounds the round's footprint to k of every 8
 CUs (its grid sized for them): ``async_op=True`` rounds then overlap compute
 on the other CUs (``bounded_footprint``; the DDP hook issues async rounds).
+All ``cu_keep`` lanes of a process with the same ``k`` share ONE masked
+stream (each extra stream is a hardware queue, csrc/transport/onesided.cpp
+``cu_mask_stream``), so their rounds run in issue order: every rank must call
+those lanes in the same order (one training loop does), or a rank's later
+round queues behind one that waits for a peer still in the other lane.
 
 Usage::
 
@@ -268,6 +273,10 @@ class OneSidedAllreduce:
         reuse = out is not None
         lane_out = out is None and self._rows is not None and self.data_sink is None
         if lane_out:
+            # refused BEFORE the launch: a round enqueued into the capture
+            # would replay with no Python output and shift the call ids
+            if torch.cuda.is_current_stream_capturing():
+                raise RuntimeError("a captured call needs an output buffer (out=...)")
             out = None  # the kernel writes the window row of this call's id
         elif out is None:
             out = torch.empty_like(x)

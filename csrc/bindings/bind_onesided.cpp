@@ -36,13 +36,22 @@ struct DLManagedTensor {
 };
 constexpr int32_t kDLROCM = 10;
 
+// The tensor holds a strong reference to the Python object that owns the lane
+// (manager_ctx): a window row handed to torch keeps the lane -- and so the
+// window memory -- alive after the allreduce object is dropped.  torch may free
+// the tensor on a thread without the GIL.
 void dl_delete(DLManagedTensor* t) {
   delete[] t->dl_tensor.shape;
+  if (t->manager_ctx != nullptr && Py_IsInitialized()) {
+    const PyGILState_STATE g = PyGILState_Ensure();
+    Py_DECREF(static_cast<PyObject*>(t->manager_ctx));
+    PyGILState_Release(g);
+  }
   delete t;
 }
 
-// A capsule over device memory the lane owns (no deleter of the memory).
-py::capsule window_capsule(void* data, int32_t device, int64_t n, bool bf16) {
+// A capsule over device memory the lane owns; `owner` is kept alive by it.
+py::capsule window_capsule(void* data, int32_t device, int64_t n, bool bf16, const py::object& owner) {
   auto* t = new DLManagedTensor();
   t->dl_tensor.data = data;
   t->dl_tensor.device = {kDLROCM, device};
@@ -51,7 +60,7 @@ py::capsule window_capsule(void* data, int32_t device, int64_t n, bool bf16) {
   t->dl_tensor.shape = new int64_t[1]{n};
   t->dl_tensor.strides = nullptr;
   t->dl_tensor.byte_offset = 0;
-  t->manager_ctx = nullptr;
+  t->manager_ctx = owner.inc_ref().ptr();
   t->deleter = dl_delete;
   return py::capsule(t, "dltensor", [](PyObject* cap) {
     // consumed capsules are renamed "used_dltensor" (the consumer owns them)
@@ -97,10 +106,11 @@ void bind_onesided(py::module_& m) {
            py::arg("role_wgs") = 0, py::arg("cu_keep") = 0, py::arg("fenced") = false,
            py::arg("window_output") = false)
       .def("gather_row_dlpack",
-           [](const OneSidedLane& l, int32_t row, const std::string& dtype, int32_t device) {
+           [](py::object self, int32_t row, const std::string& dtype, int32_t device) {
+             const auto& l = self.cast<const OneSidedLane&>();
              AKKA_CHECK(l.on_gpu() && l.window_output(), "onesided lane: no window output");
              AKKA_CHECK(row >= 0 && row < l.rows(), "onesided lane: no such row");
-             return window_capsule(l.gather_row(row), device, l.geometry().S, dtype == "bfloat16");
+             return window_capsule(l.gather_row(row), device, l.geometry().S, dtype == "bfloat16", self);
            })
       .def("set_fenced", &OneSidedLane::set_fenced)
       .def_property_readonly("fenced", &OneSidedLane::fenced)
@@ -206,9 +216,9 @@ void bind_onesided(py::module_& m) {
       .def("outbox_bytes", [](const OneSidedLane& l, int64_t i) { return py::bytes(l.outbox_bytes(i)); })
       .def("inject",
            [](OneSidedLane& l, int32_t phase, int32_t dst, int32_t k, int32_t j, uint32_t r, uint32_t cnt,
-              py::bytes data) { l.inject(phase, dst, k, j, r, cnt, std::string(data)); },
+              py::bytes data, int32_t stage) { l.inject(phase, dst, k, j, r, cnt, std::string(data), stage); },
            py::arg("phase"), py::arg("dst"), py::arg("chunk"), py::arg("part"), py::arg("round"),
-           py::arg("count") = 0, py::arg("data") = py::bytes(""))
+           py::arg("count") = 0, py::arg("data") = py::bytes(""), py::arg("stage") = 0)
       .def("drop", &OneSidedLane::drop)
       .def("note_replays", &OneSidedLane::note_replays)
       .def("error", &OneSidedLane::error)

@@ -83,6 +83,27 @@ __device__ inline int64_t part_off(const Args& a, int32_t k, int32_t j) {
   return int64_t(k) * a.C + int64_t(j) * a.part_len;
 }
 
+// One thread: wait until no peer is still storing into gather row `row` of my
+// window (writer_in_flight) -- every part of every peer block, or only part
+// (k, j) of block p when p >= 0.  Bounded by the lane's timeout (a writer that
+// died mid-copy): then the error is flagged and the caller goes on.
+__device__ void wait_row_writers(const Args& a, const uint32_t* fl, int32_t row, int32_t p0, int32_t kj) {
+  const Layout& L = a.L;
+  const uint64_t deadline = wall_clock64() + a.timeout;
+  for (int32_t p = p0 < 0 ? 0 : p0; p < (p0 < 0 ? L.N : p0 + 1); ++p) {
+    if (p == a.me) continue;
+    for (int32_t c = kj < 0 ? 0 : kj; c < (kj < 0 ? a.tab->nch[p] * L.P : kj + 1); ++c) {
+      while (writer_in_flight(DevMem::ld(fl + L.gtag(row, p, c / L.P, c % L.P)), row, L.D)) {
+        if (wall_clock64() > deadline) {
+          set_err(a);
+          return;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
+  }
+}
+
 // ---- begin (workgroup 0): round selection (catch-up), announcements --------------
 __device__ void begin_role(const Args& a) {
   if (threadIdx.x != 0) return;
@@ -102,7 +123,17 @@ __device__ void begin_role(const Args& a) {
   if (DevMem::ld(fl + L.done()) < r) DevMem::st(fl + L.done(), r);
   // from now on this call reads its gather row: announce before any copy
   // workgroup looks at a tag (the overwrite hand-shake)
-  DevMem::st_sc(fl + L.gread(int32_t(r % uint32_t(L.D))), r + 1u);
+  const int32_t row = int32_t(r % uint32_t(L.D));
+  DevMem::st_sc(fl + L.gread(row), r + 1u);
+  const int32_t vrow = int32_t(seq % uint32_t(L.D));
+  if (a.wo && vrow != row) {
+    // window output of a call that caught up: its result is row vrow (the
+    // call id's), not the served round's row.  Announce that row too -- later
+    // writers of its rounds drop -- and let any writer that passed its gate
+    // before the announcement finish before a byte of the result is written
+    DevMem::st_sc(fl + L.gread(vrow), r + 1u);
+    wait_row_writers(a, fl, vrow, -1, -1);
+  }
   sys_store(loc + L.state(kBegun), seq + 1u);
 }
 
@@ -686,6 +717,12 @@ __device__ void copy_role(const Args& a, char* out, bool in_place, uint32_t r, i
     if (k >= a.tab->nch[p]) continue;
     if (threadIdx.x == 0) {
       int32_t z = sys_load(a.loc + L.cmask(p, k)) == 0u ? 1 : 0;
+      if (z && p != me && in_place) {
+        // the output is the row: a writer that passed its gate before the
+        // completion (gather_gate looks at `done` after its marker) finishes
+        // before the zeros go in, or its bytes would land on top of them
+        wait_row_writers(a, fl, row, p, k * L.P + j);
+      }
       if (z && p == me) {
         // my own part: its reduce pieces may still be writing it (a chunk
         // reduced after the decision) -- zero it once they are done
@@ -734,6 +771,8 @@ __device__ void finish_if_last(const Args& a) {
   uint32_t* fl = a.tab->fl[me];
   for (int32_t k = 0; k < a.kme; ++k) DevMem::st(fl + L.sread(row, k), 0u);
   DevMem::st(fl + L.gread(row), 0u);
+  const uint32_t seq0 = sys_load(a.loc + L.state(kCallSeq));
+  if (a.wo && int32_t(seq0 % uint32_t(L.D)) != row) DevMem::st(fl + L.gread(int32_t(seq0 % uint32_t(L.D))), 0u);
   const uint32_t landed = sys_load(a.loc + L.state(kCompLanded));
   int64_t total = 0;
   for (int32_t p = 0; p < N; ++p) total += a.tab->nch[p];

@@ -313,7 +313,24 @@ OS_HD inline int32_t gather_gate(uint32_t* q_fl, const Layout& L, int32_t row, i
     retract<M>(q_fl + L.gtag(row, me, k, j), r);
     return kConflict;
   }
+  // q may have completed round r between the first look and the marker:
+  // look again AFTER the marker (q stores done, then reads the tags it
+  // zeroes under), so either this write drops or q sees "writing r" and
+  // waits for it before zeroing -- with the window output the row IS the
+  // caller's result, and a late write must not land on top of its zeros
+  if (M::ld_sc(q_fl + L.done()) >= r + 1u) {
+    retract<M>(q_fl + L.gtag(row, me, k, j), r);
+    return kOutdated;
+  }
   return kGo;
+}
+
+// A tag of gather row `row` that says a writer may still be storing into the
+// row: "writing y" for a round y that lives in this row.  A retracted marker
+// ("writing x + 1" after x's write dropped, x in this row) names a round of
+// the NEXT row (D >= 2), so it never reads as in flight.
+OS_HD inline bool writer_in_flight(uint32_t t, int32_t row, int32_t D) {
+  return t != 0u && (t & 1u) == 0u && int32_t((t / 2u - 1u) % uint32_t(D)) == row;
 }
 
 // Host-visible per-call status record (host memory, written by the last

@@ -193,8 +193,10 @@ OneSidedLane::OneSidedLane(int32_t device, int64_t S, int32_t N, int64_t C, int3
   const int64_t total = g_.total_chunks();
   need_c_ = int32_t(std::clamp<int64_t>(float_threshold(p.th_complete, total), 1, std::max<int64_t>(total, 1)));
   // window output: gather rows laid out as the output itself (slot = step,
-  // block p at p * step), exact thresholds only (nothing is ever zeroed in
-  // place while a late writer could still be storing into the row)
+  // block p at p * step), exact thresholds only.  Nothing is zeroed in place
+  // while a writer could still be storing into the row: gather_gate looks at
+  // `done` after its marker and copy_role waits for in-flight markers before
+  // zeroing; a call that caught up announces its output row too (begin_role)
   wo_ = p.window_output && device >= 0 && need_r_ == N && need_c_ == total && g_.step > 0 &&
         (g_.step * int64_t(es_)) % 16 == 0;
   if (wo_) slot_ = g_.step;
@@ -422,7 +424,7 @@ void OneSidedLane::map_peer(int32_t q, const std::string& h) {
   }
 }
 
-void OneSidedLane::write_tables() {
+void OneSidedLane::write_tables(void* stream) {
   if (device_ < 0) return;
   Tables t;
   std::memset(&t, 0, sizeof(t));
@@ -436,7 +438,29 @@ void OneSidedLane::write_tables() {
       t.gd[d][q] = pgd_[size_t(d)][size_t(q)];
     }
   }
-  AKKA_OS_HIP(hipMemcpy(tab_dev_, &t, sizeof(t), hipMemcpyHostToDevice));
+  if (stream) {
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    AKKA_OS_HIP(hipMemcpyAsync(tab_dev_, &t, sizeof(t), hipMemcpyHostToDevice, s));
+    AKKA_OS_HIP(hipStreamSynchronize(s));
+  } else {
+    AKKA_OS_HIP(hipMemcpy(tab_dev_, &t, sizeof(t), hipMemcpyHostToDevice));
+  }
+}
+
+void OneSidedLane::wait_own_calls() const {
+  // Only THIS lane's calls: other lanes' round kernels on the device may be
+  // waiting for this rank's next call, so a device-wide synchronize could
+  // stall for their whole timeout.  The last call's status record (host
+  // memory its final workgroup writes) names it once the call is done.
+  if (calls_ == 0) return;
+  const int64_t last = calls_ - 1;
+  const auto t0 = std::chrono::steady_clock::now();
+  const auto limit = std::chrono::milliseconds(3 * p_.timeout_ms + 1000);
+  while (__atomic_load_n(&hw_->status[last % kStatusSlots].call, __ATOMIC_ACQUIRE) < last) {
+    if (std::chrono::steady_clock::now() - t0 > limit)
+      throw AkkaError("onesided lane: call " + std::to_string(last) + " did not finish");
+    std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
 }
 
 void OneSidedLane::open(const std::vector<std::string>& handles) {
@@ -520,25 +544,33 @@ void OneSidedLane::add_peer(int32_t q, const std::string& handle) {
   AKKA_CHECK(absent_[size_t(q)], "onesided lane: rank " + std::to_string(q) +
                                      " is already mapped (a rank's window is mapped once; a departed rank stays dead)");
   AKKA_CHECK(!cr_.active, "onesided lane: add_peer between rounds only");
+  hipStream_t hs = nullptr;
   if (device_ >= 0) {
     AKKA_OS_HIP(hipSetDevice(device_));
     // a round boundary on the device too: no call of this lane still reads
-    // the pointer tables (they are rewritten below)
-    AKKA_OS_HIP(hipDeviceSynchronize());
+    // the pointer tables (they are rewritten below, on the process's
+    // non-blocking side stream: nothing queues behind a waiting round)
+    wait_own_calls();
+    hs = host_side_stream(device_);
   }
   map_peer(q, handle);
-  write_tables();
+  write_tables(hs);
   // Announce my position to the newcomer: I serve no round before my next
   // one any more, so its waits for my copies of those rounds end at once
   // (source_past) and its first call catches up to my window (select_round)
   // -- without this, a newcomer serving an old round would wait for copies
   // this rank already moved past until a force or its timeout.
   uint32_t next = 0;
-  if (device_ >= 0) AKKA_OS_HIP(hipMemcpy(&next, loc_ + L_.state(kNext), sizeof(next), hipMemcpyDeviceToHost));
-  else next = loc_[L_.state(kNext)];
+  if (device_ >= 0) {
+    AKKA_OS_HIP(hipMemcpyAsync(&next, loc_ + L_.state(kNext), sizeof(next), hipMemcpyDeviceToHost, hs));
+    AKKA_OS_HIP(hipStreamSynchronize(hs));
+  } else {
+    next = loc_[L_.state(kNext)];
+  }
   const uint32_t seen = next + 1u;
   if (device_ >= 0) {
-    AKKA_OS_HIP(hipMemcpy(pfl_[size_t(q)] + L_.seen(me_), &seen, sizeof(seen), hipMemcpyHostToDevice));
+    AKKA_OS_HIP(hipMemcpyAsync(pfl_[size_t(q)] + L_.seen(me_), &seen, sizeof(seen), hipMemcpyHostToDevice, hs));
+    AKKA_OS_HIP(hipStreamSynchronize(hs));
   } else {
     HostMem::st(pfl_[size_t(q)] + L_.seen(me_), seen);
   }
@@ -788,7 +820,7 @@ std::string OneSidedLane::outbox_bytes(int64_t i) const {
 }
 
 void OneSidedLane::inject(int32_t phase, int32_t dst, int32_t k, int32_t j, uint32_t r, uint32_t cnt,
-                          const std::string& bytes) {
+                          const std::string& bytes, int32_t stage) {
   AKKA_CHECK(ready_, "onesided lane: open() the peer windows first");
   AKKA_CHECK(phase == 0 || phase == 1, "onesided lane: phase 0 (scatter) or 1 (gather)");
   AKKA_CHECK(dst >= 0 && dst < g_.N && dst != me_, "onesided lane: bad destination");
@@ -797,7 +829,8 @@ void OneSidedLane::inject(int32_t phase, int32_t dst, int32_t k, int32_t j, uint
   const int64_t clen = std::min(g_.C, g_.block_len(blk) - int64_t(k) * g_.C);
   const int64_t n = std::max<int64_t>(0, std::min(part_len_, clen - int64_t(j) * part_len_));
   AKKA_CHECK(int64_t(bytes.size()) == n * int64_t(es_), "onesided lane: injected part has the wrong size");
-  Msg m{phase, dst, k, j, r, cnt, std::vector<char>(bytes.begin(), bytes.end())};
+  AKKA_CHECK(stage == 0 || device_ >= 0, "onesided lane: staged pushes are injected into GPU lanes");
+  Msg m{phase, dst, k, j, r, cnt, std::vector<char>(bytes.begin(), bytes.end()), stage};
   if (device_ >= 0) exec_gpu(m);
   else exec(m, nullptr);
 }
@@ -817,17 +850,19 @@ void OneSidedLane::exec_gpu(const Msg& m) {
     return;
   }
   uint32_t* qfl = pfl_[size_t(q)];
-  if (k == 0 && j == 0) DevFromHost::st(qfl + L_.seen(me), r + 1u);  // implicit start at the receiver
   const int64_t tag = m.phase == 0 ? L_.stag(row, me, k, j) : L_.gtag(row, me, k, j);
-  if (DevFromHost::ld(qfl + tag) >= tag_writing(r + 1u)) {  // the slot's single writer moved past r
-    ++inj_stats_[m.phase == 0 ? kScatterOutdated : kGatherOutdated];
-    return;
+  if (m.stage != 2) {  // (stage 2: the gate passed at stage 1)
+    if (k == 0 && j == 0) DevFromHost::st(qfl + L_.seen(me), r + 1u);  // implicit start at the receiver
+    if (DevFromHost::ld(qfl + tag) >= tag_writing(r + 1u)) {  // the slot's single writer moved past r
+      ++inj_stats_[m.phase == 0 ? kScatterOutdated : kGatherOutdated];
+      return;
+    }
+    const int32_t g = m.phase == 0 ? scatter_gate<DevFromHost>(qfl, L_, row, me, k, j, r)
+                                   : gather_gate<DevFromHost>(qfl, L_, row, me, k, j, r);
+    if (m.phase == 0) ++inj_stats_[g == kGo ? kScatterPushed : g == kOutdated ? kScatterOutdated : kScatterConflict];
+    else ++inj_stats_[g == kGo ? kGatherPushed : g == kOutdated ? kGatherOutdated : kGatherConflict];
+    if (g != kGo || m.stage == 1) return;
   }
-  const int32_t g = m.phase == 0 ? scatter_gate<DevFromHost>(qfl, L_, row, me, k, j, r)
-                                 : gather_gate<DevFromHost>(qfl, L_, row, me, k, j, r);
-  if (m.phase == 0) ++inj_stats_[g == kGo ? kScatterPushed : g == kOutdated ? kScatterOutdated : kScatterConflict];
-  else ++inj_stats_[g == kGo ? kGatherPushed : g == kOutdated ? kGatherOutdated : kGatherConflict];
-  if (g != kGo) return;
   const int64_t off = int64_t(k) * g_.C + int64_t(j) * part_len_;
   if (m.phase == 1) DevFromHost::st(qfl + tag + 1, m.cnt);  // count before the "done" tag
   char* dst = (m.phase == 0 ? psd_ : pgd_)[size_t(row)][size_t(q)] + (int64_t(me) * slot_ + off) * int64_t(es_);

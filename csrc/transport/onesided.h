@@ -140,7 +140,11 @@ class OneSidedLane {
   // GPU lanes: the host performs the push into the receiver's device window
   // (blocking copies on a side stream) -- the receiver's kernel may be
   // running; its decisions are the real os_round_kernel's.
-  void inject(int32_t phase, int32_t dst, int32_t k, int32_t j, uint32_t r, uint32_t cnt, const std::string& bytes);
+  // stage (GPU lanes): 0 the whole push; 1 only its gate (a writer that
+  // passed it and has not stored yet: the "writing r" marker stays); 2 the
+  // bytes and the "done" tag of a push whose gate already passed
+  void inject(int32_t phase, int32_t dst, int32_t k, int32_t j, uint32_t r, uint32_t cnt, const std::string& bytes,
+              int32_t stage = 0);
   // stats() without synchronising the device (GPU: read while a call runs).
   std::vector<uint64_t> stats_nowait();
   // Test access to this rank's own window (GPU: copies on the side stream,
@@ -185,6 +189,7 @@ class OneSidedLane {
     int32_t phase, dst, k, j;
     uint32_t r, cnt;
     std::vector<char> bytes;
+    int32_t stage = 0;  // inject() on a GPU lane: 0 all, 1 gate only, 2 bytes + tag only
   };
   struct CpuRound {
     bool active = false;
@@ -212,7 +217,8 @@ class OneSidedLane {
   void flush();
   void dump(const char* role, int32_t k) const;
   void map_peer(int32_t q, const std::string& handle);
-  void write_tables();  // GPU: the device's pointer tables from pfl_ / psd_ / pgd_
+  void write_tables(void* stream = nullptr);  // GPU: the device's pointer tables from pfl_ / psd_ / pgd_
+  void wait_own_calls() const;  // GPU: this lane's last call finished (its status record names it)
 
   int32_t device_;
   Geometry g_;

@@ -247,6 +247,23 @@ def main():
         sync()
     res["error"] = ar.error()
     res["stats"] = ar.stats()
+    if a.mode == "exact" and ar.window_output and not a.async_op:
+        # a window row outlives the allreduce object: the tensor keeps the
+        # lane (and its window memory) alive -- read it after every rank
+        # dropped its object and the lanes' teardown would have freed it
+        import gc
+        import weakref
+
+        keep, want_last = o.data, want.to(dtype)
+        lane_ref = weakref.ref(ar.lane)
+        del o, ar
+        gc.collect()
+        dist.barrier()
+        res["kept_row_alive"] = lane_ref() is not None
+        res["kept_row_exact"] = bool(torch.equal(keep.cpu(), want_last))
+        del keep
+        gc.collect()
+        res["row_dropped_frees_lane"] = lane_ref() is None
     with open(os.path.join(a.out_dir, f"rank{rank}.json"), "w") as f:
         json.dump(res, f)
     sys.stdout.flush()

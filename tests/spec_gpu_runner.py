@@ -18,11 +18,15 @@ def main():
     out = sys.argv[1]
     res = {}
     todo = [(name, None) for name in sg.CASES] + [("test_random_orders_match_reference_rules", s) for s in sg.SEEDS]
+    todo += [(name, None) for name in sorted(sg.EXTRA)]
     for name, seed in todo:
         key = name if seed is None else f"random_orders_{seed}"
         t0 = time.monotonic()
         try:
-            sg.run_case(name, sg.WindowSpecHarness, seed=seed)
+            if name in sg.EXTRA:
+                sg.EXTRA[name]()
+            else:
+                sg.run_case(name, sg.WindowSpecHarness, seed=seed)
             res[key] = {"ok": True, "error": "", "s": round(time.monotonic() - t0, 2)}
         except Exception:  # noqa: BLE001 - recorded per case
             res[key] = {"ok": False, "error": traceback.format_exc()[-2500:], "s": round(time.monotonic() - t0, 2)}

@@ -53,6 +53,8 @@ def test_onesided_gpu_window_output(n, size, chunk, dtype, wo, handoff):
         assert d["exact"] == [True] * 5 and d["rounds"] == list(range(5)), d
         assert d.get("in_window", [True] * 5 if wo else None) == ([True] * 5 if wo else None), d
         assert d["error"] == 0 and d["stats"]["missing_chunks"] == 0, d["stats"]
+        if wo:  # a kept row holds its lane: still the last sum after the object went, freed with the row
+            assert d["kept_row_alive"] and d["kept_row_exact"] and d["row_dropped_frees_lane"], d
 
 
 def test_onesided_gpu_exact_rounds_async():

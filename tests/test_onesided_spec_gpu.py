@@ -57,7 +57,7 @@ class WindowSpecHarness:
     poll_s = 0.015
     max_settle_s = 2.0
 
-    def __init__(self, N, S, C, th_reduce, th_complete, max_lag, me=0, rows=0, members=None):
+    def __init__(self, N, S, C, th_reduce, th_complete, max_lag, me=0, rows=0, members=None, window_output=False):
         nat = load()
         self.N, self.S, self.C, self.me = N, S, C, me
         self.g = Geometry(S, N, C)
@@ -65,7 +65,8 @@ class WindowSpecHarness:
         dev = self.device
         self.lanes = [nat.OneSidedLane(dev, S, N, C, r, "float32", th_reduce=th_reduce, th_complete=th_complete,
                                        max_lag=max_lag, rows=rows, part_bytes=1 << 40,
-                                       timeout_ms=20_000 if dev >= 0 else 3_600_000)
+                                       timeout_ms=20_000 if dev >= 0 else 3_600_000,
+                                       window_output=window_output and dev >= 0)
                       for r in range(N)]
         hs = [ln.handle() for ln in self.lanes]
         self.handles = hs
@@ -241,6 +242,78 @@ class CpuWindowSpecHarness(WindowSpecHarness):
     device = -1
 
 
+def window_catchup_waits_for_held_writer():
+    """Window output: the result of a call is the gather row of
+    its CALL id.  A call that caught up serves another round, in another row,
+    and must not return a row a peer is still writing.  Replayed on the GPU
+    kernel with a peer whose gather push of round 1 (row 1) passed its gate
+    before call 1 began and stores its bytes only after the call's own round
+    (2, row 0) has fully landed: call 1 waits for that writer before it
+    writes its result into row 1, so the late bytes can never land on top of
+    it.  N=2, S=8, C=2 (two chunks of 2 per block), thresholds 1, maxLag 1."""
+    from torch.utils.dlpack import from_dlpack
+
+    N, S, C = 2, 8, 2
+    h = WindowSpecHarness(N, S, C, 1.0, 1.0, 1, rows=2, window_output=True)
+    try:
+        w, peer = h.w, h.lanes[1]
+        assert w.info()["window_output"], w.info()
+        rows = [from_dlpack(w.gather_row_dlpack(d, "float32", h.device)) for d in range(h.D)]
+        f32 = lambda v: np.asarray(v, dtype=np.float32).tobytes()  # noqa: E731
+
+        def call(xv):
+            with torch.cuda.stream(h.stream):
+                x = torch.tensor(xv, dtype=torch.float32, device=h.cuda)
+                counts = torch.full((N, h.kmax), -1, dtype=torch.int32, device=h.cuda)
+                c = w.round(h.stream.cuda_stream, x.data_ptr(), 0, counts.data_ptr(), h.kmax)
+                ev = torch.cuda.Event()
+                ev.record(h.stream)
+            return x, counts, c, ev
+
+        def wait(ev, s=10.0):
+            t_end = time.monotonic() + s
+            while not ev.query():
+                assert time.monotonic() < t_end, "the call did not finish"
+                time.sleep(0.005)
+
+        def result(c, counts):
+            with torch.cuda.stream(h.copy_stream):
+                return rows[c % h.D].cpu().tolist(), counts.cpu().tolist(), w.status(c)
+
+        # round 0, call 0 -> row 0
+        x0 = [1.0] * S
+        t0 = call(x0)
+        for k in range(2):
+            peer.inject(0, 0, k, 0, 0, 0, f32([10.0, 10.0]))        # peer's copy of my block
+            peer.inject(1, 0, k, 0, 0, 2, f32([7.0, 7.0]))          # block 1 reduced
+        wait(t0[3])
+        d0, n0, st0 = result(t0[2], t0[1])
+        assert st0["round"] == 0 and d0 == [11.0] * 4 + [7.0] * 4, (st0, d0)
+        # a peer's gather push of round 1 into row 1 passes its gate, then stalls
+        peer.inject(1, 0, 0, 0, 1, 2, f32([999.0, 999.0]), stage=1)
+        # the peer moves on to round 3: call 1 catches up to round 2 (lo = 3 - maxLag)
+        peer.inject(0, 0, 0, 0, 3, 0, f32([0.0, 0.0]))
+        x1 = [2.0] * S
+        t1 = call(x1)   # call id 1 -> its result is row 1; the round it serves lives in row 0
+        for k in range(2):
+            peer.inject(0, 0, k, 0, 2, 0, f32([20.0, 20.0]))
+            peer.inject(1, 0, k, 0, 2, 2, f32([5.0, 5.0]))
+        time.sleep(0.2)
+        assert not t1[3].query(), "call 1 must wait for the writer still storing into its result row"
+        peer.inject(1, 0, 0, 0, 1, 2, f32([999.0, 999.0]), stage=2)   # the stalled bytes land now
+        wait(t1[3])
+        d1, n1, st1 = result(t1[2], t1[1])
+        assert st1["round"] == 2, st1
+        assert d1 == [22.0] * 4 + [5.0] * 4, d1          # not a 999 in it
+        assert all(v == 2 for r_ in n1 for v in r_), n1
+        assert w.error() == 0
+    finally:
+        h.close()
+        _OPEN.remove(h) if h in _OPEN else None
+
+
+EXTRA = {"window_catchup_waits_for_held_writer": window_catchup_waits_for_held_writer}
+
 CASES = sorted(name for name, f in inspect.getmembers(spec, inspect.isfunction)
                if name.startswith("test_") and "seed" not in inspect.signature(f).parameters)
 SEEDS = range(4)
@@ -301,4 +374,11 @@ def test_spec_case_on_gpu_kernel(name, gpu_results):
 @pytest.mark.parametrize("seed", SEEDS)
 def test_spec_random_orders_on_gpu_kernel(seed, gpu_results):
     res = gpu_results[f"random_orders_{seed}"]
+    assert res["ok"], res["error"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", sorted(EXTRA))
+def test_window_case_on_gpu_kernel(name, gpu_results):
+    res = gpu_results[name]
     assert res["ok"], res["error"]
