@@ -210,6 +210,7 @@ void DataPlane::bind_input(int32_t round, const void* input, StreamH ready_strea
   Binding& b = bind_[round];
   b.input = input;
   b.input_pending = false;
+  b.input_idle = false;
   b.ready = ready_stream;
   b.has_ready = has_stream && (!dev_->is_host() || dev_->models_streams());
   b.input_waited_compute = b.input_waited_comm = false;
@@ -241,6 +242,10 @@ void DataPlane::bind_input(int32_t round, const void* input, StreamH ready_strea
     }
     if (!b.input_ready) b.input_ready = binding_event();
     if (defer_record) b.input_pending = true;  // recorded by the first wait_input, if any
+    // an async call on an idle stream: everything that wrote the input (or
+    // last used the output / counts memory) has completed -- no marker on the
+    // caller's stream, no barrier on the engine's (back-to-back async rounds)
+    else if (dev_->stream_idle(ready_stream)) b.input_idle = true;
     else dev_->record(b.input_ready, ready_stream);
   }
 }
@@ -353,7 +358,7 @@ void DataPlane::wait_input(int32_t round, StreamH s) {
       od = true;
     }
   }
-  if (!b.input_ready) return;
+  if (!b.input_ready || b.input_idle) return;
   if (b.input_pending) {
     dev_->record(b.input_ready, b.ready);
     b.input_pending = false;

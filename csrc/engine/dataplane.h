@@ -168,6 +168,7 @@ class DataPlane {
     bool input_waited_compute = false;
     bool input_waited_comm = false;
     bool input_pending = false;    // input_ready not recorded yet (bind_input defer_record)
+    bool input_idle = false;       // the producer stream was idle at bind time: nothing to wait for
     EventH output_ready = nullptr;  // recorded on the stream that allocated output/counts
     bool output_waited_compute = false;
     bool output_waited_comm = false;

@@ -78,6 +78,9 @@ class Device {
   virtual bool query(EventH e) = 0;
   virtual void sync_event(EventH e) = 0;
   virtual void sync_stream(StreamH s) = 0;
+  // Every op enqueued on `s` so far has completed (a hand-over point of `s`
+  // needs no event).  Conservative: false when unknown.
+  virtual bool stream_idle(StreamH) { return false; }
 
   virtual void reduce(StreamH s, const ReduceSpec* specs, int32_t nspecs, DType dt) = 0;
   virtual void copy(StreamH s, void* dst, const void* src, size_t bytes, CopyKind kind) = 0;

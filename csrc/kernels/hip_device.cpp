@@ -117,6 +117,14 @@ class HipDevice final : public Device {
     flush_if(s);
     AKKA_HIP(hipStreamSynchronize(static_cast<hipStream_t>(s)));
   }
+  bool stream_idle(StreamH s) override {
+    if (capturing_) return false;  // (a captured stream's ops have not run: the graph needs the edge)
+    flush_if(s);
+    hipStreamCaptureStatus cst = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(static_cast<hipStream_t>(s), &cst) != hipSuccess || cst != hipStreamCaptureStatusNone)
+      return false;
+    return hipStreamQuery(static_cast<hipStream_t>(s)) == hipSuccess;
+  }
 
   bool begin_capture(StreamH s) override {
     flush_all();

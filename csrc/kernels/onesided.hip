@@ -697,6 +697,11 @@ __device__ void copy_role(const Args& a, char* out, bool in_place, uint32_t r, i
     __syncthreads();  // `act` is rewritten by the next item
   }
   // the output set (the complete role is a lower workgroup id)
+  // (a flag of its own: lane 0 rewrites `act` for the first zeroing item
+  // below while slower waves may still be reading this verdict -- with `act`
+  // reused, a wave could take that item's 0 for "no output set", return, and
+  // leave its share of every later item unzeroed)
+  __shared__ int32_t set_ok;
   if (threadIdx.x == 0) {
     const uint64_t deadline = wall_clock64() + 3 * a.timeout + 1;
     int32_t v = 1;
@@ -708,10 +713,10 @@ __device__ void copy_role(const Args& a, char* out, bool in_place, uint32_t r, i
       }
       __builtin_amdgcn_s_sleep(4);
     }
-    act = v;
+    set_ok = v;
   }
   __syncthreads();
-  if (!act) return;
+  if (!set_ok) return;
   for (int32_t w = w0; w < items; w += stride) {
     const auto [p, k, j] = item(w);
     if (k >= a.tab->nch[p]) continue;
