@@ -75,6 +75,11 @@ def main():
             rec["mean_count"] = float(sum(int(cpc[p, k]) for p in range(g.workerNum)
                                           for k in range(g.num_chunks(p)))) / max(1, n)
             rec["block_counts"] = [int(cpc[p, 0]) if g.num_chunks(p) else 0 for p in range(g.workerNum)]
+            # per worker id: chunks whose contributor set includes it
+            rec["with"] = [sum((int(float(data[g.chunk_range(p, k)[0]])) >> q) & 1 for p in range(g.workerNum)
+                               for k in range(g.num_chunks(p)) if g.chunk_range(p, k)[1] > g.chunk_range(p, k)[0])
+                           for q in range(g.workerNum)]
+            rec["chunks"] = n
         else:
             rec["mean_count"] = 0.0
             rec["block_counts"] = None  # a round force-completed by catch-up: zeros, count 0 (W:100-106)

@@ -64,6 +64,20 @@ def check_sets(o, world, me, dtype, detail=None):
     return bad, own_has_me
 
 
+def bit_share(o, bit):
+    """(chunks whose contributor set includes rank ``bit``, chunks): a rank
+    whose rounds waited for ``bit``'s copies would have it in every chunk."""
+    g = o.geometry
+    data, n, hit = o.data.float().cpu(), 0, 0
+    for p in range(g.workerNum):
+        for k in range(g.num_chunks(p)):
+            s, e = g.chunk_range(p, k)
+            if e > s:
+                n += 1
+                hit += (int(float(data[s])) >> bit) & 1
+    return hit, n
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--mode", default="exact", choices=["exact", "straggler", "chaos", "dead"])
@@ -218,6 +232,7 @@ def main():
         # master ends the job at maxRound the same way, M:58-63).
         for pi, phase in enumerate(("no_straggler", "straggler")):
             times, rounds, bad, own_ok, reasons, detail = [], [], 0, True, [], []
+            with_s, nchunks = 0, 0
             target, last, c = (pi + 1) * a.rounds - 1, -1 if pi == 0 else res["no_straggler"]["rounds"][-1], 0
             while last < target:
                 c += 1
@@ -238,11 +253,15 @@ def main():
                 b, mine = check_sets(o, world, rank, dtype, detail)
                 bad += b
                 own_ok &= mine
+                if a.straggler >= 0:
+                    h, n = bit_share(o, a.straggler)
+                    with_s, nchunks = with_s + h, nchunks + n
                 last = o.iteration
                 rounds.append(last)
                 reasons.append(o.status["reason"])
             res[phase] = {"ms": times, "rounds": rounds, "bad_chunks": bad, "own_block_has_me": own_ok,
-                          "reasons": reasons, "stats": ar.stats(), "bad_detail": detail}
+                          "reasons": reasons, "stats": ar.stats(), "bad_detail": detail,
+                          "chunks_with_straggler": with_s, "chunks": nchunks}
         ar.retire()
         sync()
     res["error"] = ar.error()

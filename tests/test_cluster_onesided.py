@@ -2,9 +2,9 @@
 pacing (AllreduceMaster.scala:54-63 + AllreduceWorker.scala:7-8, 197-210):
 a master process and 4 worker processes (``--transport onesided``),
 thAllreduce = thReduce = thComplete = 0.75, maxLag 1, one worker's data
-source sleeping 50 ms per round.  The fast workers keep their pace: their
-median round stays within 2x of the same job without the straggler, the
-straggler catches up by skipping rounds (force-completed, W:100-106), and
+source sleeping 50 ms per round.  The fast workers keep their pace: the
+straggler's contribution is in few of their output chunks (their rounds
+did not wait for it), the straggler catches up by skipping rounds (force-completed, W:100-106), and
 every sink sees chunks whose value encodes a contributor set of the size of
 its count.  CPU processes here (shared-memory windows, the GPU kernels'
 protocol functions); tests/test_cluster_onesided_gpu.py runs the same job
@@ -109,7 +109,7 @@ def fast_median_ms(rows):
     return max(meds)
 
 
-def check_job(device, rounds=64, slack_ms=1.0, **kw):
+def check_job(device, rounds=64, **kw):
     import os as _os
 
     kw.setdefault("log_dir", _os.environ.get("AKKA_TEST_LOGS") or None)
@@ -134,8 +134,18 @@ def check_job(device, rounds=64, slack_ms=1.0, **kw):
         full += len(rs) == rounds
     assert full >= 3, [len(r["records"]) for r in base]
     b, s = fast_median_ms(base), fast_median_ms(strag)
-    assert s <= 2 * b + slack_ms, (b, s)
     st = [r for r in strag if r["straggler"]][0]
+    # the fast workers never waited for the straggler, from their sinks'
+    # records rather than a wall-clock ratio: its 2^id bit is in few of their
+    # output chunks (a worker whose rounds waited would have it in all of
+    # them); one loose sanity bound stays on the clock
+    for r in strag:
+        if r["straggler"]:
+            continue
+        recs = [x for x in r["records"] if x.get("with") is not None]
+        share = sum(x["with"][st["id"]] for x in recs) / max(1, sum(x["chunks"] for x in recs))
+        assert share <= 0.25, (r["id"], share)
+    assert s < 50.0 / 4, (b, s)
     assert st["forced_rounds"] > 0 and len(st["records"]) < rounds + st["forced_rounds"] + 1
     fast = [r for r in strag if not r["straggler"]]
     for r in fast:

@@ -2,8 +2,8 @@
 processes on the box's one MI355X (``--transport onesided``: windows in HBM
 mapped through IPC handles, rounds on the gfx950 kernels), thAllreduce =
 thReduce = thComplete = 0.75, maxLag 1, one worker's data source sleeping
-50 ms per round, 64 rounds: the fast workers' median round stays within 2x
-of the straggler-free job, sinks see consistent contributor sets, the
+50 ms per round, 64 rounds: the fast workers' rounds do not wait for it
+(its contribution is in few of their chunks), sinks see consistent contributor sets, the
 straggler catches up by skipping rounds."""
 import pytest
 
@@ -13,7 +13,7 @@ pytestmark = pytest.mark.gpu
 
 
 def test_cluster_onesided_master_pacing_gpu():
-    b, s = check_job("cuda", slack_ms=0.2, size=1 << 20, chunk=1 << 16)
+    b, s = check_job("cuda", size=1 << 20, chunk=1 << 16)
     print(f"fast workers' median ms per round: {b:.3f} without, {s:.3f} with the straggler")
 
 

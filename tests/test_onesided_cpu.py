@@ -70,11 +70,26 @@ def _median_tail(ms):
     return statistics.median(ms[len(ms) // 2:])
 
 
+def assert_fast_rank_did_not_wait(d, delay_ms):
+    """A fast rank's straggler phase, from the lane's own records rather than
+    a wall-clock ratio: its calls complete on the threshold (not forced), and
+    the straggler's copy is in few of its output chunks -- a rank whose rounds
+    waited for the straggler would have it in every chunk (each rank
+    contributes 2^rank, so a chunk's value names its contributor set).  One
+    loose wall-clock sanity bound stays: a fast round far below the delay."""
+    p = d["straggler"]
+    thr = sum(x == "threshold" for x in p["reasons"]) / max(1, len(p["reasons"]))
+    share = p["chunks_with_straggler"] / max(1, p["chunks"])
+    assert thr >= 0.9, (d["rank"], thr, p["reasons"][:20])
+    assert share <= 0.25, (d["rank"], share, p["chunks_with_straggler"], p["chunks"])
+    assert _median_tail(p["ms"]) < delay_ms / 4, (d["rank"], _median_tail(p["ms"]))
+
+
 def test_onesided_straggler_steady_state():
     """N=4, thresholds 0.75 / 0.75, maxLag 1, rank 3 sleeps 50 ms before each
     call, 64 rounds after 64 without the straggler.  The fast ranks never
-    wait for it (their median round time stays within 2x of the straggler-free
-    phase), every chunk's value encodes a contributor set whose size is its
+    wait for it (assert_fast_rank_did_not_wait: threshold completions, the
+    straggler's copy in few of their chunks), every chunk's value encodes a contributor set whose size is its
     count, the straggler's late pushes are dropped by the senders (outdated)
     and its calls catch up (skipped rounds)."""
     # (compute 0.5 ms per call: the fast ranks need each other at 0.75, and
@@ -91,14 +106,8 @@ def test_onesided_straggler_steady_state():
             assert p["bad_chunks"] == 0, (d["rank"], ph)
             assert p["own_block_has_me"], (d["rank"], ph)
             assert all(b > a for a, b in zip(p["rounds"], p["rounds"][1:])), p["rounds"]
-    fast = rows[:3]
-    for d in fast:
-        base, strag = _median_tail(d["no_straggler"]["ms"]), _median_tail(d["straggler"]["ms"])
-        # CPU processes share 8 cores: allow the scheduler 1 ms on top of
-        # 2x -- a fast rank that waited for the straggler would show its 50 ms
-        # delay, 50x this bound's slack
-        assert strag <= 2 * base + 1.0, (d["rank"], base, strag)
-        assert strag < 50.0 / 4, (d["rank"], base, strag)
+    for d in rows[:3]:
+        assert_fast_rank_did_not_wait(d, delay_ms=50.0)
         assert d["straggler"]["rounds"][-1] >= 127
     s = rows[3]
     assert s["stats"]["skipped_rounds"] > 0, s["stats"]

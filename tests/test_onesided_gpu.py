@@ -5,7 +5,7 @@ hand-offs; the same code crosses xGMI on a node).  Same scenarios as
 tests/test_onesided_cpu.py, whose protocol functions these kernels share."""
 import pytest
 
-from test_onesided_cpu import _median_tail, run_ranks
+from test_onesided_cpu import assert_fast_rank_did_not_wait, run_ranks
 
 pytestmark = pytest.mark.gpu
 
@@ -81,7 +81,8 @@ def test_onesided_gpu_timeline_stamps():
 @pytest.mark.parametrize("handoff", ["lite", "fenced"])
 def test_onesided_gpu_straggler_steady_state(handoff):
     """N=4 on the card, 0.75 / 0.75, maxLag 1, rank 3 sleeps 50 ms per call,
-    64 rounds: fast ranks' median round within 2x of the straggler-free phase,
+    64 rounds: fast ranks' calls complete on the threshold with the
+    straggler's copy in few of their chunks (assert_fast_rank_did_not_wait),
     contributor sets consistent with counts, straggler's pushes dropped --
     in both hand-off modes."""
     r, rows = run_ranks(4, "--mode", "straggler", "--straggler", "3", "--rounds", "64", "--compute-ms", "2",
@@ -93,8 +94,7 @@ def test_onesided_gpu_straggler_steady_state(handoff):
         for ph in ("no_straggler", "straggler"):
             assert d[ph]["bad_chunks"] == 0 and d[ph]["own_block_has_me"], (d["rank"], ph, d[ph]["bad_detail"], d[ph]["stats"])
     for d in rows[:3]:
-        base, strag = _median_tail(d["no_straggler"]["ms"]), _median_tail(d["straggler"]["ms"])
-        assert strag <= 2 * base + 0.2, (d["rank"], base, strag)
+        assert_fast_rank_did_not_wait(d, delay_ms=50.0)
     s = rows[3]["stats"]
     assert s["skipped_rounds"] > 0 and s["scatter_outdated"] + s["gather_outdated"] > 0, s
 
