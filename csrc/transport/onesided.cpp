@@ -18,6 +18,7 @@
 #include <mutex>
 #include <random>
 #include <thread>
+#include <tuple>
 
 #include "../kernels/onesided_kernels.h"
 #include "ipc_lane.h"
@@ -93,11 +94,13 @@ hipStream_t host_side_stream(int32_t device) {
 // would oversubscribe the GPU's queues (then the scheduler time-slices
 // them: 10-20 ms stalls, profiles/r05/bounded/).  Returns the stream and
 // the CUs kept.
-std::pair<hipStream_t, int32_t> cu_mask_stream(int32_t device, int32_t keep) {
+// `offset` rotates the kept CUs of every group of 8 (measurement knob
+// AKKA_OS_CU_DISJOINT: ranks sharing one card each on CUs of their own).
+std::pair<hipStream_t, int32_t> cu_mask_stream(int32_t device, int32_t keep, int32_t offset = 0) {
   static std::mutex mu;
-  static std::map<std::pair<int32_t, int32_t>, std::pair<hipStream_t, int32_t>> streams;
+  static std::map<std::tuple<int32_t, int32_t, int32_t>, std::pair<hipStream_t, int32_t>> streams;
   std::lock_guard<std::mutex> lk(mu);
-  auto it = streams.find({device, keep});
+  auto it = streams.find({device, keep, offset});
   if (it != streams.end()) return it->second;
   hipDeviceProp_t prop;
   AKKA_OS_HIP(hipGetDeviceProperties(&prop, device));
@@ -105,13 +108,13 @@ std::pair<hipStream_t, int32_t> cu_mask_stream(int32_t device, int32_t keep) {
   std::vector<uint32_t> mask(size_t((ncu + 31) / 32), 0u);
   int32_t on = 0;
   for (int32_t cu = 0; cu < ncu; ++cu)
-    if (cu % 8 < keep) {
+    if ((cu % 8 - offset + 8) % 8 < keep) {
       mask[size_t(cu / 32)] |= 1u << (cu % 32);
       ++on;
     }
   hipStream_t s = nullptr;
   AKKA_OS_HIP(hipExtStreamCreateWithCUMask(&s, uint32_t(mask.size()), mask.data()));
-  return streams[{device, keep}] = {s, on};
+  return streams[{device, keep, offset}] = {s, on};
 }
 
 // Memory policy of the protocol functions on the host (shared memory between
@@ -626,7 +629,10 @@ int32_t OneSidedLane::make_cu_stream(int32_t keep) {
   hipDeviceProp_t prop;
   AKKA_OS_HIP(hipGetDeviceProperties(&prop, device_));
   const int32_t ncu = std::max(1, prop.multiProcessorCount);
-  const auto [s, on] = cu_mask_stream(device_, keep);
+  int32_t offset = 0;
+  if (const char* dv = std::getenv("AKKA_OS_CU_DISJOINT"); dv && std::strcmp(dv, "1") == 0)
+    offset = (me_ * keep) % 8;  // rank me on CUs [me * keep, me * keep + keep) of every 8
+  const auto [s, on] = cu_mask_stream(device_, keep, offset);
   cu_stream_ = s;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   AKKA_OS_HIP(hipEventCreateWithFlags(&e0, hipEventDisableTiming));
