@@ -42,7 +42,7 @@ constexpr int32_t kDLROCM = 10;
 // the tensor on a thread without the GIL.
 void dl_delete(DLManagedTensor* t) {
   delete[] t->dl_tensor.shape;
-  if (t->manager_ctx != nullptr && Py_IsInitialized()) {
+  if (t->manager_ctx != nullptr && Py_IsInitialized() && !_Py_IsFinalizing()) {  // (at exit: leak, never block)
     const PyGILState_STATE g = PyGILState_Ensure();
     Py_DECREF(static_cast<PyObject*>(t->manager_ctx));
     PyGILState_Release(g);
