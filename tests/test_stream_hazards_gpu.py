@@ -66,3 +66,35 @@ def test_counts_written_after_callers_pending_work(path):
     side.synchronize()
     torch.cuda.synchronize()
     assert int(pc.min()) == n and int(pc.max()) == n, pc
+
+
+@pytest.mark.parametrize("busy", [True, False])
+def test_async_round_input_hand_over(busy):
+    """An async round on the engine's streams reads the caller's input only
+    after the caller's stream produced it.  Busy caller stream (a spin, then
+    the kernel that writes the input): the hand-over event must be kept.
+    Idle caller stream (everything synchronised): the engine skips that
+    event (DataPlane::bind_input, Device::stream_idle) and the round is still
+    the exact sum."""
+    n, S, C = 4, 1 << 16, 1 << 12
+    w = _shape_worker(n, S, C)
+    x = torch.randn(S, device="cuda")
+    for _ in range(2):
+        w.allreduce(x, async_op=True).wait()
+    torch.cuda.synchronize()
+    side = torch.cuda.Stream()
+    with torch.cuda.stream(side):
+        y = torch.empty_like(x)
+        if busy:
+            torch.cuda._sleep(200_000_000)  # ~0.1 s of GPU time before the input exists
+            torch.mul(x, 3.0, out=y)
+        else:
+            torch.mul(x, 3.0, out=y)
+            side.synchronize()
+        o = w.allreduce(y, async_op=True)
+        o.wait()
+        got = o.data.clone()
+    side.synchronize()
+    torch.cuda.synchronize()
+    want = (x * 3.0) * n  # every rank of the shape contributes the same input
+    assert torch.allclose(got, want, rtol=1e-6, atol=1e-5), (got - want).abs().max()
