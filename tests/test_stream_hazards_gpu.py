@@ -78,23 +78,22 @@ def test_async_round_input_hand_over(busy):
     the exact sum."""
     n, S, C = 4, 1 << 16, 1 << 12
     w = _shape_worker(n, S, C)
-    x = torch.randn(S, device="cuda")
+    x = torch.ones(S, device="cuda")  # (constant: the shape transport sends every op to itself)
     for _ in range(2):
         w.allreduce(x, async_op=True).wait()
     torch.cuda.synchronize()
     side = torch.cuda.Stream()
     with torch.cuda.stream(side):
-        y = torch.empty_like(x)
+        y = torch.full((S,), -1.0, device="cuda")
         if busy:
-            torch.cuda._sleep(200_000_000)  # ~0.1 s of GPU time before the input exists
-            torch.mul(x, 3.0, out=y)
+            torch.cuda._sleep(200_000_000)  # ~0.1 s of GPU time before the input's final value
+            y.fill_(3.0)
         else:
-            torch.mul(x, 3.0, out=y)
+            y.fill_(3.0)
             side.synchronize()
         o = w.allreduce(y, async_op=True)
         o.wait()
         got = o.data.clone()
     side.synchronize()
     torch.cuda.synchronize()
-    want = (x * 3.0) * n  # every rank of the shape contributes the same input
-    assert torch.allclose(got, want, rtol=1e-6, atol=1e-5), (got - want).abs().max()
+    assert torch.equal(got, torch.full_like(got, 3.0 * n)), (got.min(), got.max())
