@@ -2,10 +2,14 @@
 
 What the reference gets from Akka, rebuilt small:
   * ``Node``: one process-level endpoint (host:port) hosting one actor (the
-    master or a worker, like the reference's one actor per JVM).  A TCP server
-    thread per inbound connection decodes frames into the actor's mailbox; one
-    dispatcher thread delivers them in order, so the actor's ``receive`` is
-    single-threaded exactly like an Akka actor's.
+    master or a worker, like the reference's one actor per JVM).  ONE
+    dispatcher thread reads every inbound connection through a selector,
+    splits the bytes into frames and runs the actor's ``receive`` on each in
+    arrival order -- single-threaded exactly like an Akka actor's, with no
+    hand-off between a reader thread and the dispatcher per message (a round
+    of the reference's demo is ~7 tiny messages per worker, so the hand-offs
+    were most of its time).  Local messages (self-sends, the failure
+    detector's notices) go through a mailbox that wakes the selector.
   * ``RemoteRef``: ``tell`` encodes and writes to a persistent connection per
     destination -- per sender->receiver FIFO, the ordering the reference's
     tests rely on (SPEC:590, SPEC:721).
@@ -14,8 +18,10 @@ What the reference gets from Akka, rebuilt small:
 """
 from __future__ import annotations
 
+import collections
 import logging
-import queue
+import os
+import selectors
 import socket
 import threading
 import time
@@ -41,6 +47,10 @@ class RemoteRef:
     def tell(self, msg: Any, sender: Any = None) -> None:
         self._node.send(self.address, msg)
 
+    def tell_many(self, msgs: List[Any]) -> None:
+        """Several messages in order, written as one batch (one system call)."""
+        self._node.send_many(self.address, msgs)
+
     def __repr__(self) -> str:
         return f"RemoteRef({self.address})"
 
@@ -64,7 +74,14 @@ class Node:
         self.address = f"{host}:{self.port}"
         self.actor: Any = None
         self.aliases: List[Any] = []  # inner objects that stand for this node (e.g. the master logic)
-        self.mailbox: "queue.Queue[Any]" = queue.Queue()
+        self._wake_r, self._wake_w = os.pipe()
+        os.set_blocking(self._wake_r, False)
+        os.set_blocking(self._wake_w, False)
+        self._wake_lock = threading.Lock()  # no write into the pipe's fd numbers once they are closed
+        self._wake_open = True
+        self.mailbox = _Mailbox(self._wake)
+        self._accepted: List[socket.socket] = []  # inbound connections the dispatcher has not registered yet
+        self._accepted_lock = threading.Lock()
         self._conns: Dict[str, socket.socket] = {}
         self._conn_lock = threading.Lock()
         self._send_locks: Dict[str, threading.Lock] = {}
@@ -108,6 +125,15 @@ class Node:
             self._threads.append(t)
         return self
 
+    def _wake(self) -> None:
+        with self._wake_lock:
+            if not self._wake_open:
+                return  # a stopped node
+            try:
+                os.write(self._wake_w, b"x")
+            except BlockingIOError:
+                pass  # a full pipe is already a pending wake-up
+
     def stop(self) -> None:
         self._stop.set()
         self.mailbox.put(None)
@@ -144,12 +170,20 @@ class Node:
 
     # ---- sending ---------------------------------------------------------------------
     def send(self, address: str, msg: Any) -> None:
+        self.send_many(address, [msg])
+
+    def send_many(self, address: str, msgs: List[Any]) -> None:
+        """``msgs`` to ``address`` in order: their frames go out in ONE write
+        (the receiver's FrameReader splits them), so the per-pair FIFO order
+        of the reference holds and a burst costs one system call."""
         if address == self.address:
-            self.mailbox.put(msg)
+            for m in msgs:
+                self.mailbox.put(m)
             return
-        if self._stop.is_set():
+        if self._stop.is_set() or not msgs:
             return  # a stopped node sends nothing (and opens no new connection)
-        frame = wire.encode(msg, self.addr_of)
+        frame = wire.encode(msgs[0], self.addr_of) if len(msgs) == 1 else \
+            b"".join(wire.encode(m, self.addr_of) for m in msgs)
         with self._conn_lock:
             lock = self._send_locks.setdefault(address, threading.Lock())
         with lock:
@@ -181,54 +215,116 @@ class Node:
             except OSError:
                 return
             conn.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
-            t = threading.Thread(target=self._read_loop, args=(conn,), name=f"{self.name}-reader", daemon=True)
-            t.start()
+            with self._accepted_lock:
+                self._accepted.append(conn)
+            self._wake()
 
-    def _read_loop(self, conn: socket.socket) -> None:
+    def _deliver(self, msg: Any) -> None:
+        if self.on_message:
+            self.on_message(msg)
         try:
-            while not self._stop.is_set():
-                body = wire.read_frame(conn)
-                if body is None:
-                    return
-                self.mailbox.put(wire.decode(body, self.ref))
-        except (OSError, ValueError) as e:
-            if not self._stop.is_set():
-                log.debug("%s: reader closed: %s", self.name, e)
-        finally:
-            conn.close()
+            if hasattr(self.actor, "receive"):
+                self.actor.receive(msg)
+            else:
+                self.actor.tell(msg)
+        except Exception as e:  # an actor never dies from one message (W:287-299)
+            log.exception("%s: error in receive(%s): %s", self.name, type(msg).__name__, e)
 
-    def _next_message(self) -> Any:
+    def _poll_timeout(self) -> Optional[float]:
+        """Run the progress hook: None -> block until a message, 0 -> progress
+        was made (look again at once), else the idle-but-pending back-off."""
         poller = self.poller
-        while poller is not None and not self._stop.is_set():
-            try:
-                return self.mailbox.get_nowait()
-            except queue.Empty:
-                pass
-            try:
-                st = poller()
-            except Exception as e:  # keep the node alive (W:287-299)
-                log.exception("%s: error in poller: %s", self.name, e)
-                st = None
-            if st is None:
-                break  # nothing in flight: block on the mailbox
-            if not st:
-                time.sleep(20e-6)
-        return self.mailbox.get()
+        if poller is None:
+            return None
+        try:
+            st = poller()
+        except Exception as e:  # keep the node alive (W:287-299)
+            log.exception("%s: error in poller: %s", self.name, e)
+            st = None
+        if st is None:
+            return None  # nothing in flight: block
+        return 0.0 if st else 20e-6
 
     def _dispatch_loop(self) -> None:
-        while not self._stop.is_set():
-            msg = self._next_message()
-            if msg is None:
-                return
-            if self.on_message:
-                self.on_message(msg)
+        sel = selectors.DefaultSelector()
+        sel.register(self._wake_r, selectors.EVENT_READ, None)
+        inbound: List[socket.socket] = []
+
+        def close(conn: socket.socket) -> None:
             try:
-                if hasattr(self.actor, "receive"):
-                    self.actor.receive(msg)
-                else:
-                    self.actor.tell(msg)
-            except Exception as e:  # an actor never dies from one message (W:287-299)
-                log.exception("%s: error in receive(%s): %s", self.name, type(msg).__name__, e)
+                sel.unregister(conn)
+            except (KeyError, ValueError):
+                pass
+            conn.close()
+            if conn in inbound:
+                inbound.remove(conn)
+
+        try:
+            while not self._stop.is_set():
+                while True:  # local messages, in order
+                    try:
+                        msg = self.mailbox.get_nowait()
+                    except IndexError:
+                        break
+                    if msg is None:
+                        return
+                    self._deliver(msg)
+                timeout = self._poll_timeout()
+                if len(self.mailbox):
+                    continue  # the poller or a handler posted locally: deliver first
+                for key, _ in sel.select(timeout):
+                    if key.data is None:  # wake-up: drain, register accepted connections
+                        try:
+                            while os.read(self._wake_r, 4096):
+                                pass
+                        except BlockingIOError:
+                            pass
+                        with self._accepted_lock:
+                            new, self._accepted = self._accepted, []
+                        for conn in new:
+                            sel.register(conn, selectors.EVENT_READ, wire.FrameReader(conn))
+                            inbound.append(conn)
+                        continue
+                    conn, reader = key.fileobj, key.data
+                    try:
+                        chunk = conn.recv(1 << 16)
+                        bodies = reader.feed(chunk) if chunk else None
+                        if bodies is None:
+                            close(conn)  # the peer closed the connection
+                            continue
+                        for body in bodies:
+                            self._deliver(wire.decode(body, self.ref))
+                    except (OSError, ValueError) as e:
+                        if not self._stop.is_set():
+                            log.debug("%s: reader closed: %s", self.name, e)
+                        close(conn)
+        finally:
+            for conn in list(inbound):
+                close(conn)
+            sel.close()
+            with self._wake_lock:
+                self._wake_open = False
+                for fd in (self._wake_r, self._wake_w):
+                    os.close(fd)
+
+
+class _Mailbox:
+    """A node's local messages (self-sends, notices posted by other threads):
+    a thread-safe deque whose ``put`` wakes the dispatcher's selector."""
+
+    def __init__(self, wake: Callable[[], None]):
+        self._q: "collections.deque[Any]" = collections.deque()
+        self._wake = wake
+
+    def put(self, msg: Any) -> None:
+        self._q.append(msg)
+        self._wake()
+
+    def get_nowait(self) -> Any:
+        return self._q.popleft()  # IndexError when empty
+
+    def __len__(self) -> int:
+        return len(self._q)
 
 
 class LocalRef:

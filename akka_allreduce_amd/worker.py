@@ -685,6 +685,9 @@ class AllreduceWorker:
 
     # ------------------------------------------------------------------ helpers
     def _payload(self, value: Any) -> torch.Tensor:
+        if isinstance(value, torch.Tensor) and value.dtype is self.dtype and value.dim() == 1 \
+                and value.device.type == "cpu" and value.is_contiguous():
+            return value  # (a decoded wire payload: nothing to convert)
         t = value if isinstance(value, torch.Tensor) else torch.as_tensor(value)
         if t.dtype != self.dtype:
             t = t.to(self.dtype)
@@ -698,6 +701,9 @@ class AllreduceWorker:
             self._core.sync_all()  # the async D2D copy must finish before `t` can be freed
 
     def _flush_outbox(self) -> None:
+        # one batch per remote destination, in emission order (per-pair FIFO,
+        # as the reference's tests rely on): one write per peer per handler
+        batches: Dict[int, list] = {}
         for m in self._core.drain():
             value = torch.frombuffer(bytearray(m.data), dtype=self.dtype) if len(m.data) else torch.empty(0, dtype=self.dtype)
             if m.kind == 1:
@@ -707,7 +713,12 @@ class AllreduceWorker:
             ref = self.peers.get(m.dest)
             if ref is None:
                 continue  # peer left the cluster
-            ref.tell(msg, self)
+            if hasattr(ref, "tell_many"):
+                batches.setdefault(m.dest, []).append(msg)
+            else:
+                ref.tell(msg, self)
+        for dest, msgs in batches.items():
+            self.peers[dest].tell_many(msgs)
 
     def _release_pending(self) -> None:
         if not self._to_release:
