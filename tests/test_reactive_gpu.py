@@ -64,13 +64,32 @@ def test_reactive_loopback_bf16():
 
 def test_reactive_loopback_sleeping_rank():
     """Rank 3 sleeps 3 s; at thresholds 0.75 ranks 0-2 finish all rounds long
-    before it wakes, summing only each other's data; then rank 3 catches up."""
+    before it wakes, summing only each other's data; then rank 3 catches up.
+
+    Runs in a fresh child process: its ranks' 20 streams must each get a
+    hardware queue of their own.  In the suite's process, streams of earlier
+    tests can push a fast rank's stream onto a queue shared with a stream
+    parked on the sleeper, and that fast rank then waits for the sleeper (a
+    harness artefact: one process per GPU on a node)."""
+    import os
+    import subprocess
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    r = subprocess.run([sys.executable, "-c", "import test_reactive_gpu as t; t._sleeping_child()"], cwd=here,
+                       env=dict(os.environ, GPU_MAX_HW_QUEUES="32"), capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
+    assert "sleeping ok" in r.stdout, r.stdout[-2000:]
+
+
+def _sleeping_child():
     n, S, C, R = 4, 1 << 14, 1 << 10, 4
     cl = ReactiveLoopbackCluster(n, S, C, th_reduce=0.75, th_complete=0.75, max_lag=2)
     try:
         _sleeping(cl, n, S, C, R)
     finally:
         cl.close()
+    print("sleeping ok", flush=True)
 
 
 def _sleeping(cl, n, S, C, R):
