@@ -77,7 +77,10 @@ def test_reactive_loopback_sleeping_rank():
 
     here = os.path.dirname(os.path.abspath(__file__))
     r = subprocess.run([sys.executable, "-c", "import test_reactive_gpu as t; t._sleeping_child()"], cwd=here,
-                       env=dict(os.environ, GPU_MAX_HW_QUEUES="32"), capture_output=True, text=True, timeout=180)
+                       env=dict(os.environ, GPU_MAX_HW_QUEUES="32",
+                                PYTHONPATH=os.pathsep.join([os.path.dirname(here), here,
+                                                            os.environ.get("PYTHONPATH", "")])),
+                       capture_output=True, text=True, timeout=180)
     assert r.returncode == 0, (r.stdout[-2000:], r.stderr[-3000:])
     assert "sleeping ok" in r.stdout, r.stdout[-2000:]
 
