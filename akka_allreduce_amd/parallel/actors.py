@@ -84,7 +84,7 @@ class Node:
         self._accepted_lock = threading.Lock()
         self._conns: Dict[str, socket.socket] = {}
         self._conn_lock = threading.Lock()
-        self._send_locks: Dict[str, threading.Lock] = {}
+        self._outs: Dict[str, "_Outbound"] = {}  # per destination: socket, pending bytes, flusher state
         self._refs: Dict[str, RemoteRef] = {}
         self._stop = threading.Event()
         self._threads: List[threading.Thread] = []
@@ -175,7 +175,15 @@ class Node:
     def send_many(self, address: str, msgs: List[Any]) -> None:
         """``msgs`` to ``address`` in order: their frames go out in ONE write
         (the receiver's FrameReader splits them), so the per-pair FIFO order
-        of the reference holds and a burst costs one system call."""
+        of the reference holds and a burst costs one system call.
+
+        Never blocks the caller -- which is usually this node's dispatcher,
+        the thread that must keep reading the node's sockets.  The write is
+        non-blocking (MSG_DONTWAIT); whatever the socket buffer cannot take
+        goes to the destination's pending bytes, which a flusher thread writes
+        out (later sends queue behind them, so order holds).  Two nodes that
+        send each other large payloads from their handlers therefore cannot
+        deadlock on full socket buffers."""
         if address == self.address:
             for m in msgs:
                 self.mailbox.put(m)
@@ -185,27 +193,71 @@ class Node:
         frame = wire.encode(msgs[0], self.addr_of) if len(msgs) == 1 else \
             b"".join(wire.encode(m, self.addr_of) for m in msgs)
         with self._conn_lock:
-            lock = self._send_locks.setdefault(address, threading.Lock())
-        with lock:
+            out = self._outs.get(address)
+            if out is None:
+                out = self._outs[address] = _Outbound()
+        with out.lock:
             try:
-                with self._conn_lock:
-                    s = self._conns.get(address)
-                if s is None:
-                    s = socket.create_connection(parse_addr(address), timeout=10.0)
-                    s.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
-                    s.settimeout(None)
+                if out.sock is None:
+                    out.sock = socket.create_connection(parse_addr(address), timeout=10.0)
+                    out.sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+                    out.sock.settimeout(None)
                     with self._conn_lock:
                         if self._stop.is_set():
-                            s.close()
+                            out.sock.close()
+                            out.sock = None
                             return
-                        self._conns[address] = s
-                s.sendall(frame)
+                        self._conns[address] = out.sock
+                if out.flushing:
+                    out.pending += frame  # behind the bytes the flusher still writes
+                    return
+                try:
+                    n = out.sock.send(frame, socket.MSG_DONTWAIT)
+                except BlockingIOError:
+                    n = 0
+                if n == len(frame):
+                    return
+                out.pending += memoryview(frame)[n:]
+                out.flushing = True
             except OSError as e:
-                with self._conn_lock:
-                    self._conns.pop(address, None)
-                log.warning("%s: send to %s failed: %s", self.name, address, e)
-                if self.on_send_failure:
-                    self.on_send_failure(address, e)
+                self._send_failed(address, out, e)
+                return
+        threading.Thread(target=self._flush_pending, args=(address, out), name=f"{self.name}-flush",
+                         daemon=True).start()
+
+    def _flush_pending(self, address: str, out: "_Outbound") -> None:
+        while True:
+            with out.lock:
+                if not out.pending or out.sock is None:
+                    out.flushing = False
+                    out.pending.clear()
+                    return
+                data, out.pending = out.pending, bytearray()
+                sock = out.sock
+            try:
+                sock.sendall(data)  # blocking, off the dispatcher
+            except OSError as e:
+                with out.lock:
+                    self._send_failed(address, out, e)
+                return
+
+    def _send_failed(self, address: str, out: "_Outbound", e: BaseException) -> None:
+        """(out.lock held) drop the connection and its pending bytes, report."""
+        if out.sock is not None:
+            try:
+                out.sock.close()
+            except OSError:
+                pass
+        out.sock = None
+        out.pending.clear()
+        out.flushing = False
+        with self._conn_lock:
+            self._conns.pop(address, None)
+        if self._stop.is_set():
+            return  # the node's own shutdown closed the socket under a flusher
+        log.warning("%s: send to %s failed: %s", self.name, address, e)
+        if self.on_send_failure:
+            self.on_send_failure(address, e)
 
     # ---- receiving -----------------------------------------------------------------
     def _accept_loop(self) -> None:
@@ -306,6 +358,18 @@ class Node:
                 self._wake_open = False
                 for fd in (self._wake_r, self._wake_w):
                     os.close(fd)
+
+
+class _Outbound:
+    """One destination's connection and the bytes not yet written to it."""
+
+    __slots__ = ("sock", "lock", "pending", "flushing")
+
+    def __init__(self):
+        self.sock: Optional[socket.socket] = None
+        self.lock = threading.Lock()
+        self.pending = bytearray()
+        self.flushing = False  # a flusher thread owns the pending bytes
 
 
 class _Mailbox:

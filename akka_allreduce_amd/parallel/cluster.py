@@ -276,7 +276,11 @@ class WorkerProcess:
                     from ..utils.node_metrics import sample
 
                     metrics, last_metrics = sample(), now
-                self.master.tell(Heartbeat(self.worker.id, self.worker.round, metrics))
+                try:
+                    hb = Heartbeat(self.worker.id, self.worker.round, metrics)
+                except AttributeError:
+                    return  # the worker was closed under this thread (the job's end)
+                self.master.tell(hb)
 
     def wait(self, timeout: Optional[float] = None) -> bool:
         return self.stopped.wait(timeout)

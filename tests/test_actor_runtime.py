@@ -92,3 +92,37 @@ def test_local_posts_from_other_threads_and_stop():
     node.mailbox.put(StartAllreduce(9))  # after stop: dropped, no write into a closed pipe
     time.sleep(0.05)
     assert len(rec.got) == 3
+
+
+def test_large_payloads_both_ways_from_handlers_do_not_deadlock():
+    """Each node answers every big message with a big message of its own from
+    inside its handler.  Its dispatcher is the only thread reading its
+    sockets, so a blocking write there could wait for a peer that is itself
+    blocked writing back, once both socket buffers are full.  Sends never
+    block the handler: what the buffer cannot take goes to a flusher."""
+    K, big = 12, 1 << 21  # 8 MiB fp32 per message, well past a socket buffer
+
+    class Pong:
+        def __init__(self):
+            self.node = None
+            self.peer = None
+            self.seen = 0
+            self.done = threading.Event()
+
+        def receive(self, m):
+            self.seen += 1
+            if m.round < K:
+                self.node.send(self.peer, ScatterBlock(torch.full((big,), float(m.round + 1)), 0, 1, 0, m.round + 1))
+            if self.seen >= K // 2:
+                self.done.set()
+
+    a, b = Pong(), Pong()
+    na, nb = Node(name="a").start(a), Node(name="b").start(b)
+    a.node, b.node, a.peer, b.peer = na, nb, nb.address, na.address
+    for r in range(4):  # both sides start at once: four big messages in flight each way
+        na.send(nb.address, ScatterBlock(torch.zeros(big), 0, 1, 0, 2 * r))
+        nb.send(na.address, ScatterBlock(torch.zeros(big), 0, 1, 0, 2 * r))
+    assert a.done.wait(60) and b.done.wait(60), (a.seen, b.seen)
+    for n in (na, nb):
+        n.stop()
+        n.join(5)

@@ -64,7 +64,9 @@ def test_node_metrics_on_heartbeats():
     assert (hb.srcId, hb.round, hb.metrics) == (3, 7, s)
     assert decode(encode(Heartbeat(1, 2), lambda r: None)[4:], lambda a: None).metrics is None
 
-    size, rounds = 100, 200
+    # (enough rounds to outlast several heartbeats: the job must still run
+    # when the first samples go out -- 200 rounds take ~0.1 s now)
+    size, rounds = 100, 1_000_000
     m = start_master(ThresholdConfig(1.0, 1.0, 1.0), DataConfig(size, 10, rounds), WorkerConfig(2, 1), port=0,
                      transport="tcp", unreachable_after_s=30.0, heartbeat_interval_s=0.1)
     ws = [start_worker(m.address, size, checkpoint=1000, printer=lambda *_: None, heartbeat_interval_s=0.1,
