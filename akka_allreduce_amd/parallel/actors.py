@@ -51,6 +51,10 @@ class RemoteRef:
         """Several messages in order, written as one batch (one system call)."""
         self._node.send_many(self.address, msgs)
 
+    def tell_frames(self, frames: bytes) -> None:
+        """Already-encoded wire frames (the native outbox), in order."""
+        self._node.send_frames(self.address, frames)
+
     def __repr__(self) -> str:
         return f"RemoteRef({self.address})"
 
@@ -90,6 +94,10 @@ class Node:
         self._threads: List[threading.Thread] = []
         self.on_send_failure: Optional[Callable[[str, BaseException], None]] = None
         self.on_message: Optional[Callable[[Any], None]] = None  # observer hook (failure detector)
+        # Fast path for data frames (the worker's native codec): called with a
+        # frame body that starts like a ScatterBlock / ReduceBlock, returns
+        # True when it consumed it; otherwise the frame is decoded here.
+        self.frame_handler: Optional[Callable[[bytes], bool]] = None
         # Progress hook run by the dispatcher thread between messages: returns
         # None when there is nothing to drive (the dispatcher then blocks on the
         # mailbox), True after progress, False while work is pending but idle
@@ -192,6 +200,17 @@ class Node:
             return  # a stopped node sends nothing (and opens no new connection)
         frame = wire.encode(msgs[0], self.addr_of) if len(msgs) == 1 else \
             b"".join(wire.encode(m, self.addr_of) for m in msgs)
+        self.send_frames(address, frame)
+
+    def send_frames(self, address: str, frame: bytes) -> None:
+        """Encoded frames to ``address`` (see send_many)."""
+        if address == self.address:
+            r = wire.FrameReader(None)
+            for body in r.feed(frame):
+                self.mailbox.put(wire.decode(body, self.ref))
+            return
+        if self._stop.is_set() or not frame:
+            return
         with self._conn_lock:
             out = self._outs.get(address)
             if out is None:
@@ -344,7 +363,10 @@ class Node:
                         if bodies is None:
                             close(conn)  # the peer closed the connection
                             continue
+                        fast = self.frame_handler if self.on_message is None else None
                         for body in bodies:
+                            if fast is not None and body.startswith(_DATA_PREFIXES) and fast(body):
+                                continue
                             self._deliver(wire.decode(body, self.ref))
                     except (OSError, ValueError) as e:
                         if not self._stop.is_set():
@@ -358,6 +380,11 @@ class Node:
                 self._wake_open = False
                 for fd in (self._wake_r, self._wake_w):
                     os.close(fd)
+
+
+# How wire.encode starts a ScatterBlock / ReduceBlock body: a fixmap of 7 / 8
+# entries, the key "t", then the type name (a cheap test before the fast path)
+_DATA_PREFIXES = (b"\x87\xa1t\xacScatterBlock", b"\x88\xa1t\xabReduceBlock")
 
 
 class _Outbound:

@@ -233,6 +233,8 @@ class WorkerProcess:
                                           name=f"worker@{self.node.address}")
         self.stopped = threading.Event()
         self.node.aliases.append(self.worker)
+        if hasattr(self.worker, "receive_frame"):
+            self.node.frame_handler = self.worker.receive_frame  # data frames to the native codec
         if transport == "reactive":
             # the dispatcher thread drives the in-flight transfers between messages
             self.node.poller = self._poll

@@ -54,6 +54,8 @@ def _tensor_bytes(v: Any) -> tuple[bytes, str]:
 
 
 def _bytes_tensor(b: bytes, dt: str) -> torch.Tensor:
+    if not b:  # (torch.frombuffer refuses an empty buffer)
+        return torch.empty(0, dtype=_DT_INV[dt])
     if dt == "bfloat16":
         return torch.frombuffer(bytearray(b), dtype=torch.int16).view(torch.bfloat16)
     return torch.frombuffer(bytearray(b), dtype=_DT_INV[dt])

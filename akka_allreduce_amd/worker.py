@@ -123,6 +123,7 @@ class AllreduceWorker:
         self._outputs: Dict[int, AllReduceOutput] = {}
         self._next_round = 0
         self._in_call = 0
+        self._frames_ok: Optional[bool] = None  # every peer takes wire frames (see _flush_outbox)
         self._stream_cache: Optional[int] = None
         # CPU race checking (AKKA_RACECHECK=1): a stream of the simulated
         # device standing for the caller's stream (producer of inputs,
@@ -176,6 +177,31 @@ class AllreduceWorker:
             if self._in_call == 0:
                 self._flush_outbox()
                 self._release_pending()
+
+    def receive_frame(self, body: bytes) -> bool:
+        """A data frame straight off the wire (the actor runtime's fast path,
+        Node.frame_handler): applied by the native codec when this worker is
+        initialized on the message-driven (TCP) data plane and the frame is a
+        ScatterBlock / ReduceBlock of its dtype.  False: not consumed -- the
+        runtime decodes it and calls ``receive`` as usual."""
+        core = self._core
+        if core is None or not self.initialized or self._pre_init or self.transport != "outbox":
+            return False
+        self._in_call += 1
+        try:
+            done = core.apply_frame(body)
+        except Exception as e:  # tryCatch semantics as in receive() (W:287-299)
+            self.errors.append(e)
+            log.error("%s: error handling a data frame: %s", self.name, e)
+            if self.strict:
+                raise
+            done = True
+        finally:
+            self._in_call -= 1
+            if self._in_call == 0:
+                self._flush_outbox()
+                self._release_pending()
+        return bool(done)
 
     def _dispatch(self, msg: Any) -> None:
         if isinstance(msg, InitWorkers):
@@ -239,6 +265,7 @@ class AllreduceWorker:
         first = self._core.init(int(m.destId), int(m.workerNum), float(m.thReduce), float(m.thComplete),
                                 int(m.maxLag), int(m.dataSize), int(m.maxChunkSize), peers)
         self.peers = dict(m.workers)
+        self._frames_ok = None
         if not first:
             # re-init only replaces the peer map (W:87-89) -- and, on the RCCL
             # data plane, starts a new membership epoch: a communicator over
@@ -702,7 +729,26 @@ class AllreduceWorker:
 
     def _flush_outbox(self) -> None:
         # one batch per remote destination, in emission order (per-pair FIFO,
-        # as the reference's tests rely on): one write per peer per handler
+        # as the reference's tests rely on): one write per peer per handler.
+        # Peers that are all network references take the outbox as wire
+        # frames built natively (no message object per chunk)
+        if self._frames_ok is None:
+            self._frames_ok = bool(self.peers) and all(hasattr(r, "tell_frames") for r in self.peers.values()
+                                                       if r is not self)
+        if self._frames_ok and self.transport == "outbox":
+            for dest, frames in self._core.drain_frames():
+                ref = self.peers.get(dest)
+                if ref is None:
+                    continue  # peer left the cluster
+                if ref is self or not hasattr(ref, "tell_frames"):
+                    self._frames_ok = None  # the peer map changed: look again
+                    from .parallel.wire import FrameReader, decode  # noqa: PLC0415
+
+                    for body in FrameReader(None).feed(frames):
+                        ref.tell(decode(body, lambda a: None), self)
+                    continue
+                ref.tell_frames(frames)
+            return
         batches: Dict[int, list] = {}
         for m in self._core.drain():
             value = torch.frombuffer(bytearray(m.data), dtype=self.dtype) if len(m.data) else torch.empty(0, dtype=self.dtype)

@@ -16,11 +16,13 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <map>
 #include <mutex>
 #include <set>
 
 #include "../engine/engine.h"
 #include "../kernels/kernels.h"
+#include "../runtime/frames.h"
 #include "../runtime/watchdog.h"
 #include "../transport/ipc_p2p.h"
 #include "../transport/p2p.h"
@@ -46,7 +48,7 @@ struct PySimHub {
 struct OutMsg {
   int32_t kind;  // 1 scatter, 2 reduce
   int32_t src, dest, chunk, round, count;
-  py::bytes data;
+  std::string data;  // the payload's bytes (py::bytes on access)
 };
 
 class OutboxLink final : public Link {
@@ -71,7 +73,7 @@ class OutboxLink final : public Link {
     if (p.kind == PayloadKind::InputView) dp_->wait_input(round, dp_->device()->compute_stream());
     std::string buf(size_t(p.len) * dp_->esize(), '\0');
     dp_->read_payload(p, buf.data());
-    return OutMsg{kind, me_, dest, chunk, round, count, py::bytes(buf)};
+    return OutMsg{kind, me_, dest, chunk, round, count, std::move(buf)};
   }
   int32_t me_;
   DataPlane* dp_ = nullptr;
@@ -426,6 +428,49 @@ class WorkerCore final : public EngineHost {
     return {reinterpret_cast<uintptr_t>(dev_->comm_stream()), reinterpret_cast<uintptr_t>(dev_->compute_stream())};
   }
   std::vector<OutMsg> drain() { return outbox_ ? outbox_->drain() : std::vector<OutMsg>{}; }
+
+  // The outbox as wire frames (csrc/runtime/frames.h), one byte string per
+  // destination in first-emission order, each destination's messages in
+  // emission order (per-pair FIFO): the CPU data plane's sends without a
+  // Python message object per chunk.
+  std::vector<std::pair<int32_t, py::bytes>> drain_frames() {
+    std::vector<std::pair<int32_t, py::bytes>> res;
+    if (!outbox_) return res;
+    std::vector<OutMsg> msgs = outbox_->drain();
+    if (msgs.empty()) return res;
+    const char* dt = dt_ == DType::F32 ? "float32" : "bfloat16";
+    std::vector<int32_t> order;
+    std::map<int32_t, std::string> by;
+    for (const OutMsg& m : msgs) {
+      auto it = by.find(m.dest);
+      if (it == by.end()) {
+        order.push_back(m.dest);
+        it = by.emplace(m.dest, std::string()).first;
+      }
+      frames::append_data_frame(it->second, m.kind, m.data.data(), m.data.size(), dt, m.src, m.dest, m.chunk,
+                                m.round, m.count);
+    }
+    for (int32_t d : order) res.emplace_back(d, py::bytes(by[d]));
+    return res;
+  }
+
+  // One arriving frame BODY, if it is a ScatterBlock / ReduceBlock of this
+  // worker's dtype: parsed in place and handed to the engine with a pointer
+  // into the frame.  False: anything else (the caller decodes it in Python).
+  bool apply_frame(py::bytes body) {
+    char* p = nullptr;
+    Py_ssize_t n = 0;
+    if (PyBytes_AsStringAndSize(body.ptr(), &p, &n) != 0) throw py::error_already_set();
+    frames::DataFrame f;
+    if (!frames::parse_data_frame(p, size_t(n), f)) return false;
+    const char* dt = dt_ == DType::F32 ? "float32" : "bfloat16";
+    const size_t es = dt_ == DType::F32 ? 4 : 2;
+    if (f.dtype != dt || f.nbytes % es != 0) return false;
+    const Payload pl{f.value, int64_t(f.nbytes / es), PayloadKind::External, true};
+    if (f.kind == 1) engine_->on_scatter(int32_t(f.src), int32_t(f.dest), int32_t(f.chunk), int32_t(f.round), pl);
+    else engine_->on_reduce(int32_t(f.src), int32_t(f.dest), int32_t(f.chunk), int32_t(f.round), int32_t(f.count), pl);
+    return true;
+  }
   Device* device() const { return dev_.get(); }
 
   // ---- introspection -------------------------------------------------------
@@ -690,6 +735,28 @@ PYBIND11_MODULE(_native, m) {
   bind_onesided(m);
   bind_probe(m);
 
+  // the native data-frame codec alone (tests: interop with wire.py both ways)
+  m.def("frame_encode", [](int32_t kind, py::bytes value, const std::string& dtype, int32_t src, int32_t dest,
+                           int32_t chunk, int32_t round, int32_t count) {
+    std::string v = value, out;
+    frames::append_data_frame(out, kind, v.data(), v.size(), dtype.c_str(), src, dest, chunk, round, count);
+    return py::bytes(out);
+  });
+  m.def("frame_parse", [](py::bytes body) -> py::object {
+    std::string b = body;
+    frames::DataFrame f;
+    if (!frames::parse_data_frame(b.data(), b.size(), f)) return py::none();
+    py::dict d;
+    d["kind"] = f.kind;
+    d["value"] = py::bytes(f.value, f.nbytes);
+    d["dtype"] = f.dtype;
+    d["src"] = f.src;
+    d["dest"] = f.dest;
+    d["chunk"] = f.chunk;
+    d["round"] = f.round;
+    d["count"] = f.count;
+    return d;
+  });
   py::class_<OutMsg>(m, "OutMsg")
       .def_readonly("kind", &OutMsg::kind)
       .def_readonly("src", &OutMsg::src)
@@ -697,7 +764,7 @@ PYBIND11_MODULE(_native, m) {
       .def_readonly("chunk", &OutMsg::chunk)
       .def_readonly("round", &OutMsg::round)
       .def_readonly("count", &OutMsg::count)
-      .def_readonly("data", &OutMsg::data);
+      .def_property_readonly("data", [](const OutMsg& o) { return py::bytes(o.data); });
 
   py::class_<PyLoopbackHub>(m, "LoopbackHub")
       .def(py::init([](int32_t n) { return PyLoopbackHub{std::make_shared<LoopbackHub>(n)}; }))
@@ -763,6 +830,8 @@ PYBIND11_MODULE(_native, m) {
       .def("expand_counts", &WorkerCore::expand_counts)
       .def("count_mean", &WorkerCore::count_mean)
       .def("drain", &WorkerCore::drain)
+      .def("drain_frames", &WorkerCore::drain_frames)
+      .def("apply_frame", &WorkerCore::apply_frame)
       .def("streams", &WorkerCore::streams)
       .def("state", &WorkerCore::state)
       .def("p2p_info", &WorkerCore::p2p_info)

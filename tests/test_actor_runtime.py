@@ -126,3 +126,51 @@ def test_large_payloads_both_ways_from_handlers_do_not_deadlock():
     for n in (na, nb):
         n.stop()
         n.join(5)
+
+
+def _native():
+    from akka_allreduce_amd._native_loader import load
+
+    return load()
+
+
+def test_native_data_frames_interoperate_with_the_python_codec():
+    """csrc/runtime/frames.h against wire.py: frames the native outbox builds
+    decode in Python to the same messages, and frames Python encodes (every
+    integer width msgpack picks, fp32 and bf16, empty and long values) parse
+    natively to the same fields; other messages are never taken natively."""
+    import numpy as np
+
+    from akka_allreduce_amd.messages import ReduceBlock
+
+    n = _native()
+    rng = np.random.default_rng(0)
+    for kind in (1, 2):
+        for nvals in (0, 1, 3, 70, 20000):
+            for dtype in ("float32", "bfloat16"):
+                for ints in ((0, 1, 2, 3, 4), (127, 128, 255, 256, 65535), (65536, 2**31 - 1, 7, 300, 2**20)):
+                    src, dest, chunk, rnd, cnt = ints
+                    es = 4 if dtype == "float32" else 2
+                    val = rng.integers(0, 255, nvals * es, dtype=np.uint8).tobytes()
+                    frame = n.frame_encode(kind, val, dtype, src, dest, chunk, rnd, cnt)
+                    body = frame[4:]
+                    assert int.from_bytes(frame[:4], "big") == len(body)
+                    m = wire.decode(body, lambda a: None)
+                    assert type(m) is (ScatterBlock if kind == 1 else ReduceBlock)
+                    assert (m.srcId, m.destId, m.chunkId, m.round) == (src, dest, chunk, rnd)
+                    assert wire._tensor_bytes(m.value) == (val, dtype)
+                    if kind == 2:
+                        assert m.count == cnt
+                    # and back: Python's encoding parses natively
+                    t = m.value
+                    py = (ScatterBlock(t, src, dest, chunk, rnd) if kind == 1
+                          else ReduceBlock(t, src, dest, chunk, rnd, cnt))
+                    pb = wire.encode(py, lambda r: None)[4:]
+                    d = n.frame_parse(pb)
+                    assert d is not None and d["kind"] == kind and d["value"] == val and d["dtype"] == dtype
+                    assert (d["src"], d["dest"], d["chunk"], d["round"]) == (src, dest, chunk, rnd)
+                    if kind == 2:
+                        assert d["count"] == cnt
+    for other in (StartAllreduce(5),):
+        assert n.frame_parse(wire.encode(other, lambda r: None)[4:]) is None
+    assert n.frame_parse(b"\x87") is None and n.frame_parse(b"") is None  # truncated: not taken
