@@ -445,17 +445,25 @@ def run_cfg1(rounds: int = 300, gpu: bool = False) -> dict:
     cp = max(1, rounds // 3)
     res = {"workers": 2, "data_size": 10, "max_chunk_size": 2, "max_lag": 1, "rounds": rounds,
            "transport": "tcp, one process per worker (cpu)"}
-    runs = [("demo_thresholds", 0.8, 0, "tcp", "cpu", None), ("exact_assert", 1.0, 2, "tcp", "cpu", None)]
+    # (tag, thComplete, assertMultiple, master transport, worker device, worker transport,
+    #  workers, dataSize, maxChunkSize, maxLag)
+    runs = [("demo_thresholds", 0.8, 0, "tcp", "cpu", None, 2, 10, 2, 1),
+            ("exact_assert", 1.0, 2, "tcp", "cpu", None, 2, 10, 2, 1),
+            # the reference's script config (scripts/testAllreduceMaster.sc:7-24):
+            # 4 workers, 778 floats, 3-float chunks (65 per block), maxLag 3,
+            # every round asserted x4 -- ~390 data messages per worker per round
+            ("script_config_exact_assert", 1.0, 4, "tcp", "cpu", None, 4, 778, 3, 3)]
     if gpu:
-        runs.append(("gpu_onesided_exact_assert", 1.0, 2, "onesided", "cuda", "onesided"))
-    for tag, thc, mult, mtransport, wdev, wtransport in runs:
+        runs.append(("gpu_onesided_exact_assert", 1.0, 2, "onesided", "cuda", "onesided", 2, 10, 2, 1))
+    for tag, thc, mult, mtransport, wdev, wtransport, nw, dsize, csize, lag in runs:
         with socket.socket() as sk:
             sk.bind(("127.0.0.1", 0))
             port = sk.getsockname()[1]
         with tempfile.TemporaryDirectory() as td:
-            logs = [open(os.path.join(td, f"p{i}.log"), "w+") for i in range(3)]
-            procs = [subprocess.Popen(base + ["master", "--port", str(port), "--workers", "2", "--data-size", "10",
-                                              "--max-chunk-size", "2", "--max-round", str(rounds), "--max-lag", "1",
+            logs = [open(os.path.join(td, f"p{i}.log"), "w+") for i in range(nw + 1)]
+            procs = [subprocess.Popen(base + ["master", "--port", str(port), "--workers", str(nw), "--data-size",
+                                              str(dsize), "--max-chunk-size", str(csize), "--max-round", str(rounds),
+                                              "--max-lag", str(lag),
                                               "--th-reduce", "1.0", "--th-complete", str(thc), "--transport",
                                               mtransport],
                                       stdout=logs[0], stderr=subprocess.STDOUT, cwd=os.path.dirname(__file__) or ".")]
@@ -468,10 +476,10 @@ def run_cfg1(rounds: int = 300, gpu: bool = False) -> dict:
                 except OSError:
                     time.sleep(0.1)
             wextra = ["--transport", wtransport] if wtransport else []
-            procs += [subprocess.Popen(base + ["worker", "--master", f"127.0.0.1:{port}", "--data-size", "10",
+            procs += [subprocess.Popen(base + ["worker", "--master", f"127.0.0.1:{port}", "--data-size", str(dsize),
                                                "--checkpoint", str(cp), "--assert-multiple", str(mult), "--device",
                                                wdev, *wextra], stdout=logs[i], stderr=subprocess.STDOUT,
-                                       cwd=os.path.dirname(__file__) or ".") for i in (1, 2)]
+                                       cwd=os.path.dirname(__file__) or ".") for i in range(1, nw + 1)]
             for p in procs[1:]:
                 wd.watchdog_track_child(p.pid)
             rcs = []
@@ -486,6 +494,8 @@ def run_cfg1(rounds: int = 300, gpu: bool = False) -> dict:
                     wd.watchdog_untrack_child(p.pid)
             entry = {"rcs": rcs, "rounds_per_s": [], "sink_MBps": [], "failures": [], "workers_on": wdev,
                      "data_plane": "one-sided lane (GPU windows)" if wtransport == "onesided" else "tcp"}
+            if (nw, dsize, csize, lag) != (2, 10, 2, 1):
+                entry.update({"workers": nw, "data_size": dsize, "max_chunk_size": csize, "max_lag": lag})
             for f in logs[1:]:
                 f.seek(0)
                 txt = f.read()
