@@ -98,6 +98,9 @@ class Node:
         # frame body that starts like a ScatterBlock / ReduceBlock, returns
         # True when it consumed it; otherwise the frame is decoded here.
         self.frame_handler: Optional[Callable[[bytes], bool]] = None
+        # (begin, end) around the frames of one recv: the actor may hold its
+        # sends until `end`, so replies to a burst leave as one write per peer
+        self.batch_hooks: Optional[Tuple[Callable[[], None], Callable[[], None]]] = None
         # Progress hook run by the dispatcher thread between messages: returns
         # None when there is nothing to drive (the dispatcher then blocks on the
         # mailbox), True after progress, False while work is pending but idle
@@ -364,10 +367,17 @@ class Node:
                             close(conn)  # the peer closed the connection
                             continue
                         fast = self.frame_handler if self.on_message is None else None
-                        for body in bodies:
-                            if fast is not None and body.startswith(_DATA_PREFIXES) and fast(body):
-                                continue
-                            self._deliver(wire.decode(body, self.ref))
+                        hooks = self.batch_hooks if len(bodies) > 1 else None
+                        if hooks is not None:
+                            hooks[0]()
+                        try:
+                            for body in bodies:
+                                if fast is not None and body.startswith(_DATA_PREFIXES) and fast(body):
+                                    continue
+                                self._deliver(wire.decode(body, self.ref))
+                        finally:
+                            if hooks is not None:
+                                hooks[1]()
                     except (OSError, ValueError) as e:
                         if not self._stop.is_set():
                             log.debug("%s: reader closed: %s", self.name, e)

@@ -235,6 +235,7 @@ class WorkerProcess:
         self.node.aliases.append(self.worker)
         if hasattr(self.worker, "receive_frame"):
             self.node.frame_handler = self.worker.receive_frame  # data frames to the native codec
+            self.node.batch_hooks = (self.worker.begin_batch, self.worker.end_batch)
         if transport == "reactive":
             # the dispatcher thread drives the in-flight transfers between messages
             self.node.poller = self._poll

@@ -178,6 +178,24 @@ class AllreduceWorker:
                 self._flush_outbox()
                 self._release_pending()
 
+    def begin_batch(self) -> None:
+        """Hold this worker's sends until end_batch (the actor runtime brackets
+        the frames of one recv with these): the replies to a burst of chunks
+        leave as one write per peer instead of one per chunk."""
+        self._in_call += 1
+
+    def end_batch(self) -> None:
+        self._in_call -= 1
+        if self._in_call == 0 and self._core is not None:
+            try:
+                self._flush_outbox()
+                self._release_pending()
+            except Exception as e:  # tryCatch semantics (W:287-299)
+                self.errors.append(e)
+                log.error("%s: error flushing a batch: %s", self.name, e)
+                if self.strict:
+                    raise
+
     def receive_frame(self, body: bytes) -> bool:
         """A data frame straight off the wire (the actor runtime's fast path,
         Node.frame_handler): applied by the native codec when this worker is
