@@ -94,13 +94,11 @@ class Node:
         self._threads: List[threading.Thread] = []
         self.on_send_failure: Optional[Callable[[str, BaseException], None]] = None
         self.on_message: Optional[Callable[[Any], None]] = None  # observer hook (failure detector)
-        # Fast path for data frames (the worker's native codec): called with a
-        # frame body that starts like a ScatterBlock / ReduceBlock, returns
-        # True when it consumed it; otherwise the frame is decoded here.
-        self.frame_handler: Optional[Callable[[bytes], bool]] = None
-        # (begin, end) around the frames of one recv: the actor may hold its
-        # sends until `end`, so replies to a burst leave as one write per peer
-        self.batch_hooks: Optional[Tuple[Callable[[], None], Callable[[], None]]] = None
+        # Native frame path (a worker on the TCP data plane): connections are
+        # read into a native FrameSplitter and ``frame_consumer(splitter,
+        # deliver)`` applies its data frames in C++, handing every other frame
+        # body to ``deliver`` in order.  Set before start(); not with on_message.
+        self.frame_consumer: Optional[Callable[[Any, Callable[[bytes], None]], None]] = None
         # Progress hook run by the dispatcher thread between messages: returns
         # None when there is nothing to drive (the dispatcher then blocks on the
         # mailbox), True after progress, False while work is pending but idle
@@ -304,6 +302,16 @@ class Node:
         except Exception as e:  # an actor never dies from one message (W:287-299)
             log.exception("%s: error in receive(%s): %s", self.name, type(msg).__name__, e)
 
+    def _deliver_body(self, body: bytes) -> None:
+        self._deliver(wire.decode(body, self.ref))
+
+    def _new_reader(self, conn: socket.socket) -> Any:
+        if self.frame_consumer is not None and self.on_message is None:
+            from .._native_loader import load
+
+            return load().FrameSplitter()
+        return wire.FrameReader(conn)
+
     def _poll_timeout(self) -> Optional[float]:
         """Run the progress hook: None -> block until a message, 0 -> progress
         was made (look again at once), else the idle-but-pending back-off."""
@@ -356,28 +364,21 @@ class Node:
                         with self._accepted_lock:
                             new, self._accepted = self._accepted, []
                         for conn in new:
-                            sel.register(conn, selectors.EVENT_READ, wire.FrameReader(conn))
+                            sel.register(conn, selectors.EVENT_READ, self._new_reader(conn))
                             inbound.append(conn)
                         continue
                     conn, reader = key.fileobj, key.data
                     try:
                         chunk = conn.recv(1 << 16)
-                        bodies = reader.feed(chunk) if chunk else None
-                        if bodies is None:
+                        if not chunk:
                             close(conn)  # the peer closed the connection
                             continue
-                        fast = self.frame_handler if self.on_message is None else None
-                        hooks = self.batch_hooks if len(bodies) > 1 else None
-                        if hooks is not None:
-                            hooks[0]()
-                        try:
-                            for body in bodies:
-                                if fast is not None and body.startswith(_DATA_PREFIXES) and fast(body):
-                                    continue
+                        if isinstance(reader, wire.FrameReader):
+                            for body in reader.feed(chunk):
                                 self._deliver(wire.decode(body, self.ref))
-                        finally:
-                            if hooks is not None:
-                                hooks[1]()
+                        else:  # native splitter: the consumer applies data frames in C++
+                            reader.append(chunk)
+                            self.frame_consumer(reader, self._deliver_body)
                     except (OSError, ValueError) as e:
                         if not self._stop.is_set():
                             log.debug("%s: reader closed: %s", self.name, e)
@@ -390,11 +391,6 @@ class Node:
                 self._wake_open = False
                 for fd in (self._wake_r, self._wake_w):
                     os.close(fd)
-
-
-# How wire.encode starts a ScatterBlock / ReduceBlock body: a fixmap of 7 / 8
-# entries, the key "t", then the type name (a cheap test before the fast path)
-_DATA_PREFIXES = (b"\x87\xa1t\xacScatterBlock", b"\x88\xa1t\xabReduceBlock")
 
 
 class _Outbound:

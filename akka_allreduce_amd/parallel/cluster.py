@@ -233,9 +233,8 @@ class WorkerProcess:
                                           name=f"worker@{self.node.address}")
         self.stopped = threading.Event()
         self.node.aliases.append(self.worker)
-        if hasattr(self.worker, "receive_frame"):
-            self.node.frame_handler = self.worker.receive_frame  # data frames to the native codec
-            self.node.batch_hooks = (self.worker.begin_batch, self.worker.end_batch)
+        if hasattr(self.worker, "consume_frames"):
+            self.node.frame_consumer = self.worker.consume_frames  # data frames to the native codec
         if transport == "reactive":
             # the dispatcher thread drives the in-flight transfers between messages
             self.node.poller = self._poll

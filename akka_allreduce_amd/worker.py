@@ -178,48 +178,36 @@ class AllreduceWorker:
                 self._flush_outbox()
                 self._release_pending()
 
-    def begin_batch(self) -> None:
-        """Hold this worker's sends until end_batch (the actor runtime brackets
-        the frames of one recv with these): the replies to a burst of chunks
-        leave as one write per peer instead of one per chunk."""
-        self._in_call += 1
-
-    def end_batch(self) -> None:
-        self._in_call -= 1
-        if self._in_call == 0 and self._core is not None:
-            try:
-                self._flush_outbox()
-                self._release_pending()
-            except Exception as e:  # tryCatch semantics (W:287-299)
-                self.errors.append(e)
-                log.error("%s: error flushing a batch: %s", self.name, e)
-                if self.strict:
-                    raise
-
-    def receive_frame(self, body: bytes) -> bool:
-        """A data frame straight off the wire (the actor runtime's fast path,
-        Node.frame_handler): applied by the native codec when this worker is
-        initialized on the message-driven (TCP) data plane and the frame is a
-        ScatterBlock / ReduceBlock of its dtype.  False: not consumed -- the
-        runtime decodes it and calls ``receive`` as usual."""
-        core = self._core
-        if core is None or not self.initialized or self._pre_init or self.transport != "outbox":
-            return False
+    def consume_frames(self, splitter: Any, deliver: Callable[[bytes], None]) -> None:
+        """The frames one ``recv`` completed (the actor runtime's native path,
+        Node.frame_consumer): the native splitter applies every ScatterBlock /
+        ReduceBlock of this worker's dtype in C++ with a pointer into the
+        frame; any other frame -- or every frame while the worker is not
+        initialized on the message-driven (TCP) data plane -- comes back in
+        order and goes to ``deliver`` (decode + ``receive``).  Sends are held
+        until the end, so the replies to a burst of chunks leave as one write
+        per peer."""
         self._in_call += 1
         try:
-            done = core.apply_frame(body)
-        except Exception as e:  # tryCatch semantics as in receive() (W:287-299)
-            self.errors.append(e)
-            log.error("%s: error handling a data frame: %s", self.name, e)
-            if self.strict:
-                raise
-            done = True
+            while True:
+                core = self._core
+                ok = core is not None and self.initialized and not self._pre_init and self.transport == "outbox"
+                try:
+                    body = splitter.run(core if ok else None)
+                except Exception as e:  # the frame is consumed; tryCatch semantics (W:287-299)
+                    self.errors.append(e)
+                    log.error("%s: error handling a data frame: %s", self.name, e)
+                    if self.strict:
+                        raise
+                    continue
+                if body is None:
+                    return
+                deliver(body)
         finally:
             self._in_call -= 1
-            if self._in_call == 0:
+            if self._in_call == 0 and self._core is not None:
                 self._flush_outbox()
                 self._release_pending()
-        return bool(done)
 
     def _dispatch(self, msg: Any) -> None:
         if isinstance(msg, InitWorkers):

@@ -461,8 +461,11 @@ class WorkerCore final : public EngineHost {
     char* p = nullptr;
     Py_ssize_t n = 0;
     if (PyBytes_AsStringAndSize(body.ptr(), &p, &n) != 0) throw py::error_already_set();
+    return apply_frame_raw(p, size_t(n));
+  }
+  bool apply_frame_raw(const char* p, size_t n) {
     frames::DataFrame f;
-    if (!frames::parse_data_frame(p, size_t(n), f)) return false;
+    if (!frames::parse_data_frame(p, n, f)) return false;
     const char* dt = dt_ == DType::F32 ? "float32" : "bfloat16";
     const size_t es = dt_ == DType::F32 ? 4 : 2;
     if (f.dtype != dt || f.nbytes % es != 0) return false;
@@ -727,7 +730,57 @@ class WorkerCore final : public EngineHost {
 
 hipStream_t as_stream(uintptr_t s) { return reinterpret_cast<hipStream_t>(s); }
 
+// The frames of one connection, split natively: data frames a worker core
+// takes are applied in place without returning to Python; the first frame it
+// does not take (another message type, another dtype, no core) is handed back
+// -- frames stay in order.  One Python call per recv instead of one per chunk
+// (csrc/runtime/frames.h: the reference's ~400 messages per worker per round).
+class FrameSplitter {
+ public:
+  void append(py::bytes chunk) {
+    char* p = nullptr;
+    Py_ssize_t n = 0;
+    if (PyBytes_AsStringAndSize(chunk.ptr(), &p, &n) != 0) throw py::error_already_set();
+    if (pos_ > 0 && pos_ == buf_.size()) {
+      buf_.clear();
+      pos_ = 0;
+    }
+    buf_.append(p, size_t(n));
+  }
+  // Applies frames to `core` until one it does not take; returns that body
+  // (bytes), or None once no complete frame is left.  A frame whose apply
+  // raised is consumed and the error re-raised.
+  py::object run(WorkerCore* core) {
+    while (buf_.size() - pos_ >= 4) {
+      const unsigned char* h = reinterpret_cast<const unsigned char*>(buf_.data() + pos_);
+      const size_t n = (size_t(h[0]) << 24) | (size_t(h[1]) << 16) | (size_t(h[2]) << 8) | size_t(h[3]);
+      if (n > (size_t(1) << 31)) throw AkkaError("frame exceeds the size limit");
+      if (buf_.size() - pos_ < 4 + n) break;
+      const char* body = buf_.data() + pos_ + 4;
+      pos_ += 4 + n;
+      if (core != nullptr && core->apply_frame_raw(body, n)) continue;
+      py::bytes out(body, n);
+      compact();
+      return out;
+    }
+    compact();
+    return py::none();
+  }
+  size_t pending() const { return buf_.size() - pos_; }
+
+ private:
+  void compact() {
+    if (pos_ > (size_t(1) << 16) && pos_ * 2 > buf_.size()) {
+      buf_.erase(0, pos_);
+      pos_ = 0;
+    }
+  }
+  std::string buf_;
+  size_t pos_ = 0;
+};
+
 }  // namespace
+
 
 PYBIND11_MODULE(_native, m) {
   m.doc() = "MI355X-native threshold allreduce core (engine, gfx950 kernels, RCCL/xGMI transport)";
@@ -757,6 +810,11 @@ PYBIND11_MODULE(_native, m) {
     d["count"] = f.count;
     return d;
   });
+  py::class_<FrameSplitter>(m, "FrameSplitter")
+      .def(py::init<>())
+      .def("append", &FrameSplitter::append)
+      .def("run", &FrameSplitter::run, py::arg("core").none(true))
+      .def_property_readonly("pending", &FrameSplitter::pending);
   py::class_<OutMsg>(m, "OutMsg")
       .def_readonly("kind", &OutMsg::kind)
       .def_readonly("src", &OutMsg::src)
