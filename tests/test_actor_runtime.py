@@ -174,3 +174,27 @@ def test_native_data_frames_interoperate_with_the_python_codec():
     for other in (StartAllreduce(5),):
         assert n.frame_parse(wire.encode(other, lambda r: None)[4:]) is None
     assert n.frame_parse(b"\x87") is None and n.frame_parse(b"") is None  # truncated: not taken
+
+
+def test_native_splitter_keeps_frame_order_across_cuts():
+    """FrameSplitter (the native path of a worker's connections): frames cut
+    anywhere across recvs come out whole and in order; with no worker core
+    every frame is handed back (nothing is applied natively)."""
+    n = _native()
+    frames = [wire.encode(StartAllreduce(r), lambda ref: None) for r in range(3)]
+    frames.append(wire.encode(ScatterBlock(torch.arange(5, dtype=torch.float32), 0, 1, 2, 3), lambda ref: None))
+    frames.append(wire.encode(StartAllreduce(9), lambda ref: None))
+    blob = b"".join(frames)
+    for cuts in ((1,), (4, 5), (7, 30, 31), tuple(range(1, len(blob)))):
+        sp = n.FrameSplitter()
+        got, last = [], 0
+        for c in cuts + (len(blob),):
+            sp.append(blob[last:c])
+            last = c
+            while True:
+                body = sp.run(None)
+                if body is None:
+                    break
+                got.append(wire.decode(body, lambda a: None))
+        assert [type(m).__name__ for m in got] == ["StartAllreduce"] * 3 + ["ScatterBlock", "StartAllreduce"]
+        assert [m.round for m in got] == [0, 1, 2, 3, 9] and sp.pending == 0
