@@ -151,7 +151,7 @@ class OneSidedAllreduce:
         device: Optional[torch.device] = None,
         store: Any = None,
         rows: int = 0,
-        part_bytes: int = 256 << 10,
+        part_bytes: int = 0,
         timeout_s: float = 30.0,
         threads: int = 256,
         role_wgs: int = 0,

@@ -102,7 +102,7 @@ void bind_onesided(py::module_& m) {
            }),
            py::arg("device"), py::arg("S"), py::arg("N"), py::arg("C"), py::arg("me"), py::arg("dtype") = "float32",
            py::arg("th_reduce") = 1.f, py::arg("th_complete") = 1.f, py::arg("max_lag") = 1, py::arg("rows") = 0,
-           py::arg("part_bytes") = int64_t(256) << 10, py::arg("timeout_ms") = 30000, py::arg("threads") = 256,
+           py::arg("part_bytes") = 0, py::arg("timeout_ms") = 30000, py::arg("threads") = 256,
            py::arg("role_wgs") = 0, py::arg("cu_keep") = 0, py::arg("fenced") = false,
            py::arg("window_output") = false)
       .def("gather_row_dlpack",
