@@ -532,10 +532,33 @@ __device__ void reduce_role(const Args& a, char* out, uint32_t r, int32_t w0, in
   }
 }
 
+// State of peer chunk (p, k) of round r from its P gather tags: lost if any
+// part is lost, else pending if any is, else landed.  The tags are loaded in
+// batches of 8 before any is looked at (independent uncached loads in
+// flight together): one thread scans a whole chunk, and a chunk of many parts
+// must not cost one memory latency per part.
+__device__ inline int32_t chunk_tags_state(const uint32_t* fl, const Layout& L, int32_t row, int32_t p, int32_t k,
+                                           uint32_t r) {
+  constexpr int kBatch = 8;
+  int32_t st = kLanded;
+  for (int32_t j0 = 0; j0 < L.P; j0 += kBatch) {
+    uint32_t t[kBatch];
+#pragma unroll
+    for (int u = 0; u < kBatch; ++u) t[u] = j0 + u < L.P ? DevMem::ld(fl + L.gtag(row, p, k, j0 + u)) : tag_done(r);
+#pragma unroll
+    for (int u = 0; u < kBatch; ++u) {
+      const int32_t s = tag_state(t[u], r);
+      if (s == kLost) return kLost;
+      if (s == kPending) st = kPending;
+    }
+  }
+  return st;
+}
+
 // ---- complete: the thComplete decision -------------------------------------------
 __device__ void complete_role(const Args& a, uint32_t r) {
   const Layout& L = a.L;
-  const int32_t N = L.N, P = L.P, me = a.me, K = L.Kmax;
+  const int32_t N = L.N, me = a.me, K = L.Kmax;
   const int32_t row = int32_t(r % uint32_t(L.D));
   uint32_t* fl = a.tab->fl[me];
   __shared__ int32_t landed_s, pending_s, own_s, verdict;
@@ -561,15 +584,7 @@ __device__ void complete_role(const Args& a, uint32_t r) {
         my_o += sys_load(a.loc + L.odone(k)) == r + 1u;
         continue;
       }
-      int32_t st = kLanded;
-      for (int32_t j = 0; j < P; ++j) {
-        const int32_t s = tag_state(DevMem::ld(fl + L.gtag(row, p, k, j)), r);
-        if (s == kLost) {
-          st = kLost;
-          break;
-        }
-        if (s == kPending) st = kPending;
-      }
+      int32_t st = chunk_tags_state(fl, L, row, p, k, r);
       if (st == kPending && (past[p] || sys_load(a.dead + p))) st = kLost;
       my_l += st == kLanded;
       my_p += st == kPending;
@@ -600,8 +615,7 @@ __device__ void complete_role(const Args& a, uint32_t r) {
     if (p == me) {
       in = sys_load(a.loc + L.odone(k)) == r + 1u;
     } else {
-      in = true;
-      for (int32_t j = 0; j < P && in; ++j) in = tag_state(DevMem::ld(fl + L.gtag(row, p, k, j)), r) == kLanded;
+      in = chunk_tags_state(fl, L, row, p, k, r) == kLanded;
     }
     sys_store(a.loc + L.cmask(p, k), in ? 1u : 0u);
     // the output's per-chunk contributor counts (0 outside the output set)
@@ -878,7 +892,6 @@ void with_ns(int32_t N, F&& f) {
 
 template <typename T>
 void launch_call(hipStream_t s, const Args& a) {
-  constexpr int ES = sizeof(T);
   const unsigned nt = a.threads <= 256 ? 256u : 1024u;
   const unsigned grid = unsigned(onesided_grid(a));
   with_ns(a.L.N, [&](auto ns) {
