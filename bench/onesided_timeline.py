@@ -45,6 +45,7 @@ def main():
     ap.add_argument("--calls", type=int, default=5)
     ap.add_argument("--out-dir", required=True)
     ap.add_argument("--window-output", action="store_true", help="calls without out: the lane's window row")
+    ap.add_argument("--part-bytes", type=int, default=0, help="0: the lane's auto part size")
     a = ap.parse_args()
     rank = int(os.environ["RANK"])
     dist.init_process_group("gloo")
@@ -56,7 +57,8 @@ def main():
     for mb in [float(s) for s in a.sizes_mb.split(",")]:
         S = int(mb * (1 << 20)) // 4
         C = min(S, int(a.chunk_mb * (1 << 20)) // 4)
-        ar = OneSidedAllreduce(S, max_chunk_size=C, device=dev, window_output=a.window_output)
+        ar = OneSidedAllreduce(S, max_chunk_size=C, device=dev, window_output=a.window_output,
+                               part_bytes=a.part_bytes)
         info = ar.info()
         info["kme"] = ar.geometry.num_chunks(rank)
         x = torch.randn(S, device=dev)
