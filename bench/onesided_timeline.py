@@ -45,7 +45,7 @@ def main():
     ap.add_argument("--calls", type=int, default=5)
     ap.add_argument("--out-dir", required=True)
     ap.add_argument("--window-output", action="store_true", help="calls without out: the lane's window row")
-    ap.add_argument("--part-bytes", type=int, default=0, help="0: the lane's auto part size")
+    ap.add_argument("--part-bytes", type=int, default=0, help="0: the lane default part size")
     a = ap.parse_args()
     rank = int(os.environ["RANK"])
     dist.init_process_group("gloo")

@@ -187,23 +187,10 @@ OneSidedLane::OneSidedLane(int32_t device, int64_t S, int32_t N, int64_t C, int3
   const int64_t want = std::max<int64_t>(64, (p.part_bytes > 0 ? p.part_bytes : kAutoPartBytes) / int64_t(es_));
   part_len_ = std::min(round_up(want, 64), round_up(C, 64));
   P_ = int32_t((C + part_len_ - 1) / part_len_);
-  if (p.part_bytes <= 0) {
-    // Auto: a small round has few (peer, chunk, part) items, and one
-    // workgroup per item moves it -- a 64 Ki-float round at N=2 was ONE
-    // 128 KiB part, 9 of its 37 us in one push workgroup
-    // (profiles/r06/onesided_small/).  Split the chunks so the push and copy
-    // roles get >= kAutoMinItems workgroups, parts of >= 1024 elements.
-    const int64_t per_part = int64_t(N - 1) * Kmax_;
-    const int64_t items = per_part * P_;
-    if (items < kAutoMinItems) {
-      const int64_t parts = std::min<int64_t>(kMaxParts, (kAutoMinItems + per_part - 1) / per_part);
-      const int64_t len = std::max<int64_t>(1024, round_up((C + parts - 1) / parts, 64));
-      if (len < part_len_) {
-        part_len_ = len;
-        P_ = int32_t((C + part_len_ - 1) / part_len_);
-      }
-    }
-  }
+  // (Splitting a small round's chunks into more parts, for more push / copy
+  // workgroups, made it slower: 42-44 vs 33-37 us at 64 Ki floats, N=2 --
+  // its time is hand-off latency, and every part adds a gate and a tag to
+  // scan, profiles/r06/onesided_small/.)
   if (P_ > 64) {
     part_len_ = round_up((C + 63) / 64, 64);
     P_ = int32_t((C + part_len_ - 1) / part_len_);

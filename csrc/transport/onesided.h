@@ -44,7 +44,7 @@ struct OneSidedParams {
   float th_reduce = 1.f, th_complete = 1.f;
   int32_t max_lag = 1;
   int32_t rows = 0;                      // ring depth D (0: max(3, maxLag + 2))
-  int64_t part_bytes = 0;  // <= 0: auto (256 KiB parts, finer for rounds with few items)
+  int64_t part_bytes = 0;  // <= 0: the default part size (kAutoPartBytes)
   int64_t timeout_ms = 30000;            // bound of every wait (then forced + error)
   int32_t threads = 256;                 // workgroup size of the round launch (256 or 1024)
   int32_t role_wgs = 0;                  // workgroups per data role (push / reduce / copy); 0: automatic
@@ -204,8 +204,7 @@ class OneSidedLane {
     int64_t deadline_ms = 0;
   };
   static constexpr int64_t kDefaultRoleWgs = 256;
-  static constexpr int64_t kAutoPartBytes = int64_t(256) << 10;  // part size of big rounds (auto)
-  static constexpr int64_t kAutoMinItems = 32;                    // push items a small round is split into (auto)
+  static constexpr int64_t kAutoPartBytes = int64_t(256) << 10;  // default part size (part_bytes <= 0)
   // wgs: reduce = 2 x wgs; push / copy = wgs unless given
   void size_roles(int64_t wgs, int64_t push_wgs = 0, int64_t copy_wgs = 0);
   void gpu_call(uintptr_t stream, const char* in, char* out, int32_t* counts, int32_t kcols);

@@ -97,7 +97,7 @@ def main():
     ap.add_argument("--delay-ms", type=float, default=50.0)
     ap.add_argument("--kill-after", type=int, default=-1)
     ap.add_argument("--compute-ms", type=float, default=0.0, help="every rank 'computes' this long before a call")
-    ap.add_argument("--part-bytes", type=int, default=0, help="0: the lane's auto part size")
+    ap.add_argument("--part-bytes", type=int, default=0, help="0: the lane default part size")
     ap.add_argument("--timeout-s", type=float, default=30.0)
     ap.add_argument("--handoff", default="lite", choices=["lite", "fenced"])
     ap.add_argument("--window-output", action="store_true", help="exact: calls without out return window rows")
