@@ -206,7 +206,7 @@ class Node:
     def send_frames(self, address: str, frame: bytes) -> None:
         """Encoded frames to ``address`` (see send_many)."""
         if address == self.address:
-            r = wire.FrameReader(None)
+            r = wire.FrameReader()
             for body in r.feed(frame):
                 self.mailbox.put(wire.decode(body, self.ref))
             return
@@ -305,12 +305,12 @@ class Node:
     def _deliver_body(self, body: bytes) -> None:
         self._deliver(wire.decode(body, self.ref))
 
-    def _new_reader(self, conn: socket.socket) -> Any:
+    def _new_reader(self) -> Any:
         if self.frame_consumer is not None and self.on_message is None:
             from .._native_loader import load
 
             return load().FrameSplitter()
-        return wire.FrameReader(conn)
+        return wire.FrameReader()
 
     def _poll_timeout(self) -> Optional[float]:
         """Run the progress hook: None -> block until a message, 0 -> progress
@@ -364,7 +364,7 @@ class Node:
                         with self._accepted_lock:
                             new, self._accepted = self._accepted, []
                         for conn in new:
-                            sel.register(conn, selectors.EVENT_READ, self._new_reader(conn))
+                            sel.register(conn, selectors.EVENT_READ, self._new_reader())
                             inbound.append(conn)
                         continue
                     conn, reader = key.fileobj, key.data

@@ -9,7 +9,6 @@ travel as raw little-endian bytes plus a dtype tag.
 """
 from __future__ import annotations
 
-import socket
 import struct
 from typing import Any, Callable, Dict, Optional
 
@@ -129,25 +128,16 @@ def decode(body: bytes, addr_to_ref: Callable[[Optional[str]], Any]) -> Any:
 
 
 class FrameReader:
-    """Frames of one connection, read through a buffer: one ``recv`` may hold
-    several frames (a sender's batch, ``Node.send_many``), so a burst costs
-    one system call instead of two per frame."""
+    """Frames of one connection: bytes as they arrive -> complete frame
+    bodies.  One ``recv`` may hold several frames (a sender's batch,
+    ``Node.send_many``) or part of one."""
 
-    def __init__(self, sock: socket.socket, bufsize: int = 1 << 16):
-        self._sock = sock
+    def __init__(self):
         self._buf = bytearray()
-        self._bufsize = bufsize
-
-    def _fill(self) -> bool:
-        chunk = self._sock.recv(self._bufsize)
-        if not chunk:
-            return False
-        self._buf += chunk
-        return True
 
     def feed(self, chunk: bytes) -> list:
         """Bytes received on the connection -> the bodies of the frames they
-        complete (a selector-driven reader: no blocking recv)."""
+        complete."""
         self._buf += chunk
         out = []
         while len(self._buf) >= 4:
@@ -159,40 +149,3 @@ class FrameReader:
             out.append(bytes(self._buf[4:4 + n]))
             del self._buf[:4 + n]
         return out
-
-    def read(self) -> Optional[bytes]:
-        """The next frame's body, or None once the peer closed the connection."""
-        while len(self._buf) < 4:
-            if not self._fill():
-                return None
-        (n,) = _HDR.unpack_from(self._buf, 0)
-        if n > MAX_FRAME:
-            raise ValueError(f"frame of {n} bytes exceeds limit")
-        while len(self._buf) < 4 + n:
-            if not self._fill():
-                return None
-        body = bytes(self._buf[4:4 + n])
-        del self._buf[:4 + n]
-        return body
-
-
-def read_frame(sock: socket.socket) -> Optional[bytes]:
-    hdr = _recv_exact(sock, 4)
-    if hdr is None:
-        return None
-    (n,) = _HDR.unpack(hdr)
-    if n > MAX_FRAME:
-        raise ValueError(f"frame of {n} bytes exceeds limit")
-    return _recv_exact(sock, n)
-
-
-def _recv_exact(sock: socket.socket, n: int) -> Optional[bytes]:
-    buf = bytearray(n)
-    view = memoryview(buf)
-    got = 0
-    while got < n:
-        k = sock.recv_into(view[got:], n - got)
-        if k == 0:
-            return None
-        got += k
-    return bytes(buf)

@@ -750,7 +750,7 @@ class AllreduceWorker:
                     self._frames_ok = None  # the peer map changed: look again
                     from .parallel.wire import FrameReader, decode  # noqa: PLC0415
 
-                    for body in FrameReader(None).feed(frames):
+                    for body in FrameReader().feed(frames):
                         ref.tell(decode(body, lambda a: None), self)
                     continue
                 ref.tell_frames(frames)

@@ -71,7 +71,7 @@ def test_frames_split_across_and_within_recvs():
     frames.append(wire.encode(ScatterBlock(torch.arange(7, dtype=torch.float32), 0, 1, 2, 3), lambda ref: None))
     blob = b"".join(frames)
     for cut in (1, 3, 4, 5, 17, len(blob) - 1):
-        r = wire.FrameReader(None)
+        r = wire.FrameReader()
         bodies = r.feed(blob[:cut]) + r.feed(blob[cut:])
         msgs = [wire.decode(b, lambda a: None) for b in bodies]
         assert [m.round for m in msgs] == [0, 1, 2, 3, 4, 3]
