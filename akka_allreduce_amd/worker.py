@@ -194,6 +194,8 @@ class AllreduceWorker:
                 ok = core is not None and self.initialized and not self._pre_init and self.transport == "outbox"
                 try:
                     body = splitter.run(core if ok else None)
+                except ValueError:
+                    raise  # a corrupt stream: the runtime closes the connection
                 except Exception as e:  # the frame is consumed; tryCatch semantics (W:287-299)
                     self.errors.append(e)
                     log.error("%s: error handling a data frame: %s", self.name, e)

@@ -754,7 +754,9 @@ class FrameSplitter {
     while (buf_.size() - pos_ >= 4) {
       const unsigned char* h = reinterpret_cast<const unsigned char*>(buf_.data() + pos_);
       const size_t n = (size_t(h[0]) << 24) | (size_t(h[1]) << 16) | (size_t(h[2]) << 8) | size_t(h[3]);
-      if (n > (size_t(1) << 31)) throw AkkaError("frame exceeds the size limit");
+      // a corrupt stream: ValueError, which makes the runtime close the
+      // connection (as wire.FrameReader does) instead of retrying forever
+      if (n > (size_t(1) << 31)) throw py::value_error("frame of " + std::to_string(n) + " bytes exceeds limit");
       if (buf_.size() - pos_ < 4 + n) break;
       const char* body = buf_.data() + pos_ + 4;
       pos_ += 4 + n;

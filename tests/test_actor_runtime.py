@@ -220,3 +220,14 @@ def test_native_splitter_large_frames_and_compaction():
     assert [m.round for m in got] == list(range(12)) and sp.pending == 0
     for r, m in enumerate(got):
         assert m.value.numel() == 50_000 + r and bool((m.value == float(r)).all())
+
+
+def test_native_splitter_refuses_an_oversized_frame():
+    """A length prefix past the frame limit is a corrupt stream: ValueError
+    (the runtime closes the connection), never a frame handed on."""
+    import pytest
+
+    sp = _native().FrameSplitter()
+    sp.append(b"\xff\xff\xff\xff" + b"x" * 16)
+    with pytest.raises(ValueError):
+        sp.run(None)
